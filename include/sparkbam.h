@@ -1,0 +1,200 @@
+/*
+ * sparkbam.h -- C-ABI of libsparkbam_hip.so, the MI355X (gfx950) implementation of
+ * spark-bam's BGZF-inflate + BAM record-boundary hot path.
+ *
+ * This is the drop-in boundary: plain pointers and sizes, no framework types.  Each
+ * entry point names the reference interface it replaces (paths relative to the
+ * reference repository root).  The reference's host side is Scala on the JVM; the
+ * JNI binding a maintainer would add is shown in INTEGRATION.md.
+ *
+ * Conventions:
+ *  - Every call returns an int status: SBH_OK or one of SBH_E_*, which map one-to-one
+ *    onto the reference's exceptions (see below).  sbh_last_error() gives the message.
+ *  - The caller owns every host buffer.  A context owns its device memory.
+ *  - One context per device.  Calls on distinct contexts are thread-safe; a single
+ *    context (and its shards) must be externally synchronized, like the reference's
+ *    Checker instances (check/.../PosChecker.scala:19-20 share buffers).
+ *  - Offsets: "file offsets" are byte offsets in the compressed BGZF file; "flat"
+ *    offsets index the shard's concatenated uncompressed bytes (the reference's
+ *    UncompressedBytes view, bgzf/.../block/UncompressedBytes.scala:13-87).  A
+ *    virtual position Pos(blockPos, offset) is the htsjdk long blockPos<<16|offset
+ *    (bgzf/.../Pos.scala:24).
+ */
+#ifndef SPARKBAM_H
+#define SPARKBAM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---- */
+#define SBH_OK 0
+#define SBH_E_ARG 1                  /* IllegalArgumentException                     */
+#define SBH_E_HIP 2                  /* device/runtime failure                       */
+#define SBH_E_NOMEM 3
+#define SBH_E_HEADER_PARSE 10        /* HeaderParseException (Header.scala:50-57)    */
+#define SBH_E_HEADER_SEARCH_FAILED 11 /* HeaderSearchFailedException (FindBlockStart.scala:31-35) */
+#define SBH_E_TRUNCATED 12           /* EOFException escaping MetadataStream         */
+#define SBH_E_INFLATE_SIZE 13        /* IOException "Expected N decompressed bytes"  (Stream.scala:52-54) */
+#define SBH_E_INFLATE_DATA 14        /* java.util.zip.DataFormatException             */
+#define SBH_E_BAD_ISIZE 15           /* ISIZE outside [0, 65536]                      */
+#define SBH_E_NO_READ_FOUND 16       /* NoReadFoundException (FindRecordStart.scala:66-71) */
+#define SBH_E_NEED_HALO 17           /* result depends on bytes past the resident range */
+#define SBH_E_STATE 18               /* call order violated (e.g. check before inflate) */
+#define SBH_E_NOT_FOUND 19           /* Pos not in the indexed block chain            */
+
+/* ---- full-checker result word (check/.../full/error/Flags.scala:21-45) ----
+ *  bit 31     : Success(readsParsed)
+ *  bit 30     : unknown (needs bytes past an open shard end; never in a valid run)
+ *  bits 20-29 : readsParsed (Success) or readsBeforeError (Flags)
+ *  bits 0-18  : the 19 Flags booleans in the serde order of Flags.scala:203-222:
+ *    0 tooFewFixedBlockBytes  1 negativeReadIdx  2 tooLargeReadIdx  3 negativeReadPos
+ *    4 tooLargeReadPos  5 negativeNextReadIdx  6 tooLargeNextReadIdx
+ *    7 negativeNextReadPos  8 tooLargeNextReadPos  9 tooFewBytesForReadName
+ *    10 nonNullTerminatedReadName  11 nonASCIIReadName  12 noReadName  13 emptyReadName
+ *    14 tooFewBytesForCigarOps  15 invalidCigarOp  16 emptyMappedCigar
+ *    17 emptyMappedSeq  18 tooFewRemainingBytesImplied                              */
+#define SBH_FULL_SUCCESS 0x80000000u
+#define SBH_FULL_UNKNOWN 0x40000000u
+#define SBH_FULL_N_SHIFT 20
+#define SBH_FULL_FLAGS_MASK 0x7FFFFu
+/* Counts aggregation layout: counts[nnz * 19 + flag], nnz = Flags.numNonZeroFields
+ * (Flags.scala:118-123) in [0, 21); rbe_hist[nnz * 64 + readsBeforeError]. */
+#define SBH_NNZ_MAX 21
+#define SBH_RBE_MAX 64
+
+/* block flags */
+#define SBH_BLOCK_EMPTY 1u     /* dataLength == 2: the stream ends at this block (Stream.scala:56-58) */
+#define SBH_BLOCK_TRUNCATED 2u /* runs past the resident bytes                     */
+
+typedef struct sbh_ctx sbh_ctx;
+typedef struct sbh_shard sbh_shard;
+
+/* bgzf Metadata(start, compressedSize, uncompressedSize) (bgzf/.../block/Metadata.scala:6-8)
+ * plus the header size, flat start and inflate status. */
+typedef struct {
+  uint64_t start;  /* file offset of the block header */
+  uint64_t ustart; /* flat offset of its first uncompressed byte */
+  uint32_t csize;
+  uint32_t hsize;
+  uint32_t usize;
+  uint32_t flags;  /* SBH_BLOCK_* */
+} sbh_block;
+
+/* ---- context ---- */
+int sbh_ctx_create(int device, sbh_ctx **out);
+int sbh_ctx_destroy(sbh_ctx *ctx);
+const char *sbh_last_error(const sbh_ctx *ctx);
+/* Use a caller-owned hipStream_t (e.g. torch.cuda.current_stream().cuda_stream). */
+int sbh_ctx_set_stream(sbh_ctx *ctx, void *hip_stream);
+int sbh_ctx_synchronize(sbh_ctx *ctx);
+const char *sbh_version(void);
+
+/* Header.make (bgzf/.../block/Header.scala:48-83): host-side parse of 18 bytes. */
+int sbh_header_make(const uint8_t *bytes, uint64_t avail, int32_t *hsize, int32_t *csize);
+
+/* ---- shards: compressed bytes [file_offset, file_offset + n) resident in HBM ----
+ * comp may be a host or a device pointer (comp_on_device); the shard keeps a copy
+ * (device pointers are copied device-to-device).  file_size locates EOF: when
+ * file_offset + n == file_size the resident bytes end at EOF, otherwise the end is
+ * "open" and results that would need later bytes report SBH_E_NEED_HALO. */
+int sbh_shard_create(sbh_ctx *ctx, const void *comp, uint64_t n, uint64_t file_offset,
+                     uint64_t file_size, int comp_on_device, sbh_shard **out);
+int sbh_shard_destroy(sbh_shard *sh);
+/* Device pointer of the resident compressed bytes (padded). */
+const void *sbh_shard_comp_device_ptr(sbh_shard *sh);
+
+/* FindBlockStart.apply(path, start, in, bgzfBlocksToCheck) (FindBlockStart.scala:8-36):
+ * smallest file offset >= start where bgzf_blocks_to_check consecutive headers parse. */
+int sbh_find_block_start(sbh_shard *sh, uint64_t start, int32_t bgzf_blocks_to_check,
+                         uint64_t *out);
+
+/* MetadataStream from `start` (MetadataStream.scala:16-58) over the resident bytes:
+ * builds the device block table (the chain of blocks from start, empty blocks
+ * included and flagged) and the flat layout.  start must be a block start. */
+int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_size);
+int sbh_get_blocks(sbh_shard *sh, uint64_t first, uint64_t count, sbh_block *out);
+
+/* StreamI._advance's Inflater(nowrap=true).inflate (Stream.scala:31-71) for every
+ * indexed block: the shard's flat uncompressed buffer in HBM.  Fails with the first
+ * block error in file order (SBH_E_INFLATE_SIZE / _DATA / _BAD_ISIZE, *bad_block). */
+int sbh_inflate(sbh_shard *sh, uint64_t *bad_block);
+/* Copy flat bytes [flat, flat + n) to host memory. */
+int sbh_read_flat(sbh_shard *sh, uint64_t flat, uint64_t n, uint8_t *out);
+const void *sbh_flat_device_ptr(sbh_shard *sh);
+
+/* Pos <-> flat (canonical positions, Pos.scala; curPos rolls to the next block). */
+int sbh_flat_of(sbh_shard *sh, uint64_t block_pos, uint32_t offset, uint64_t *flat);
+int sbh_pos_of(sbh_shard *sh, uint64_t flat, uint64_t *block_pos, uint32_t *offset);
+/* Flat offset of the first block whose file offset is >= file_off (the flat image
+ * of Pos(file_off, 0) as an exclusive bound). */
+int sbh_flat_bound(sbh_shard *sh, uint64_t file_off, uint64_t *flat);
+
+/* Contig lengths (BAM header n_ref x l_ref; check/.../header/Header.scala:37-53). */
+int sbh_set_contigs(sbh_shard *sh, const int32_t *lens, int32_t n);
+
+/* eager.Checker.apply at every flat position of [begin, end)
+ * (check/.../eager/Checker.scala:24-126).  The bitmap stays on the device (used by
+ * find_record_start / count_records); out_bits (optional, (end-begin+7)/8 bytes,
+ * bit i = position begin+i, LSB first) receives a copy. */
+int sbh_check_eager(sbh_shard *sh, uint64_t begin, uint64_t end, int32_t reads_to_check,
+                    uint8_t *out_bits, uint64_t *n_true);
+
+/* full.Checker.apply at every flat position of [begin, end)
+ * (check/.../full/Checker.scala:22-184) with the FullCheck aggregation
+ * (cli/.../check/full/FullCheck.scala:142-192).  Optional outputs: out_words
+ * (end-begin words), counts (21*19), rbe_hist (21*64), close-call positions
+ * (numNonZeroFields <= 2) as (flat, word) pairs up to close_cap. */
+int sbh_check_full(sbh_shard *sh, uint64_t begin, uint64_t end, int32_t reads_to_check,
+                   uint32_t *out_words, uint64_t *counts, uint64_t *rbe_hist,
+                   uint64_t *n_success, uint64_t *close_flat, uint32_t *close_word,
+                   uint64_t close_cap, uint64_t *n_close);
+
+/* FindRecordStart.withDelta (check/.../spark/FindRecordStart.scala:30-63) from flat
+ * position from_flat: first eager-true position within max_read_size positions of
+ * the stream. */
+int sbh_find_record_start(sbh_shard *sh, uint64_t from_flat, int32_t reads_to_check,
+                          int32_t max_read_size, uint64_t *out_flat, int32_t *out_delta);
+
+/* Record chain from first_flat (PosStream.scala:14-22): number of records whose
+ * start is < end_flat (RecordStream.takeWhile(pos < Pos(end, 0)),
+ * CanLoadBam.scala:350-355).  Uses the eager bitmap when it covers the range and
+ * the chain verifies against it; otherwise an exact sequential walk. */
+int sbh_count_records(sbh_shard *sh, uint64_t first_flat, uint64_t end_flat,
+                      uint64_t *count);
+
+/* One Hadoop split of loadReadsAndPositions / loadSplitsAndReads
+ * (load/.../CanLoadBam.scala:316-356): FindBlockStart(start) -> FindRecordStart ->
+ * records while vpos < Pos(end, 0).  first_vpos = htsjdk virtual offset of the
+ * first record (valid when *count > 0). */
+int sbh_split(sbh_shard *sh, uint64_t start, uint64_t end, int32_t bgzf_blocks_to_check,
+              int32_t reads_to_check, int32_t max_read_size, uint64_t *first_vpos,
+              uint64_t *count);
+
+/* The whole per-shard hot path as one call (the benchmark step): index from
+ * index_start, inflate, eager check at every position of the owned flat range
+ * [flat(own_begin_file), flat_bound(own_end_file)), then the owned split:
+ * first record >= Pos(own_begin_block, 0) and the record count while
+ * vpos < Pos(own_end_file, 0).  All device work is enqueued on the context stream;
+ * results are read back at the end. */
+typedef struct {
+  uint64_t n_blocks;
+  uint64_t comp_bytes;   /* compressed bytes of the owned blocks              */
+  uint64_t flat_bytes;   /* uncompressed bytes of the owned blocks (positions) */
+  uint64_t n_true;       /* eager-true positions in the owned range           */
+  uint64_t first_vpos;   /* first record of the owned split (if count > 0)    */
+  uint64_t count;        /* records of the owned split                        */
+  uint64_t exit_flat;    /* first chain record at/after the owned end         */
+  int32_t status;
+  int32_t anomalies;     /* chain/bitmap disagreements resolved by the walk   */
+} sbh_shard_result;
+
+int sbh_run_shard(sbh_shard *sh, uint64_t index_start, uint64_t own_end_file,
+                  int32_t reads_to_check, int32_t max_read_size, sbh_shard_result *res);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPARKBAM_H */

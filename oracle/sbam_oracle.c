@@ -126,7 +126,7 @@ int or_stream_next(const uint8_t *file, int64_t fsize, int64_t pos, uint8_t *out
   zs.next_out = out;
   zs.avail_out = (uInt)usize;
   int zr = Z_OK;
-  if (usize > 0) zr = inflate(&zs, Z_PARTIAL_FLUSH);
+  zr = inflate(&zs, Z_PARTIAL_FLUSH); /* zlib runs even with avail_out == 0 */
   int32_t produced = usize - (int32_t)zs.avail_out;
   inflateEnd(&zs);
   if (zr == Z_DATA_ERROR || zr == Z_NEED_DICT || zr == Z_MEM_ERROR || zr == Z_STREAM_ERROR)

@@ -1,0 +1,22 @@
+"""spark-bam on MI355X: host-side mirror of spark-bam's BGZF + record-boundary API over
+the C-ABI in include/sparkbam.h (libsparkbam_hip.so, hand-written gfx950 kernels).
+
+Import name: ``spark_bam_amd`` (the directory name contains a hyphen, so load it with
+``__graft_entry__.load_package()`` or importlib).  Names follow the reference:
+
+  bgzf:   Pos, Header.make, Metadata, FindBlockStart, Stream (blocks / inflated bytes)
+  check:  eager.Checker / full.Checker (batched over positions), FindRecordStart
+  load:   load_splits_and_reads / load_bam_count (CanLoadBam), FileSplits
+"""
+from ._lib import (BLOCK_EMPTY, BLOCK_TRUNCATED, FULL_FLAGS_MASK, FULL_N_SHIFT,  # noqa: F401
+                   FULL_SUCCESS, FULL_UNKNOWN, SparkBamError, lib)
+from .device import Context, Shard  # noqa: F401
+from .api import (FLAG_NAMES, Header, Metadata, Pos, Split, bam_header, check_bam,  # noqa: F401
+                  file_splits, full_check, load_bam_count, load_splits_and_reads,
+                  parse_bam_header)
+
+__all__ = [
+    "Context", "Shard", "SparkBamError", "Pos", "Header", "Metadata", "Split", "FLAG_NAMES",
+    "file_splits", "load_splits_and_reads", "load_bam_count", "check_bam", "full_check",
+    "bam_header", "parse_bam_header", "lib",
+]

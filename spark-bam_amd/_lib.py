@@ -1,0 +1,109 @@
+"""ctypes binding of libsparkbam_hip.so (the C-ABI declared in include/sparkbam.h).
+
+There is no CPU fallback: if the HIP library is missing or cannot be loaded, every
+entry point raises.  The library is built in-tree by spark-bam_amd/csrc/Makefile
+(``__graft_entry__.build()``).
+"""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libsparkbam_hip.so")
+
+SBH_OK = 0
+STATUS_NAMES = {
+    0: "SBH_OK", 1: "SBH_E_ARG", 2: "SBH_E_HIP", 3: "SBH_E_NOMEM", 10: "SBH_E_HEADER_PARSE",
+    11: "SBH_E_HEADER_SEARCH_FAILED", 12: "SBH_E_TRUNCATED", 13: "SBH_E_INFLATE_SIZE",
+    14: "SBH_E_INFLATE_DATA", 15: "SBH_E_BAD_ISIZE", 16: "SBH_E_NO_READ_FOUND",
+    17: "SBH_E_NEED_HALO", 18: "SBH_E_STATE", 19: "SBH_E_NOT_FOUND",
+}
+SBH_E_ARG, SBH_E_HIP, SBH_E_HEADER_PARSE, SBH_E_HEADER_SEARCH_FAILED = 1, 2, 10, 11
+SBH_E_TRUNCATED, SBH_E_INFLATE_SIZE, SBH_E_INFLATE_DATA, SBH_E_BAD_ISIZE = 12, 13, 14, 15
+SBH_E_NO_READ_FOUND, SBH_E_NEED_HALO, SBH_E_STATE, SBH_E_NOT_FOUND = 16, 17, 18, 19
+
+FULL_SUCCESS = 0x80000000
+FULL_UNKNOWN = 0x40000000
+FULL_N_SHIFT = 20
+FULL_FLAGS_MASK = 0x7FFFF
+BLOCK_EMPTY, BLOCK_TRUNCATED = 1, 2
+
+# Every symbol include/sparkbam.h declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "sbh_ctx_create", "sbh_ctx_destroy", "sbh_last_error", "sbh_ctx_set_stream",
+    "sbh_ctx_synchronize", "sbh_version", "sbh_header_make", "sbh_shard_create",
+    "sbh_shard_destroy", "sbh_shard_comp_device_ptr", "sbh_find_block_start", "sbh_index",
+    "sbh_get_blocks", "sbh_inflate", "sbh_read_flat", "sbh_flat_device_ptr", "sbh_flat_of",
+    "sbh_pos_of", "sbh_flat_bound", "sbh_set_contigs", "sbh_check_eager", "sbh_check_full",
+    "sbh_find_record_start", "sbh_count_records", "sbh_split", "sbh_run_shard",
+]
+
+
+class SbhBlock(C.Structure):
+    _fields_ = [("start", C.c_uint64), ("ustart", C.c_uint64), ("csize", C.c_uint32),
+                ("hsize", C.c_uint32), ("usize", C.c_uint32), ("flags", C.c_uint32)]
+
+
+class SbhShardResult(C.Structure):
+    _fields_ = [("n_blocks", C.c_uint64), ("comp_bytes", C.c_uint64), ("flat_bytes", C.c_uint64),
+                ("n_true", C.c_uint64), ("first_vpos", C.c_uint64), ("count", C.c_uint64),
+                ("exit_flat", C.c_uint64), ("status", C.c_int32), ("anomalies", C.c_int32)]
+
+
+class SparkBamError(RuntimeError):
+    """Maps an SBH_E_* status onto the reference's exception vocabulary."""
+
+    def __init__(self, code, message=""):
+        self.code = code
+        super().__init__(f"{STATUS_NAMES.get(code, code)}: {message}")
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise SparkBamError(SBH_E_STATE, f"HIP library not built: {LIB_PATH} "
+                                         "(run __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    P, I32, U32, U64 = C.c_void_p, C.c_int32, C.c_uint32, C.c_uint64
+    PU64, PI32, PU32 = C.POINTER(U64), C.POINTER(I32), C.POINTER(U32)
+    sig = {
+        "sbh_ctx_create": [I32, C.POINTER(P)],
+        "sbh_ctx_destroy": [P],
+        "sbh_ctx_set_stream": [P, P],
+        "sbh_ctx_synchronize": [P],
+        "sbh_header_make": [P, U64, PI32, PI32],
+        "sbh_shard_create": [P, P, U64, U64, U64, C.c_int, C.POINTER(P)],
+        "sbh_shard_destroy": [P],
+        "sbh_find_block_start": [P, U64, I32, PU64],
+        "sbh_index": [P, U64, PU64, PU64],
+        "sbh_get_blocks": [P, U64, U64, P],
+        "sbh_inflate": [P, PU64],
+        "sbh_read_flat": [P, U64, U64, P],
+        "sbh_flat_of": [P, U64, U32, PU64],
+        "sbh_pos_of": [P, U64, PU64, PU32],
+        "sbh_flat_bound": [P, U64, PU64],
+        "sbh_set_contigs": [P, P, I32],
+        "sbh_check_eager": [P, U64, U64, I32, P, PU64],
+        "sbh_check_full": [P, U64, U64, I32, P, P, P, PU64, P, P, U64, PU64],
+        "sbh_find_record_start": [P, U64, I32, I32, PU64, PI32],
+        "sbh_count_records": [P, U64, U64, PU64],
+        "sbh_split": [P, U64, U64, I32, I32, I32, PU64, PU64],
+        "sbh_run_shard": [P, U64, U64, I32, I32, C.POINTER(SbhShardResult)],
+    }
+    for name, args in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = C.c_int
+    L.sbh_last_error.argtypes = [P]
+    L.sbh_last_error.restype = C.c_char_p
+    L.sbh_version.argtypes = []
+    L.sbh_version.restype = C.c_char_p
+    for name in ("sbh_shard_comp_device_ptr", "sbh_flat_device_ptr"):
+        getattr(L, name).argtypes = [P]
+        getattr(L, name).restype = P
+    _lib = L
+    return L

@@ -1,0 +1,258 @@
+"""Reference-shaped host API over the C-ABI.
+
+Each function names the spark-bam entry point it mirrors (paths relative to the
+reference repository root).  All byte work runs in libsparkbam_hip.so on the GPU;
+this module only moves small results around (splits, counts, histograms).
+"""
+import ctypes as C
+import os
+from collections import namedtuple
+
+import numpy as np
+
+from ._lib import FULL_FLAGS_MASK, FULL_N_SHIFT, SBH_OK, SparkBamError, lib
+from .device import Context
+
+FLAG_NAMES = [  # check/.../full/error/Flags.scala:203-222 (serde order)
+    "tooFewFixedBlockBytes", "negativeReadIdx", "tooLargeReadIdx", "negativeReadPos",
+    "tooLargeReadPos", "negativeNextReadIdx", "tooLargeNextReadIdx", "negativeNextReadPos",
+    "tooLargeNextReadPos", "tooFewBytesForReadName", "nonNullTerminatedReadName",
+    "nonASCIIReadName", "noReadName", "emptyReadName", "tooFewBytesForCigarOps",
+    "invalidCigarOp", "emptyMappedCigar", "emptyMappedSeq", "tooFewRemainingBytesImplied",
+]
+
+DEFAULT_BGZF_BLOCKS_TO_CHECK = 5      # bgzf/.../block/package.scala:20
+DEFAULT_READS_TO_CHECK = 10          # check/.../check/package.scala:17-18
+DEFAULT_MAX_READ_SIZE = 100000000    # check/.../check/package.scala:28-29
+DEFAULT_SPLIT_SIZE = 32 * 1024 * 1024  # Hadoop local-FS block size (MaxSplitSize default)
+
+
+class Pos(namedtuple("Pos", "block_pos offset")):
+    """bgzf Pos(blockPos, offset) (bgzf/.../Pos.scala:12-43)."""
+
+    def to_htsjdk(self):
+        return (self.block_pos << 16) | self.offset
+
+    @classmethod
+    def from_htsjdk(cls, v):
+        return cls(v >> 16, v & 0xFFFF)
+
+    def __str__(self):
+        return f"{self.block_pos}:{self.offset}"
+
+    def minus(self, other, ratio=3.0):  # Pos.- with EstimatedCompressionRatio (Pos.scala:17-22)
+        return float(max(0, self.block_pos - other.block_pos + int((self.offset - other.offset) / ratio)))
+
+
+Split = namedtuple("Split", "start end")  # check/.../spark/Split.scala:9-13
+Metadata = namedtuple("Metadata", "start compressed_size uncompressed_size")  # Metadata.scala:6-8
+
+
+class Header:
+    @staticmethod
+    def make(b):
+        """Header.make (bgzf/.../block/Header.scala:48-83) -> (size, compressedSize)."""
+        arr = np.frombuffer(bytes(b), dtype=np.uint8)
+        hs, cs = C.c_int32(), C.c_int32()
+        rc = lib().sbh_header_make(arr.ctypes.data_as(C.c_void_p), arr.size, C.byref(hs), C.byref(cs))
+        if rc != SBH_OK:
+            raise SparkBamError(rc, "bad BGZF header")
+        return hs.value, cs.value
+
+
+def file_splits(file_size, split_size):
+    """Hadoop FileInputFormat.getSplits arithmetic (SPLIT_SLOP 1.1), as driven by
+    FileSplits.asJava(path, splitSize) (load/.../CanLoadBam.scala:205,314)."""
+    out, rem = [], file_size
+    while rem / split_size > 1.1:
+        out.append((file_size - rem, file_size - rem + split_size))
+        rem -= split_size
+    if rem != 0:
+        out.append((file_size - rem, file_size))
+    return out
+
+
+def parse_bam_header(flat):
+    """check/.../header/Header.scala:26-60: contig lengths + flat end of the header."""
+    b = bytes(flat)
+    if b[:4] != b"BAM\1":
+        raise SparkBamError(1, "not a BAM file (missing BAM\\1 magic)")
+    l_text = int.from_bytes(b[4:8], "little", signed=True)
+    c = 8 + l_text
+    n_ref = int.from_bytes(b[c:c + 4], "little", signed=True)
+    c += 4
+    names, lens = [], []
+    for _ in range(n_ref):
+        l_name = int.from_bytes(b[c:c + 4], "little", signed=True)
+        names.append(b[c + 4:c + 4 + l_name].rstrip(b"\0").decode())
+        c += 4 + l_name
+        lens.append(int.from_bytes(b[c:c + 4], "little", signed=True))
+        c += 4
+    return names, np.asarray(lens, dtype=np.int32), c
+
+
+def bam_header(shard):
+    """Header(path) over an indexed + inflated shard starting at file offset 0."""
+    n = min(shard.flat_size, 1 << 16)
+    while True:
+        try:
+            return parse_bam_header(shard.read_flat(0, n))
+        except (IndexError, ValueError):
+            if n >= shard.flat_size:
+                raise
+            n = min(shard.flat_size, n * 4)
+
+
+def _read(path_or_bytes):
+    if isinstance(path_or_bytes, (bytes, bytearray, memoryview, np.ndarray)):
+        return np.frombuffer(bytes(path_or_bytes), dtype=np.uint8) if not isinstance(
+            path_or_bytes, np.ndarray) else path_or_bytes
+    with open(path_or_bytes, "rb") as f:
+        return np.frombuffer(f.read(), dtype=np.uint8)
+
+
+class _Loaded:
+    """A whole BGZF file resident on one device: indexed, inflated, header parsed."""
+
+    def __init__(self, path_or_bytes, ctx=None, reads_to_check=DEFAULT_READS_TO_CHECK):
+        self.data = _read(path_or_bytes)
+        self.own_ctx = ctx is None
+        self.ctx = ctx or Context(0)
+        self.shard = self.ctx.shard(self.data)
+        self.shard.index(0)
+        self.shard.inflate()
+        self.names, self.contig_len, self.header_end = bam_header(self.shard)
+        self.shard.set_contigs(self.contig_len)
+        self.reads_to_check = reads_to_check
+
+    def close(self):
+        self.shard.close()
+        if self.own_ctx:
+            self.ctx.close()
+
+
+def load_splits_and_reads(path_or_bytes, split_size=DEFAULT_SPLIT_SIZE, ctx=None,
+                          bgzf_blocks_to_check=DEFAULT_BGZF_BLOCKS_TO_CHECK,
+                          reads_to_check=DEFAULT_READS_TO_CHECK, max_read_size=DEFAULT_MAX_READ_SIZE):
+    """CanLoadBam.loadSplitsAndReads (load/.../CanLoadBam.scala:268-302): the splits
+    (first record of every non-empty partition, sliding2 with Pos(fileSize, 0)) and
+    the per-partition record counts."""
+    L = _Loaded(path_or_bytes, ctx, reads_to_check)
+    try:
+        sh = L.shard
+        sh.check_eager(0, sh.flat_size, reads_to_check, want_bits=False)  # one pass, reused
+        firsts, counts = [], []
+        for s, e in file_splits(L.data.size, split_size):
+            try:
+                v, n = sh.split(s, e, bgzf_blocks_to_check, reads_to_check, max_read_size)
+            except SparkBamError:
+                raise
+            counts.append(n)
+            if n > 0:
+                firsts.append(Pos.from_htsjdk(v))
+        ends = firsts[1:] + [Pos(L.data.size, 0)]
+        return [Split(a, b) for a, b in zip(firsts, ends)], counts
+    finally:
+        L.close()
+
+
+def load_bam_count(path_or_bytes, split_size=DEFAULT_SPLIT_SIZE, ctx=None, **kw):
+    """sc.loadBam(path, splitSize).count (CanLoadBam.scala:196-266; CountReads)."""
+    _, counts = load_splits_and_reads(path_or_bytes, split_size, ctx, **kw)
+    return sum(counts)
+
+
+def _selected_flat_ranges(shard, ranges):
+    """Blocks.apply's `-i` filter: blocks whose START lies in one of the byte ranges
+    (check/.../check/Blocks.scala:89-96) -> merged flat ranges."""
+    blocks = shard.blocks()
+    out = []
+    for start, csize, usize, ustart, _h, flags in blocks:
+        if usize == 0:
+            continue
+        if ranges is not None and not any(a <= start < b for a, b in ranges):
+            continue
+        if out and out[-1][1] == ustart:
+            out[-1][1] = ustart + usize
+        else:
+            out.append([ustart, ustart + usize])
+    comp = sum(c for s, c, u, *_ in blocks if u and (ranges is None or any(a <= s < b for a, b in ranges)))
+    return [(a, b) for a, b in out], comp
+
+
+def check_bam(path_or_bytes, records=None, ranges=None, ctx=None,
+              reads_to_check=DEFAULT_READS_TO_CHECK):
+    """CheckBam -s (cli/.../check/eager/CheckBam.scala + CheckerApp.scala:65-227): the
+    eager checker at every position of the selected blocks vs the `.records` truth.
+    `records` is a list of (blockPos, offset); returns the summary numbers."""
+    L = _Loaded(path_or_bytes, ctx, reads_to_check)
+    try:
+        sh = L.shard
+        fr, comp = _selected_flat_ranges(sh, ranges)
+        truth = None
+        if records is not None:
+            truth = np.asarray(sorted(sh.flat_of(b, o) for b, o in records), dtype=np.int64)
+        tp = fp = fn = positions = 0
+        fps, fns = [], []
+        for a, b in fr:
+            n, bits = sh.check_eager(a, b, reads_to_check)
+            called = np.flatnonzero(np.unpackbits(bits, bitorder="little")[: b - a]) + a
+            positions += b - a
+            if truth is not None:
+                t = truth[(truth >= a) & (truth < b)]
+                tp += np.intersect1d(called, t).size
+                fpl = np.setdiff1d(called, t)
+                fnl = np.setdiff1d(t, called)
+                fp += fpl.size
+                fn += fnl.size
+                fps += [Pos(*sh.pos_of(int(x))) for x in fpl]
+                fns += [Pos(*sh.pos_of(int(x))) for x in fnl]
+            else:
+                tp += n
+        return {"positions": positions, "compressed": comp, "reads": tp + fn,
+                "true_positives": tp, "false_positives": fp, "false_negatives": fn,
+                "fp_positions": fps, "fn_positions": fns}
+    finally:
+        L.close()
+
+
+def full_check(path_or_bytes, ranges=None, ctx=None, reads_to_check=DEFAULT_READS_TO_CHECK):
+    """FullCheck (cli/.../check/full/FullCheck.scala:88-329) aggregation: Counts per
+    numNonZeroFields, totals, and the critical (1-flag) / close (2-flag) positions."""
+    L = _Loaded(path_or_bytes, ctx, reads_to_check)
+    try:
+        sh = L.shard
+        fr, comp = _selected_flat_ranges(sh, ranges)
+        counts = np.zeros((21, 19), dtype=np.uint64)
+        rbe = np.zeros((21, 64), dtype=np.uint64)
+        n_success = positions = 0
+        close = []
+        for a, b in fr:
+            r = sh.check_full(a, b, reads_to_check)
+            counts += r["counts"]
+            rbe += r["rbe"]
+            n_success += r["n_success"]
+            positions += b - a
+            for f, w in zip(r["close_flat"].tolist(), r["close_word"].tolist()):
+                close.append((Pos(*sh.pos_of(int(f))), int(w)))
+        totals = dict(zip(FLAG_NAMES, counts.sum(axis=0).astype(np.int64).tolist()))
+        return {"positions": positions, "compressed": comp, "n_success": n_success,
+                "counts_by_nnz": counts, "rbe_by_nnz": rbe, "totals": totals, "close": close}
+    finally:
+        L.close()
+
+
+def flags_of(word):
+    return [FLAG_NAMES[i] for i in range(19) if word & (1 << i)]
+
+
+def reads_before_error(word):
+    return (word >> FULL_N_SHIFT) & 0x3FF
+
+
+def word_flags_mask(word):
+    return word & FULL_FLAGS_MASK
+
+
+def here():
+    return os.path.dirname(os.path.abspath(__file__))

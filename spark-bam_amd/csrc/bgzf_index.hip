@@ -1,0 +1,308 @@
+// bgzf_index.hip -- BGZF header scan, FindBlockStart and block-chain indexing on CDNA4.
+//
+// Replaces, for a whole shard at once:
+//  * Header.make            (bgzf/.../block/Header.scala:48-83)
+//  * MetadataStream         (bgzf/.../block/MetadataStream.scala:23-54)
+//  * FindBlockStart.apply   (bgzf/.../block/FindBlockStart.scala:8-36)
+// Compressed bytes are resident in HBM.  The scan is byte-parallel (one thread per 16
+// candidate offsets, coalesced 16 B loads); the block chain from a known start is
+// recovered exactly with pointer jumping over the (sparse) candidate list, so a
+// false header pattern inside stored (level-0) data can never enter the chain.
+#include "sbh_internal.h"
+
+namespace sbh {
+namespace {
+
+constexpr int SCAN_T = 256;       // threads per workgroup
+constexpr int SCAN_PER = 8;       // elements per thread in the scans
+constexpr uint64_t CHUNK = 4096;  // bytes per candidate-count workgroup (256 x 16)
+
+__device__ __forceinline__ bool header_at(const uint8_t *c, uint64_t p) {
+  // gzip magic 31 139 8 4 and 'B' 'C' 2 (Header.scala:61-75; byte 15 unchecked)
+  return c[p] == 31 && c[p + 1] == 139 && c[p + 2] == 8 && c[p + 3] == 4 && c[p + 12] == 66 &&
+         c[p + 13] == 67 && c[p + 14] == 2;
+}
+__device__ __forceinline__ uint32_t u16_at(const uint8_t *c, uint64_t p) {
+  return (uint32_t)c[p] | ((uint32_t)c[p + 1] << 8);
+}
+__device__ __forceinline__ uint32_t u32_at(const uint8_t *c, uint64_t p) {
+  return (uint32_t)c[p] | ((uint32_t)c[p + 1] << 8) | ((uint32_t)c[p + 2] << 16) |
+         ((uint32_t)c[p + 3] << 24);
+}
+
+// ---------------------------------------------------------------- exclusive scan
+__global__ __launch_bounds__(SCAN_T) void k_scan_local(const uint64_t *in, uint64_t *out,
+                                                       uint64_t *sums, uint64_t n) {
+  __shared__ uint64_t s[SCAN_T];
+  const uint64_t base = ((uint64_t)blockIdx.x * SCAN_T + threadIdx.x) * SCAN_PER;
+  uint64_t v[SCAN_PER];
+  uint64_t t = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_PER; ++k) {
+    v[k] = base + k < n ? in[base + k] : 0;
+    t += v[k];
+  }
+  s[threadIdx.x] = t;
+  __syncthreads();
+  for (int off = 1; off < SCAN_T; off <<= 1) {
+    uint64_t x = threadIdx.x >= (unsigned)off ? s[threadIdx.x - off] : 0;
+    __syncthreads();
+    s[threadIdx.x] += x;
+    __syncthreads();
+  }
+  uint64_t run = s[threadIdx.x] - t;  // exclusive prefix of this thread
+#pragma unroll
+  for (int k = 0; k < SCAN_PER; ++k) {
+    if (base + k < n) out[base + k] = run;
+    run += v[k];
+  }
+  if (threadIdx.x == SCAN_T - 1) sums[blockIdx.x] = s[SCAN_T - 1];
+}
+
+__global__ __launch_bounds__(SCAN_T) void k_scan_add(uint64_t *out, const uint64_t *pref, uint64_t n) {
+  const uint64_t base = ((uint64_t)blockIdx.x * SCAN_T + threadIdx.x) * SCAN_PER;
+  const uint64_t add = pref[blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < SCAN_PER; ++k)
+    if (base + k < n) out[base + k] += add;
+}
+
+// ---------------------------------------------------------------- FindBlockStart
+// For each pos in [0, 65536): the MetadataStream.take(k).size attempt from start+pos.
+// Outcome per pos: 0 ok, 1 HeaderParseException (retry), 2 other exception (escapes),
+// 3 needs bytes beyond the resident range.  The smallest non-1 pos wins.
+__global__ void k_find_block_start(const uint8_t *comp, uint64_t n, uint64_t start, int32_t k_check,
+                                   int at_eof, unsigned long long *best) {
+  const uint64_t pos = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (pos >= 65536) return;
+  uint64_t q = start + pos;
+  uint32_t outcome = 0;
+  for (int32_t k = 0; k < k_check; ++k) {
+    if (q + 18 > n) {  // readFully(18) would hit the end of the resident bytes
+      outcome = at_eof ? 0 : 3;
+      break;
+    }
+    if (!header_at(comp, q)) { outcome = 1; break; }
+    const uint32_t xlen = u16_at(comp, q + 10);
+    const int32_t hs = 18 + (int32_t)xlen - 6;
+    const int32_t cs = (int32_t)u16_at(comp, q + 16) + 1;
+    const int32_t remaining = cs - hs;
+    if (remaining - 4 < 0) { outcome = 2; break; }
+    if (q + (uint64_t)cs > n) { outcome = at_eof ? 2 : 3; break; }  // getInt EOF
+    if (remaining - 8 == 2) break;  // empty block ends the stream: success
+    q += (uint64_t)cs;
+  }
+  if (outcome != 1) atomicMin(best, (unsigned long long)((pos << 8) | outcome));
+}
+
+// ---------------------------------------------------------------- candidate scan
+__global__ __launch_bounds__(256) void k_cand_count(const uint8_t *comp, uint64_t n, uint64_t from,
+                                                     uint64_t *counts) {
+  __shared__ uint32_t c;
+  if (threadIdx.x == 0) c = 0;
+  __syncthreads();
+  const uint64_t p0 = (uint64_t)blockIdx.x * CHUNK + threadIdx.x * 16;
+  uint32_t mine = 0;
+  for (uint32_t k = 0; k < 16; ++k) {
+    const uint64_t p = p0 + k;
+    if (p >= from && p + 18 <= n && comp[p] == 31 && header_at(comp, p)) ++mine;
+  }
+  if (mine) atomicAdd(&c, mine);
+  __syncthreads();
+  if (threadIdx.x == 0) counts[blockIdx.x] = c;
+}
+
+__global__ __launch_bounds__(256) void k_cand_write(const uint8_t *comp, uint64_t n, uint64_t from,
+                                                     const uint64_t *offs, uint64_t *cand) {
+  __shared__ uint32_t pre[256];
+  const uint64_t p0 = (uint64_t)blockIdx.x * CHUNK + threadIdx.x * 16;
+  uint32_t mask = 0;
+  for (uint32_t k = 0; k < 16; ++k) {
+    const uint64_t p = p0 + k;
+    if (p >= from && p + 18 <= n && comp[p] == 31 && header_at(comp, p)) mask |= 1u << k;
+  }
+  pre[threadIdx.x] = __popc(mask);
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    uint32_t x = threadIdx.x >= (unsigned)off ? pre[threadIdx.x - off] : 0;
+    __syncthreads();
+    pre[threadIdx.x] += x;
+    __syncthreads();
+  }
+  uint64_t o = offs[blockIdx.x] + pre[threadIdx.x] - __popc(mask);
+  for (uint32_t k = 0; k < 16; ++k)
+    if (mask & (1u << k)) cand[o++] = p0 + k;
+}
+
+constexpr int64_t TERM_END = -2;     // chain reaches the end of the resident bytes exactly
+constexpr int64_t TERM_TRUNC = -3;   // block runs past the resident bytes
+constexpr int64_t TERM_BROKEN = -4;  // next offset is not a block header
+
+// Link each candidate to the candidate at (pos + csize).
+__global__ void k_cand_link(const uint8_t *comp, uint64_t n, const uint64_t *cand, uint64_t nc,
+                            int64_t *next) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nc) return;
+  const uint64_t p = cand[i];
+  const uint64_t cs = u16_at(comp, p + 16) + 1;
+  const uint64_t q = p + cs;
+  int64_t r;
+  if (q > n) r = TERM_TRUNC;
+  else if (q == n) r = TERM_END;
+  else if (q + 18 > n) r = TERM_TRUNC;  // a partial header: treat like truncation
+  else {
+    // binary search for q among cand[i+1 ..]
+    uint64_t lo = i + 1, hi = nc;
+    while (lo < hi) {
+      uint64_t m = (lo + hi) >> 1;
+      if (cand[m] < q) lo = m + 1; else hi = m;
+    }
+    r = (lo < nc && cand[lo] == q) ? (int64_t)lo : TERM_BROKEN;
+  }
+  next[i] = r;
+}
+
+// Pointer-jumping marking of the chain from candidate 0: after round k every node at
+// distance < 2^(k+1) is marked (marks only ever add true chain nodes).
+__global__ void k_jump_mark(const int64_t *J, uint8_t *on, uint64_t nc) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nc) return;
+  if (on[i] && J[i] >= 0) on[J[i]] = 1;
+}
+__global__ void k_jump_double(const int64_t *J, int64_t *J2, uint64_t nc) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nc) return;
+  const int64_t j = J[i];
+  J2[i] = j >= 0 ? J[j] : j;
+}
+
+__global__ void k_mark_u64(const uint8_t *on, uint64_t *v, uint64_t nc) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nc) return;
+  v[i] = on[i] ? 1 : 0;
+}
+
+// Emit the chain as the block table (ordered by position).
+__global__ void k_chain_emit(const uint8_t *comp, uint64_t n, const uint64_t *cand, const uint8_t *on,
+                             const uint64_t *rank, uint64_t nc, DevBlocks bl,
+                             uint64_t *usz) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nc || !on[i]) return;
+  const uint64_t r = rank[i];
+  const uint64_t p = cand[i];
+  const uint32_t xlen = u16_at(comp, p + 10);
+  const uint32_t hs = 18 + xlen - 6;
+  const uint32_t cs = u16_at(comp, p + 16) + 1;
+  uint32_t flags = 0, us = 0;
+  if (p + cs > n) {
+    flags |= BLK_TRUNCATED;
+  } else {
+    us = u32_at(comp, p + cs - 4);
+    if ((int32_t)cs - (int32_t)hs - 8 == 2) flags |= BLK_EMPTY;
+  }
+  bl.cstart[r] = p;
+  bl.csize[r] = cs;
+  bl.hsize[r] = hs;
+  bl.usize[r] = (flags & BLK_EMPTY) ? 0 : us;
+  bl.flags[r] = flags;
+  bl.status[r] = 0;
+  // flat sizes: empty or truncated blocks contribute no bytes; ISIZE > 64 KiB is an
+  // inflate error (reported by k_inflate), contributes none
+  usz[r] = (flags & (BLK_EMPTY | BLK_TRUNCATED)) || us > 65536u ? 0 : us;
+}
+
+__global__ void k_copy_u64(const uint64_t *a, uint64_t *b, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) b[i] = a[i];
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ host launchers
+static inline uint32_t nblk(uint64_t n, uint32_t t) { return (uint32_t)((n + t - 1) / t); }
+
+// Exclusive scan of n u64 values (in place allowed for out == in? no: distinct).
+// tmp must hold scan_tmp_words(n) u64.  Returns the total via *total (device->host).
+uint64_t scan_tmp_words(uint64_t n) {
+  uint64_t per = (uint64_t)SCAN_T * SCAN_PER, w = 0;
+  while (n > 1) {
+    n = (n + per - 1) / per;
+    w += 2 * n + 2;
+  }
+  return w + 4;
+}
+
+hipError_t scan_exclusive_u64(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *tmp,
+                              hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const uint64_t per = (uint64_t)SCAN_T * SCAN_PER;
+  const uint64_t nb = (n + per - 1) / per;
+  uint64_t *sums = tmp, *pref = tmp + nb + 1;
+  hipLaunchKernelGGL(k_scan_local, dim3((uint32_t)nb), dim3(SCAN_T), 0, st, in, out, sums, n);
+  if (nb > 1) {
+    hipError_t e = scan_exclusive_u64(sums, pref, nb, tmp + 2 * nb + 2, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_scan_add, dim3((uint32_t)nb), dim3(SCAN_T), 0, st, out, pref, n);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_find_block_start(const uint8_t *comp, uint64_t n, uint64_t start, int32_t k,
+                                   int at_eof, unsigned long long *best, hipStream_t st) {
+  hipLaunchKernelGGL(k_find_block_start, dim3(65536 / 256), dim3(256), 0, st, comp, n, start, k,
+                     at_eof, best);
+  return hipGetLastError();
+}
+
+hipError_t launch_cand_count(const uint8_t *comp, uint64_t n, uint64_t from, uint64_t *counts,
+                             uint64_t nchunks, hipStream_t st) {
+  hipLaunchKernelGGL(k_cand_count, dim3((uint32_t)nchunks), dim3(256), 0, st, comp, n, from, counts);
+  return hipGetLastError();
+}
+hipError_t launch_cand_write(const uint8_t *comp, uint64_t n, uint64_t from, const uint64_t *offs,
+                             uint64_t *cand, uint64_t nchunks, hipStream_t st) {
+  hipLaunchKernelGGL(k_cand_write, dim3((uint32_t)nchunks), dim3(256), 0, st, comp, n, from, offs, cand);
+  return hipGetLastError();
+}
+
+// Build the chain from cand[0] over nc candidates.  Scratch: J0, J1 (int64 x nc),
+// on (u8 x nc), v/rank (u64 x nc each), tmp (scan).  Writes the block table and
+// usz (u64 per block); returns the block count via *nchain (host).
+hipError_t build_chain(const uint8_t *comp, uint64_t n, const uint64_t *cand, uint64_t nc, int64_t *J0,
+                       int64_t *J1, uint8_t *on, uint64_t *v, uint64_t *rank, uint64_t *tmp,
+                       DevBlocks bl, uint64_t *usz, uint64_t *nchain, hipStream_t st) {
+  *nchain = 0;
+  if (nc == 0) return hipSuccess;
+  const uint32_t T = 256;
+  hipLaunchKernelGGL(k_cand_link, dim3(nblk(nc, T)), dim3(T), 0, st, comp, n, cand, nc, J0);
+  hipError_t e = hipMemsetAsync(on, 0, nc, st);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(on, 1, 1, st);
+  if (e != hipSuccess) return e;
+  int64_t *a = J0, *b = J1;
+  for (uint64_t span = 1; span < nc; span <<= 1) {
+    hipLaunchKernelGGL(k_jump_mark, dim3(nblk(nc, T)), dim3(T), 0, st, a, on, nc);
+    hipLaunchKernelGGL(k_jump_double, dim3(nblk(nc, T)), dim3(T), 0, st, a, b, nc);
+    int64_t *t = a;
+    a = b;
+    b = t;
+  }
+  hipLaunchKernelGGL(k_jump_mark, dim3(nblk(nc, T)), dim3(T), 0, st, a, on, nc);
+  // ranks of marked nodes
+  hipLaunchKernelGGL(k_mark_u64, dim3(nblk(nc, T)), dim3(T), 0, st, on, v, nc);
+  e = scan_exclusive_u64(v, rank, nc, tmp, st);
+  if (e != hipSuccess) return e;
+  uint64_t last_rank = 0, last_v = 0;
+  e = hipMemcpyAsync(&last_rank, rank + nc - 1, 8, hipMemcpyDeviceToHost, st);
+  if (e != hipSuccess) return e;
+  e = hipMemcpyAsync(&last_v, v + nc - 1, 8, hipMemcpyDeviceToHost, st);
+  if (e != hipSuccess) return e;
+  e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return e;
+  *nchain = last_rank + last_v;
+  hipLaunchKernelGGL(k_chain_emit, dim3(nblk(nc, T)), dim3(T), 0, st, comp, n, cand, on, rank, nc, bl,
+                     usz);
+  return hipGetLastError();
+}
+
+}  // namespace sbh

@@ -1,0 +1,503 @@
+// check.hip -- BAM record-boundary checkers at every uncompressed position (CDNA4).
+//
+// Replaces, for every flat position of a range at once:
+//  * eager.Checker.apply  (check/.../bam/check/eager/Checker.scala:24-126)
+//  * full.Checker.apply   (check/.../bam/check/full/Checker.scala:22-184) + the
+//    FullCheck Counts aggregation (cli/.../check/full/FullCheck.scala:142-192)
+//  * PosChecker.getRefPosError (check/.../bam/check/PosChecker.scala:43-63)
+// and the record-chain bookkeeping behind split/count computation
+// (check/.../iterator/PosStream.scala:14-22, load/.../CanLoadBam.scala:346-355).
+//
+// Layout: a workgroup owns a 4096-position tile; it stages the tile plus a 1 KiB halo
+// of the flat buffer into LDS with coalesced dword loads, so the fixed-field
+// predicates that reject ~99% of positions never touch HBM again.  The (rare) reads
+// past the staged window -- long names/CIGARs and the up-to-10-record chain of true
+// record starts -- go to HBM/L2.  Results are an eager bitmap (bit per position,
+// written 512 B per tile), or per-position full-check words + an LDS histogram that
+// is folded into global counters once per tile.
+#include "sbh_internal.h"
+
+namespace sbh {
+namespace {
+
+constexpr uint32_t TILE = 4096;
+constexpr uint32_t HALO = 1024;
+constexpr uint32_t STAGE = TILE + HALO + 8;  // bytes staged (+ slack for dword pairs)
+constexpr uint32_t T = 256;
+
+constexpr uint32_t FULL_SUCCESS = 0x80000000u;
+constexpr uint32_t FULL_UNKNOWN = 0x40000000u;  // depends on bytes past an open end
+constexpr uint32_t N_SHIFT = 20;
+
+struct Src {
+  const uint8_t *U;
+  const uint32_t *lds32;  // staged dwords; lds byte i <-> flat s0 + i
+  uint64_t s0;            // dword-aligned flat start of the staged window
+  uint32_t sn;            // staged bytes (multiple of 4)
+
+  __device__ __forceinline__ uint32_t word_at(uint64_t q) const {  // little-endian u32 at q
+    const uint64_t w = q - s0;
+    if (q >= s0 && w + 8 <= sn) {
+      const uint32_t i = (uint32_t)w >> 2;
+      return __builtin_amdgcn_alignbyte(lds32[i + 1], lds32[i], (uint32_t)w & 3);
+    }
+    const uint32_t *g = reinterpret_cast<const uint32_t *>(U + (q & ~3ull));
+    return __builtin_amdgcn_alignbyte(g[1], g[0], (uint32_t)q & 3);
+  }
+  __device__ __forceinline__ uint8_t byte_at(uint64_t q) const {
+    const uint64_t w = q - s0;
+    if (q >= s0 && w < sn) return (uint8_t)(lds32[w >> 2] >> (8 * (w & 3)));
+    return U[q];
+  }
+};
+
+struct Ctg {
+  const int32_t *len;
+  int32_t n;
+};
+
+// PosChecker.getRefPosError: bits {0 negIdx, 1 bigIdx, 2 negPos, 3 bigPos}
+__device__ __forceinline__ uint32_t ref_pos_error(int32_t idx, int32_t pos, const Ctg &c) {
+  if (idx < -1) return pos < -1 ? 5u : 1u;
+  if (idx >= c.n) return pos < -1 ? 6u : 2u;
+  if (pos < -1) return 4u;
+  if (idx >= 0 && (int64_t)pos > (int64_t)c.len[idx]) return 8u;
+  return 0;
+}
+
+__device__ __forceinline__ bool name_char_ok(uint32_t ch) {
+  return (ch >= 0x21 && ch <= 0x3F) || (ch >= 0x41 && ch <= 0x7E);
+}
+
+__device__ __forceinline__ int32_t implied_min_remaining(int32_t rnl, int32_t nc, int32_t seq_len) {
+  int32_t s1 = (int32_t)((uint32_t)seq_len + 1u);
+  int32_t nsq = (int32_t)((uint32_t)(s1 / 2) + (uint32_t)seq_len);
+  return (int32_t)(32u + (uint32_t)rnl + 4u * (uint32_t)nc + (uint32_t)nsq);
+}
+
+// Eager check at p: 0 false, 1 true, 2 unknown (needs bytes past an open end).
+__device__ uint32_t eager_at(const Src &s, uint64_t p, uint64_t total, bool open, const Ctg &c,
+                             int32_t rtc) {
+  uint64_t cur = p, start = p;
+  for (int32_t n = 0;; ++n) {
+    if (n == rtc) return 1;
+    if (cur + 36 > total) {
+      if (open) return 2;
+      return (total == start && n > 0) ? 1 : 0;
+    }
+    const int32_t rem = (int32_t)s.word_at(cur);
+    const uint64_t nominal = start + 4 + (int64_t)rem;
+    if (ref_pos_error((int32_t)s.word_at(cur + 4), (int32_t)s.word_at(cur + 8), c)) return 0;
+    const int32_t rnl = (int32_t)(s.word_at(cur + 12) & 0xff);
+    if (rnl < 2) return 0;
+    const uint32_t fnc = s.word_at(cur + 16);
+    const uint32_t flags = fnc >> 16;
+    const int32_t nc = (int32_t)(fnc & 0xffff);
+    const int32_t seq_len = (int32_t)s.word_at(cur + 20);
+    if ((flags & 4) == 0 && (seq_len == 0 || nc == 0)) return 0;
+    if (rem < implied_min_remaining(rnl, nc, seq_len)) return 0;
+    if (ref_pos_error((int32_t)s.word_at(cur + 24), (int32_t)s.word_at(cur + 28), c)) return 0;
+    cur += 36;
+    if (cur + (uint64_t)rnl > total) return open ? 2 : 0;
+    if (s.byte_at(cur + rnl - 1) != 0) return 0;
+    for (int32_t i = 0; i < rnl - 1; ++i)
+      if (!name_char_ok(s.byte_at(cur + i))) return 0;
+    cur += rnl;
+    for (int32_t k = 0; k < nc; ++k) {
+      if (cur + 4 > total) return open ? 2 : 0;
+      if ((s.byte_at(cur) & 0xf) > 8) return 0;
+      cur += 4;
+    }
+    if ((int64_t)(nominal - cur) > 0) {
+      if (nominal > total) {
+        if (open) return 2;
+        cur = total;
+      } else {
+        cur = nominal;
+      }
+    }
+    start = nominal;
+  }
+}
+
+// Full check at p: result word (see include/sparkbam.h), or FULL_UNKNOWN.
+__device__ uint32_t full_at(const Src &s, uint64_t p, uint64_t total, bool open, const Ctg &c,
+                            int32_t rtc) {
+  uint64_t cur = p, start = p;
+  for (int32_t n = 0;; ++n) {
+    if (n == rtc) return FULL_SUCCESS | ((uint32_t)n << N_SHIFT);
+    if (cur + 36 > total) {
+      if (open) return FULL_UNKNOWN;
+      if (total == start && n > 0) return FULL_SUCCESS | ((uint32_t)n << N_SHIFT);
+      return 1u | ((uint32_t)n << N_SHIFT);
+    }
+    const int32_t rem = (int32_t)s.word_at(cur);
+    const uint64_t nominal = start + 4 + (int64_t)rem;
+    uint32_t f = ref_pos_error((int32_t)s.word_at(cur + 4), (int32_t)s.word_at(cur + 8), c) << 1;
+    const int32_t rnl = (int32_t)(s.word_at(cur + 12) & 0xff);
+    const uint32_t fnc = s.word_at(cur + 16);
+    const uint32_t flags = fnc >> 16;
+    const int32_t nc = (int32_t)(fnc & 0xffff);
+    const int32_t seq_len = (int32_t)s.word_at(cur + 20);
+    if (rem < implied_min_remaining(rnl, nc, seq_len)) f |= 1u << 18;
+    f |= ref_pos_error((int32_t)s.word_at(cur + 24), (int32_t)s.word_at(cur + 28), c) << 5;
+    cur += 36;
+    bool name_eof = false;
+    if (rnl == 0) {
+      f |= 1u << 12;
+    } else if (rnl == 1) {
+      f |= 1u << 13;
+    } else if (cur + (uint64_t)rnl > total) {
+      if (open) return FULL_UNKNOWN;
+      f |= 1u << 9;
+      name_eof = true;
+    } else {
+      if (s.byte_at(cur + rnl - 1) != 0) {
+        f |= 1u << 10;
+      } else {
+        for (int32_t i = 0; i < rnl - 1; ++i)
+          if (!name_char_ok(s.byte_at(cur + i))) { f |= 1u << 11; break; }
+      }
+      cur += rnl;
+    }
+    if (!name_eof) {
+      bool cig_err = false;
+      for (int32_t k = 0; k < nc; ++k) {
+        if (cur + 4 > total) {
+          if (open) return FULL_UNKNOWN;
+          f |= 1u << 14;
+          cig_err = true;
+          break;
+        }
+        if ((s.byte_at(cur) & 0xf) > 8) {
+          f |= 1u << 15;
+          cig_err = true;
+          cur += 4;
+          break;
+        }
+        cur += 4;
+      }
+      if (!cig_err && (flags & 4) == 0 && (seq_len == 0 || nc == 0)) {
+        if (seq_len == 0) f |= 1u << 16;  // EmptyMapped(emptySeq, emptyCigar) field swap
+        if (nc == 0) f |= 1u << 17;
+      }
+    }
+    if (f) return f | ((uint32_t)n << N_SHIFT);
+    if ((int64_t)(nominal - cur) > 0) {
+      if (nominal > total) {
+        if (open) return FULL_UNKNOWN;
+        cur = total;
+      } else {
+        cur = nominal;
+      }
+    }
+    start = nominal;
+  }
+}
+
+struct Segs {
+  const uint64_t *end;  // sorted; last entry = resident flat size
+  uint32_t n;
+  uint32_t open_last;  // last segment ends at the resident end, not at a stream end
+};
+
+// Stage [s0, s0 + STAGE) of U into LDS (dword loads, zero past u_total).
+__device__ __forceinline__ void stage(uint32_t *lds32, const uint8_t *U, uint64_t s0, uint64_t u_pad) {
+  const uint32_t *g = reinterpret_cast<const uint32_t *>(U + s0);
+  for (uint32_t i = threadIdx.x; i < STAGE / 4; i += T) {
+    const uint64_t q = s0 + 4ull * i;
+    lds32[i] = q + 4 <= u_pad ? g[i] : 0u;
+  }
+}
+
+__device__ __forceinline__ uint32_t seg_index(const Segs &sg, uint64_t p, uint32_t from) {
+  uint32_t k = from;
+  while (k + 1 < sg.n && sg.end[k] <= p) ++k;
+  return k;
+}
+
+__device__ __forceinline__ uint32_t seg_first(const Segs &sg, uint64_t p) {
+  uint32_t lo = 0, hi = sg.n - 1;
+  while (lo < hi) {
+    uint32_t m = (lo + hi) >> 1;
+    if (sg.end[m] <= p) lo = m + 1; else hi = m;
+  }
+  return lo;
+}
+
+struct EagerOut {
+  uint32_t *bits;                 // bit i <-> position begin + i
+  unsigned long long *n_true;
+  unsigned long long *n_unknown;
+  unsigned long long *min_unknown;
+};
+
+__global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint64_t u_pad, uint64_t begin,
+                                             uint64_t end, Segs sg, Ctg c, int32_t rtc, EagerOut o) {
+  __shared__ uint32_t lds32[STAGE / 4];
+  __shared__ uint32_t bits[TILE / 32];
+  __shared__ uint32_t seg0, ntrue;
+  const uint64_t t0 = begin + (uint64_t)blockIdx.x * TILE;
+  const uint64_t s0 = t0 & ~3ull;
+  stage(lds32, U, s0, u_pad);
+  for (uint32_t i = threadIdx.x; i < TILE / 32; i += T) bits[i] = 0;
+  if (threadIdx.x == 0) { seg0 = seg_first(sg, t0); ntrue = 0; }
+  __syncthreads();
+  Src s{U, lds32, s0, STAGE & ~3u};
+  uint32_t mytrue = 0;
+  for (uint32_t i = threadIdx.x; i < TILE; i += T) {
+    const uint64_t p = t0 + i;
+    if (p >= end) break;
+    const uint32_t k = seg_index(sg, p, seg0);
+    const uint64_t total = sg.end[k];
+    const bool open = sg.open_last && k == sg.n - 1;
+    const uint32_t r = eager_at(s, p, total, open, c, rtc);
+    if (r == 1) {
+      atomicOr(&bits[i >> 5], 1u << (i & 31));
+      ++mytrue;
+    } else if (r == 2) {
+      atomicAdd(o.n_unknown, 1ull);
+      atomicMin(o.min_unknown, (unsigned long long)p);
+    }
+  }
+  if (mytrue) atomicAdd(&ntrue, mytrue);
+  __syncthreads();
+  const uint64_t wbase = (uint64_t)blockIdx.x * (TILE / 32);
+  const uint64_t nwords = (end - begin + 31) / 32;
+  for (uint32_t i = threadIdx.x; i < TILE / 32; i += T)
+    if (wbase + i < nwords) o.bits[wbase + i] = bits[i];
+  if (threadIdx.x == 0 && ntrue) atomicAdd(o.n_true, (unsigned long long)ntrue);
+}
+
+struct FullOut {
+  uint32_t *words;                 // optional: word per position
+  unsigned long long *counts;      // [21][19]
+  unsigned long long *rbe;         // [21][64]
+  unsigned long long *n_success;
+  unsigned long long *n_unknown;
+  unsigned long long *min_unknown;
+  unsigned long long *close_n;     // positions with numNonZeroFields <= 2
+  uint64_t *close_pos;
+  uint32_t *close_word;
+  uint64_t close_cap;
+};
+
+__global__ __launch_bounds__(T) void k_full(const uint8_t *__restrict__ U, uint64_t u_pad, uint64_t begin,
+                                            uint64_t end, Segs sg, Ctg c, int32_t rtc, FullOut o) {
+  __shared__ uint32_t lds32[STAGE / 4];
+  __shared__ uint32_t hist[21 * 19 + 21 * 64];
+  __shared__ uint32_t seg0, nsucc;
+  const uint64_t t0 = begin + (uint64_t)blockIdx.x * TILE;
+  const uint64_t s0 = t0 & ~3ull;
+  stage(lds32, U, s0, u_pad);
+  for (uint32_t i = threadIdx.x; i < 21 * 19 + 21 * 64; i += T) hist[i] = 0;
+  if (threadIdx.x == 0) { seg0 = seg_first(sg, t0); nsucc = 0; }
+  __syncthreads();
+  Src s{U, lds32, s0, STAGE & ~3u};
+  uint32_t mysucc = 0;
+  for (uint32_t i = threadIdx.x; i < TILE; i += T) {
+    const uint64_t p = t0 + i;
+    if (p >= end) break;
+    const uint32_t k = seg_index(sg, p, seg0);
+    const uint64_t total = sg.end[k];
+    const bool open = sg.open_last && k == sg.n - 1;
+    const uint32_t r = full_at(s, p, total, open, c, rtc);
+    if (o.words) o.words[p - begin] = r;
+    if (r & FULL_SUCCESS) { ++mysucc; continue; }
+    if (r & FULL_UNKNOWN) {
+      atomicAdd(o.n_unknown, 1ull);
+      atomicMin(o.min_unknown, (unsigned long long)p);
+      continue;
+    }
+    const uint32_t f = r & 0x7FFFFu;
+    const uint32_t rbe = (r >> N_SHIFT) & 0x3FFu;
+    if (f == 1u && rbe == 0) continue;  // Flags.TooFewFixedBlockBytes is excluded
+    const uint32_t nnz = __popc(f) + (rbe > 0);
+    for (uint32_t b = 0; b < 19; ++b)
+      if (f & (1u << b)) atomicAdd(&hist[nnz * 19 + b], 1u);
+    if (rbe > 0 && rbe < 64) atomicAdd(&hist[21 * 19 + nnz * 64 + rbe], 1u);
+    if (nnz <= 2) {
+      const unsigned long long slot = atomicAdd(o.close_n, 1ull);
+      if (slot < o.close_cap) { o.close_pos[slot] = p; o.close_word[slot] = r; }
+    }
+  }
+  if (mysucc) atomicAdd(&nsucc, mysucc);
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < 21 * 19; i += T)
+    if (hist[i]) atomicAdd(&o.counts[i], (unsigned long long)hist[i]);
+  for (uint32_t i = threadIdx.x; i < 21 * 64; i += T)
+    if (hist[21 * 19 + i]) atomicAdd(&o.rbe[i], (unsigned long long)hist[21 * 19 + i]);
+  if (threadIdx.x == 0 && nsucc) atomicAdd(o.n_success, (unsigned long long)nsucc);
+}
+
+// ---------------------------------------------------------------- bitmap utilities
+// First set bit at or after `from` and before `to` (positions; bit i <-> begin + i).
+__global__ void k_first_set(const uint32_t *bits, uint64_t begin, uint64_t from, uint64_t to,
+                            unsigned long long *best) {
+  const uint64_t w = (from - begin) / 32 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t w_end = (to - begin + 31) / 32;
+  if (w >= w_end) return;
+  uint32_t v = bits[w];
+  const uint64_t p0 = begin + 32 * w;
+  if (p0 < from) v &= ~0u << (uint32_t)(from - p0);
+  if (p0 + 32 > to) v &= (to - p0) >= 32 ? ~0u : ((1u << (uint32_t)(to - p0)) - 1u);
+  if (v) atomicMin(best, (unsigned long long)(p0 + __builtin_ctz(v)));
+}
+
+__global__ void k_popcount(const uint32_t *bits, uint64_t begin, uint64_t from, uint64_t to,
+                           unsigned long long *acc) {
+  const uint64_t w = (from - begin) / 32 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t w_end = (to - begin + 31) / 32;
+  uint32_t c = 0;
+  if (w < w_end) {
+    uint32_t v = bits[w];
+    const uint64_t p0 = begin + 32 * w;
+    if (p0 < from) v &= ~0u << (uint32_t)(from - p0);
+    if (p0 + 32 > to) v &= (to - p0) >= 32 ? ~0u : ((1u << (uint32_t)(to - p0)) - 1u);
+    c = __popc(v);
+  }
+  // wave reduction, one atomic per wave
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(acc, (unsigned long long)c);
+}
+
+// Chain verification over eager-true positions s in [from, E): the record chain
+// (PosStream: next = s + 4 + block_size) must step exactly from each true position
+// to the next true one (or leave [from, E) / reach the stream end).  Any other
+// step is an anomaly (a false positive inside the chain, or a chain record the
+// eager checker rejects); those ranges fall back to an exact sequential walk.
+__global__ void k_verify_chain(const uint8_t *U, const uint32_t *bits, uint64_t begin, uint64_t bits_end,
+                               uint64_t from, uint64_t E, uint64_t total, unsigned long long *n_anom,
+                               unsigned long long *first_anom) {
+  const uint64_t w = (from - begin) / 32 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t w_end = (E - begin + 31) / 32;
+  if (w >= w_end) return;
+  uint32_t v = bits[w];
+  const uint64_t p0 = begin + 32 * w;
+  if (p0 < from) v &= ~0u << (uint32_t)(from - p0);
+  if (p0 + 32 > E) v &= (E - p0) >= 32 ? ~0u : ((1u << (uint32_t)(E - p0)) - 1u);
+  const uint64_t w_lim = (bits_end - begin + 31) / 32;
+  while (v) {
+    const uint32_t b = __builtin_ctz(v);
+    v &= v - 1;
+    const uint64_t s = p0 + b;
+    // next set bit after s (bounded by E)
+    uint64_t nxt_set = ~0ull;
+    if (v) {
+      nxt_set = p0 + __builtin_ctz(v);
+    } else {
+      for (uint64_t ww = w + 1; ww < w_lim && begin + 32 * ww < E; ++ww) {
+        const uint32_t x = bits[ww];
+        if (x) { nxt_set = begin + 32 * ww + __builtin_ctz(x); break; }
+      }
+      if (nxt_set >= E) nxt_set = ~0ull;
+    }
+    uint64_t step;
+    if (s + 4 > total) {
+      step = ~0ull;  // getInt at EOF: the chain ends here
+    } else {
+      const uint32_t *g = reinterpret_cast<const uint32_t *>(U + (s & ~3ull));
+      const int32_t rem = (int32_t)__builtin_amdgcn_alignbyte(g[1], g[0], (uint32_t)s & 3);
+      step = s + 4 + (int64_t)rem;
+    }
+    bool ok;
+    if (nxt_set != ~0ull) ok = step == nxt_set;
+    else ok = step >= E || step + 4 > total;  // leaves the counted range or hits EOF
+    if (!ok) {
+      atomicAdd(n_anom, 1ull);
+      atomicMin(first_anom, (unsigned long long)s);
+    }
+  }
+}
+
+// Exact sequential chain walk (fallback): counts records r in [first, E) following
+// next = r + 4 + block_size, stopping at the stream end.
+__global__ void k_chain_walk(const uint8_t *U, uint64_t first, uint64_t E, uint64_t total,
+                             unsigned long long *count, unsigned long long *last) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint64_t r = first, n = 0, prev = first;
+  while (r < E && r + 4 <= total) {
+    ++n;
+    prev = r;
+    const int32_t rem = (int32_t)((uint32_t)U[r] | ((uint32_t)U[r + 1] << 8) | ((uint32_t)U[r + 2] << 16) |
+                                  ((uint32_t)U[r + 3] << 24));
+    const int64_t nx = (int64_t)r + 4 + rem;
+    if (nx <= (int64_t)r) break;  // malformed: htsjdk would fail; stop the walk
+    r = (uint64_t)nx;
+  }
+  *count = n;
+  *last = prev;
+}
+
+}  // namespace
+
+static inline uint32_t ngrid(uint64_t n, uint32_t t) { return (uint32_t)((n + t - 1) / t); }
+
+hipError_t launch_eager(const uint8_t *U, uint64_t u_pad, uint64_t begin, uint64_t end, const uint64_t *seg_end,
+                        uint32_t nseg, uint32_t open_last, const int32_t *ctg, int32_t nctg, int32_t rtc,
+                        uint32_t *bits, unsigned long long *counters, hipStream_t st) {
+  if (end <= begin) return hipSuccess;
+  Segs sg{seg_end, nseg, open_last};
+  Ctg c{ctg, nctg};
+  EagerOut o{bits, counters, counters + 1, counters + 2};
+  hipLaunchKernelGGL(k_eager, dim3(ngrid(end - begin, TILE)), dim3(T), 0, st, U, u_pad, begin, end, sg, c,
+                     rtc, o);
+  return hipGetLastError();
+}
+
+hipError_t launch_full(const uint8_t *U, uint64_t u_pad, uint64_t begin, uint64_t end, const uint64_t *seg_end,
+                       uint32_t nseg, uint32_t open_last, const int32_t *ctg, int32_t nctg, int32_t rtc,
+                       uint32_t *words, unsigned long long *counters /* [2+21*19+21*64+2] */,
+                       uint64_t *close_pos, uint32_t *close_word, uint64_t close_cap, hipStream_t st) {
+  if (end <= begin) return hipSuccess;
+  Segs sg{seg_end, nseg, open_last};
+  Ctg c{ctg, nctg};
+  FullOut o;
+  o.words = words;
+  o.n_success = counters + 0;
+  o.n_unknown = counters + 1;
+  o.min_unknown = counters + 2;
+  o.close_n = counters + 3;
+  o.counts = counters + 4;
+  o.rbe = counters + 4 + 21 * 19;
+  o.close_pos = close_pos;
+  o.close_word = close_word;
+  o.close_cap = close_cap;
+  hipLaunchKernelGGL(k_full, dim3(ngrid(end - begin, TILE)), dim3(T), 0, st, U, u_pad, begin, end, sg, c, rtc,
+                     o);
+  return hipGetLastError();
+}
+
+hipError_t launch_first_set(const uint32_t *bits, uint64_t begin, uint64_t from, uint64_t to,
+                            unsigned long long *best, hipStream_t st) {
+  if (to <= from) return hipSuccess;
+  const uint64_t nw = (to - begin + 31) / 32 - (from - begin) / 32;
+  hipLaunchKernelGGL(k_first_set, dim3(ngrid(nw, 256)), dim3(256), 0, st, bits, begin, from, to, best);
+  return hipGetLastError();
+}
+
+hipError_t launch_popcount(const uint32_t *bits, uint64_t begin, uint64_t from, uint64_t to,
+                           unsigned long long *acc, hipStream_t st) {
+  if (to <= from) return hipSuccess;
+  const uint64_t nw = (to - begin + 31) / 32 - (from - begin) / 32;
+  hipLaunchKernelGGL(k_popcount, dim3(ngrid(nw, 256)), dim3(256), 0, st, bits, begin, from, to, acc);
+  return hipGetLastError();
+}
+
+hipError_t launch_verify_chain(const uint8_t *U, const uint32_t *bits, uint64_t begin, uint64_t bits_end,
+                               uint64_t from, uint64_t E, uint64_t total, unsigned long long *n_anom,
+                               unsigned long long *first_anom, hipStream_t st) {
+  if (E <= from) return hipSuccess;
+  const uint64_t nw = (E - begin + 31) / 32 - (from - begin) / 32;
+  hipLaunchKernelGGL(k_verify_chain, dim3(ngrid(nw, 256)), dim3(256), 0, st, U, bits, begin, bits_end, from,
+                     E, total, n_anom, first_anom);
+  return hipGetLastError();
+}
+
+hipError_t launch_chain_walk(const uint8_t *U, uint64_t first, uint64_t E, uint64_t total,
+                             unsigned long long *count, unsigned long long *last, hipStream_t st) {
+  hipLaunchKernelGGL(k_chain_walk, dim3(1), dim3(64), 0, st, U, first, E, total, count, last);
+  return hipGetLastError();
+}
+
+}  // namespace sbh

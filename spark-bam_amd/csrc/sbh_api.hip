@@ -1,0 +1,771 @@
+// sbh_api.hip -- the C-ABI (include/sparkbam.h): context/shard lifetime, device
+// buffers, and the orchestration of the HIP kernels (bgzf_index.hip, inflate.hip,
+// check.hip) that replace spark-bam's per-split Scala/JDK-zlib work.
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "sbh_internal.h"
+
+namespace sbh {
+uint64_t scan_tmp_words(uint64_t n);
+hipError_t scan_exclusive_u64(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *tmp, hipStream_t st);
+hipError_t launch_find_block_start(const uint8_t *comp, uint64_t n, uint64_t start, int32_t k, int at_eof,
+                                   unsigned long long *best, hipStream_t st);
+hipError_t launch_cand_count(const uint8_t *comp, uint64_t n, uint64_t from, uint64_t *counts, uint64_t nchunks,
+                             hipStream_t st);
+hipError_t launch_cand_write(const uint8_t *comp, uint64_t n, uint64_t from, const uint64_t *offs, uint64_t *cand,
+                             uint64_t nchunks, hipStream_t st);
+hipError_t build_chain(const uint8_t *comp, uint64_t n, const uint64_t *cand, uint64_t nc, int64_t *J0, int64_t *J1,
+                       uint8_t *on, uint64_t *v, uint64_t *rank, uint64_t *tmp, DevBlocks bl, uint64_t *usz,
+                       uint64_t *nchain, hipStream_t st);
+hipError_t launch_eager(const uint8_t *U, uint64_t u_pad, uint64_t begin, uint64_t end, const uint64_t *seg_end,
+                        uint32_t nseg, uint32_t open_last, const int32_t *ctg, int32_t nctg, int32_t rtc,
+                        uint32_t *bits, unsigned long long *counters, hipStream_t st);
+hipError_t launch_full(const uint8_t *U, uint64_t u_pad, uint64_t begin, uint64_t end, const uint64_t *seg_end,
+                       uint32_t nseg, uint32_t open_last, const int32_t *ctg, int32_t nctg, int32_t rtc,
+                       uint32_t *words, unsigned long long *counters, uint64_t *close_pos, uint32_t *close_word,
+                       uint64_t close_cap, hipStream_t st);
+hipError_t launch_first_set(const uint32_t *bits, uint64_t begin, uint64_t from, uint64_t to,
+                            unsigned long long *best, hipStream_t st);
+hipError_t launch_popcount(const uint32_t *bits, uint64_t begin, uint64_t from, uint64_t to,
+                           unsigned long long *acc, hipStream_t st);
+hipError_t launch_verify_chain(const uint8_t *U, const uint32_t *bits, uint64_t begin, uint64_t bits_end,
+                               uint64_t from, uint64_t E, uint64_t total, unsigned long long *n_anom,
+                               unsigned long long *first_anom, hipStream_t st);
+hipError_t launch_chain_walk(const uint8_t *U, uint64_t first, uint64_t E, uint64_t total,
+                             unsigned long long *count, unsigned long long *last, hipStream_t st);
+}  // namespace sbh
+
+using namespace sbh;
+
+struct sbh_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  std::string err;
+};
+
+namespace {
+
+template <typename T>
+struct DBuf {  // grow-only device buffer
+  T *p = nullptr;
+  uint64_t cap = 0;
+  hipError_t ensure(uint64_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(reinterpret_cast<void **>(&p), std::max<uint64_t>(n, 1) * sizeof(T));
+    if (e == hipSuccess) cap = n;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+}  // namespace
+
+struct sbh_shard {
+  sbh_ctx *ctx = nullptr;
+  uint64_t file_off = 0, n = 0, file_size = 0;
+  bool at_eof = false;
+  DBuf<uint8_t> comp;
+  // index
+  bool indexed = false;
+  uint64_t index_start = 0, nblocks = 0, utotal = 0;
+  DBuf<uint64_t> b_cstart, b_ustart, usz;
+  DBuf<uint32_t> b_csize, b_hsize, b_usize, b_flags, b_status;
+  DBuf<uint64_t> counts, offs, cand, v, rank, tmp;
+  DBuf<int64_t> J0, J1;
+  DBuf<uint8_t> on;
+  std::vector<sbh_block> hb;
+  std::vector<uint64_t> seg_end;
+  bool open_last = false, broken_end = false;
+  DBuf<uint64_t> d_seg;
+  // inflate
+  bool inflated = false;
+  DBuf<uint8_t> U;
+  // checker
+  DBuf<int32_t> ctg;
+  int32_t nctg = -1;
+  DBuf<uint32_t> bits;
+  bool bits_valid = false;
+  uint64_t bits_begin = 0, bits_end = 0;
+  int32_t bits_rtc = 0;
+  DBuf<uint32_t> words;
+  DBuf<uint64_t> close_pos;
+  DBuf<uint32_t> close_word;
+  DBuf<unsigned long long> ctr;  // scratch counters
+  unsigned long long *h_ctr = nullptr;  // pinned mirror
+  uint64_t pad = 4096;
+
+  DevBlocks dev_blocks() {
+    return DevBlocks{b_cstart.p, b_csize.p, b_hsize.p, b_usize.p, b_ustart.p, b_flags.p, b_status.p};
+  }
+};
+
+static int fail(sbh_ctx *ctx, int code, const char *fmt, ...) {
+  if (ctx) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    ctx->err = buf;
+  }
+  return code;
+}
+
+#define HIPCHK(ctx, x)                                                                              \
+  do {                                                                                              \
+    hipError_t e_ = (x);                                                                            \
+    if (e_ != hipSuccess) return fail((ctx), SBH_E_HIP, "%s: %s", #x, hipGetErrorString(e_));       \
+  } while (0)
+
+static int set_device(sbh_ctx *ctx) {
+  HIPCHK(ctx, hipSetDevice(ctx->device));
+  return SBH_OK;
+}
+
+extern "C" {
+
+const char *sbh_version(void) { return "sparkbam-hip 0.1 (gfx950)"; }
+
+int sbh_ctx_create(int device, sbh_ctx **out) {
+  if (!out) return SBH_E_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return SBH_E_HIP;
+  sbh_ctx *c = new sbh_ctx();
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return SBH_E_HIP;
+  }
+  c->own_stream = true;
+  *out = c;
+  return SBH_OK;
+}
+
+int sbh_ctx_destroy(sbh_ctx *ctx) {
+  if (!ctx) return SBH_OK;
+  if (ctx->own_stream && ctx->stream) {
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamDestroy(ctx->stream);
+  }
+  delete ctx;
+  return SBH_OK;
+}
+
+const char *sbh_last_error(const sbh_ctx *ctx) { return ctx ? ctx->err.c_str() : "no context"; }
+
+int sbh_ctx_set_stream(sbh_ctx *ctx, void *hip_stream) {
+  if (!ctx) return SBH_E_ARG;
+  if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  ctx->stream = reinterpret_cast<hipStream_t>(hip_stream);
+  ctx->own_stream = false;
+  return SBH_OK;
+}
+
+int sbh_ctx_synchronize(sbh_ctx *ctx) {
+  if (!ctx) return SBH_E_ARG;
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return SBH_OK;
+}
+
+// Header.make (bgzf/.../block/Header.scala:48-83)
+int sbh_header_make(const uint8_t *b, uint64_t avail, int32_t *hsize, int32_t *csize) {
+  if (!b || avail < 18) return SBH_E_TRUNCATED;
+  if (b[0] != 31 || b[1] != 139 || b[2] != 8 || b[3] != 4) return SBH_E_HEADER_PARSE;
+  if (b[12] != 66 || b[13] != 67 || b[14] != 2) return SBH_E_HEADER_PARSE;
+  const int32_t xlen = (int32_t)b[10] | ((int32_t)b[11] << 8);
+  if (hsize) *hsize = 18 + xlen - 6;
+  if (csize) *csize = ((int32_t)b[16] | ((int32_t)b[17] << 8)) + 1;
+  return SBH_OK;
+}
+
+int sbh_shard_create(sbh_ctx *ctx, const void *src, uint64_t n, uint64_t file_offset, uint64_t file_size,
+                     int comp_on_device, sbh_shard **out) {
+  if (!ctx || !out || (!src && n) || file_offset + n > file_size) return SBH_E_ARG;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  sbh_shard *sh = new sbh_shard();
+  sh->ctx = ctx;
+  sh->file_off = file_offset;
+  sh->n = n;
+  sh->file_size = file_size;
+  sh->at_eof = file_offset + n == file_size;
+  hipError_t e = sh->comp.ensure(n + sh->pad);
+  if (e == hipSuccess && n)
+    e = hipMemcpyAsync(sh->comp.p, src, n, comp_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                       ctx->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(sh->comp.p + n, 0, sh->pad, ctx->stream);
+  if (e == hipSuccess) e = sh->ctr.ensure(1024);
+  if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&sh->h_ctr), 1024 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) {
+    sbh_shard_destroy(sh);
+    return fail(ctx, SBH_E_HIP, "shard create: %s", hipGetErrorString(e));
+  }
+  *out = sh;
+  return SBH_OK;
+}
+
+int sbh_shard_destroy(sbh_shard *sh) {
+  if (!sh) return SBH_OK;
+  (void)hipSetDevice(sh->ctx->device);
+  (void)hipStreamSynchronize(sh->ctx->stream);
+  sh->comp.release();
+  sh->b_cstart.release(); sh->b_ustart.release(); sh->usz.release();
+  sh->b_csize.release(); sh->b_hsize.release(); sh->b_usize.release(); sh->b_flags.release();
+  sh->b_status.release();
+  sh->counts.release(); sh->offs.release(); sh->cand.release(); sh->v.release(); sh->rank.release();
+  sh->tmp.release(); sh->J0.release(); sh->J1.release(); sh->on.release(); sh->d_seg.release();
+  sh->U.release(); sh->ctg.release(); sh->bits.release(); sh->words.release(); sh->close_pos.release();
+  sh->close_word.release(); sh->ctr.release();
+  if (sh->h_ctr) (void)hipHostFree(sh->h_ctr);
+  delete sh;
+  return SBH_OK;
+}
+
+const void *sbh_shard_comp_device_ptr(sbh_shard *sh) { return sh ? sh->comp.p : nullptr; }
+
+// FindBlockStart.apply (bgzf/.../block/FindBlockStart.scala:8-36)
+int sbh_find_block_start(sbh_shard *sh, uint64_t start, int32_t k, uint64_t *out) {
+  if (!sh || !out || k < 0 || start < sh->file_off) return SBH_E_ARG;
+  sbh_ctx *ctx = sh->ctx;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  const uint64_t rel = start - sh->file_off;
+  unsigned long long *best = sh->ctr.p;
+  HIPCHK(ctx, hipMemsetAsync(best, 0xff, 8, ctx->stream));
+  HIPCHK(ctx, launch_find_block_start(sh->comp.p, sh->n, rel, k, sh->at_eof ? 1 : 0, best, ctx->stream));
+  HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr, best, 8, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  const unsigned long long b = sh->h_ctr[0];
+  if (b == ~0ull) return fail(ctx, SBH_E_HEADER_SEARCH_FAILED, "no BGZF block start in [%llu, %llu)",
+                              (unsigned long long)start, (unsigned long long)(start + 65536));
+  const uint32_t outcome = (uint32_t)(b & 0xff);
+  const uint64_t pos = b >> 8;
+  if (outcome == 2) return fail(ctx, SBH_E_TRUNCATED, "truncated BGZF block near %llu", (unsigned long long)(start + pos));
+  if (outcome == 3) return fail(ctx, SBH_E_NEED_HALO, "FindBlockStart(%llu) needs bytes past the shard", (unsigned long long)start);
+  *out = start + pos;
+  return SBH_OK;
+}
+
+// MetadataStream from `start` (bgzf/.../block/MetadataStream.scala:16-58)
+int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_size) {
+  if (!sh || start < sh->file_off || start > sh->file_off + sh->n) return SBH_E_ARG;
+  sbh_ctx *ctx = sh->ctx;
+  hipStream_t st = ctx->stream;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  sh->indexed = sh->inflated = sh->bits_valid = false;
+  const uint64_t rel = start - sh->file_off;
+  const uint64_t n = sh->n;
+  // the start must itself be a header
+  uint8_t h18[18] = {0};
+  if (rel + 18 <= n) {
+    HIPCHK(ctx, hipMemcpyAsync(h18, sh->comp.p + rel, 18, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    if (sbh_header_make(h18, 18, nullptr, nullptr) != SBH_OK)
+      return fail(ctx, SBH_E_HEADER_PARSE, "no BGZF header at %llu", (unsigned long long)start);
+  }
+  const uint64_t nchunks = (n + 4095) / 4096;
+  uint64_t nc = 0;
+  if (nchunks && rel + 18 <= n) {
+    HIPCHK(ctx, sh->counts.ensure(nchunks));
+    HIPCHK(ctx, sh->offs.ensure(nchunks));
+    HIPCHK(ctx, sh->tmp.ensure(scan_tmp_words(nchunks) + scan_tmp_words(1 << 24)));
+    HIPCHK(ctx, launch_cand_count(sh->comp.p, n, rel, sh->counts.p, nchunks, st));
+    HIPCHK(ctx, scan_exclusive_u64(sh->counts.p, sh->offs.p, nchunks, sh->tmp.p, st));
+    HIPCHK(ctx, hipMemcpyAsync(&sh->h_ctr[0], sh->offs.p + nchunks - 1, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(&sh->h_ctr[1], sh->counts.p + nchunks - 1, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    nc = sh->h_ctr[0] + sh->h_ctr[1];
+  }
+  uint64_t nchain = 0;
+  if (nc) {
+    HIPCHK(ctx, sh->cand.ensure(nc));
+    HIPCHK(ctx, sh->J0.ensure(nc));
+    HIPCHK(ctx, sh->J1.ensure(nc));
+    HIPCHK(ctx, sh->on.ensure(nc));
+    HIPCHK(ctx, sh->v.ensure(nc));
+    HIPCHK(ctx, sh->rank.ensure(nc));
+    HIPCHK(ctx, sh->tmp.ensure(scan_tmp_words(nc) + scan_tmp_words(nchunks)));
+    HIPCHK(ctx, launch_cand_write(sh->comp.p, n, rel, sh->offs.p, sh->cand.p, nchunks, st));
+    HIPCHK(ctx, sh->b_cstart.ensure(nc));
+    HIPCHK(ctx, sh->b_ustart.ensure(nc));
+    HIPCHK(ctx, sh->usz.ensure(nc));
+    HIPCHK(ctx, sh->b_csize.ensure(nc));
+    HIPCHK(ctx, sh->b_hsize.ensure(nc));
+    HIPCHK(ctx, sh->b_usize.ensure(nc));
+    HIPCHK(ctx, sh->b_flags.ensure(nc));
+    HIPCHK(ctx, sh->b_status.ensure(nc));
+    HIPCHK(ctx, build_chain(sh->comp.p, n, sh->cand.p, nc, sh->J0.p, sh->J1.p, sh->on.p, sh->v.p, sh->rank.p,
+                            sh->tmp.p, sh->dev_blocks(), sh->usz.p, &nchain, st));
+    HIPCHK(ctx, scan_exclusive_u64(sh->usz.p, sh->b_ustart.p, nchain, sh->tmp.p, st));
+  }
+  // host copy of the block table (Pos mapping, segments)
+  sh->hb.assign(nchain, sbh_block{});
+  if (nchain) {
+    std::vector<uint64_t> cs(nchain), us(nchain);
+    std::vector<uint32_t> csz(nchain), hsz(nchain), usz(nchain), fl(nchain);
+    HIPCHK(ctx, hipMemcpyAsync(cs.data(), sh->b_cstart.p, nchain * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(us.data(), sh->b_ustart.p, nchain * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(csz.data(), sh->b_csize.p, nchain * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(hsz.data(), sh->b_hsize.p, nchain * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(usz.data(), sh->b_usize.p, nchain * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(fl.data(), sh->b_flags.p, nchain * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    for (uint64_t i = 0; i < nchain; ++i)
+      sh->hb[i] = sbh_block{cs[i] + sh->file_off, us[i], csz[i], hsz[i], usz[i], fl[i]};
+  }
+  // stream end: a truncated last block is not part of the resident stream
+  sh->open_last = !sh->at_eof;
+  sh->broken_end = false;
+  if (!sh->hb.empty() && (sh->hb.back().flags & SBH_BLOCK_TRUNCATED)) {
+    sh->hb.pop_back();
+    --nchain;
+  } else if (!sh->hb.empty()) {
+    const sbh_block &l = sh->hb.back();
+    const uint64_t q = l.start - sh->file_off + l.csize;
+    if (q + 18 <= n) {  // the next header does not parse: HeaderParseException if read
+      uint8_t nx[18];
+      HIPCHK(ctx, hipMemcpyAsync(nx, sh->comp.p + q, 18, hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipStreamSynchronize(st));
+      if (sbh_header_make(nx, 18, nullptr, nullptr) != SBH_OK) {
+        sh->broken_end = true;
+        sh->open_last = false;
+      }
+    }
+  }
+  uint64_t total = 0;
+  sh->seg_end.clear();
+  for (const sbh_block &b : sh->hb) {
+    if (b.flags & SBH_BLOCK_EMPTY) sh->seg_end.push_back(b.ustart);
+    if (!(b.flags & SBH_BLOCK_EMPTY) && b.usize <= 65536) total = b.ustart + b.usize;
+  }
+  sh->seg_end.push_back(total);
+  HIPCHK(ctx, sh->d_seg.ensure(sh->seg_end.size()));
+  HIPCHK(ctx, hipMemcpyAsync(sh->d_seg.p, sh->seg_end.data(), sh->seg_end.size() * 8, hipMemcpyHostToDevice, st));
+  sh->nblocks = nchain;
+  sh->utotal = total;
+  sh->index_start = start;
+  sh->indexed = true;
+  if (n_blocks) *n_blocks = nchain;
+  if (flat_size) *flat_size = total;
+  return SBH_OK;
+}
+
+int sbh_get_blocks(sbh_shard *sh, uint64_t first, uint64_t count, sbh_block *out) {
+  if (!sh || !out) return SBH_E_ARG;
+  if (!sh->indexed) return fail(sh->ctx, SBH_E_STATE, "not indexed");
+  if (first + count > sh->hb.size()) return SBH_E_ARG;
+  std::memcpy(out, sh->hb.data() + first, count * sizeof(sbh_block));
+  return SBH_OK;
+}
+
+int sbh_inflate(sbh_shard *sh, uint64_t *bad_block) {
+  if (!sh) return SBH_E_ARG;
+  sbh_ctx *ctx = sh->ctx;
+  if (!sh->indexed) return fail(ctx, SBH_E_STATE, "inflate before index");
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  hipStream_t st = ctx->stream;
+  HIPCHK(ctx, sh->U.ensure(sh->utotal + sh->pad));
+  HIPCHK(ctx, hipMemsetAsync(sh->U.p + sh->utotal, 0, sh->pad, st));
+  HIPCHK(ctx, launch_inflate(sh->comp.p, sh->dev_blocks(), sh->nblocks, sh->U.p, st));
+  std::vector<uint32_t> status(sh->nblocks);
+  if (sh->nblocks) HIPCHK(ctx, hipMemcpyAsync(status.data(), sh->b_status.p, sh->nblocks * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  for (uint64_t i = 0; i < sh->nblocks; ++i) {
+    if (status[i] == INF_OK) continue;
+    if (bad_block) *bad_block = i;
+    const sbh_block &b = sh->hb[i];
+    if (status[i] == INF_SIZE)
+      return fail(ctx, SBH_E_INFLATE_SIZE, "block %llu: expected %u decompressed bytes", (unsigned long long)b.start,
+                  b.usize);
+    if (status[i] == INF_BAD_ISIZE) return fail(ctx, SBH_E_BAD_ISIZE, "block %llu: ISIZE %u", (unsigned long long)b.start, b.usize);
+    return fail(ctx, SBH_E_INFLATE_DATA, "block %llu: invalid deflate data", (unsigned long long)b.start);
+  }
+  sh->inflated = true;
+  sh->bits_valid = false;
+  return SBH_OK;
+}
+
+int sbh_read_flat(sbh_shard *sh, uint64_t flat, uint64_t n, uint8_t *out) {
+  if (!sh || (!out && n)) return SBH_E_ARG;
+  if (!sh->inflated) return fail(sh->ctx, SBH_E_STATE, "not inflated");
+  if (flat + n > sh->utotal) return SBH_E_ARG;
+  int rc = set_device(sh->ctx);
+  if (rc) return rc;
+  HIPCHK(sh->ctx, hipMemcpyAsync(out, sh->U.p + flat, n, hipMemcpyDeviceToHost, sh->ctx->stream));
+  HIPCHK(sh->ctx, hipStreamSynchronize(sh->ctx->stream));
+  return SBH_OK;
+}
+
+const void *sbh_flat_device_ptr(sbh_shard *sh) { return sh ? sh->U.p : nullptr; }
+
+static int64_t block_index_of(const sbh_shard *sh, uint64_t file_pos) {
+  auto it = std::lower_bound(sh->hb.begin(), sh->hb.end(), file_pos,
+                             [](const sbh_block &b, uint64_t v) { return b.start < v; });
+  if (it == sh->hb.end() || it->start != file_pos) return -1;
+  return it - sh->hb.begin();
+}
+
+int sbh_flat_of(sbh_shard *sh, uint64_t block_pos, uint32_t offset, uint64_t *flat) {
+  if (!sh || !flat) return SBH_E_ARG;
+  if (!sh->indexed) return fail(sh->ctx, SBH_E_STATE, "not indexed");
+  const int64_t i = block_index_of(sh, block_pos);
+  if (i < 0) return fail(sh->ctx, SBH_E_NOT_FOUND, "%llu is not an indexed block start", (unsigned long long)block_pos);
+  *flat = sh->hb[i].ustart + offset;
+  return SBH_OK;
+}
+
+int sbh_pos_of(sbh_shard *sh, uint64_t flat, uint64_t *block_pos, uint32_t *offset) {
+  if (!sh || !block_pos || !offset) return SBH_E_ARG;
+  if (!sh->indexed) return fail(sh->ctx, SBH_E_STATE, "not indexed");
+  // last block with ustart <= flat and flat < ustart + usize (skips empty blocks)
+  auto it = std::upper_bound(sh->hb.begin(), sh->hb.end(), flat,
+                             [](uint64_t v, const sbh_block &b) { return v < b.ustart; });
+  int64_t i = (it - sh->hb.begin()) - 1;
+  while (i >= 0 && (uint64_t)i < sh->hb.size() && sh->hb[i].ustart + sh->hb[i].usize <= flat) ++i;
+  if (i < 0 || (uint64_t)i >= sh->hb.size()) {
+    // one past the last byte: Pos(next block, 0)
+    if (!sh->hb.empty() && flat == sh->utotal) {
+      const sbh_block &l = sh->hb.back();
+      *block_pos = l.start + l.csize;
+      *offset = 0;
+      return SBH_OK;
+    }
+    return fail(sh->ctx, SBH_E_NOT_FOUND, "flat %llu outside the indexed stream", (unsigned long long)flat);
+  }
+  // skip zero-size blocks sharing this ustart
+  while ((uint64_t)i < sh->hb.size() && (sh->hb[i].usize == 0 || (sh->hb[i].flags & SBH_BLOCK_EMPTY))) ++i;
+  if ((uint64_t)i >= sh->hb.size()) return SBH_E_NOT_FOUND;
+  *block_pos = sh->hb[i].start;
+  *offset = (uint32_t)(flat - sh->hb[i].ustart);
+  return SBH_OK;
+}
+
+int sbh_flat_bound(sbh_shard *sh, uint64_t file_off, uint64_t *flat) {
+  if (!sh || !flat) return SBH_E_ARG;
+  if (!sh->indexed) return fail(sh->ctx, SBH_E_STATE, "not indexed");
+  auto it = std::lower_bound(sh->hb.begin(), sh->hb.end(), file_off,
+                             [](const sbh_block &b, uint64_t v) { return b.start < v; });
+  *flat = it == sh->hb.end() ? sh->utotal : it->ustart;
+  return SBH_OK;
+}
+
+int sbh_set_contigs(sbh_shard *sh, const int32_t *lens, int32_t n) {
+  if (!sh || n < 0 || (n && !lens)) return SBH_E_ARG;
+  int rc = set_device(sh->ctx);
+  if (rc) return rc;
+  HIPCHK(sh->ctx, sh->ctg.ensure(n + 1));
+  if (n) HIPCHK(sh->ctx, hipMemcpyAsync(sh->ctg.p, lens, (uint64_t)n * 4, hipMemcpyHostToDevice, sh->ctx->stream));
+  HIPCHK(sh->ctx, hipStreamSynchronize(sh->ctx->stream));
+  sh->nctg = n;
+  sh->bits_valid = false;
+  return SBH_OK;
+}
+
+static int need_checkable(sbh_shard *sh, uint64_t begin, uint64_t end, int32_t rtc) {
+  if (!sh->inflated) return fail(sh->ctx, SBH_E_STATE, "check before inflate");
+  if (sh->nctg < 0) return fail(sh->ctx, SBH_E_STATE, "contig lengths not set");
+  if (begin > end || end > sh->utotal) return fail(sh->ctx, SBH_E_ARG, "range [%llu,%llu) outside [0,%llu)",
+                                                  (unsigned long long)begin, (unsigned long long)end,
+                                                  (unsigned long long)sh->utotal);
+  if (rtc < 0 || rtc > 1023) return fail(sh->ctx, SBH_E_ARG, "readsToCheck must be in [0, 1023]");
+  return SBH_OK;
+}
+
+static int eager_range(sbh_shard *sh, uint64_t begin, uint64_t end, int32_t rtc, uint64_t *n_true) {
+  sbh_ctx *ctx = sh->ctx;
+  hipStream_t st = ctx->stream;
+  const uint64_t nwords = (end - begin + 31) / 32;
+  HIPCHK(ctx, sh->bits.ensure(nwords + 1));
+  unsigned long long *c = sh->ctr.p;
+  HIPCHK(ctx, hipMemsetAsync(c, 0, 16, st));
+  HIPCHK(ctx, hipMemsetAsync(c + 2, 0xff, 8, st));
+  HIPCHK(ctx, launch_eager(sh->U.p, sh->utotal + sh->pad, begin, end, sh->d_seg.p, (uint32_t)sh->seg_end.size(),
+                           sh->open_last ? 1 : 0, sh->ctg.p, sh->nctg, rtc, sh->bits.p, c, st));
+  HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr, c, 24, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  sh->bits_valid = true;
+  sh->bits_begin = begin;
+  sh->bits_end = end;
+  sh->bits_rtc = rtc;
+  if (n_true) *n_true = sh->h_ctr[0];
+  if (sh->h_ctr[1]) {
+    sh->bits_valid = false;
+    return fail(ctx, SBH_E_NEED_HALO, "%llu positions (first %llu) need bytes past the shard",
+                sh->h_ctr[1], sh->h_ctr[2]);
+  }
+  return SBH_OK;
+}
+
+int sbh_check_eager(sbh_shard *sh, uint64_t begin, uint64_t end, int32_t rtc, uint8_t *out_bits, uint64_t *n_true) {
+  if (!sh) return SBH_E_ARG;
+  int rc = need_checkable(sh, begin, end, rtc);
+  if (rc) return rc;
+  rc = set_device(sh->ctx);
+  if (rc) return rc;
+  rc = eager_range(sh, begin, end, rtc, n_true);
+  if (rc) return rc;
+  if (out_bits && end > begin) {
+    HIPCHK(sh->ctx, hipMemcpyAsync(out_bits, sh->bits.p, (end - begin + 7) / 8, hipMemcpyDeviceToHost, sh->ctx->stream));
+    HIPCHK(sh->ctx, hipStreamSynchronize(sh->ctx->stream));
+  }
+  return SBH_OK;
+}
+
+int sbh_check_full(sbh_shard *sh, uint64_t begin, uint64_t end, int32_t rtc, uint32_t *out_words, uint64_t *counts,
+                   uint64_t *rbe_hist, uint64_t *n_success, uint64_t *close_flat, uint32_t *close_word,
+                   uint64_t close_cap, uint64_t *n_close) {
+  if (!sh) return SBH_E_ARG;
+  int rc = need_checkable(sh, begin, end, rtc);
+  if (rc) return rc;
+  rc = set_device(sh->ctx);
+  if (rc) return rc;
+  sbh_ctx *ctx = sh->ctx;
+  hipStream_t st = ctx->stream;
+  const uint64_t nctr = 4 + 21 * 19 + 21 * 64;
+  unsigned long long *c = sh->ctr.p;
+  HIPCHK(ctx, hipMemsetAsync(c, 0, nctr * 8, st));
+  HIPCHK(ctx, hipMemsetAsync(c + 2, 0xff, 8, st));
+  uint32_t *words = nullptr;
+  if (out_words) {
+    HIPCHK(ctx, sh->words.ensure(end - begin + 1));
+    words = sh->words.p;
+  }
+  const uint64_t cap = close_cap;
+  HIPCHK(ctx, sh->close_pos.ensure(cap + 1));
+  HIPCHK(ctx, sh->close_word.ensure(cap + 1));
+  HIPCHK(ctx, launch_full(sh->U.p, sh->utotal + sh->pad, begin, end, sh->d_seg.p, (uint32_t)sh->seg_end.size(),
+                          sh->open_last ? 1 : 0, sh->ctg.p, sh->nctg, rtc, words, c, sh->close_pos.p,
+                          sh->close_word.p, cap, st));
+  HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr, c, nctr * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  if (sh->h_ctr[1])
+    return fail(ctx, SBH_E_NEED_HALO, "%llu positions (first %llu) need bytes past the shard", sh->h_ctr[1],
+                sh->h_ctr[2]);
+  if (n_success) *n_success = sh->h_ctr[0];
+  const uint64_t nclose = sh->h_ctr[3];
+  if (n_close) *n_close = nclose;
+  if (counts) for (int i = 0; i < 21 * 19; ++i) counts[i] = sh->h_ctr[4 + i];
+  if (rbe_hist) for (int i = 0; i < 21 * 64; ++i) rbe_hist[i] = sh->h_ctr[4 + 21 * 19 + i];
+  const uint64_t ncopy = std::min<uint64_t>(nclose, cap);
+  if (ncopy && (close_flat || close_word)) {
+    // positions arrive in atomic order: sort them on the host
+    std::vector<uint64_t> p(ncopy);
+    std::vector<uint32_t> w(ncopy);
+    HIPCHK(ctx, hipMemcpyAsync(p.data(), sh->close_pos.p, ncopy * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(w.data(), sh->close_word.p, ncopy * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    std::vector<uint64_t> idx(ncopy);
+    for (uint64_t i = 0; i < ncopy; ++i) idx[i] = i;
+    std::sort(idx.begin(), idx.end(), [&](uint64_t a, uint64_t b) { return p[a] < p[b]; });
+    for (uint64_t i = 0; i < ncopy; ++i) {
+      if (close_flat) close_flat[i] = p[idx[i]];
+      if (close_word) close_word[i] = w[idx[i]];
+    }
+  }
+  if (out_words && end > begin) {
+    HIPCHK(ctx, hipMemcpyAsync(out_words, sh->words.p, (end - begin) * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+  }
+  return SBH_OK;
+}
+
+static uint64_t seg_end_of(const sbh_shard *sh, uint64_t p) {
+  for (uint64_t e : sh->seg_end)
+    if (e > p) return e;
+  return sh->seg_end.back();
+}
+static bool seg_is_open(const sbh_shard *sh, uint64_t p) {
+  return sh->open_last && seg_end_of(sh, p) == sh->seg_end.back();
+}
+
+// FindRecordStart.withDelta (check/.../spark/FindRecordStart.scala:30-63)
+int sbh_find_record_start(sbh_shard *sh, uint64_t from, int32_t rtc, int32_t max_read_size, uint64_t *out_flat,
+                          int32_t *out_delta) {
+  if (!sh || !out_flat) return SBH_E_ARG;
+  sbh_ctx *ctx = sh->ctx;
+  int rc = need_checkable(sh, from, from, rtc);
+  if (rc) return rc;
+  rc = set_device(ctx);
+  if (rc) return rc;
+  hipStream_t st = ctx->stream;
+  const uint64_t seg = seg_end_of(sh, from);
+  const uint64_t limit = std::min<uint64_t>(seg, from + (uint64_t)std::max(max_read_size, 0));
+  uint64_t lo = from;
+  uint64_t window = 1 << 20;
+  while (lo < limit) {
+    uint64_t hi;
+    bool covered = sh->bits_valid && sh->bits_rtc == rtc && sh->bits_begin <= lo && lo < sh->bits_end;
+    if (covered) {
+      hi = std::min(limit, sh->bits_end);
+    } else {
+      hi = std::min(limit, lo + window);
+      window = std::min<uint64_t>(window * 4, 1ull << 28);
+      rc = eager_range(sh, lo, hi, rtc, nullptr);
+      if (rc == SBH_E_NEED_HALO) {
+        // unknowns are fine only if a true position precedes the first unknown
+        const uint64_t first_unknown = sh->h_ctr[2];
+        unsigned long long *best = sh->ctr.p + 8;
+        HIPCHK(ctx, hipMemsetAsync(best, 0xff, 8, st));
+        sh->bits_valid = true;
+        HIPCHK(ctx, launch_first_set(sh->bits.p, lo, lo, first_unknown, best, st));
+        HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 8, best, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(ctx, hipStreamSynchronize(st));
+        sh->bits_valid = false;
+        if (sh->h_ctr[8] != ~0ull) {
+          *out_flat = sh->h_ctr[8];
+          if (out_delta) *out_delta = (int32_t)(sh->h_ctr[8] - from);
+          return SBH_OK;
+        }
+        return rc;
+      }
+      if (rc) return rc;
+    }
+    unsigned long long *best = sh->ctr.p + 8;
+    HIPCHK(ctx, hipMemsetAsync(best, 0xff, 8, st));
+    HIPCHK(ctx, launch_first_set(sh->bits.p, sh->bits_begin, lo, hi, best, st));
+    HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 8, best, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    if (sh->h_ctr[8] != ~0ull) {
+      *out_flat = sh->h_ctr[8];
+      if (out_delta) *out_delta = (int32_t)(sh->h_ctr[8] - from);
+      return SBH_OK;
+    }
+    lo = hi;
+  }
+  if (lo >= seg && seg_is_open(sh, from) && (uint64_t)max_read_size > seg - from)
+    return fail(ctx, SBH_E_NEED_HALO, "record search from %llu runs past the shard", (unsigned long long)from);
+  return fail(ctx, SBH_E_NO_READ_FOUND, "no read start within %d positions of flat %llu", max_read_size,
+              (unsigned long long)from);
+}
+
+static int count_records_impl(sbh_shard *sh, uint64_t first, uint64_t E, uint64_t *count, int32_t *anomalies) {
+  sbh_ctx *ctx = sh->ctx;
+  hipStream_t st = ctx->stream;
+  const uint64_t total = seg_end_of(sh, first);
+  E = std::min(E, total);
+  if (anomalies) *anomalies = 0;
+  if (first >= E) {
+    *count = 0;
+    return SBH_OK;
+  }
+  unsigned long long *c = sh->ctr.p + 16;
+  const bool covered = sh->bits_valid && sh->bits_begin <= first && E <= sh->bits_end;
+  if (covered) {
+    HIPCHK(ctx, hipMemsetAsync(c, 0, 16, st));
+    HIPCHK(ctx, hipMemsetAsync(c + 1, 0xff, 8, st));
+    HIPCHK(ctx, hipMemsetAsync(c + 2, 0, 8, st));
+    HIPCHK(ctx, launch_verify_chain(sh->U.p, sh->bits.p, sh->bits_begin, sh->bits_end, first, E, total, c, c + 1, st));
+    HIPCHK(ctx, launch_popcount(sh->bits.p, sh->bits_begin, first, E, c + 2, st));
+    HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 16, c, 24, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    if (sh->h_ctr[16] == 0) {
+      *count = sh->h_ctr[18];
+      return SBH_OK;
+    }
+    if (anomalies) *anomalies = (int32_t)std::min<uint64_t>(sh->h_ctr[16], INT32_MAX);
+  }
+  HIPCHK(ctx, launch_chain_walk(sh->U.p, first, E, total, c + 4, c + 5, st));
+  HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 20, c + 4, 16, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  *count = sh->h_ctr[20];
+  return SBH_OK;
+}
+
+int sbh_count_records(sbh_shard *sh, uint64_t first, uint64_t end_flat, uint64_t *count) {
+  if (!sh || !count) return SBH_E_ARG;
+  if (!sh->inflated) return fail(sh->ctx, SBH_E_STATE, "count before inflate");
+  if (first > sh->utotal) return SBH_E_ARG;
+  int rc = set_device(sh->ctx);
+  if (rc) return rc;
+  return count_records_impl(sh, first, std::min(end_flat, sh->utotal), count, nullptr);
+}
+
+// CanLoadBam.loadReadsAndPositions, one split (load/.../CanLoadBam.scala:316-356)
+int sbh_split(sbh_shard *sh, uint64_t start, uint64_t end, int32_t k, int32_t rtc, int32_t mrs, uint64_t *first_vpos,
+              uint64_t *count) {
+  if (!sh || !first_vpos || !count) return SBH_E_ARG;
+  sbh_ctx *ctx = sh->ctx;
+  if (!sh->inflated) return fail(ctx, SBH_E_STATE, "split before inflate");
+  uint64_t b = 0;
+  int rc = sbh_find_block_start(sh, start, k, &b);
+  if (rc) return rc;
+  const int64_t bi = block_index_of(sh, b);
+  if (bi < 0) {
+    if (b >= sh->file_size || (sh->at_eof && b >= sh->file_off + sh->n))
+      return fail(ctx, SBH_E_NO_READ_FOUND, "split at %llu: no blocks left", (unsigned long long)start);
+    return fail(ctx, SBH_E_NOT_FOUND, "block start %llu is not on the indexed chain", (unsigned long long)b);
+  }
+  if (sh->hb[bi].flags & SBH_BLOCK_EMPTY)  // the stream from an empty block ends at once
+    return fail(ctx, SBH_E_NO_READ_FOUND, "split at %llu starts at an empty block", (unsigned long long)start);
+  uint64_t first = 0;
+  int32_t delta = 0;
+  rc = sbh_find_record_start(sh, sh->hb[bi].ustart, rtc, mrs, &first, &delta);
+  if (rc) return rc;
+  uint64_t E = 0;
+  (void)sbh_flat_bound(sh, end, &E);
+  if (!sh->at_eof && end > sh->hb.back().start && E == sh->utotal)
+    return fail(ctx, SBH_E_NEED_HALO, "split end %llu past the resident blocks", (unsigned long long)end);
+  rc = count_records_impl(sh, first, E, count, nullptr);
+  if (rc) return rc;
+  uint64_t bp = 0;
+  uint32_t off = 0;
+  rc = sbh_pos_of(sh, first, &bp, &off);
+  if (rc) return rc;
+  *first_vpos = (bp << 16) | off;
+  return SBH_OK;
+}
+
+int sbh_run_shard(sbh_shard *sh, uint64_t index_start, uint64_t own_end_file, int32_t rtc, int32_t mrs,
+                  sbh_shard_result *res) {
+  if (!sh || !res) return SBH_E_ARG;
+  std::memset(res, 0, sizeof *res);
+  sbh_ctx *ctx = sh->ctx;
+  int rc = sbh_index(sh, index_start, &res->n_blocks, nullptr);
+  if (!rc) rc = sbh_inflate(sh, nullptr);
+  if (rc) return res->status = rc;
+  uint64_t E = 0;
+  (void)sbh_flat_bound(sh, own_end_file, &E);
+  if (!sh->at_eof && E == sh->utotal) return res->status = fail(ctx, SBH_E_NEED_HALO, "no halo past %llu", (unsigned long long)own_end_file);
+  uint64_t owned_blocks = 0, cbytes = 0;
+  for (const sbh_block &b : sh->hb)
+    if (b.start < own_end_file) { ++owned_blocks; cbytes += b.csize; }
+  res->n_blocks = owned_blocks;
+  res->comp_bytes = cbytes;
+  res->flat_bytes = E;
+  rc = sbh_check_eager(sh, 0, E, rtc, nullptr, &res->n_true);
+  if (rc) return res->status = rc;
+  uint64_t first = 0;
+  int32_t delta = 0;
+  rc = sbh_find_record_start(sh, 0, rtc, mrs, &first, &delta);
+  if (rc == SBH_E_NO_READ_FOUND) {
+    res->count = 0;
+    return res->status = SBH_OK;
+  }
+  if (rc) return res->status = rc;
+  rc = count_records_impl(sh, first, E, &res->count, &res->anomalies);
+  if (rc) return res->status = rc;
+  uint64_t bp = 0;
+  uint32_t off = 0;
+  if (sbh_pos_of(sh, first, &bp, &off) == SBH_OK) res->first_vpos = (bp << 16) | off;
+  res->exit_flat = E;
+  return res->status = SBH_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,39 @@
+// sbh_internal.h -- device-side layouts shared by the HIP kernels and the C-ABI layer.
+// CDNA4 (gfx950) only: 64-lane waves, 160 KiB LDS per CU.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/sparkbam.h"
+
+namespace sbh {
+
+constexpr int WAVE = 64;
+
+// Block table (struct of arrays, one entry per BGZF block of the chain, in file
+// order).  Mirrors bgzf Metadata(start, compressedSize, uncompressedSize)
+// (bgzf/.../block/Metadata.scala:6-8) plus the header size and flat start.
+struct DevBlocks {
+  uint64_t *cstart;  // compressed offset relative to the shard's first byte
+  uint32_t *csize;   // BSIZE + 1
+  uint32_t *hsize;   // 18 + XLEN - 6
+  uint32_t *usize;   // ISIZE (0 for an empty block)
+  uint64_t *ustart;  // flat offset of the block's first uncompressed byte
+  uint32_t *flags;   // BLK_* bits
+  uint32_t *status;  // inflate status per block (SBH_OK / SBH_E_INFLATE_*)
+};
+
+constexpr uint32_t BLK_EMPTY = 1u;     // dataLength == 2: the stream ends here
+constexpr uint32_t BLK_TRUNCATED = 2u;  // block runs past the resident bytes
+
+// Inflate status codes per block (written by k_inflate).
+constexpr uint32_t INF_OK = 0;
+constexpr uint32_t INF_SIZE = 1;      // fewer than ISIZE bytes produced
+constexpr uint32_t INF_DATA = 2;      // DataFormatException (zlib Z_DATA_ERROR)
+constexpr uint32_t INF_BAD_ISIZE = 3; // ISIZE outside [0, 65536]
+
+// Launchers (defined in the .hip files, called from sbh_api.hip).
+hipError_t launch_inflate(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks,
+                          uint8_t *U, hipStream_t stream);
+
+}  // namespace sbh

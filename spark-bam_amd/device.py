@@ -1,0 +1,188 @@
+"""Context / Shard: thin owners of the C-ABI handles (include/sparkbam.h)."""
+import ctypes as C
+
+import numpy as np
+
+from ._lib import (SBH_OK, SbhBlock, SbhShardResult, SparkBamError, lib)
+
+
+def _check(ctx_handle, rc):
+    if rc != SBH_OK:
+        msg = lib().sbh_last_error(ctx_handle) if ctx_handle else b""
+        raise SparkBamError(rc, (msg or b"").decode(errors="replace"))
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+class Context:
+    """One per device (sbh_ctx_create).  Owns a HIP stream unless one is supplied."""
+
+    def __init__(self, device=0, stream=None):
+        h = C.c_void_p()
+        rc = lib().sbh_ctx_create(device, C.byref(h))
+        if rc != SBH_OK:
+            raise SparkBamError(rc, f"cannot create a context on device {device}")
+        self.h = h
+        self.device = device
+        if stream is not None:
+            _check(self.h, lib().sbh_ctx_set_stream(self.h, C.c_void_p(stream)))
+
+    def synchronize(self):
+        _check(self.h, lib().sbh_ctx_synchronize(self.h))
+
+    def close(self):
+        if self.h:
+            lib().sbh_ctx_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def shard(self, comp, file_offset=0, file_size=None, on_device=False, nbytes=None):
+        return Shard(self, comp, file_offset, file_size, on_device, nbytes)
+
+
+class Shard:
+    """Compressed bytes [file_offset, file_offset + n) of a BGZF file, resident in HBM."""
+
+    def __init__(self, ctx, comp, file_offset=0, file_size=None, on_device=False, nbytes=None):
+        self.ctx = ctx
+        if on_device:
+            ptr, n = int(comp), int(nbytes)
+            src = C.c_void_p(ptr)
+        else:
+            arr = np.ascontiguousarray(np.frombuffer(comp, dtype=np.uint8)
+                                       if not isinstance(comp, np.ndarray) else comp)
+            n = int(arr.size)
+            src = _ptr(arr)
+            self._keep = arr
+        self.n = n
+        self.file_offset = int(file_offset)
+        self.file_size = int(file_size if file_size is not None else file_offset + n)
+        h = C.c_void_p()
+        _check(ctx.h, lib().sbh_shard_create(ctx.h, src, n, self.file_offset, self.file_size,
+                                             1 if on_device else 0, C.byref(h)))
+        self.h = h
+        self._keep = None
+        self.n_blocks = 0
+        self.flat_size = 0
+
+    def _c(self, rc):
+        _check(self.ctx.h, rc)
+
+    def close(self):
+        if self.h:
+            lib().sbh_shard_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- bgzf --------------------------------------------------------------
+    def find_block_start(self, start, bgzf_blocks_to_check=5):
+        out = C.c_uint64()
+        self._c(lib().sbh_find_block_start(self.h, start, bgzf_blocks_to_check, C.byref(out)))
+        return out.value
+
+    def index(self, start=None):
+        nb, fs = C.c_uint64(), C.c_uint64()
+        s = self.file_offset if start is None else start
+        self._c(lib().sbh_index(self.h, s, C.byref(nb), C.byref(fs)))
+        self.n_blocks, self.flat_size = nb.value, fs.value
+        return self.n_blocks, self.flat_size
+
+    def blocks(self):
+        arr = (SbhBlock * max(self.n_blocks, 1))()
+        if self.n_blocks:
+            self._c(lib().sbh_get_blocks(self.h, 0, self.n_blocks, arr))
+        return [(b.start, b.csize, b.usize, b.ustart, b.hsize, b.flags)
+                for b in arr[: self.n_blocks]]
+
+    def inflate(self):
+        bad = C.c_uint64()
+        self._c(lib().sbh_inflate(self.h, C.byref(bad)))
+
+    def read_flat(self, flat=0, n=None):
+        n = self.flat_size - flat if n is None else n
+        out = np.empty(n, dtype=np.uint8)
+        if n:
+            self._c(lib().sbh_read_flat(self.h, flat, n, _ptr(out)))
+        return out
+
+    def flat_of(self, block_pos, offset=0):
+        out = C.c_uint64()
+        self._c(lib().sbh_flat_of(self.h, block_pos, offset, C.byref(out)))
+        return out.value
+
+    def pos_of(self, flat):
+        bp, off = C.c_uint64(), C.c_uint32()
+        self._c(lib().sbh_pos_of(self.h, flat, C.byref(bp), C.byref(off)))
+        return bp.value, off.value
+
+    def flat_bound(self, file_off):
+        out = C.c_uint64()
+        self._c(lib().sbh_flat_bound(self.h, file_off, C.byref(out)))
+        return out.value
+
+    # -- check ---------------------------------------------------------------
+    def set_contigs(self, lens):
+        a = np.ascontiguousarray(np.asarray(lens, dtype=np.int32))
+        self._c(lib().sbh_set_contigs(self.h, _ptr(a), int(a.size)))
+
+    def check_eager(self, begin=0, end=None, reads_to_check=10, want_bits=True):
+        end = self.flat_size if end is None else end
+        bits = np.zeros((end - begin + 7) // 8, dtype=np.uint8) if want_bits else None
+        n = C.c_uint64()
+        self._c(lib().sbh_check_eager(self.h, begin, end, reads_to_check, _ptr(bits), C.byref(n)))
+        return n.value, bits
+
+    def check_full(self, begin=0, end=None, reads_to_check=10, want_words=False, close_cap=1 << 20):
+        end = self.flat_size if end is None else end
+        words = np.zeros(end - begin, dtype=np.uint32) if want_words else None
+        counts = np.zeros(21 * 19, dtype=np.uint64)
+        rbe = np.zeros(21 * 64, dtype=np.uint64)
+        close_flat = np.zeros(max(close_cap, 1), dtype=np.uint64)
+        close_word = np.zeros(max(close_cap, 1), dtype=np.uint32)
+        ns, nclose = C.c_uint64(), C.c_uint64()
+        self._c(lib().sbh_check_full(self.h, begin, end, reads_to_check, _ptr(words), _ptr(counts),
+                                     _ptr(rbe), C.byref(ns), _ptr(close_flat), _ptr(close_word),
+                                     close_cap, C.byref(nclose)))
+        k = min(nclose.value, close_cap)
+        return {
+            "n_success": ns.value, "counts": counts.reshape(21, 19), "rbe": rbe.reshape(21, 64),
+            "words": words, "close_flat": close_flat[:k], "close_word": close_word[:k],
+            "n_close": nclose.value,
+        }
+
+    def find_record_start(self, from_flat, reads_to_check=10, max_read_size=100000000):
+        out, d = C.c_uint64(), C.c_int32()
+        self._c(lib().sbh_find_record_start(self.h, from_flat, reads_to_check, max_read_size,
+                                            C.byref(out), C.byref(d)))
+        return out.value, d.value
+
+    def count_records(self, first_flat, end_flat):
+        out = C.c_uint64()
+        self._c(lib().sbh_count_records(self.h, first_flat, end_flat, C.byref(out)))
+        return out.value
+
+    def split(self, start, end, bgzf_blocks_to_check=5, reads_to_check=10,
+              max_read_size=100000000):
+        v, n = C.c_uint64(), C.c_uint64()
+        self._c(lib().sbh_split(self.h, start, end, bgzf_blocks_to_check, reads_to_check,
+                                max_read_size, C.byref(v), C.byref(n)))
+        return v.value, n.value
+
+    def run(self, index_start, own_end_file, reads_to_check=10, max_read_size=100000000):
+        r = SbhShardResult()
+        rc = lib().sbh_run_shard(self.h, index_start, own_end_file, reads_to_check,
+                                 max_read_size, C.byref(r))
+        self._c(rc)
+        return {f: getattr(r, f) for f, _ in SbhShardResult._fields_}

@@ -1,0 +1,347 @@
+"""GPU parity: the HIP path (through the C-ABI) vs the CPU oracle and the reference's
+golden fixtures.  Bit-exact for every byte, bit and count.
+
+Reference tests restated are named per test (paths relative to the reference root).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, golden_bam, parse_total_error_counts, read_blocks, read_records
+from oracle_lib import FLAG_NAMES, OR_OK, OracleFile, file_splits, lib as olib
+from pkg import sb
+
+pytestmark = pytest.mark.gpu
+
+FIXTURES = ["2.bam", "1.bam", "5k.bam", "1.2203053-2211029.bam", "2.100-1000.bam"]
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = sb.Context(0)
+    yield c
+    c.close()
+
+
+def load(ctx, data, contigs=None):
+    sh = ctx.shard(data)
+    sh.index(0)
+    sh.inflate()
+    if contigs is not None:
+        sh.set_contigs(contigs)
+    return sh
+
+
+def first_diff(a, b):
+    n = min(a.size, b.size)
+    d = np.flatnonzero(a[:n] != b[:n])
+    return int(d[0]) if d.size else (n if a.size != b.size else -1)
+
+
+@pytest.fixture(scope="module")
+def golden(ctx):
+    out = {}
+    for name in FIXTURES:
+        data = np.fromfile(golden_bam(name), dtype=np.uint8)
+        of = OracleFile(data)
+        sh = load(ctx, data, of.contig_len)
+        out[name] = (data, of, sh)
+    yield out
+    for _, _, sh in out.values():
+        sh.close()
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_index_blocks(golden, name):
+    # IndexBlocksTest / MetadataStreamTest: (start, csize, usize) of every data block
+    data, of, sh = golden[name]
+    bl = [(s, c, u) for s, c, u, _us, _h, f in sh.blocks() if not f & sb.BLOCK_EMPTY]
+    assert bl == read_blocks(name)
+    assert sh.flat_size == of.flat_size
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_inflate_bytes(golden, name):
+    # StreamTest: inflated bytes identical to java.util.zip.Inflater (zlib)
+    data, of, sh = golden[name]
+    got, want = sh.read_flat(), of.uncompressed()
+    i = first_diff(got, want)
+    assert i < 0, f"first differing flat byte {i} at Pos {of.pos_of(i) if i < want.size else 'end'}"
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_eager_every_position(golden, name):
+    # CheckBamTest "eager 1.bam": eager at every position == .records (All calls matched!)
+    data, of, sh = golden[name]
+    n, bits = sh.check_eager(0, sh.flat_size)
+    n_ref, bits_ref = of.eager_range(0, of.flat_size)
+    i = first_diff(np.unpackbits(bits, bitorder="little"), np.unpackbits(bits_ref, bitorder="little"))
+    assert i < 0, f"first differing position {i}"
+    assert n == n_ref == len(read_records(name))
+
+
+@pytest.mark.parametrize("golden_name,name,end", [("2.bam", "2.bam", None),
+                                                  ("2.bam.first", "2.bam", 65498),
+                                                  ("1.bam", "1.bam", None)])
+def test_full_check_totals(golden, golden_name, name, end):
+    # FullCheckTest + output/full-check/*: "Total error counts", per-nnz Counts == oracle
+    data, of, sh = golden[name]
+    e = sh.flat_size if end is None else end
+    r = sh.check_full(0, e)
+    _, counts_ref, rbe_ref, _ = of.full_range(0, e)
+    assert np.array_equal(r["counts"].astype(np.int64), counts_ref)
+    assert np.array_equal(r["rbe"].astype(np.int64), rbe_ref)
+    tot = dict(zip(FLAG_NAMES, r["counts"].sum(axis=0).tolist()))
+    for k, v in parse_total_error_counts(f"{GOLDEN}/output/full-check/{golden_name}").items():
+        assert tot[k] == v, k
+
+
+def test_full_words_match_oracle(golden):
+    data, of, sh = golden["2.bam"]
+    r = sh.check_full(0, 200000, want_words=True)
+    _, _, _, w_ref = of.full_range(0, 200000, want_words=True)
+    i = first_diff(r["words"], w_ref)
+    assert i < 0, f"position {i}: {hex(r['words'][i])} vs {hex(w_ref[i])}"
+
+
+def test_full_close_calls_2bam(golden):
+    # output/full-check/2.bam: 2880 positions where exactly two checks failed, no 1-flag
+    data, of, sh = golden["2.bam"]
+    r = sh.check_full(0, sh.flat_size)
+    words = r["close_word"]
+    nnz = np.array([bin(int(w) & 0x7FFFF).count("1") + (((int(w) >> 20) & 0x3FF) > 0) for w in words])
+    assert (nnz == 2).sum() == 2880 and (nnz == 1).sum() == 0
+    first = [str(sb.Pos(*sh.pos_of(int(f)))) for f in r["close_flat"][:3]]
+    assert first == ["0:5649", "0:6273", "0:6893"]
+
+
+def test_full_checker_unit(golden):
+    # check/.../full/CheckerTest.scala
+    data, of, sh = golden["2.bam"]
+    p = sh.flat_of(439897, 52186)
+    r = sh.check_full(p, p + 1, want_words=True)
+    assert r["words"][0] == sb.FULL_SUCCESS | (10 << sb.FULL_N_SHIFT)
+    p = sh.flat_of(0, 5649)
+    r = sh.check_full(p, p + 1, want_words=True)
+    assert r["words"][0] == (1 << 12) | (1 << 15)
+
+
+def test_find_block_start(golden):
+    # FindBlockStartTest: FindBlockStart(2.bam, 26170, 5) == 50249
+    data, of, sh = golden["2.bam"]
+    assert sh.find_block_start(26170) == 50249
+    rng = np.random.default_rng(7)
+    for s in rng.integers(0, data.size - 1, 25).tolist() + [0, 1, data.size - 28, data.size - 30]:
+        rc, want = of.find_block_start(int(s))
+        if rc == OR_OK:
+            assert sh.find_block_start(int(s)) == want, s
+        else:
+            with pytest.raises(sb.SparkBamError):
+                sh.find_block_start(int(s))
+
+
+def test_find_record_start(golden):
+    # FindRecordStartTest: FindRecordStart(1.bam, 239479) == Pos(239479, 312)
+    data, of, sh = golden["1.bam"]
+    f, delta = sh.find_record_start(sh.flat_of(239479, 0))
+    assert sh.pos_of(f) == (239479, 312) and delta == 312
+
+
+@pytest.mark.parametrize("size,expected", [
+    (230 * 1024, ["0:45846-239479:312", "239479:312-484396:25", "484396:25-597482:0"]),
+    (240 * 1024, ["0:45846-263656:191", "263656:191-508565:287", "508565:287-597482:0"]),
+])
+def test_compute_splits_1bam(ctx, size, expected):
+    # ComputeSplitsTest "eager 230KB" / "compare 240KB"
+    splits, counts = sb.load_splits_and_reads(golden_bam("1.bam"), size, ctx=ctx)
+    assert [f"{a}-{b}" for a, b in splits] == expected
+    assert sum(counts) == 4917  # CountReadsTest
+
+
+@pytest.mark.parametrize("size,expected", [
+    (1000000, [2500]),
+    (100000, [503, 414, 518, 421, 493, 151]),
+    (20000, [96, 102, 105, 101, 99, 102, 101, 106, 0, 105, 105, 102, 104, 103, 104, 106,
+             104, 106, 0, 105, 195, 101, 0, 99, 98, 99, 52]),
+])
+def test_load_bam_partition_counts(ctx, size, expected):
+    # LoadBAMTest 1e6 / 1e5 / 2e4
+    _, counts = sb.load_splits_and_reads(golden_bam("2.bam"), size, ctx=ctx)
+    assert counts == expected
+
+
+def test_check_bam_summary(ctx):
+    # CheckBamTest "eager 1.bam": 1608257 positions, 4917 reads, All calls matched!
+    r = sb.check_bam(golden_bam("1.bam"), records=read_records("1.bam"), ctx=ctx)
+    assert r["positions"] == 1608257 and r["reads"] == 4917
+    assert r["false_positives"] == 0 and r["false_negatives"] == 0
+
+
+def test_run_shard_whole_file(golden):
+    data, of, sh = golden["1.bam"]
+    r = sh.run(0, data.size)
+    assert r["status"] == 0 and r["count"] == 4917 and r["n_true"] == 4917
+    assert sb.Pos.from_htsjdk(r["first_vpos"]) == (0, 45846)
+    sh.index(0)  # run() re-indexed: restore for other tests
+    sh.inflate()
+    sh.set_contigs(of.contig_len)
+
+
+# ------------------------------------------------------------- synthetic corpora
+SYN = [
+    ("short_l6", dict(seed=0x5B4D0001, shape=0, level=6), 30000),
+    ("short_l1", dict(seed=0x5B4D0002, shape=0, level=1), 20000),
+    ("short_l9", dict(seed=0x5B4D0003, shape=0, level=9), 20000),
+    ("short_l0", dict(seed=0x5B4D0004, shape=0, level=0), 8000),
+    ("long", dict(seed=0x5B4D004C, shape=1, level=6), 150),
+    ("adversarial", dict(seed=0x5B4D00AD, shape=2, level=-1), 30000),
+    ("adversarial_empty", dict(seed=0x5B4D00AE, shape=2, level=-1, empty_every=5), 30000),
+]
+
+
+@pytest.fixture(scope="module")
+def synth_files():
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tools"))
+    import synth
+    out = {}
+    for name, kw, nrec in SYN:
+        p = synth.params(kw["seed"], shape=kw["shape"], level=kw["level"],
+                         empty_every=kw.get("empty_every", 0))
+        data, _, _ = synth.make_bam(p, nrec)
+        out[name] = data
+    return out
+
+
+@pytest.mark.parametrize("name", [s[0] for s in SYN])
+def test_synthetic_inflate_and_eager(ctx, synth_files, name):
+    data = synth_files[name]
+    of = OracleFile(data)
+    sh = load(ctx, data, of.contig_len)
+    try:
+        # the GPU index covers every segment; the oracle stream from 0 stops at the
+        # first empty block: compare that prefix (later segments: see the next test)
+        got = sh.read_flat(0, of.flat_size)
+        i = first_diff(got, of.uncompressed())
+        assert i < 0, f"inflate differs at flat {i}"
+        n, bits = sh.check_eager(0, of.flat_size)
+        n_ref, bits_ref = of.eager_range(0, of.flat_size)
+        i = first_diff(np.unpackbits(bits, bitorder="little"), np.unpackbits(bits_ref, bitorder="little"))
+        assert i < 0 and n == n_ref, f"eager differs at {i} ({n} vs {n_ref})"
+        e = min(of.flat_size, 300000)
+        r = sh.check_full(0, e, want_words=True)
+        _, counts_ref, _, w_ref = of.full_range(0, e, want_words=True)
+        i = first_diff(r["words"], w_ref)
+        assert i < 0, f"full word differs at {i}: {hex(r['words'][i])} vs {hex(w_ref[i])}"
+    finally:
+        sh.close()
+
+
+def test_synthetic_empty_block_segments(ctx, synth_files):
+    # empty BGZF blocks end the stream (Stream.scala:56-58): a stream opened after the
+    # k-th empty block sees only that segment
+    data = synth_files["adversarial_empty"]
+    sh = load(ctx, data)
+    of0 = OracleFile(data)
+    sh.set_contigs(of0.contig_len)
+    blocks = sh.blocks()
+    empties = [i for i, b in enumerate(blocks) if b[5] & sb.BLOCK_EMPTY]
+    assert len(empties) >= 3
+    try:
+        for k in empties[:3]:
+            nxt = blocks[k + 1] if k + 1 < len(blocks) else None
+            if nxt is None or nxt[5] & sb.BLOCK_EMPTY:
+                continue
+            of = OracleFile(data, start=nxt[0])
+            base = nxt[3]
+            got = sh.read_flat(base, of.flat_size)
+            assert np.array_equal(got, of.uncompressed())
+            n, bits = sh.check_eager(base, base + of.flat_size)
+            # oracle stream positions are relative to its start block
+            cl = of0.contig_len
+            ref = np.zeros(of.flat_size, dtype=bool)
+            for p in range(of.flat_size):
+                ref[p] = of.eager(p, contig_len=cl)
+            assert np.array_equal(np.unpackbits(bits, bitorder="little")[:of.flat_size].astype(bool), ref)
+    finally:
+        sh.close()
+
+
+@pytest.mark.parametrize("name", ["short_l6", "long", "adversarial"])
+def test_synthetic_splits(ctx, synth_files, name):
+    data = synth_files[name]
+    of = OracleFile(data)
+    size = max(data.size // 7, 70000)
+    splits, counts = sb.load_splits_and_reads(data, size, ctx=ctx)
+    ref_counts, firsts = [], []
+    for s, e in file_splits(data.size, size):
+        rc, v, n = of.split(s, e)
+        assert rc == OR_OK
+        ref_counts.append(n)
+        if n:
+            firsts.append(v)
+    assert counts == ref_counts
+    assert [a.to_htsjdk() for a, _ in splits] == firsts
+
+
+def test_inflate_corrupt_matches_zlib(ctx, synth_files):
+    """Flip bytes inside deflate data: the per-block outcome (ok / size / data error)
+    must be what zlib (Inflater) reports for that block."""
+    data0 = synth_files["short_l1"]
+    of = OracleFile(data0)
+    L = olib()
+    import ctypes as C
+    rng = np.random.default_rng(3)
+    mism = []
+    for trial in range(40):
+        data = data0.copy()
+        b = of.blocks[int(rng.integers(0, len(of.blocks)))]
+        start, csize = b[0], b[1]
+        off = start + 18 + int(rng.integers(0, csize - 26))
+        data[off] ^= np.uint8(1 << int(rng.integers(0, 8)))
+        out = np.zeros(65536, dtype=np.uint8)
+        blk = (C.c_int64 * 3)()
+        rc_ref = L.or_stream_next(data.ctypes.data_as(C.c_void_p), data.size, start,
+                                  out.ctypes.data_as(C.c_void_p), blk)
+        sh = ctx.shard(data)
+        sh.index(0)
+        try:
+            sh.inflate()
+            rc = 0
+        except sb.SparkBamError as e:
+            rc = e.code
+        sh.close()
+        want = {0: 0, 1: 0, 4: 13, 5: 14, 6: 15}.get(rc_ref, -1)
+        if rc != want:
+            mism.append((trial, off, rc, rc_ref))
+    assert not mism, mism
+
+
+def test_shard_with_halo_matches_whole_file(ctx, synth_files):
+    """A byte-range shard (not at EOF) with a halo: eager bits of its owned blocks equal
+    the whole-file result; with no halo the call reports SBH_E_NEED_HALO."""
+    data = synth_files["short_l6"]
+    of = OracleFile(data)
+    whole = load(ctx, data, of.contig_len)
+    blocks = whole.blocks()
+    try:
+        k0, k1 = 10, 30
+        s0 = blocks[k0][0]
+        own_end = blocks[k1][0]
+        halo_end = blocks[k1 + 3][0]
+        sh = ctx.shard(data[s0:halo_end], file_offset=s0, file_size=data.size)
+        sh.index(s0)
+        sh.inflate()
+        sh.set_contigs(of.contig_len)
+        E = sh.flat_bound(own_end)
+        n, bits = sh.check_eager(0, E)
+        base = blocks[k0][3]
+        n2, bits2 = whole.check_eager(base, base + E)
+        assert n == n2 and np.array_equal(bits, bits2)
+        with pytest.raises(sb.SparkBamError) as e:
+            sh.check_eager(0, sh.flat_size)
+        assert e.value.code == 17
+        sh.close()
+    finally:
+        whole.close()
