@@ -194,6 +194,11 @@ typedef struct {
 int sbh_run_shard(sbh_shard *sh, uint64_t index_start, uint64_t own_end_file,
                   int32_t reads_to_check, int32_t max_read_size, sbh_shard_result *res);
 
+/* Device time (ms, HIP events on the context stream) of the stages of the last
+ * sbh_run_shard: [0] index, [1] inflate (k_inflate), [2] eager check (k_eager),
+ * [3] record split/count.  Returns the number of stages written (<= cap). */
+int sbh_stage_times(sbh_shard *sh, double *ms, int32_t cap);
+
 #ifdef __cplusplus
 }
 #endif

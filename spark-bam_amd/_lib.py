@@ -35,6 +35,7 @@ EXPORTS = [
     "sbh_get_blocks", "sbh_inflate", "sbh_read_flat", "sbh_flat_device_ptr", "sbh_flat_of",
     "sbh_pos_of", "sbh_flat_bound", "sbh_set_contigs", "sbh_check_eager", "sbh_check_full",
     "sbh_find_record_start", "sbh_count_records", "sbh_split", "sbh_run_shard",
+    "sbh_stage_times",
 ]
 
 
@@ -98,6 +99,8 @@ def lib():
         f = getattr(L, name)
         f.argtypes = args
         f.restype = C.c_int
+    L.sbh_stage_times.argtypes = [P, C.POINTER(C.c_double), I32]
+    L.sbh_stage_times.restype = C.c_int
     L.sbh_last_error.argtypes = [P]
     L.sbh_last_error.restype = C.c_char_p
     L.sbh_version.argtypes = []

@@ -106,6 +106,9 @@ struct sbh_shard {
   DBuf<unsigned long long> ctr;  // scratch counters
   unsigned long long *h_ctr = nullptr;  // pinned mirror
   uint64_t pad = 4096;
+  hipEvent_t ev[8] = {};
+  bool ev_ok = false, timing = false;
+  double stage_ms[4] = {0, 0, 0, 0};
 
   DevBlocks dev_blocks() {
     return DevBlocks{b_cstart.p, b_csize.p, b_hsize.p, b_usize.p, b_ustart.p, b_flags.p, b_status.p};
@@ -129,6 +132,16 @@ static int fail(sbh_ctx *ctx, int code, const char *fmt, ...) {
     hipError_t e_ = (x);                                                                            \
     if (e_ != hipSuccess) return fail((ctx), SBH_E_HIP, "%s: %s", #x, hipGetErrorString(e_));       \
   } while (0)
+
+static void mark(sbh_shard *sh, int i) {
+  if (!sh->timing) return;
+  if (!sh->ev_ok) {
+    sh->ev_ok = true;
+    for (hipEvent_t &e : sh->ev)
+      if (hipEventCreate(&e) != hipSuccess) sh->ev_ok = false;
+  }
+  if (sh->ev_ok) (void)hipEventRecord(sh->ev[i], sh->ctx->stream);
+}
 
 static int set_device(sbh_ctx *ctx) {
   HIPCHK(ctx, hipSetDevice(ctx->device));
@@ -208,8 +221,8 @@ int sbh_shard_create(sbh_ctx *ctx, const void *src, uint64_t n, uint64_t file_of
     e = hipMemcpyAsync(sh->comp.p, src, n, comp_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
                        ctx->stream);
   if (e == hipSuccess) e = hipMemsetAsync(sh->comp.p + n, 0, sh->pad, ctx->stream);
-  if (e == hipSuccess) e = sh->ctr.ensure(1024);
-  if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&sh->h_ctr), 1024 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = sh->ctr.ensure(4096);
+  if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&sh->h_ctr), 4096 * sizeof(unsigned long long));
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   if (e != hipSuccess) {
     sbh_shard_destroy(sh);
@@ -231,6 +244,8 @@ int sbh_shard_destroy(sbh_shard *sh) {
   sh->tmp.release(); sh->J0.release(); sh->J1.release(); sh->on.release(); sh->d_seg.release();
   sh->U.release(); sh->ctg.release(); sh->bits.release(); sh->words.release(); sh->close_pos.release();
   sh->close_word.release(); sh->ctr.release();
+  for (hipEvent_t &e : sh->ev)
+    if (e) (void)hipEventDestroy(e);
   if (sh->h_ctr) (void)hipHostFree(sh->h_ctr);
   delete sh;
   return SBH_OK;
@@ -383,7 +398,9 @@ int sbh_inflate(sbh_shard *sh, uint64_t *bad_block) {
   hipStream_t st = ctx->stream;
   HIPCHK(ctx, sh->U.ensure(sh->utotal + sh->pad));
   HIPCHK(ctx, hipMemsetAsync(sh->U.p + sh->utotal, 0, sh->pad, st));
+  mark(sh, 2);
   HIPCHK(ctx, launch_inflate(sh->comp.p, sh->dev_blocks(), sh->nblocks, sh->U.p, st));
+  mark(sh, 3);
   std::vector<uint32_t> status(sh->nblocks);
   if (sh->nblocks) HIPCHK(ctx, hipMemcpyAsync(status.data(), sh->b_status.p, sh->nblocks * 4, hipMemcpyDeviceToHost, st));
   HIPCHK(ctx, hipStreamSynchronize(st));
@@ -496,8 +513,10 @@ static int eager_range(sbh_shard *sh, uint64_t begin, uint64_t end, int32_t rtc,
   unsigned long long *c = sh->ctr.p;
   HIPCHK(ctx, hipMemsetAsync(c, 0, 16, st));
   HIPCHK(ctx, hipMemsetAsync(c + 2, 0xff, 8, st));
+  mark(sh, 4);
   HIPCHK(ctx, launch_eager(sh->U.p, sh->utotal + sh->pad, begin, end, sh->d_seg.p, (uint32_t)sh->seg_end.size(),
                            sh->open_last ? 1 : 0, sh->ctg.p, sh->nctg, rtc, sh->bits.p, c, st));
+  mark(sh, 5);
   HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr, c, 24, hipMemcpyDeviceToHost, st));
   HIPCHK(ctx, hipStreamSynchronize(st));
   sh->bits_valid = true;
@@ -737,12 +756,17 @@ int sbh_run_shard(sbh_shard *sh, uint64_t index_start, uint64_t own_end_file, in
   if (!sh || !res) return SBH_E_ARG;
   std::memset(res, 0, sizeof *res);
   sbh_ctx *ctx = sh->ctx;
+  (void)hipGetLastError();
+  sh->timing = true;
+  mark(sh, 0);
   int rc = sbh_index(sh, index_start, &res->n_blocks, nullptr);
+  mark(sh, 1);
   if (!rc) rc = sbh_inflate(sh, nullptr);
-  if (rc) return res->status = rc;
+  if (rc) { sh->timing = false; return res->status = rc; }
   uint64_t E = 0;
   (void)sbh_flat_bound(sh, own_end_file, &E);
-  if (!sh->at_eof && E == sh->utotal) return res->status = fail(ctx, SBH_E_NEED_HALO, "no halo past %llu", (unsigned long long)own_end_file);
+  if (!sh->at_eof && E == sh->utotal)
+    return res->status = fail(ctx, SBH_E_NEED_HALO, "no halo past %llu", (unsigned long long)own_end_file);
   uint64_t owned_blocks = 0, cbytes = 0;
   for (const sbh_block &b : sh->hb)
     if (b.start < own_end_file) { ++owned_blocks; cbytes += b.csize; }
@@ -750,22 +774,39 @@ int sbh_run_shard(sbh_shard *sh, uint64_t index_start, uint64_t own_end_file, in
   res->comp_bytes = cbytes;
   res->flat_bytes = E;
   rc = sbh_check_eager(sh, 0, E, rtc, nullptr, &res->n_true);
-  if (rc) return res->status = rc;
+  if (rc) { sh->timing = false; return res->status = rc; }
   uint64_t first = 0;
   int32_t delta = 0;
   rc = sbh_find_record_start(sh, 0, rtc, mrs, &first, &delta);
   if (rc == SBH_E_NO_READ_FOUND) {
     res->count = 0;
-    return res->status = SBH_OK;
+    rc = SBH_OK;
+  } else if (rc == SBH_OK) {
+    rc = count_records_impl(sh, first, E, &res->count, &res->anomalies);
+    uint64_t bp = 0;
+    uint32_t off = 0;
+    if (!rc && sbh_pos_of(sh, first, &bp, &off) == SBH_OK) res->first_vpos = (bp << 16) | off;
   }
-  if (rc) return res->status = rc;
-  rc = count_records_impl(sh, first, E, &res->count, &res->anomalies);
-  if (rc) return res->status = rc;
-  uint64_t bp = 0;
-  uint32_t off = 0;
-  if (sbh_pos_of(sh, first, &bp, &off) == SBH_OK) res->first_vpos = (bp << 16) | off;
+  mark(sh, 6);
+  sh->timing = false;
   res->exit_flat = E;
-  return res->status = SBH_OK;
+  if (sh->ev_ok) {
+    (void)hipEventSynchronize(sh->ev[6]);
+    const int from[4] = {0, 2, 4, 5}, to[4] = {1, 3, 5, 6};
+    for (int i = 0; i < 4; ++i) {
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, sh->ev[from[i]], sh->ev[to[i]]);
+      sh->stage_ms[i] = ms;
+    }
+  }
+  return res->status = rc;
+}
+
+int sbh_stage_times(sbh_shard *sh, double *ms, int32_t cap) {
+  if (!sh || !ms || cap < 0) return 0;
+  int n = cap < 4 ? cap : 4;
+  for (int i = 0; i < n; ++i) ms[i] = sh->stage_ms[i];
+  return n;
 }
 
 }  // extern "C"

@@ -1,5 +1,6 @@
 """Context / Shard: thin owners of the C-ABI handles (include/sparkbam.h)."""
 import ctypes as C
+import weakref
 
 import numpy as np
 
@@ -26,6 +27,7 @@ class Context:
             raise SparkBamError(rc, f"cannot create a context on device {device}")
         self.h = h
         self.device = device
+        self._shards = weakref.WeakSet()
         if stream is not None:
             _check(self.h, lib().sbh_ctx_set_stream(self.h, C.c_void_p(stream)))
 
@@ -33,9 +35,18 @@ class Context:
         _check(self.h, lib().sbh_ctx_synchronize(self.h))
 
     def close(self):
+        """Destroys every live shard first (a shard must not outlive its context)."""
         if self.h:
+            for sh in list(self._shards):
+                sh.close()
             lib().sbh_ctx_destroy(self.h)
             self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     def __enter__(self):
         return self
@@ -69,6 +80,7 @@ class Shard:
                                              1 if on_device else 0, C.byref(h)))
         self.h = h
         self._keep = None
+        ctx._shards.add(self)
         self.n_blocks = 0
         self.flat_size = 0
 
@@ -77,7 +89,8 @@ class Shard:
 
     def close(self):
         if self.h:
-            lib().sbh_shard_destroy(self.h)
+            if self.ctx.h:
+                lib().sbh_shard_destroy(self.h)
             self.h = None
 
     def __del__(self):
@@ -186,3 +199,9 @@ class Shard:
                                  max_read_size, C.byref(r))
         self._c(rc)
         return {f: getattr(r, f) for f, _ in SbhShardResult._fields_}
+
+    def stage_times(self):
+        """[index, inflate, eager, records] device ms of the last run() (HIP events)."""
+        ms = (C.c_double * 4)()
+        n = lib().sbh_stage_times(self.h, ms, 4)
+        return list(ms[:n])

@@ -68,3 +68,108 @@ def make_bam(p, n_records):
     if n < 0:
         raise RuntimeError("synth_bam failed")
     return out[:n], us.value, nb.value
+
+
+def header_bytes():
+    L = lib()
+    n = L.synth_header(None, 0)
+    out = np.empty(n, dtype=np.uint8)
+    L.synth_header(out.ctypes.data_as(C.c_void_p), n)
+    return out
+
+
+def records_size(p, a, b):
+    return lib().synth_records_size(C.byref(p), a, b)
+
+
+def records(p, a, b):
+    size = records_size(p, a, b)
+    out = np.empty(size, dtype=np.uint8)
+    n = lib().synth_records(C.byref(p), a, b, out.ctypes.data_as(C.c_void_p), size)
+    assert n == size
+    return out
+
+
+def bgzf(p, U, kbase, add_eof):
+    """BGZF-compress U (cut into p.payload blocks; levels by global block index)."""
+    cap = U.size + (U.size // 32768 + 4) * 128 + 1024
+    out = np.empty(cap, dtype=np.uint8)
+    nb = C.c_int64()
+    n = lib().synth_bgzf(C.byref(p), U.ctypes.data_as(C.c_void_p), U.size, kbase, int(add_eof),
+                         out.ctypes.data_as(C.c_void_p), cap, C.byref(nb))
+    if n < 0:
+        raise RuntimeError("synth_bgzf failed")
+    return out[:n], nb.value
+
+
+def block_sizes(comp):
+    """Compressed sizes of consecutive BGZF blocks (BSIZE + 1 of each header)."""
+    sizes, pos = [], 0
+    while pos + 18 <= comp.size:
+        cs = int(comp[pos + 16]) | (int(comp[pos + 17]) << 8)
+        sizes.append(cs + 1)
+        pos += cs + 1
+    return sizes
+
+
+class Segment:
+    """Rank `rank`'s byte-range shard of a synthetic BAM of world * records_per_rank
+    records (weak scaling: per-rank work fixed).
+
+    The global uncompressed stream is header + records; it is cut into BGZF blocks
+    of `payload` bytes (block k = U[k*P, (k+1)*P)), so records straddle block and
+    shard edges exactly as in a real file.  Rank i owns the blocks whose first byte
+    lies in its record range, K_i = ceil(U_i / P), and regenerates `halo_blocks`
+    blocks of rank i+1 (or the EOF block) as its halo.  Only the per-rank compressed
+    sizes must be exchanged to place the shard in the file (see set_offsets)."""
+
+    def __init__(self, p, records_per_rank, world, rank, halo_blocks=16):
+        if p.level < 0:
+            raise ValueError("segments need a uniform payload size (level >= 0)")
+        self.p, self.R, self.world, self.rank = p, records_per_rank, world, rank
+        P = p.payload
+        hdr = header_bytes()
+        h = hdr.size
+        # U offset of the first record of each rank (prefix of record sizes)
+        self.u_start = [0] * (world + 1)
+        acc = h
+        for i in range(world):
+            self.u_start[i] = h if i == 0 else acc
+            acc += records_size(p, i * records_per_rank, (i + 1) * records_per_rank)
+        self.u_start[0] = 0
+        self.u_total = acc
+        ceil = lambda x: (x + P - 1) // P  # noqa: E731
+        self.k = [ceil(self.u_start[i]) if i else 0 for i in range(world)] + [ceil(self.u_total)]
+        k0, k1 = self.k[rank], self.k[rank + 1]
+        k_halo = min(k1 + halo_blocks, self.k[world])
+        u0, u1 = k0 * P, min(k_halo * P, self.u_total)
+        # generate records covering [u0, u1)
+        first_rec = rank * records_per_rank
+        base = self.u_start[rank] if rank else 0
+        parts = [hdr] if rank == 0 else []
+        rec_end = first_rec
+        have = base + sum(x.size for x in parts)
+        total_recs = world * records_per_rank
+        step = max(1024, records_per_rank // 8)
+        while have < u1 and rec_end < total_recs:
+            nxt = min(total_recs, rec_end + (records_per_rank if rec_end == first_rec else step))
+            parts.append(records(p, rec_end, nxt))
+            have += parts[-1].size
+            rec_end = nxt
+        U = np.concatenate(parts) if len(parts) > 1 else parts[0]
+        U = U[u0 - base:u1 - base]
+        self.own_blocks = k1 - k0
+        comp, nb = bgzf(p, U, k0, add_eof=(k_halo == self.k[world]))
+        sizes = block_sizes(comp)
+        self.own_csize = sum(sizes[:self.own_blocks])
+        self.comp = comp
+        self.n_records_owned = None  # known only by the chain walk (GPU result)
+        self.file_offset = None
+        self.file_size = None
+
+    def set_offsets(self, own_csizes):
+        """own_csizes: every rank's owned compressed size (the setup allgather)."""
+        self.file_offset = sum(own_csizes[:self.rank])
+        self.own_end = self.file_offset + own_csizes[self.rank]
+        self.file_size = sum(own_csizes) + 28
+        return self
