@@ -202,6 +202,7 @@ def cpu_baseline(shard, comp, contig_len, budget_s, threads):
     from oracle_lib import Block, lib as olib  # the CPU oracle, timed as the baseline
 
     lib = olib()
+    shard.index(shard.file_offset)  # host copy of the block table
     blocks = shard.blocks()
     base = shard.file_offset
     arr = (Block * len(blocks))()

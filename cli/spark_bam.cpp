@@ -1,0 +1,634 @@
+// spark-bam CLI on MI355X: the reference's commands (cli/.../Main.scala:19-28) over the
+// C-ABI in include/sparkbam.h.  Host side in C++ (the reference's Scala/JVM toolchain
+// is not part of this build); all byte work runs in libsparkbam_hip.so on the GPU.
+//
+//   spark-bam compute-splits [-s] [-m SIZE] [-l N] BAM      (ComputeSplits.scala:18-156)
+//   spark-bam count-reads   [-s] [-m SIZE] BAM              (compare/CountReads.scala:21-213)
+//   spark-bam check-bam -s  [-m SIZE] [-i RANGES] [-r RECORDS] BAM  (check/eager/CheckBam.scala)
+//   spark-bam full-check    [-m SIZE] [-i RANGES] [-l N] BAM       (check/full/FullCheck.scala)
+//   spark-bam index-blocks  BAM [OUT]                        (bgzf/index/IndexBlocks.scala)
+//   spark-bam index-records BAM [OUT]                        (check/index/IndexRecords.scala)
+//
+// The hadoop-bam ("seqdoop", -u) comparisons are out of scope: hadoop-bam's
+// BAMSplitGuesser is a competitor's algorithm, not part of spark-bam's path.
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../include/sparkbam.h"
+
+namespace {
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+sbh_ctx *g_ctx = nullptr;
+
+void chk(int rc, const char *what) {
+  if (rc != SBH_OK) throw Error(rc, std::string(what) + ": " + sbh_last_error(g_ctx));
+}
+
+// hammerlab Bytes parser: integers or shorthands (k = 1024, "230k" = 235520)
+uint64_t parse_bytes(const std::string &s) {
+  size_t i = 0;
+  while (i < s.size() && (isdigit((unsigned char)s[i]) || s[i] == '.')) ++i;
+  double v = std::stod(s.substr(0, i));
+  std::string u = s.substr(i);
+  for (auto &c : u) c = (char)tolower(c);
+  if (!u.empty() && u.back() == 'b') u.pop_back();
+  double m = 1;
+  if (u == "k") m = 1024.0;
+  else if (u == "m") m = 1024.0 * 1024;
+  else if (u == "g") m = 1024.0 * 1024 * 1024;
+  else if (u == "t") m = 1024.0 * 1024 * 1024 * 1024;
+  else if (!u.empty()) throw Error(SBH_E_ARG, "bad byte size: " + s);
+  return (uint64_t)(v * m);
+}
+
+// ByteRanges (check/.../args/ByteRanges.scala, Range.scala): a-b | a+len | pos
+std::vector<std::pair<uint64_t, uint64_t>> parse_ranges(const std::string &s) {
+  std::vector<std::pair<uint64_t, uint64_t>> out;
+  size_t p = 0;
+  while (p <= s.size()) {
+    size_t q = s.find(',', p);
+    std::string t = s.substr(p, q == std::string::npos ? std::string::npos : q - p);
+    size_t d = t.find('-'), pl = t.find('+');
+    if (d != std::string::npos) out.push_back({parse_bytes(t.substr(0, d)), parse_bytes(t.substr(d + 1))});
+    else if (pl != std::string::npos) {
+      uint64_t a = parse_bytes(t.substr(0, pl));
+      out.push_back({a, a + parse_bytes(t.substr(pl + 1))});
+    } else {
+      uint64_t a = parse_bytes(t);
+      out.push_back({a, a + 1});
+    }
+    if (q == std::string::npos) break;
+    p = q + 1;
+  }
+  return out;
+}
+
+std::vector<uint8_t> read_file(const std::string &path) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) throw Error(SBH_E_ARG, "cannot open " + path);
+  return std::vector<uint8_t>((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+}
+
+struct Pos {
+  uint64_t block = 0;
+  uint32_t off = 0;
+  std::string str() const { return std::to_string(block) + ":" + std::to_string(off); }
+  double minus(const Pos &o, double ratio = 3.0) const {  // Pos.- (Pos.scala:17-22)
+    int64_t v = (int64_t)block - (int64_t)o.block + (int64_t)(((int64_t)off - (int64_t)o.off) / ratio);
+    return (double)std::max<int64_t>(0, v);
+  }
+};
+
+struct BamHeader {
+  std::vector<std::string> names;
+  std::vector<int32_t> lens;
+  uint64_t end = 0;
+};
+
+int32_t rd32(const uint8_t *p) { return (int32_t)((uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24); }
+
+// header.Header.apply (check/.../header/Header.scala:26-60)
+BamHeader parse_header(sbh_shard *sh, uint64_t flat_size) {
+  uint64_t n = std::min<uint64_t>(flat_size, 1 << 16);
+  for (;;) {
+    std::vector<uint8_t> b(n);
+    chk(sbh_read_flat(sh, 0, n, b.data()), "read header");
+    BamHeader h;
+    bool ok = n >= 12 && std::memcmp(b.data(), "BAM\1", 4) == 0;
+    if (!ok) throw Error(SBH_E_ARG, "not a BAM file");
+    uint64_t c = 8 + (uint64_t)rd32(&b[4]);
+    bool done = false;
+    if (c + 4 <= n) {
+      int32_t nref = rd32(&b[c]);
+      c += 4;
+      done = true;
+      for (int32_t i = 0; i < nref; ++i) {
+        if (c + 4 > n) { done = false; break; }
+        int32_t l = rd32(&b[c]);
+        if (c + 8 + (uint64_t)l > n) { done = false; break; }
+        h.names.emplace_back((const char *)&b[c + 4], strnlen((const char *)&b[c + 4], l));
+        h.lens.push_back(rd32(&b[c + 4 + l]));
+        c += 8 + l;
+      }
+    }
+    if (done) { h.end = c; return h; }
+    if (n >= flat_size) throw Error(SBH_E_TRUNCATED, "truncated BAM header");
+    n = std::min<uint64_t>(flat_size, n * 4);
+  }
+}
+
+struct Loaded {
+  std::vector<uint8_t> data;
+  sbh_shard *sh = nullptr;
+  uint64_t nblocks = 0, flat = 0;
+  BamHeader hdr;
+  std::vector<sbh_block> blocks;
+  explicit Loaded(const std::string &path) : data(read_file(path)) {
+    chk(sbh_shard_create(g_ctx, data.data(), data.size(), 0, data.size(), 0, &sh), "shard");
+    chk(sbh_index(sh, 0, &nblocks, &flat), "index");
+    chk(sbh_inflate(sh, nullptr), "inflate");
+    hdr = parse_header(sh, flat);
+    chk(sbh_set_contigs(sh, hdr.lens.data(), (int32_t)hdr.lens.size()), "contigs");
+    blocks.resize(nblocks);
+    if (nblocks) chk(sbh_get_blocks(sh, 0, nblocks, blocks.data()), "blocks");
+  }
+  ~Loaded() { sbh_shard_destroy(sh); }
+  Pos pos(uint64_t flat_pos) const {
+    Pos p;
+    chk(sbh_pos_of(sh, flat_pos, &p.block, &p.off), "pos");
+    return p;
+  }
+};
+
+std::vector<std::pair<uint64_t, uint64_t>> file_splits(uint64_t size, uint64_t split) {
+  std::vector<std::pair<uint64_t, uint64_t>> out;
+  uint64_t rem = size;
+  while ((double)rem / (double)split > 1.1) {
+    out.push_back({size - rem, size - rem + split});
+    rem -= split;
+  }
+  if (rem) out.push_back({size - rem, size});
+  return out;
+}
+
+// hammerlab stats number rendering (as in the reference's golden outputs)
+std::string num(double v) {
+  char b[64];
+  if (std::fabs(v) >= 1e5) {
+    snprintf(b, sizeof b, "%.1e", v);
+    std::string s(b);
+    size_t e = s.find('e');
+    std::string mant = s.substr(0, e), ex = s.substr(e + 1);
+    int x = std::stoi(ex);
+    return mant + "e" + std::to_string(x);
+  }
+  if (std::fabs(v - std::round(v)) < 1e-9 || std::fabs(v) >= 100) {
+    snprintf(b, sizeof b, "%.0f", v);
+    return b;
+  }
+  snprintf(b, sizeof b, "%.1f", v);
+  return b;
+}
+
+std::string stats_lines(const std::vector<double> &xs) {
+  std::string out;
+  size_t n = xs.size();
+  if (!n) return "(empty)\n";
+  double mean = 0;
+  for (double x : xs) mean += x;
+  mean /= n;
+  double var = 0;
+  for (double x : xs) var += (x - mean) * (x - mean);
+  double sd = std::sqrt(var / n);
+  auto median = [](std::vector<double> v) {
+    std::sort(v.begin(), v.end());
+    size_t m = v.size();
+    return m % 2 ? v[m / 2] : (v[m / 2 - 1] + v[m / 2]) / 2;
+  };
+  double med = median(xs);
+  std::vector<double> dev;
+  for (double x : xs) dev.push_back(std::fabs(x - med));
+  double mad = median(dev);
+  out += "N: " + std::to_string(n) + ", μ/σ: " + num(mean) + "/" + num(sd) + ", med/mad: " + num(med) + "/" + num(mad) + "\n";
+  std::string el = " elems:", so = "sorted:";
+  std::vector<double> s = xs;
+  std::sort(s.begin(), s.end());
+  for (double x : xs) el += " " + num(x);
+  for (double x : s) so += " " + num(x);
+  out += el + "\n" + so + "\n";
+  return out;
+}
+
+// hammerlab Bytes.format: 583K, 25.6K, 1.2M ...
+std::string bytes_fmt(uint64_t b) {
+  const char *u[] = {"B", "K", "M", "G", "T"};
+  double v = (double)b;
+  int i = 0;
+  while (v >= 1024 && i < 4) { v /= 1024; ++i; }
+  char buf[64];
+  if (i == 0) snprintf(buf, sizeof buf, "%lluB", (unsigned long long)b);
+  else if (v >= 100) snprintf(buf, sizeof buf, "%.0f%s", std::floor(v + 0.5 - 1e-9), u[i]);
+  else snprintf(buf, sizeof buf, "%.1f%s", v, u[i]);
+  return buf;
+}
+
+struct Args {
+  std::string cmd, path, out, records;
+  uint64_t split = 0;
+  bool has_split = false, s = false, u = false;
+  long limit = 1000000;
+  std::vector<std::pair<uint64_t, uint64_t>> ranges;
+  bool has_ranges = false;
+  int reads_to_check = 10, max_read_size = 100000000, blocks_to_check = 5;
+};
+
+Args parse(int argc, char **argv) {
+  Args a;
+  if (argc < 2) throw Error(SBH_E_ARG, "usage: spark-bam <command> [options] <bam>");
+  a.cmd = argv[1];
+  std::vector<std::string> pos;
+  for (int i = 2; i < argc; ++i) {
+    std::string t = argv[i];
+    auto next = [&]() -> std::string {
+      if (i + 1 >= argc) throw Error(SBH_E_ARG, "missing value for " + t);
+      return argv[++i];
+    };
+    if (t == "-m" || t == "--max-split-size") { a.split = parse_bytes(next()); a.has_split = true; }
+    else if (t == "-s" || t == "--spark-bam") a.s = true;
+    else if (t == "-u" || t == "--upstream" || t == "--hadoop-bam") a.u = true;
+    else if (t == "-l" || t == "--print-limit") a.limit = std::stol(next());
+    else if (t == "-i" || t == "--intervals") { a.ranges = parse_ranges(next()); a.has_ranges = true; }
+    else if (t == "-r" || t == "--records-path") a.records = next();
+    else if (t == "--reads-to-check") a.reads_to_check = std::stoi(next());
+    else if (t == "--max-read-size") a.max_read_size = std::stoi(next());
+    else if (t == "-z" || t == "--bgzf-blocks-to-check") a.blocks_to_check = std::stoi(next());
+    else if (t == "-w" || t == "--warn") {}
+    else pos.push_back(t);
+  }
+  if (pos.empty()) throw Error(SBH_E_ARG, "missing BAM path");
+  a.path = pos[0];
+  if (pos.size() > 1) a.out = pos[1];
+  return a;
+}
+
+void no_hadoop_bam() {
+  throw Error(SBH_E_ARG, "hadoop-bam (seqdoop) comparison is not part of the MI355X build; use -s");
+}
+
+struct SplitsResult {
+  std::vector<std::pair<Pos, Pos>> splits;
+  std::vector<uint64_t> counts;
+};
+
+// CanLoadBam.loadSplitsAndReads (load/.../CanLoadBam.scala:268-302)
+SplitsResult spark_bam_splits(Loaded &L, const Args &a, uint64_t split_size) {
+  uint64_t n_true = 0;
+  chk(sbh_check_eager(L.sh, 0, L.flat, a.reads_to_check, nullptr, &n_true), "eager");
+  SplitsResult r;
+  std::vector<Pos> firsts;
+  for (auto &sp : file_splits(L.data.size(), split_size)) {
+    uint64_t v = 0, n = 0;
+    chk(sbh_split(L.sh, sp.first, sp.second, a.blocks_to_check, a.reads_to_check, a.max_read_size, &v, &n), "split");
+    r.counts.push_back(n);
+    if (n) firsts.push_back(Pos{v >> 16, (uint32_t)(v & 0xffff)});
+  }
+  for (size_t i = 0; i < firsts.size(); ++i)
+    r.splits.push_back({firsts[i], i + 1 < firsts.size() ? firsts[i + 1] : Pos{L.data.size(), 0}});
+  return r;
+}
+
+uint64_t default_split(const Args &a) { return a.has_split ? a.split : 32ull << 20; }
+
+int compute_splits(const Args &a) {
+  if (a.u && !a.s) no_hadoop_bam();
+  auto t0 = std::chrono::steady_clock::now();
+  Loaded L(a.path);
+  SplitsResult r = spark_bam_splits(L, a, default_split(a));
+  long ms = (long)std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
+  printf("Get spark-bam splits: %ldms\n\n", ms);
+  std::vector<double> lens;
+  for (auto &s : r.splits) lens.push_back((double)(int64_t)s.second.minus(s.first));
+  printf("Split-size distribution:\n%s\n", stats_lines(lens).c_str());
+  size_t n = r.splits.size();
+  if ((long)n <= a.limit) printf("%zu splits:\n", n);
+  else printf("First %ld of %zu splits:\n", a.limit, n);
+  for (size_t i = 0; i < n && (long)i < a.limit; ++i)
+    printf("\t%s-%s\n", r.splits[i].first.str().c_str(), r.splits[i].second.str().c_str());
+  if ((long)n > a.limit) printf("\t…\n");
+  printf("\n");
+  return 0;
+}
+
+int count_reads(const Args &a) {
+  auto t0 = std::chrono::steady_clock::now();
+  Loaded L(a.path);
+  SplitsResult r = spark_bam_splits(L, a, default_split(a));
+  uint64_t total = 0;
+  for (uint64_t c : r.counts) total += c;
+  long ms = (long)std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
+  printf("spark-bam read-count time: %ld\n\n", ms);
+  printf("spark-bam found %llu reads, hadoop-bam threw exception:\n", (unsigned long long)total);
+  printf("\thadoop-bam is not part of the MI355X build\n");
+  return 0;
+}
+
+// Blocks.apply `-i` filter: blocks whose start is in the ranges (Blocks.scala:89-96)
+std::vector<std::pair<uint64_t, uint64_t>> selected(const Loaded &L, const Args &a, uint64_t *comp) {
+  std::vector<std::pair<uint64_t, uint64_t>> fr;
+  *comp = 0;
+  for (const sbh_block &b : L.blocks) {
+    if (b.flags & SBH_BLOCK_EMPTY || b.usize == 0) continue;
+    if (a.has_ranges) {
+      bool in = false;
+      for (auto &r : a.ranges) in |= r.first <= b.start && b.start < r.second;
+      if (!in) continue;
+    }
+    *comp += b.csize;
+    if (!fr.empty() && fr.back().second == b.ustart) fr.back().second = b.ustart + b.usize;
+    else fr.push_back({b.ustart, b.ustart + b.usize});
+  }
+  return fr;
+}
+
+std::vector<Pos> read_records_file(const std::string &p) {
+  std::ifstream f(p);
+  if (!f) throw Error(SBH_E_ARG, "no records file " + p + " (run index-records first)");
+  std::vector<Pos> out;
+  std::string line;
+  while (std::getline(f, line)) {
+    size_t c = line.find(',');
+    if (c == std::string::npos) continue;
+    out.push_back(Pos{std::stoull(line.substr(0, c)), (uint32_t)std::stoul(line.substr(c + 1))});
+  }
+  return out;
+}
+
+std::vector<uint64_t> bits_to_positions(const std::vector<uint8_t> &bits, uint64_t base, uint64_t n) {
+  std::vector<uint64_t> out;
+  for (uint64_t i = 0; i < n; ++i)
+    if (bits[i >> 3] & (1u << (i & 7))) out.push_back(base + i);
+  return out;
+}
+
+int check_bam(const Args &a) {
+  if (!a.s) no_hadoop_bam();
+  Loaded L(a.path);
+  std::vector<Pos> recs = read_records_file(a.records.empty() ? a.path + ".records" : a.records);
+  std::vector<uint64_t> truth;
+  for (auto &r : recs) {
+    uint64_t f = 0;
+    chk(sbh_flat_of(L.sh, r.block, r.off, &f), "records file position");
+    truth.push_back(f);
+  }
+  std::sort(truth.begin(), truth.end());
+  uint64_t comp = 0;
+  auto fr = selected(L, a, &comp);
+  uint64_t tp = 0, fp = 0, fn = 0, positions = 0;
+  std::vector<uint64_t> fps, fns;
+  for (auto &r : fr) {
+    std::vector<uint8_t> bits((r.second - r.first + 7) / 8);
+    uint64_t n = 0;
+    chk(sbh_check_eager(L.sh, r.first, r.second, a.reads_to_check, bits.data(), &n), "eager");
+    auto called = bits_to_positions(bits, r.first, r.second - r.first);
+    auto lo = std::lower_bound(truth.begin(), truth.end(), r.first);
+    auto hi = std::lower_bound(truth.begin(), truth.end(), r.second);
+    std::vector<uint64_t> t(lo, hi), both;
+    std::set_intersection(called.begin(), called.end(), t.begin(), t.end(), std::back_inserter(both));
+    std::set_difference(called.begin(), called.end(), t.begin(), t.end(), std::back_inserter(fps));
+    std::set_difference(t.begin(), t.end(), called.begin(), called.end(), std::back_inserter(fns));
+    tp += both.size();
+    positions += r.second - r.first;
+  }
+  fp = fps.size();
+  fn = fns.size();
+  printf("%llu uncompressed positions\n%s compressed\nCompression ratio: %.2f\n%llu reads\n",
+         (unsigned long long)positions, bytes_fmt(comp).c_str(), (double)positions / (double)comp,
+         (unsigned long long)(tp + fn));
+  if (!fp && !fn) {
+    printf("All calls matched!\n");
+    return 0;
+  }
+  printf("%llu false positives, %llu false negatives\n\n", (unsigned long long)fp, (unsigned long long)fn);
+  if (fp) {
+    printf("False positives:\n");
+    for (size_t i = 0; i < fps.size() && (long)i < a.limit; ++i) printf("\t%s\n", L.pos(fps[i]).str().c_str());
+  }
+  if (fn) {
+    printf("%llu false negatives:\n", (unsigned long long)fn);
+    for (size_t i = 0; i < fns.size() && (long)i < a.limit; ++i) printf("\t%s\n", L.pos(fns[i]).str().c_str());
+  }
+  return 0;
+}
+
+const char *FLAG_NAMES[19] = {
+    "tooFewFixedBlockBytes", "negativeReadIdx", "tooLargeReadIdx", "negativeReadPos", "tooLargeReadPos",
+    "negativeNextReadIdx", "tooLargeNextReadIdx", "negativeNextReadPos", "tooLargeNextReadPos",
+    "tooFewBytesForReadName", "nonNullTerminatedReadName", "nonASCIIReadName", "noReadName", "emptyReadName",
+    "tooFewBytesForCigarOps", "invalidCigarOp", "emptyMappedCigar", "emptyMappedSeq",
+    "tooFewRemainingBytesImplied"};
+
+std::string flags_str(uint32_t w) {
+  std::string s;
+  for (int i = 0; i < 19; ++i)
+    if (w & (1u << i)) s += (s.empty() ? "" : ",") + std::string(FLAG_NAMES[i]);
+  return s;
+}
+
+// PosMetadata show (check/.../PosMetadata.scala:20-53) with htsjdk SAMRecord.toString
+std::string pos_metadata(Loaded &L, const Args &a, uint64_t flat, uint32_t word) {
+  std::string rec = "no next record";
+  uint64_t nxt = 0;
+  int32_t delta = 0;
+  if (sbh_find_record_start(L.sh, flat, a.reads_to_check, a.max_read_size, &nxt, &delta) == SBH_OK &&
+      nxt + 36 <= L.flat) {
+    uint8_t f[36];
+    chk(sbh_read_flat(L.sh, nxt, 36, f), "read record");
+    int32_t ref = rd32(f + 4), pos = rd32(f + 8);
+    uint32_t rnl = (uint32_t)rd32(f + 12) & 0xff;
+    uint32_t flag = (uint32_t)rd32(f + 16) >> 16;
+    int32_t lseq = rd32(f + 20);
+    std::vector<uint8_t> name(rnl ? rnl : 1, 0);
+    if (rnl) chk(sbh_read_flat(L.sh, nxt + 36, rnl, name.data()), "read name");
+    std::string s = std::to_string(delta) + " before " + std::string((const char *)name.data(), strnlen((const char *)name.data(), rnl));
+    if (flag & 1) s += (flag & 0x40) ? " 1/2" : " 2/2";
+    s += " " + std::to_string(lseq) + "b";
+    const bool unmapped = flag & 4;
+    s += unmapped ? " unmapped read" : " aligned read";
+    auto where = [&]() { return L.hdr.names[ref] + ":" + std::to_string(pos + 1); };
+    if (unmapped && pos + 1 >= 0 && ref >= 0 && ref < (int32_t)L.hdr.names.size()) s += " (placed at " + where() + ")";
+    else if (!unmapped && ref >= 0 && ref < (int32_t)L.hdr.names.size()) s += " @ " + where();
+    rec = s;
+  }
+  return L.pos(flat).str() + ":\t" + rec + ". Failing checks: " + flags_str(word & SBH_FULL_FLAGS_MASK);
+}
+
+std::vector<std::string> counts_lines(const std::vector<uint64_t> &c, const std::map<uint32_t, uint64_t> &rbe,
+                                      bool include_zeros, bool hide_first) {
+  std::vector<std::pair<std::string, uint64_t>> kv;
+  for (int i = 0; i < 19; ++i) kv.push_back({FLAG_NAMES[i], c[i]});
+  std::stable_sort(kv.begin(), kv.end(), [](auto &x, auto &y) { return x.second > y.second; });
+  std::vector<std::pair<std::string, std::string>> pairs;
+  for (auto &p : kv) {
+    if ((p.second > 0 || include_zeros) && (p.first != "tooFewFixedBlockBytes" || !hide_first))
+      pairs.push_back({p.first, std::to_string(p.second)});
+  }
+  if (!rbe.empty()) {
+    std::string v;
+    for (auto &r : rbe) v += (v.empty() ? "" : " ") + std::to_string(r.first) + "ⅹ" + std::to_string(r.second);
+    pairs.push_back({"readsBeforeError", v});
+  }
+  size_t mk = 0, mv = 0;
+  for (auto &p : pairs) { mk = std::max(mk, p.first.size()); mv = std::max(mv, p.second.size()); }
+  std::vector<std::string> out;
+  for (auto &p : pairs)
+    out.push_back(std::string(mk - p.first.size(), ' ') + p.first + ":\t" + std::string(mv - p.second.size(), ' ') + p.second);
+  return out;
+}
+
+int full_check(const Args &a) {
+  Loaded L(a.path);
+  uint64_t comp = 0;
+  auto fr = selected(L, a, &comp);
+  std::vector<uint64_t> counts(21 * 19, 0), rbe(21 * 64, 0);
+  std::vector<std::pair<uint64_t, uint32_t>> close;
+  uint64_t positions = 0;
+  const uint64_t cap = 1 << 22;
+  std::vector<uint64_t> cf(cap);
+  std::vector<uint32_t> cw(cap);
+  for (auto &r : fr) {
+    std::vector<uint64_t> c(21 * 19), rb(21 * 64);
+    uint64_t ns = 0, nclose = 0;
+    chk(sbh_check_full(L.sh, r.first, r.second, a.reads_to_check, nullptr, c.data(), rb.data(), &ns, cf.data(),
+                       cw.data(), cap, &nclose),
+        "full");
+    for (int i = 0; i < 21 * 19; ++i) counts[i] += c[i];
+    for (int i = 0; i < 21 * 64; ++i) rbe[i] += rb[i];
+    for (uint64_t i = 0; i < std::min(nclose, cap); ++i) close.push_back({cf[i], cw[i]});
+    positions += r.second - r.first;
+  }
+  // records file, if present: the indexed comparison summary first (FullCheck.scala:94-106)
+  std::string rp = a.records.empty() ? a.path + ".records" : a.records;
+  if (std::ifstream(rp)) {
+    Args e = a;
+    e.s = true;
+    e.records = rp;
+    check_bam(e);
+    printf("\n");
+  }
+  auto nnz_of = [](uint32_t w) { return __builtin_popcount(w & SBH_FULL_FLAGS_MASK) + (((w >> SBH_FULL_N_SHIFT) & 0x3FF) > 0); };
+  auto per = [&](int k) {
+    std::vector<uint64_t> c(19);
+    for (int i = 0; i < 19; ++i) c[i] = counts[k * 19 + i];
+    std::map<uint32_t, uint64_t> r;
+    for (int j = 1; j < 64; ++j)
+      if (rbe[k * 64 + j]) r[j] = rbe[k * 64 + j];
+    return std::make_pair(c, r);
+  };
+  std::vector<std::pair<uint64_t, uint32_t>> ones, twos;
+  for (auto &c : close) (nnz_of(c.second) == 1 ? ones : twos).push_back(c);
+  if (ones.empty()) {
+    printf("No positions where only one check failed\n");
+  } else {
+    auto pc = per(1);
+    printf("Critical error counts (true negatives where only one check failed):\n");
+    for (auto &l : counts_lines(pc.first, pc.second, false, false)) printf("\t%s\n", l.c_str());
+    printf("\n");
+    if ((long)ones.size() <= a.limit) printf("%zu critical positions:\n", ones.size());
+    else printf("%ld of %zu critical positions:\n", a.limit, ones.size());
+    for (size_t i = 0; i < ones.size() && (long)i < a.limit; ++i)
+      printf("\t%s\n", pos_metadata(L, a, ones[i].first, ones[i].second).c_str());
+    if ((long)ones.size() > a.limit) printf("\t…\n");
+  }
+  printf("\n");
+  if (twos.empty()) {
+    printf("No positions where exactly two checks failed\n\n");
+  } else {
+    if ((long)twos.size() <= a.limit) printf("%zu positions where exactly two checks failed:\n", twos.size());
+    else printf("%ld of %zu positions where exactly two checks failed:\n", a.limit, twos.size());
+    for (size_t i = 0; i < twos.size() && (long)i < a.limit; ++i)
+      printf("\t%s\n", pos_metadata(L, a, twos[i].first, twos[i].second).c_str());
+    if ((long)twos.size() > a.limit) printf("\t…\n");
+    printf("\n");
+    std::map<uint32_t, uint64_t> hist;
+    for (auto &t : twos) hist[t.second & SBH_FULL_FLAGS_MASK]++;
+    std::vector<std::pair<uint64_t, uint32_t>> h;
+    for (auto &x : hist) h.push_back({x.second, x.first});
+    std::stable_sort(h.begin(), h.end(), [](auto &x, auto &y) { return x.first > y.first; });
+    if (h.front().first > 1) {
+      printf("\tHistogram:\n");
+      for (size_t i = 0; i < h.size() && (long)i < a.limit; ++i)
+        printf("\t\t%llu:\t%s\n", (unsigned long long)h[i].first, flags_str(h[i].second).c_str());
+      printf("\n");
+    }
+    auto pc = per(2);
+    printf("\tPer-flag totals:\n");
+    for (auto &l : counts_lines(pc.first, pc.second, false, false)) printf("\t\t%s\n", l.c_str());
+    printf("\n");
+  }
+  std::vector<uint64_t> tot(19, 0);
+  std::map<uint32_t, uint64_t> trbe;
+  for (int k = 0; k < 21; ++k) {
+    for (int i = 0; i < 19; ++i) tot[i] += counts[k * 19 + i];
+    for (int j = 1; j < 64; ++j)
+      if (rbe[k * 64 + j]) trbe[j] += rbe[k * 64 + j];
+  }
+  printf("Total error counts:\n");
+  for (auto &l : counts_lines(tot, trbe, true, true)) printf("\t%s\n", l.c_str());
+  printf("\n");
+  return 0;
+}
+
+int index_blocks(const Args &a) {
+  Loaded L(a.path);
+  std::string out = a.out.empty() ? a.path + ".blocks" : a.out;
+  FILE *f = fopen(out.c_str(), "w");
+  if (!f) throw Error(SBH_E_ARG, "cannot write " + out);
+  for (const sbh_block &b : L.blocks) {
+    if (b.flags & SBH_BLOCK_EMPTY) break;  // MetadataStream ends at the first empty block
+    fprintf(f, "%llu,%u,%u\n", (unsigned long long)b.start, b.csize, b.usize);
+  }
+  fclose(f);
+  return 0;
+}
+
+int index_records(const Args &a) {
+  Loaded L(a.path);
+  uint64_t seg_end = L.flat;
+  for (const sbh_block &b : L.blocks)
+    if (b.flags & SBH_BLOCK_EMPTY) { seg_end = b.ustart; break; }
+  std::vector<uint8_t> bits((seg_end - L.hdr.end + 7) / 8);
+  uint64_t n = 0, chain = 0;
+  chk(sbh_check_eager(L.sh, L.hdr.end, seg_end, a.reads_to_check, bits.data(), &n), "eager");
+  chk(sbh_count_records(L.sh, L.hdr.end, seg_end, &chain), "records");
+  if (chain != n) throw Error(SBH_E_STATE, "record chain and eager calls disagree; refusing to write .records");
+  std::string out = a.out.empty() ? a.path + ".records" : a.out;
+  FILE *f = fopen(out.c_str(), "w");
+  if (!f) throw Error(SBH_E_ARG, "cannot write " + out);
+  for (uint64_t p : bits_to_positions(bits, L.hdr.end, seg_end - L.hdr.end)) {
+    Pos q = L.pos(p);
+    fprintf(f, "%llu,%u\n", (unsigned long long)q.block, q.off);
+  }
+  fclose(f);
+  return 0;
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+  try {
+    Args a = parse(argc, argv);
+    chk(sbh_ctx_create(0, &g_ctx), "context");
+    int rc;
+    if (a.cmd == "compute-splits") rc = compute_splits(a);
+    else if (a.cmd == "count-reads") rc = count_reads(a);
+    else if (a.cmd == "check-bam") rc = check_bam(a);
+    else if (a.cmd == "full-check") rc = full_check(a);
+    else if (a.cmd == "index-blocks") rc = index_blocks(a);
+    else if (a.cmd == "index-records") rc = index_records(a);
+    else throw Error(SBH_E_ARG, "unknown command " + a.cmd);
+    sbh_ctx_destroy(g_ctx);
+    return rc;
+  } catch (const Error &e) {
+    fprintf(stderr, "spark-bam: %s\n", e.what());
+    if (g_ctx) sbh_ctx_destroy(g_ctx);
+    return 1;
+  } catch (const std::exception &e) {
+    fprintf(stderr, "spark-bam: %s\n", e.what());
+    return 1;
+  }
+}
