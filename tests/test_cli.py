@@ -1,0 +1,74 @@
+"""CLI parity: `spark-bam <cmd>` output vs the reference's golden CLI outputs
+(cli/src/test/resources/output/**, ComputeSplitsTest, CheckBamTest, FullCheckTest)."""
+import os
+import subprocess
+
+import pytest
+
+from conftest import BAMS, GOLDEN, ROOT
+
+pytestmark = pytest.mark.gpu
+CLI = os.path.join(ROOT, "cli", "spark-bam")
+
+
+def run(*args):
+    r = subprocess.run([CLI, *args], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    return r.stdout
+
+
+def test_compute_splits_230k():
+    # ComputeSplitsTest "eager 230KB"
+    out = run("compute-splits", "-s", "-m", "230k", os.path.join(BAMS, "1.bam")).splitlines()
+    assert out[0].startswith("Get spark-bam splits: ") and out[0].endswith("ms")
+    assert out[1:] == [
+        "", "Split-size distribution:", "N: 3, μ/σ: 1.9e5/57877, med/mad: 2.2e5/20521",
+        " elems: 224301 244822 113078", "sorted: 113078 224301 244822", "", "3 splits:",
+        "\t0:45846-239479:312", "\t239479:312-484396:25", "\t484396:25-597482:0", ""]
+
+
+def test_compute_splits_240k():
+    # ComputeSplitsTest "compare 240KB" (the spark-bam half)
+    out = run("compute-splits", "-s", "-m", "240k", os.path.join(BAMS, "1.bam")).splitlines()
+    assert out[2:] == [
+        "Split-size distribution:", "N: 3, μ/σ: 1.9e5/74433, med/mad: 2.4e5/3497",
+        " elems: 248438 244941 88822", "sorted: 88822 244941 248438", "", "3 splits:",
+        "\t0:45846-263656:191", "\t263656:191-508565:287", "\t508565:287-597482:0", ""]
+
+
+def test_check_bam_eager_1bam():
+    # CheckBamTest "eager 1.bam"
+    out = run("check-bam", "-s", "-m", "200k", os.path.join(BAMS, "1.bam"))
+    assert out == ("1608257 uncompressed positions\n583K compressed\nCompression ratio: 2.69\n"
+                   "4917 reads\nAll calls matched!\n")
+
+
+@pytest.mark.parametrize("golden,args", [
+    ("2.bam", ["2.bam"]),
+    ("2.bam.first", ["-i", "0", "2.bam"]),
+    ("2.bam.second", ["-i", "26169", "2.bam"]),
+    ("2.bam.200k", ["-i", "0-200k", "-m", "100k", "2.bam"]),
+    ("1.bam", ["-m", "200k", "1.bam"]),
+])
+def test_full_check_outputs(golden, args):
+    # FullCheckTest: whole output files (with -l 10, as the reference test passes)
+    args = args[:-1] + [os.path.join(BAMS, args[-1])]
+    out = run("full-check", "-l", "10", *args)
+    with open(os.path.join(GOLDEN, "output", "full-check", golden), encoding="utf-8") as f:
+        want = f.read()
+    assert out.splitlines() == want.splitlines()
+
+
+def test_count_reads_1bam():
+    out = run("count-reads", "-m", "100k", os.path.join(BAMS, "1.bam"))
+    assert "spark-bam found 4917 reads" in out
+
+
+def test_index_blocks_and_records(tmp_path):
+    # IndexBlocksTest / IndexRecordsTest: byte-exact .blocks / .records
+    for name in ("2.bam", "1.bam"):
+        ob, orc = tmp_path / (name + ".blocks"), tmp_path / (name + ".records")
+        run("index-blocks", os.path.join(BAMS, name), str(ob))
+        run("index-records", os.path.join(BAMS, name), str(orc))
+        assert ob.read_text() == open(os.path.join(BAMS, name + ".blocks")).read()
+        assert orc.read_text() == open(os.path.join(BAMS, name + ".records")).read()
