@@ -208,8 +208,8 @@ std::string stats_lines(const std::vector<double> &xs) {
   std::string el = " elems:", so = "sorted:";
   std::vector<double> s = xs;
   std::sort(s.begin(), s.end());
-  for (double x : xs) el += " " + num(x);
-  for (double x : s) so += " " + num(x);
+  for (double x : xs) el += " " + std::to_string((long long)x);
+  for (double x : s) so += " " + std::to_string((long long)x);
   out += el + "\n" + so + "\n";
   return out;
 }

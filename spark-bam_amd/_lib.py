@@ -8,7 +8,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libsparkbam_hip.so")
+LIB_PATH = os.environ.get("SBH_LIB_PATH") or os.path.join(HERE, "libsparkbam_hip.so")
 
 SBH_OK = 0
 STATUS_NAMES = {

@@ -15,6 +15,8 @@
 // the window (long reads) or touch an EOF edge re-read HBM/L2.  Full: per-position
 // words + an LDS histogram folded into global counters once per tile.  Results are a
 // bit per position (512 B per tile) or a word per position.
+#include <algorithm>
+
 #include "sbh_internal.h"
 
 namespace sbh {
@@ -436,21 +438,27 @@ __global__ void k_first_set(const uint32_t *bits, uint64_t begin, uint64_t from,
   if (v) atomicMin(best, (unsigned long long)(p0 + __builtin_ctz(v)));
 }
 
-__global__ void k_popcount(const uint32_t *bits, uint64_t begin, uint64_t from, uint64_t to,
-                           unsigned long long *acc) {
-  const uint64_t w = (from - begin) / 32 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void k_popcount(const uint32_t *bits, uint64_t begin, uint64_t from,
+                                                   uint64_t to, unsigned long long *acc) {
+  __shared__ uint32_t part[4];
+  const uint64_t w0 = (from - begin) / 32;
   const uint64_t w_end = (to - begin + 31) / 32;
   uint32_t c = 0;
-  if (w < w_end) {
+  for (uint64_t w = w0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < w_end;
+       w += (uint64_t)gridDim.x * blockDim.x) {
     uint32_t v = bits[w];
     const uint64_t p0 = begin + 32 * w;
     if (p0 < from) v &= ~0u << (uint32_t)(from - p0);
     if (p0 + 32 > to) v &= (to - p0) >= 32 ? ~0u : ((1u << (uint32_t)(to - p0)) - 1u);
-    c = __popc(v);
+    c += __popc(v);
   }
-  // wave reduction, one atomic per wave
   for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off);
-  if ((threadIdx.x & 63) == 0 && c) atomicAdd(acc, (unsigned long long)c);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t t = part[0] + part[1] + part[2] + part[3];
+    if (t) atomicAdd(acc, (unsigned long long)t);
+  }
 }
 
 // Chain verification over eager-true positions s in [from, E): the record chain
@@ -572,7 +580,8 @@ hipError_t launch_popcount(const uint32_t *bits, uint64_t begin, uint64_t from, 
                            unsigned long long *acc, hipStream_t st) {
   if (to <= from) return hipSuccess;
   const uint64_t nw = (to - begin + 31) / 32 - (from - begin) / 32;
-  hipLaunchKernelGGL(k_popcount, dim3(ngrid(nw, 256)), dim3(256), 0, st, bits, begin, from, to, acc);
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(ngrid(nw, 256 * 8), 2048);
+  hipLaunchKernelGGL(k_popcount, dim3(grid), dim3(256), 0, st, bits, begin, from, to, acc);
   return hipGetLastError();
 }
 

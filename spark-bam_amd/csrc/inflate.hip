@@ -34,14 +34,22 @@ namespace {
 constexpr int LIT_FAST = 10;
 constexpr int DIST_FAST = 8;
 constexpr int CL_FAST = 7;
-constexpr uint32_t RING = 32768;  // = the DEFLATE window: every copy source is in the ring
+#ifndef SBH_RING
+#define SBH_RING 32768
+#endif
+#ifndef SBH_WAVES
+#define SBH_WAVES 4
+#endif
+constexpr uint32_t RING = SBH_RING;  // 32768 = the whole DEFLATE window
 constexpr uint32_t RMASK = RING - 1;
 constexpr uint32_t GROUP = 1024;  // flush group: 64 lanes x 16 B
-constexpr int WAVES = 4;
-// A round of 64 lanes reads its sources before writing, and a slot is rewritten only
-// by a position 32768 later, so dist <= 32768 never reads a clobbered slot; unflushed
-// bytes (< GROUP + 258) are never overwritten by the next match.
-static_assert(RING >= 32768 && GROUP + 2 * 258 < RING, "ring must hold the window");
+constexpr int WAVES = SBH_WAVES;
+// With RING = 32768 a round of 64 lanes reads its sources before writing and a slot is
+// rewritten only by a position 32768 later, so dist <= 32768 never reads a clobbered
+// slot.  A smaller ring serves dist > NEAR_MAX from HBM (bytes flushed >= 2 groups
+// earlier, drained by s_waitcnt vmcnt(0) before the read).
+constexpr uint32_t NEAR_MAX = RING >= 32768 ? 32768 : RING - 258;
+static_assert(RING >= 2 * GROUP + 2 * 258 + 16, "ring too small");
 
 // Table entry: [4:0] code length, [7:5] kind, [15:8] byte/extra/sym, [31:16] base.
 constexpr uint32_t K_LIT = 0, K_LEN = 1, K_EOB = 2, K_BAD = 3, K_DIST = 4, K_CL = 5, K_SLOW = 7;
@@ -92,7 +100,7 @@ __device__ __forceinline__ uint32_t make_entry(uint32_t kind, uint32_t sym, uint
 // Canonical Huffman table (zlib inflate_table validity: over-subscribed -> error;
 // incomplete -> error unless type != CODES and max == 1; max == 0 -> all invalid).
 // kind: 0 lit/len, 1 dist, 2 code-length code.  Returns 0 ok, 1 error, 2 empty.
-__device__ uint32_t build_table(WaveSmem &sm, const uint8_t *lens, uint32_t nsym, uint32_t kind,
+__device__ __forceinline__ uint32_t build_table(WaveSmem &sm, const uint8_t *lens, uint32_t nsym, uint32_t kind,
                                 uint32_t *tab, int fast, uint32_t lane) {
   const uint32_t w = kind == 1 ? 1 : 0;
   uint16_t *sorted = sm.sorted + (kind == 1 ? 288 : 0);
@@ -174,7 +182,7 @@ __device__ uint32_t build_table(WaveSmem &sm, const uint8_t *lens, uint32_t nsym
 
 // Canonical slow-path decode (codes longer than the primary table): returns the
 // table entry for the symbol, or a K_BAD entry.
-__device__ uint32_t slow_decode(const WaveSmem &sm, uint64_t buf, uint32_t kind) {
+__device__ __forceinline__ uint32_t slow_decode(const WaveSmem &sm, uint64_t buf, uint32_t kind) {
   const uint32_t w = kind == 1 ? 1 : 0;
   const uint16_t *sorted = sm.sorted + (kind == 1 ? 288 : 0);
   uint32_t code = 0, first = 0, index = 0;
@@ -375,7 +383,7 @@ __global__ __launch_bounds__(WAVES *WAVE) void k_inflate(const uint8_t *__restri
           if (lane == 0) sm.cl_lens[CL_ORDER[i]] = (uint8_t)v;
         }
         __builtin_amdgcn_wave_barrier();
-        uint32_t rc = build_table(sm, sm.cl_lens, 19, 2, sm.lit, CL_FAST, lane);
+        uint32_t rc = uni(build_table(sm, sm.cl_lens, 19, 2, sm.lit, CL_FAST, lane));
         if (rc == 1) { status = INF_DATA; break; }
         const uint32_t total = nlen + ndist;
         if (rc == 2) {  // no code-length codes: zlib decodes each as 0 (1 bit) then fails
@@ -429,8 +437,8 @@ __global__ __launch_bounds__(WAVES *WAVE) void k_inflate(const uint8_t *__restri
         if (lane < 32) sm.lens[288 + lane] = (uint8_t)dv;
         __builtin_amdgcn_wave_barrier();
         if (uni(sm.lens[256]) == 0) { status = INF_DATA; break; }  // missing end-of-block
-        if (build_table(sm, sm.lens, nlen, 0, sm.lit, LIT_FAST, lane) == 1) { status = INF_DATA; break; }
-        if (build_table(sm, sm.lens + 288, ndist, 1, sm.dist, DIST_FAST, lane) == 1) { status = INF_DATA; break; }
+        if (uni(build_table(sm, sm.lens, nlen, 0, sm.lit, LIT_FAST, lane)) == 1) { status = INF_DATA; break; }
+        if (uni(build_table(sm, sm.lens + 288, ndist, 1, sm.dist, DIST_FAST, lane)) == 1) { status = INF_DATA; break; }
       }
       // ---- symbol loop ----
       bool eob = false;
@@ -439,7 +447,7 @@ __global__ __launch_bounds__(WAVES *WAVE) void k_inflate(const uint8_t *__restri
         uint32_t e = uni(sm.lit[br.peek(LIT_FAST)]);
         uint32_t kind = (e >> 5) & 7;
         if (kind == K_SLOW) {
-          e = slow_decode(sm, br.buf, 0);
+          e = uni(slow_decode(sm, br.buf, 0));
           kind = (e >> 5) & 7;
         }
         uint32_t L = e & 31;
@@ -465,7 +473,7 @@ __global__ __launch_bounds__(WAVES *WAVE) void k_inflate(const uint8_t *__restri
           uint32_t d = uni(sm.dist[br.peek(DIST_FAST)]);
           uint32_t dk = (d >> 5) & 7;
           if (dk == K_SLOW) {
-            d = slow_decode(sm, br.buf, 1);
+            d = uni(slow_decode(sm, br.buf, 1));
             dk = (d >> 5) & 7;
           }
           if (dk == K_BAD) {
@@ -483,7 +491,13 @@ __global__ __launch_bounds__(WAVES *WAVE) void k_inflate(const uint8_t *__restri
           if (dist > out) { status = INF_DATA; done = true; break; }  // too far back
           const uint32_t n = mlen < usize - out ? mlen : usize - out;
           const uint64_t dst_g = G + out;
-          if (dist >= WAVE || dist >= n) {
+          if (dist > NEAR_MAX) {  // far (only with a ring smaller than the window)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            for (uint32_t i0 = 0; i0 < n; i0 += WAVE) {
+              uint32_t i = i0 + lane;
+              if (i < n) sm.ring[(uint32_t)(dst_g + i) & RMASK] = U[dst_g - dist + i];
+            }
+          } else if (dist >= WAVE || dist >= n) {
             for (uint32_t i0 = 0; i0 < n; i0 += WAVE) {
               uint32_t i = i0 + lane;
               if (i < n) sm.ring[(uint32_t)(dst_g + i) & RMASK] = sm.ring[(uint32_t)(dst_g - dist + i) & RMASK];

@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""A/B the inflate-kernel variants (spark-bam_amd/build/variants/lib_*.so) on one
+synthetic shard: per-variant k_inflate time (HIP events) and output identity vs the
+in-tree library.  Each variant runs in its own process (the library path is bound at
+import).  Usage: python tools/ab_inflate.py [--records N] [variant ...]"""
+import argparse
+import glob
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def child(lib, records, reps):
+    if lib:
+        os.environ["SBH_LIB_PATH"] = lib
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import hashlib
+
+    import numpy as np
+    import synth
+    from __graft_entry__ import load_package
+    sb = load_package()
+    p = synth.params(synth.SEEDS["B"])
+    data, usize, nb = synth.make_bam(p, records)
+    with sb.Context(0) as ctx:
+        sh = ctx.shard(data)
+        names, cl, _ = sb.parse_bam_header(synth.header_bytes())
+        sh.set_contigs(cl)
+        times = []
+        for _ in range(reps):
+            r = sh.run(0, data.size)
+            times.append(sh.stage_times())
+        sh.index(0)
+        h = hashlib.sha1(sh.read_flat().tobytes()).hexdigest()
+        t = np.median(np.asarray(times), axis=0).tolist()
+        print(json.dumps({"lib": os.path.basename(lib or "in-tree"), "comp": int(data.size),
+                          "usize": int(usize), "blocks": int(nb), "stage_ms": t,
+                          "inflate_GBps": usize / (t[1] * 1e-3) / 1e9, "sha1": h,
+                          "count": r["count"]}))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--records", type=int, default=2_000_000)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--child", default=None)
+    ap.add_argument("variants", nargs="*")
+    a = ap.parse_args()
+    if a.child is not None:
+        return child(a.child, a.records, a.reps)
+    libs = [""] + (a.variants or sorted(glob.glob(os.path.join(ROOT, "spark-bam_amd/build/variants/lib_*.so"))))
+    for lib in libs:
+        r = subprocess.run([sys.executable, __file__, "--child", lib, "--records", str(a.records),
+                            "--reps", str(a.reps)], capture_output=True, text=True, timeout=900)
+        print(r.stdout.strip() or r.stderr[-2000:], flush=True)
+
+
+if __name__ == "__main__":
+    main()
