@@ -1,4 +1,4 @@
-// inflate.hip -- BGZF block inflate on CDNA4: one 64-lane wave per BGZF block.
+// inflate.hip -- BGZF block inflate on CDNA4, in two kernels.
 //
 // Replaces StreamI._advance's `new Inflater(true).inflate(decBuf, 0, ISIZE)`
 // (bgzf/src/main/scala/org/hammerlab/bgzf/block/Stream.scala:31-71) for every block
@@ -10,46 +10,38 @@
 // reported.  No CRC is checked (the reference does not check it either).
 //
 // Design (MI355X-first):
-//  * The Huffman decode of a DEFLATE stream is serial, so each wave runs ONE
-//    wave-uniform decoder: the bit buffer, counters and symbol state live in SGPRs
-//    (SALU work); lanes are used for the parallel parts: table construction, LZ77
-//    copies (64 bytes per instruction), stored-block copies and coalesced write-out.
-//  * Compressed input is streamed through two VGPR windows (64 lanes x 4 B each,
-//    prefetched 256 B ahead) and pulled into the bit buffer with v_readlane -- no LDS
-//    round trip on the bit path.
-//  * Decode tables (10-bit literal/length, 8-bit distance primary tables; canonical
-//    slow path beyond) live in LDS, one set per wave.
-//  * Output goes through a 32 KiB LDS ring (the whole DEFLATE window) indexed by the
-//    *flat* destination address, so 16-byte granules are aligned both in LDS and in
-//    HBM; 1 KiB groups are flushed with one 16 B store per lane.  Every LZ77 copy is
-//    served from the ring: measured on synthetic and real BAM data, ~39% of matches
-//    reach back more than 4 KiB (distances are spread over the whole window), so a
-//    smaller ring with HBM read-back was latency-bound.
-//  * ~39 KiB LDS per wave -> one 4-wave workgroup (one wave per SIMD) per CU.
+//  * k_huff -- the serial part.  One 64-lane wave per BGZF block runs a wave-uniform
+//    Huffman decoder: bit buffer, counters and symbol state in SGPRs, compressed bytes
+//    pulled in with scalar loads, decode tables in LDS (~6 KiB per wave, so many waves
+//    per SIMD hide the LDS/scalar-load latency of the serial symbol chain).  It emits
+//    LZ77 tokens (one u32 per literal or match, batched in a VGPR and stored 64 at a
+//    time) and does all of zlib's validation, so it alone decides the block status.
+//    It needs no window: a match is only checked against the bytes produced so far.
+//  * k_lz -- the parallel part.  One 256-thread workgroup per block resolves the
+//    tokens into a 64 KiB LDS image of the block: a prefix sum gives every token its
+//    output offset, literals land at once, and matches are resolved in rounds -- a
+//    match copies as soon as its source lies below the lowest unresolved output
+//    offset.  The image is then written to HBM with 16-byte stores aligned to the flat
+//    address (block images start at arbitrary flat offsets).
+//  * Token buffer: tokens of block b live at tok[ustart_b ...]; a block has at most
+//    usize tokens (every token yields >= 1 byte), so the buffer is 4 B per flat byte.
 #include "sbh_internal.h"
 
 namespace sbh {
 namespace {
 
-constexpr int LIT_FAST = 10;
+#ifndef SBH_LIT_FAST
+#define SBH_LIT_FAST 10
+#endif
+#ifndef SBH_HUFF_WAVES
+#define SBH_HUFF_WAVES 4
+#endif
+constexpr int LIT_FAST = SBH_LIT_FAST;
 constexpr int DIST_FAST = 8;
 constexpr int CL_FAST = 7;
-#ifndef SBH_RING
-#define SBH_RING 32768
-#endif
-#ifndef SBH_WAVES
-#define SBH_WAVES 4
-#endif
-constexpr uint32_t RING = SBH_RING;  // 32768 = the whole DEFLATE window
-constexpr uint32_t RMASK = RING - 1;
-constexpr uint32_t GROUP = 1024;  // flush group: 64 lanes x 16 B
-constexpr int WAVES = SBH_WAVES;
-// With RING = 32768 a round of 64 lanes reads its sources before writing and a slot is
-// rewritten only by a position 32768 later, so dist <= 32768 never reads a clobbered
-// slot.  A smaller ring serves dist > NEAR_MAX from HBM (bytes flushed >= 2 groups
-// earlier, drained by s_waitcnt vmcnt(0) before the read).
-constexpr uint32_t NEAR_MAX = RING >= 32768 ? 32768 : RING - 258;
-static_assert(RING >= 2 * GROUP + 2 * 258 + 16, "ring too small");
+constexpr int WAVES = SBH_HUFF_WAVES;  // waves (blocks) per k_huff workgroup
+constexpr uint32_t LZ_THREADS = 256;   // k_lz workgroup: one block, one token per thread per chunk
+constexpr uint32_t TOK_MATCH = 0x80000000u;  // token: literal = byte; match = bit31 | len << 16 | dist
 
 // Table entry: [4:0] code length, [7:5] kind, [15:8] byte/extra/sym, [31:16] base.
 constexpr uint32_t K_LIT = 0, K_LEN = 1, K_EOB = 2, K_BAD = 3, K_DIST = 4, K_CL = 5, K_SLOW = 7;
@@ -66,7 +58,6 @@ __constant__ uint8_t DEXT[30] = {0, 0, 0, 0, 1, 1, 2, 2,  3,  3,  4,  4,  5,  5,
 __constant__ uint8_t CL_ORDER[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
 struct __attribute__((aligned(16))) WaveSmem {
-  uint8_t ring[RING];
   uint32_t lit[1 << LIT_FAST];  // also the code-length-code table while reading headers
   uint32_t dist[1 << DIST_FAST];
   uint16_t sorted[320];  // canonical order: [0,288) lit/len (or CL), [288,320) dist
@@ -201,84 +192,68 @@ __device__ __forceinline__ uint32_t slow_decode(const WaveSmem &sm, uint64_t buf
   return 1u | (K_BAD << 5);
 }
 
-// Wave-uniform bit reader over the VGPR windows.
+// Wave-uniform bit reader: 32-bit scalar loads (s_load_dword through the scalar
+// cache) from the compressed bytes; LSB-first 64-bit bit buffer in SGPRs.
 struct Bits {
-  const uint32_t *base32;  // dword-aligned view of the compressed shard
-  uint32_t win, nwin;      // VGPR windows: lane l holds base32[wbase + l] / [wbase + 64 + l]
-  uint32_t wbase;          // dword index of `win`
-  uint32_t widx;           // next dword to pull into buf
+  const uint32_t *__restrict__ c32;  // dword view of the compressed shard
+  uint32_t idx;                      // next dword to load (absolute index)
   uint64_t buf;
   uint32_t cnt;
-  uint32_t pos;    // bits consumed, relative to dword index a0
-  uint32_t a0;     // dword index of the start of the block's deflate data (aligned down)
-  uint32_t limit;  // bits available (relative to a0): Inflater input ends here
-  uint32_t lane;
+  uint32_t a0;     // dword index of the first dword holding the block's deflate data
+  uint32_t limit;  // bits available, relative to a0 * 32: the Inflater input ends here
 
+  __device__ __forceinline__ void refill() {  // guarantees cnt >= 32
+    if (cnt <= 32) {
+      buf |= (uint64_t)c32[idx] << cnt;
+      ++idx;
+      cnt += 32;
+    }
+  }
   __device__ __forceinline__ void seek(uint32_t bitpos) {
-    pos = bitpos;
-    widx = a0 + (bitpos >> 5);
-    wbase = widx;
-    win = base32[wbase + lane];
-    nwin = base32[wbase + WAVE + lane];
+    idx = a0 + (bitpos >> 5);
     buf = 0;
     cnt = 0;
     refill();
-    uint32_t d = bitpos & 31;
+    const uint32_t d = bitpos & 31;
     buf >>= d;
     cnt -= d;
   }
-  __device__ __forceinline__ void refill() {
-    while (cnt <= 32) {
-      uint32_t rel = widx - wbase;
-      uint32_t w = rel < WAVE ? rdlane(win, rel) : rdlane(nwin, rel - WAVE);
-      buf |= (uint64_t)w << cnt;
-      cnt += 32;
-      ++widx;
-      if (widx - wbase == WAVE + 1) {  // moved into nwin: slide and prefetch
-        win = nwin;
-        wbase += WAVE;
-        nwin = base32[wbase + WAVE + lane];
-      }
-    }
-  }
+  __device__ __forceinline__ uint32_t pos() const { return (idx - a0) * 32 - cnt; }
   __device__ __forceinline__ void drop(uint32_t n) {
     buf >>= n;
     cnt -= n;
-    pos += n;
   }
-  __device__ __forceinline__ uint32_t peek(uint32_t n) const {
-    return (uint32_t)buf & ((1u << n) - 1u);
-  }
+  __device__ __forceinline__ uint32_t peek(uint32_t n) const { return (uint32_t)buf & ((1u << n) - 1u); }
   __device__ __forceinline__ uint32_t take(uint32_t n) {
-    uint32_t v = peek(n);
+    const uint32_t v = peek(n);
     drop(n);
     return v;
   }
-  __device__ __forceinline__ bool avail(uint32_t n) const { return pos + n <= limit; }
+  __device__ __forceinline__ bool avail(uint32_t n) const { return pos() + n <= limit; }
 };
 
-// Flush granules [from_g, to_g) of the ring to U (flat addresses; from_g 16-aligned);
-// bytes outside [G, to_g) are left alone (they belong to neighbouring blocks).
-__device__ __forceinline__ void flush(const WaveSmem &sm, uint8_t *U, uint64_t from_g, uint64_t to_g,
-                                      uint64_t G, uint32_t lane) {
-  for (uint64_t g0 = from_g; g0 < to_g; g0 += GROUP) {
-    uint64_t ga = g0 + 16ull * lane;
-    if (ga < to_g) {
-      if (ga >= G && ga + 16 <= to_g) {
-        uint4 v = *reinterpret_cast<const uint4 *>(&sm.ring[(uint32_t)ga & RMASK]);
-        *reinterpret_cast<uint4 *>(U + ga) = v;
-      } else {
-        for (uint32_t k = 0; k < 16; ++k) {
-          uint64_t a = ga + k;
-          if (a >= G && a < to_g) U[a] = sm.ring[(uint32_t)a & RMASK];
-        }
-      }
+// Tokens are gathered one per lane in a VGPR and stored 64 at a time.
+struct TokOut {
+  uint32_t *__restrict__ dst;  // tok + ustart of the block
+  uint32_t batch;              // VGPR: lane k = token bst + k
+  uint32_t nt, bst;            // tokens emitted / tokens stored
+
+  __device__ __forceinline__ void emit(uint32_t t, uint32_t lane) {
+    batch = lane == nt - bst ? t : batch;
+    ++nt;
+    if (nt - bst == WAVE) {
+      dst[bst + lane] = batch;
+      bst = nt;
     }
   }
-}
+  __device__ __forceinline__ void drain(uint32_t lane) {
+    if (lane < nt - bst) dst[bst + lane] = batch;
+    bst = nt;
+  }
+};
 
-__global__ __launch_bounds__(WAVES *WAVE) void k_inflate(const uint8_t *__restrict__ comp, DevBlocks bl,
-                                                          uint64_t nblocks, uint8_t *__restrict__ U) {
+__global__ __launch_bounds__(WAVES *WAVE) void k_huff(const uint8_t *__restrict__ comp, DevBlocks bl,
+                                                       uint64_t nblocks, uint32_t *__restrict__ tok) {
   __shared__ WaveSmem smem[WAVES];
   const uint32_t lane = threadIdx.x & (WAVE - 1);
   const uint32_t wid = uni(threadIdx.x / WAVE);
@@ -290,257 +265,346 @@ __global__ __launch_bounds__(WAVES *WAVE) void k_inflate(const uint8_t *__restri
   const uint32_t csize = bl.csize[b], hsize = bl.hsize[b], usize = bl.usize[b];
   const uint64_t G = bl.ustart[b];
   const uint32_t bflags = bl.flags[b];
-  if (bflags & BLK_TRUNCATED) {
-    if (lane == 0) bl.status[b] = INF_SIZE;
-    return;
-  }
-  if (usize > 65536u) {
-    if (lane == 0) bl.status[b] = INF_BAD_ISIZE;
-    return;
-  }
-  if ((int32_t)csize - (int32_t)hsize - 8 < 0) {
-    if (lane == 0) bl.status[b] = INF_DATA;
+  uint32_t early = INF_OK;
+  if (bflags & BLK_TRUNCATED) early = INF_SIZE;
+  else if (usize > 65536u) early = INF_BAD_ISIZE;
+  else if ((int32_t)csize - (int32_t)hsize - 8 < 0) early = INF_DATA;
+  if (early != INF_OK) {
+    if (lane == 0) {
+      bl.status[b] = early;
+      bl.ntok[b] = 0;
+    }
     return;
   }
   const uint32_t data_len = csize - hsize - 8;
 
   Bits br;
-  br.base32 = reinterpret_cast<const uint32_t *>(comp);
-  br.lane = lane;
+  br.c32 = reinterpret_cast<const uint32_t *>(comp);
   const uint64_t dbyte = cstart + hsize;
   br.a0 = (uint32_t)(dbyte >> 2);
   const uint32_t skip = (uint32_t)(dbyte & 3) * 8;
   br.limit = skip + data_len * 8;
   br.seek(skip);
+  // the hot loop needs no per-symbol input check while a whole symbol (<= 48 bits)
+  // is guaranteed to be available: (idx - a0) * 32 + 48 <= limit
+  const uint32_t hot_idx = br.limit >= 48 ? br.a0 + (br.limit - 48) / 32 : 0;
 
-  uint32_t out = 0;                 // bytes produced
-  uint64_t flushed = G & ~15ull;     // flat address up to which stores were issued
+  TokOut to;
+  to.dst = tok + G;
+  to.batch = 0;
+  to.nt = 0;
+  to.bst = 0;
+
+  uint32_t out = 0;  // bytes produced
   uint32_t status = INF_OK;
   bool fixed_built = false;
   bool last = false;
   bool done = false;
 
-  // ---- block loop (deflate blocks inside the BGZF block) ----
-  while (!done) {
+  while (!done) {  // deflate blocks inside the BGZF block
     br.refill();
     if (!br.avail(3)) break;  // needs input: stop
     last = br.take(1);
     const uint32_t type = br.take(2);
     if (type == 0) {
-      // stored block: byte-align, LEN, NLEN
-      br.drop((8 - (br.pos & 7)) & 7);
+      // stored block: byte-align, LEN, NLEN; bytes become literal tokens
+      br.drop((8 - (br.pos() & 7)) & 7);
       br.refill();
       if (!br.avail(32)) break;
       const uint32_t len = br.take(16), nlen = br.take(16);
       if (len != (~nlen & 0xffffu)) { status = INF_DATA; break; }
-      uint32_t src_byte = br.pos >> 3;  // relative to a0*4
-      uint32_t avail_bytes = (br.limit - br.pos) >> 3;
+      const uint32_t p0 = br.pos();
+      const uint32_t avail_bytes = (br.limit - p0) >> 3;
       uint32_t n = len;
       if (n > avail_bytes) n = avail_bytes;
       if (n > usize - out) n = usize - out;
-      const uint8_t *src = comp + (uint64_t)br.a0 * 4 + src_byte;
-      for (uint32_t c0 = 0; c0 < n; c0 += 512) {
-        uint32_t piece = n - c0 < 512 ? n - c0 : 512;
-        for (uint32_t k = 0; k < 8; ++k) {
-          uint32_t i = lane * 8 + k;
-          if (i < piece) sm.ring[(uint32_t)(G + out + i) & RMASK] = src[c0 + i];
+      const uint8_t *src = comp + (uint64_t)br.a0 * 4 + (p0 >> 3);
+      to.drain(lane);
+      for (uint32_t i = lane; i < n; i += WAVE) to.dst[to.nt + i] = src[i];
+      to.nt += n;
+      to.bst = to.nt;
+      out += n;
+      if (n < len) break;  // output full or input exhausted
+      br.seek(p0 + len * 8);
+      if (last) break;
+      continue;
+    }
+    if (type == 3) { status = INF_DATA; break; }  // invalid block type
+    if (type == 1) {
+      if (!fixed_built) {
+        for (uint32_t s = lane; s < 288; s += WAVE) sm.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
+        if (lane < 32) sm.lens[288 + lane] = 5;
+        __builtin_amdgcn_wave_barrier();
+        build_table(sm, sm.lens, 288, 0, sm.lit, LIT_FAST, lane);
+        build_table(sm, sm.lens + 288, 32, 1, sm.dist, DIST_FAST, lane);
+        fixed_built = true;
+      }
+    } else {
+      fixed_built = false;
+      br.refill();
+      if (!br.avail(14)) break;
+      const uint32_t nlen = br.take(5) + 257, ndist = br.take(5) + 1, ncode = br.take(4) + 4;
+      if (nlen > 286 || ndist > 30) { status = INF_DATA; break; }
+      if (!br.avail(ncode * 3)) break;
+      if (lane < 20) sm.cl_lens[lane] = 0;
+      __builtin_amdgcn_wave_barrier();
+      for (uint32_t i = 0; i < ncode; ++i) {
+        br.refill();
+        const uint32_t v = br.take(3);
+        if (lane == 0) sm.cl_lens[CL_ORDER[i]] = (uint8_t)v;
+      }
+      __builtin_amdgcn_wave_barrier();
+      const uint32_t rc = uni(build_table(sm, sm.cl_lens, 19, 2, sm.lit, CL_FAST, lane));
+      if (rc == 1) { status = INF_DATA; break; }
+      const uint32_t total = nlen + ndist;
+      if (rc == 2) {  // no code-length codes: zlib decodes each as 0 (1 bit) then fails
+        if (!br.avail(total)) break;
+        status = INF_DATA;
+        break;
+      }
+      uint32_t i = 0, prevlen = 0;
+      bool hdr_ok = true, starved = false;
+      while (i < total) {
+        br.refill();
+        const uint32_t e = uni(sm.lit[br.peek(CL_FAST)]);
+        const uint32_t L = e & 31;
+        if (!br.avail(L)) { starved = true; break; }
+        br.drop(L);
+        const uint32_t sym = (e >> 8) & 0xff;
+        if (sym < 16) {
+          if (lane == 0) sm.lens[i] = (uint8_t)sym;
+          prevlen = sym;
+          ++i;
+          continue;
         }
-        out += piece;
-        while (G + out >= flushed + GROUP) {
-          flush(sm, U, flushed, flushed + GROUP, G, lane);
-          flushed += GROUP;
+        uint32_t rep, val;
+        if (sym == 16) {
+          if (i == 0) { hdr_ok = false; break; }
+          if (!br.avail(2)) { starved = true; break; }
+          rep = 3 + br.take(2);
+          val = prevlen;
+        } else if (sym == 17) {
+          if (!br.avail(3)) { starved = true; break; }
+          rep = 3 + br.take(3);
+          val = 0;
+        } else {
+          if (!br.avail(7)) { starved = true; break; }
+          rep = 11 + br.take(7);
+          val = 0;
+        }
+        if (i + rep > total) { hdr_ok = false; break; }
+        for (uint32_t k = lane; k < rep; k += WAVE) sm.lens[i + k] = (uint8_t)val;
+        prevlen = val;
+        i += rep;
+      }
+      if (starved) break;
+      if (!hdr_ok) { status = INF_DATA; break; }
+      __builtin_amdgcn_wave_barrier();
+      // split: lit lens [0,nlen) (+zeros to 288); dist lens -> [288, 288+ndist)
+      const uint32_t dv = lane < ndist ? sm.lens[nlen + lane] : 0;
+      __builtin_amdgcn_wave_barrier();
+      for (uint32_t s = nlen + lane; s < 288; s += WAVE) sm.lens[s] = 0;
+      __builtin_amdgcn_wave_barrier();
+      if (lane < 32) sm.lens[288 + lane] = (uint8_t)dv;
+      __builtin_amdgcn_wave_barrier();
+      if (uni(sm.lens[256]) == 0) { status = INF_DATA; break; }  // missing end-of-block
+      if (uni(build_table(sm, sm.lens, nlen, 0, sm.lit, LIT_FAST, lane)) == 1) { status = INF_DATA; break; }
+      if (uni(build_table(sm, sm.lens + 288, ndist, 1, sm.dist, DIST_FAST, lane)) == 1) { status = INF_DATA; break; }
+    }
+
+    // ---- symbols ----
+    for (;;) {
+      // Hot loop: no input/output bound checks while a whole symbol is available and
+      // a whole match fits; rare events (EOB, long codes, bad codes) fall through to
+      // the careful single-symbol path below.
+      while (br.idx <= hot_idx && out + 258 <= usize) {
+        br.refill();
+        const uint32_t e = uni(sm.lit[(uint32_t)br.buf & ((1u << LIT_FAST) - 1)]);
+        const uint32_t kind = (e >> 5) & 7;
+        if (kind == K_LIT) {
+          br.drop(e & 31);
+          to.emit((e >> 8) & 0xff, lane);
+          ++out;
+        } else if (kind == K_LEN) {
+          br.drop(e & 31);
+          const uint32_t lx = (e >> 8) & 0xff;
+          const uint32_t mlen = (e >> 16) + br.take(lx);
+          br.refill();
+          uint32_t d = uni(sm.dist[(uint32_t)br.buf & ((1u << DIST_FAST) - 1)]);
+          if (((d >> 5) & 7) == K_SLOW) d = uni(slow_decode(sm, br.buf, 1));
+          if (((d >> 5) & 7) != K_DIST) { status = INF_DATA; done = true; break; }
+          br.drop(d & 31);
+          const uint32_t dist = (d >> 16) + br.take((d >> 8) & 0xff);
+          if (dist > out) { status = INF_DATA; done = true; break; }  // too far back
+          to.emit(TOK_MATCH | (mlen << 16) | dist, lane);
+          out += mlen;
+        } else {
+          break;
         }
       }
-      if (n < len) {  // output full or input exhausted
+      if (done) break;
+      // careful path: one symbol with every bound checked (zlib semantics at the edges)
+      br.refill();
+      uint32_t e = uni(sm.lit[br.peek(LIT_FAST)]);
+      uint32_t kind = (e >> 5) & 7;
+      if (kind == K_SLOW) {
+        e = uni(slow_decode(sm, br.buf, 0));
+        kind = (e >> 5) & 7;
+      }
+      const uint32_t L = e & 31;
+      if (kind == K_BAD) {
+        if (br.avail(1)) status = INF_DATA;
         done = true;
         break;
       }
-      br.seek(br.pos + len * 8);
-    } else if (type == 1 || type == 2) {
-      if (type == 1) {
-        if (!fixed_built) {
-          for (uint32_t s = lane; s < 288; s += WAVE)
-            sm.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
-          if (lane < 32) sm.lens[288 + lane] = 5;
-          __builtin_amdgcn_wave_barrier();
-          build_table(sm, sm.lens, 288, 0, sm.lit, LIT_FAST, lane);
-          build_table(sm, sm.lens + 288, 32, 1, sm.dist, DIST_FAST, lane);
-          fixed_built = true;
-        }
-      } else {
-        fixed_built = false;
+      if (!br.avail(L)) { done = true; break; }
+      br.drop(L);
+      if (kind == K_LIT) {
+        if (out == usize) { done = true; break; }
+        to.emit((e >> 8) & 0xff, lane);
+        ++out;
+      } else if (kind == K_EOB) {
+        break;
+      } else {  // length
+        const uint32_t lx = (e >> 8) & 0xff;
+        if (!br.avail(lx)) { done = true; break; }
+        const uint32_t mlen = (e >> 16) + br.take(lx);
         br.refill();
-        if (!br.avail(14)) break;
-        const uint32_t nlen = br.take(5) + 257, ndist = br.take(5) + 1, ncode = br.take(4) + 4;
-        if (nlen > 286 || ndist > 30) { status = INF_DATA; break; }
-        if (!br.avail(ncode * 3)) break;
-        if (lane < 20) sm.cl_lens[lane] = 0;
-        __builtin_amdgcn_wave_barrier();
-        // 3 bits each, in CL_ORDER; read serially (<= 57 bits)
-        for (uint32_t i = 0; i < ncode; ++i) {
-          br.refill();
-          uint32_t v = br.take(3);
-          if (lane == 0) sm.cl_lens[CL_ORDER[i]] = (uint8_t)v;
+        uint32_t d = uni(sm.dist[br.peek(DIST_FAST)]);
+        uint32_t dk = (d >> 5) & 7;
+        if (dk == K_SLOW) {
+          d = uni(slow_decode(sm, br.buf, 1));
+          dk = (d >> 5) & 7;
         }
-        __builtin_amdgcn_wave_barrier();
-        uint32_t rc = uni(build_table(sm, sm.cl_lens, 19, 2, sm.lit, CL_FAST, lane));
-        if (rc == 1) { status = INF_DATA; break; }
-        const uint32_t total = nlen + ndist;
-        if (rc == 2) {  // no code-length codes: zlib decodes each as 0 (1 bit) then fails
-          if (!br.avail(total)) break;
-          status = INF_DATA;
-          break;
-        }
-        uint32_t i = 0, prevlen = 0;
-        bool hdr_ok = true, starved = false;
-        while (i < total) {
-          br.refill();
-          uint32_t e = uni(sm.lit[br.peek(CL_FAST)]);
-          uint32_t L = e & 31;
-          if (!br.avail(L)) { starved = true; break; }
-          br.drop(L);
-          uint32_t sym = (e >> 8) & 0xff;
-          if (sym < 16) {
-            if (lane == 0) sm.lens[i] = (uint8_t)sym;
-            prevlen = sym;
-            ++i;
-            continue;
-          }
-          uint32_t rep, val;
-          if (sym == 16) {
-            if (i == 0) { hdr_ok = false; break; }
-            if (!br.avail(2)) { starved = true; break; }
-            rep = 3 + br.take(2);
-            val = prevlen;
-          } else if (sym == 17) {
-            if (!br.avail(3)) { starved = true; break; }
-            rep = 3 + br.take(3);
-            val = 0;
-          } else {
-            if (!br.avail(7)) { starved = true; break; }
-            rep = 11 + br.take(7);
-            val = 0;
-          }
-          if (i + rep > total) { hdr_ok = false; break; }
-          for (uint32_t k = lane; k < rep; k += WAVE) sm.lens[i + k] = (uint8_t)val;
-          prevlen = val;
-          i += rep;
-        }
-        if (starved) break;
-        if (!hdr_ok) { status = INF_DATA; break; }
-        __builtin_amdgcn_wave_barrier();
-        // split: lit lens [0,nlen) (+zeros to 288); dist lens -> [288, 288+ndist)
-        uint32_t dv = lane < ndist ? sm.lens[nlen + lane] : 0;
-        __builtin_amdgcn_wave_barrier();
-        for (uint32_t s = nlen + lane; s < 288; s += WAVE) sm.lens[s] = 0;
-        __builtin_amdgcn_wave_barrier();
-        if (lane < 32) sm.lens[288 + lane] = (uint8_t)dv;
-        __builtin_amdgcn_wave_barrier();
-        if (uni(sm.lens[256]) == 0) { status = INF_DATA; break; }  // missing end-of-block
-        if (uni(build_table(sm, sm.lens, nlen, 0, sm.lit, LIT_FAST, lane)) == 1) { status = INF_DATA; break; }
-        if (uni(build_table(sm, sm.lens + 288, ndist, 1, sm.dist, DIST_FAST, lane)) == 1) { status = INF_DATA; break; }
-      }
-      // ---- symbol loop ----
-      bool eob = false;
-      for (;;) {
-        br.refill();
-        uint32_t e = uni(sm.lit[br.peek(LIT_FAST)]);
-        uint32_t kind = (e >> 5) & 7;
-        if (kind == K_SLOW) {
-          e = uni(slow_decode(sm, br.buf, 0));
-          kind = (e >> 5) & 7;
-        }
-        uint32_t L = e & 31;
-        if (kind == K_BAD) {
+        if (dk == K_BAD) {
           if (br.avail(1)) status = INF_DATA;
           done = true;
           break;
         }
-        if (!br.avail(L)) { done = true; break; }
-        br.drop(L);
-        if (kind == K_LIT) {
-          if (out == usize) { done = true; break; }
-          if (lane == 0) sm.ring[(uint32_t)(G + out) & RMASK] = (uint8_t)(e >> 8);
-          ++out;
-        } else if (kind == K_EOB) {
-          eob = true;
-          break;
-        } else {  // length
-          const uint32_t lx = (e >> 8) & 0xff;
-          if (!br.avail(lx)) { done = true; break; }
-          const uint32_t mlen = (e >> 16) + br.take(lx);
-          br.refill();
-          uint32_t d = uni(sm.dist[br.peek(DIST_FAST)]);
-          uint32_t dk = (d >> 5) & 7;
-          if (dk == K_SLOW) {
-            d = uni(slow_decode(sm, br.buf, 1));
-            dk = (d >> 5) & 7;
-          }
-          if (dk == K_BAD) {
-            if (br.avail(1)) status = INF_DATA;
-            done = true;
-            break;
-          }
-          const uint32_t DL = d & 31;
-          if (!br.avail(DL)) { done = true; break; }
-          br.drop(DL);
-          const uint32_t dx = (d >> 8) & 0xff;
-          if (!br.avail(dx)) { done = true; break; }
-          const uint32_t dist = (d >> 16) + br.take(dx);
-          if (out == usize) { done = true; break; }  // zlib stops at MATCH when full
-          if (dist > out) { status = INF_DATA; done = true; break; }  // too far back
-          const uint32_t n = mlen < usize - out ? mlen : usize - out;
-          const uint64_t dst_g = G + out;
-          if (dist > NEAR_MAX) {  // far (only with a ring smaller than the window)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            for (uint32_t i0 = 0; i0 < n; i0 += WAVE) {
-              uint32_t i = i0 + lane;
-              if (i < n) sm.ring[(uint32_t)(dst_g + i) & RMASK] = U[dst_g - dist + i];
-            }
-          } else if (dist >= WAVE || dist >= n) {
-            for (uint32_t i0 = 0; i0 < n; i0 += WAVE) {
-              uint32_t i = i0 + lane;
-              if (i < n) sm.ring[(uint32_t)(dst_g + i) & RMASK] = sm.ring[(uint32_t)(dst_g - dist + i) & RMASK];
-            }
-          } else {  // overlapping short period: out[i] = out[i mod dist - dist]
-            const uint32_t inv = dist == 1 ? 0 : (uint32_t)((0x100000000ull + dist - 1) / dist);
-            for (uint32_t i0 = 0; i0 < n; i0 += WAVE) {
-              uint32_t i = i0 + lane;
-              uint32_t q = dist == 1 ? i : __umulhi(i, inv);
-              uint32_t si = i - q * dist;
-              if (i < n) sm.ring[(uint32_t)(dst_g + i) & RMASK] = sm.ring[(uint32_t)(dst_g - dist + si) & RMASK];
-            }
-          }
-          out += n;
-          if (n < mlen) { done = true; break; }  // output full mid-match
-        }
-        while (G + out >= flushed + GROUP) {
-          flush(sm, U, flushed, flushed + GROUP, G, lane);
-          flushed += GROUP;
-        }
+        const uint32_t DL = d & 31;
+        if (!br.avail(DL)) { done = true; break; }
+        br.drop(DL);
+        const uint32_t dx = (d >> 8) & 0xff;
+        if (!br.avail(dx)) { done = true; break; }
+        const uint32_t dist = (d >> 16) + br.take(dx);
+        if (out == usize) { done = true; break; }  // zlib stops at MATCH when full
+        if (dist > out) { status = INF_DATA; done = true; break; }  // too far back
+        const uint32_t n = mlen < usize - out ? mlen : usize - out;
+        to.emit(TOK_MATCH | (n << 16) | dist, lane);
+        out += n;
+        if (n < mlen) { done = true; break; }  // output full mid-match
       }
-      if (done) break;
-      (void)eob;
-    } else {
-      status = INF_DATA;  // invalid block type
-      break;
     }
-    if (last) break;
+    if (done || last) break;
   }
-  // final flush of [flushed, G + out)
-  if (G + out > flushed) flush(sm, U, flushed, G + out, G, lane);
+  to.drain(lane);
   if (status == INF_OK && out != usize) status = INF_SIZE;
-  if (lane == 0) bl.status[b] = status;
+  if (lane == 0) {
+    bl.status[b] = status;
+    bl.ntok[b] = to.nt;
+  }
+}
+
+// Block-wide exclusive prefix sum over LZ_THREADS threads; *total gets the sum.
+__device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t *wsum, uint32_t *total) {
+  const uint32_t lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+  uint32_t x = v;
+#pragma unroll
+  for (uint32_t d = 1; d < WAVE; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, WAVE);
+    if (lane >= d) x += y;
+  }
+  if (lane == WAVE - 1) wsum[w] = x;
+  __syncthreads();
+  uint32_t before = 0, all = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < LZ_THREADS / WAVE; ++k) {
+    const uint32_t s = wsum[k];
+    before += k < w ? s : 0;
+    all += s;
+  }
+  *total = all;
+  return before + x - v;
+}
+
+struct LzSmem {
+  uint8_t img[65536 + 16];  // block image, placed at (ustart & 15) so granules align with HBM
+  uint32_t wsum[LZ_THREADS / WAVE];
+  uint32_t front[3];  // rotating "lowest unresolved offset" slots
+};
+
+__global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblocks,
+                                                    const uint32_t *__restrict__ tok, uint8_t *__restrict__ U) {
+  __shared__ LzSmem sm;
+  const uint64_t b = blockIdx.x;
+  if (b >= nblocks) return;
+  const uint32_t t = threadIdx.x;
+  const uint32_t n = bl.ntok[b];
+  const uint64_t G = bl.ustart[b];
+  const uint32_t sh = (uint32_t)(G & 15);
+  uint8_t *img = sm.img + sh;
+  const uint32_t *tk = tok + G;
+  if (t < 3) sm.front[t] = 0xffffffffu;
+
+  uint32_t base = 0;  // output offset of the chunk's first token
+  uint32_t r = 0;     // round counter (front slot rotation)
+  for (uint32_t c0 = 0; c0 < n; c0 += LZ_THREADS) {
+    const uint32_t i = c0 + t;
+    const uint32_t x = i < n ? tk[i] : 0;
+    const bool match = (x & TOK_MATCH) != 0;
+    const uint32_t len = i >= n ? 0 : match ? (x >> 16) & 0x1ff : 1;
+    uint32_t chunk_len;
+    const uint32_t off = base + block_scan(len, sm.wsum, &chunk_len);
+    if (i < n && !match) img[off] = (uint8_t)x;
+    bool pending = match;
+    const uint32_t dist = x & 0xffff;
+    // a match may copy once every byte it reads from outside its own output is final:
+    // all bytes below the lowest unresolved match offset are
+    const uint32_t need = off < off - dist + len ? off : off - dist + len;
+    for (;;) {
+      if (pending) atomicMin(&sm.front[r % 3], off);
+      if (t == 0) sm.front[(r + 1) % 3] = 0xffffffffu;
+      __syncthreads();
+      const uint32_t F = sm.front[r % 3];
+      ++r;
+      if (F == 0xffffffffu) break;
+      if (pending && need <= F) {
+        for (uint32_t k = 0; k < len; ++k) img[off + k] = img[off - dist + k];
+        pending = false;
+      }
+    }
+    base += chunk_len;
+    __syncthreads();  // wsum reuse
+  }
+  __syncthreads();
+  // write the image: 16-byte granules aligned to the flat address
+  const uint32_t usize = base;
+  const uint64_t g0 = G & ~15ull;
+  const uint32_t ngran = (sh + usize + 15) / 16;
+  for (uint32_t q = t; q < ngran; q += LZ_THREADS) {
+    const uint32_t lo = q * 16;  // image offset (relative to sm.img) of the granule
+    if (lo >= sh && lo + 16 <= sh + usize) {
+      *reinterpret_cast<uint4 *>(U + g0 + lo) = *reinterpret_cast<const uint4 *>(sm.img + lo);
+    } else {
+      for (uint32_t k = 0; k < 16; ++k) {
+        const uint32_t a = lo + k;
+        if (a >= sh && a < sh + usize) U[g0 + a] = sm.img[a];
+      }
+    }
+  }
 }
 
 }  // namespace
 
-hipError_t launch_inflate(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, uint8_t *U,
+hipError_t launch_inflate(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, uint32_t *tok, uint8_t *U,
                           hipStream_t stream) {
   if (nblocks == 0) return hipSuccess;
   const uint64_t grid = (nblocks + WAVES - 1) / WAVES;
-  hipLaunchKernelGGL(k_inflate, dim3((uint32_t)grid), dim3(WAVES * WAVE), 0, stream, comp, blocks,
-                     nblocks, U);
+  hipLaunchKernelGGL(k_huff, dim3((uint32_t)grid), dim3(WAVES * WAVE), 0, stream, comp, blocks, nblocks, tok);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_lz, dim3((uint32_t)nblocks), dim3(LZ_THREADS), 0, stream, blocks, nblocks,
+                     (const uint32_t *)tok, U);
   return hipGetLastError();
 }
 

@@ -82,7 +82,7 @@ struct sbh_shard {
   bool indexed = false;
   uint64_t index_start = 0, nblocks = 0, utotal = 0;
   DBuf<uint64_t> b_cstart, b_ustart, usz;
-  DBuf<uint32_t> b_csize, b_hsize, b_usize, b_flags, b_status;
+  DBuf<uint32_t> b_csize, b_hsize, b_usize, b_flags, b_status, b_ntok;
   DBuf<uint64_t> counts, offs, cand, v, rank, tmp;
   DBuf<int64_t> J0, J1;
   DBuf<uint8_t> on;
@@ -93,6 +93,7 @@ struct sbh_shard {
   // inflate
   bool inflated = false;
   DBuf<uint8_t> U;
+  DBuf<uint32_t> tok;  // LZ77 tokens between k_huff and k_lz (4 B per flat byte)
   // checker
   DBuf<int32_t> ctg;
   int32_t nctg = -1;
@@ -111,7 +112,7 @@ struct sbh_shard {
   double stage_ms[4] = {0, 0, 0, 0};
 
   DevBlocks dev_blocks() {
-    return DevBlocks{b_cstart.p, b_csize.p, b_hsize.p, b_usize.p, b_ustart.p, b_flags.p, b_status.p};
+    return DevBlocks{b_cstart.p, b_csize.p, b_hsize.p, b_usize.p, b_ustart.p, b_flags.p, b_status.p, b_ntok.p};
   }
 };
 
@@ -240,6 +241,8 @@ int sbh_shard_destroy(sbh_shard *sh) {
   sh->b_cstart.release(); sh->b_ustart.release(); sh->usz.release();
   sh->b_csize.release(); sh->b_hsize.release(); sh->b_usize.release(); sh->b_flags.release();
   sh->b_status.release();
+  sh->b_ntok.release();
+  sh->tok.release();
   sh->counts.release(); sh->offs.release(); sh->cand.release(); sh->v.release(); sh->rank.release();
   sh->tmp.release(); sh->J0.release(); sh->J1.release(); sh->on.release(); sh->d_seg.release();
   sh->U.release(); sh->ctg.release(); sh->bits.release(); sh->words.release(); sh->close_pos.release();
@@ -325,6 +328,7 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
     HIPCHK(ctx, sh->b_usize.ensure(nc));
     HIPCHK(ctx, sh->b_flags.ensure(nc));
     HIPCHK(ctx, sh->b_status.ensure(nc));
+    HIPCHK(ctx, sh->b_ntok.ensure(nc));
     HIPCHK(ctx, build_chain(sh->comp.p, n, sh->cand.p, nc, sh->J0.p, sh->J1.p, sh->on.p, sh->v.p, sh->rank.p,
                             sh->tmp.p, sh->dev_blocks(), sh->usz.p, &nchain, st));
     HIPCHK(ctx, scan_exclusive_u64(sh->usz.p, sh->b_ustart.p, nchain, sh->tmp.p, st));
@@ -397,9 +401,10 @@ int sbh_inflate(sbh_shard *sh, uint64_t *bad_block) {
   if (rc) return rc;
   hipStream_t st = ctx->stream;
   HIPCHK(ctx, sh->U.ensure(sh->utotal + sh->pad));
+  HIPCHK(ctx, sh->tok.ensure(sh->utotal + 64));
   HIPCHK(ctx, hipMemsetAsync(sh->U.p + sh->utotal, 0, sh->pad, st));
   mark(sh, 2);
-  HIPCHK(ctx, launch_inflate(sh->comp.p, sh->dev_blocks(), sh->nblocks, sh->U.p, st));
+  HIPCHK(ctx, launch_inflate(sh->comp.p, sh->dev_blocks(), sh->nblocks, sh->tok.p, sh->U.p, st));
   mark(sh, 3);
   std::vector<uint32_t> status(sh->nblocks);
   if (sh->nblocks) HIPCHK(ctx, hipMemcpyAsync(status.data(), sh->b_status.p, sh->nblocks * 4, hipMemcpyDeviceToHost, st));

@@ -20,20 +20,22 @@ struct DevBlocks {
   uint32_t *usize;   // ISIZE (0 for an empty block)
   uint64_t *ustart;  // flat offset of the block's first uncompressed byte
   uint32_t *flags;   // BLK_* bits
-  uint32_t *status;  // inflate status per block (SBH_OK / SBH_E_INFLATE_*)
+  uint32_t *status;  // inflate status per block (INF_*)
+  uint32_t *ntok;    // LZ77 tokens k_huff emitted for the block (k_lz input)
 };
 
 constexpr uint32_t BLK_EMPTY = 1u;     // dataLength == 2: the stream ends here
 constexpr uint32_t BLK_TRUNCATED = 2u;  // block runs past the resident bytes
 
-// Inflate status codes per block (written by k_inflate).
+// Inflate status codes per block (written by k_huff).
 constexpr uint32_t INF_OK = 0;
 constexpr uint32_t INF_SIZE = 1;      // fewer than ISIZE bytes produced
 constexpr uint32_t INF_DATA = 2;      // DataFormatException (zlib Z_DATA_ERROR)
 constexpr uint32_t INF_BAD_ISIZE = 3; // ISIZE outside [0, 65536]
 
 // Launchers (defined in the .hip files, called from sbh_api.hip).
+// tok: scratch of >= 4 B per flat byte (block b's tokens at tok[ustart_b ...]).
 hipError_t launch_inflate(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks,
-                          uint8_t *U, hipStream_t stream);
+                          uint32_t *tok, uint8_t *U, hipStream_t stream);
 
 }  // namespace sbh

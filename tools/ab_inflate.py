@@ -35,6 +35,7 @@ def child(lib, records, reps):
             r = sh.run(0, data.size)
             times.append(sh.stage_times())
         sh.index(0)
+        sh.inflate()
         h = hashlib.sha1(sh.read_flat().tobytes()).hexdigest()
         t = np.median(np.asarray(times), axis=0).tolist()
         print(json.dumps({"lib": os.path.basename(lib or "in-tree"), "comp": int(data.size),
