@@ -234,23 +234,183 @@ struct Bits {
 
 // Tokens are gathered one per lane in a VGPR and stored 64 at a time.
 struct TokOut {
-  uint32_t *__restrict__ dst;  // tok + ustart of the block
-  uint32_t batch;              // VGPR: lane k = token bst + k
-  uint32_t nt, bst;            // tokens emitted / tokens stored
+  uint32_t *__restrict__ dst;  // next unstored token slot (wave-uniform)
+  uint32_t batch;              // VGPR: lane k = pending token k
+  uint32_t pend;               // tokens pending in batch
 
   __device__ __forceinline__ void emit(uint32_t t, uint32_t lane) {
-    batch = lane == nt - bst ? t : batch;
-    ++nt;
-    if (nt - bst == WAVE) {
-      dst[bst + lane] = batch;
-      bst = nt;
+    batch = lane == pend ? t : batch;
+    if (++pend == WAVE) {
+      dst[lane] = batch;
+      dst += WAVE;
+      pend = 0;
     }
   }
   __device__ __forceinline__ void drain(uint32_t lane) {
-    if (lane < nt - bst) dst[bst + lane] = batch;
-    bst = nt;
+    if (lane < pend) dst[lane] = batch;
+    dst += pend;
+    pend = 0;
   }
 };
+
+#ifndef SBH_HOT_ASM
+#define SBH_HOT_ASM 1
+#endif
+
+// The symbol hot loop in hand-written SALU code.  The compiler's structurized version
+// of the same loop spends ~60 scalar instructions per symbol on phi copies; the
+// scalar unit is shared by the CU's four SIMDs, so scalar instructions per symbol
+// are the decoder's throughput.  Runs while a whole symbol (<= 48 bits) is
+// available and a whole match fits (idx <= hot, out <= olim); exits with
+//   reason 0: bound reached, or a literal/length code that is not a plain
+//             literal/length in the primary table (EOB, long code, invalid): nothing
+//             of that symbol consumed;
+//   reason 2: length consumed (plen), its distance code needs the careful path;
+//   reason 3: distance too far back (DataFormatException).
+// The bit buffer may hold valid stream bits above cnt (s_load_dwordx2 refill):
+// later refills OR the same bits in again.  Fixed registers s[60:81] hold the loop
+// state so 64-bit pairs can be addressed by halves.
+__device__ __forceinline__ void hot_loop(uint64_t &buf, uint32_t &cnt, uint32_t &idx, uint32_t &out,
+                                         TokOut &to, uint32_t &reason, uint32_t &plen, const uint32_t *c32,
+                                         uint32_t hot, uint32_t olim, uint32_t litb, uint32_t distb,
+                                         uint32_t lane4) {
+  uint64_t dst = reinterpret_cast<uint64_t>(to.dst);
+  uint32_t va, ve;
+  asm volatile(
+      "s_mov_b64 s[60:61], %[buf]\n\t"
+      "s_mov_b64 s[64:65], %[c32]\n\t"
+      "s_mov_b64 s[66:67], %[dst]\n\t"
+      "s_mov_b32 s68, %[cnt]\n\t"
+      "s_mov_b32 s69, %[idx]\n\t"
+      "s_mov_b32 s70, %[hot]\n\t"
+      "s_mov_b32 s71, %[out]\n\t"
+      "s_mov_b32 s72, %[olim]\n\t"
+      "s_mov_b32 s81, m0\n\t"
+      "s_mov_b32 m0, %[pend]\n\t"
+      "s_mov_b32 s74, %[litb]\n\t"
+      "s_mov_b32 s75, %[distb]\n\t"
+      "s_mov_b32 s79, 0\n\t"
+      "s_mov_b32 s80, 0\n"
+      "L_top_%=:\n\t"
+      "s_cmp_gt_u32 s69, s70\n\t"
+      "s_cbranch_scc1 L_exit_%=\n\t"
+      "s_cmp_gt_u32 s71, s72\n\t"
+      "s_cbranch_scc1 L_exit_%=\n\t"
+      "s_cmp_gt_u32 s68, 32\n\t"
+      "s_cbranch_scc1 L_lit_%=\n\t"
+      "s_lshl_b32 s77, s69, 2\n\t"
+      "s_load_dwordx2 s[62:63], s[64:65], s77\n\t"
+      "s_add_u32 s69, s69, 1\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_lshl_b64 s[62:63], s[62:63], s68\n\t"
+      "s_or_b64 s[60:61], s[60:61], s[62:63]\n\t"
+      "s_add_u32 s68, s68, 32\n"
+      "L_lit_%=:\n\t"
+      "s_and_b32 s77, s60, %[lmask]\n\t"
+      "s_lshl_b32 s77, s77, 2\n\t"
+      "s_add_u32 s77, s77, s74\n\t"
+      "v_mov_b32 %[va], s77\n\t"
+      "ds_read_b32 %[ve], %[va]\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_nop 0\n\t"
+      "v_readfirstlane_b32 s76, %[ve]\n\t"
+      "s_and_b32 s77, s76, 31\n\t"
+      "s_and_b32 s78, s76, 0xe0\n\t"
+      "s_cbranch_scc1 L_nonlit_%=\n\t"
+      // literal
+      "s_lshr_b64 s[60:61], s[60:61], s77\n\t"
+      "s_sub_u32 s68, s68, s77\n\t"
+      "s_bfe_u32 s78, s76, 0x80008\n\t"
+      "v_writelane_b32 %[batch], s78, m0\n\t"
+      "s_add_u32 s71, s71, 1\n\t"
+      "s_add_u32 m0, m0, 1\n\t"
+      "s_cmp_eq_u32 m0, 64\n\t"
+      "s_cbranch_scc0 L_top_%=\n"
+      "L_store_%=:\n\t"
+      "global_store_dword %[lane4], %[batch], s[66:67]\n\t"
+      "s_add_u32 s66, s66, 256\n\t"
+      "s_addc_u32 s67, s67, 0\n\t"
+      "s_mov_b32 m0, 0\n\t"
+      "s_branch L_top_%=\n"
+      "L_nonlit_%=:\n\t"
+      "s_cmp_eq_u32 s78, 0x20\n\t"
+      "s_cbranch_scc0 L_exit_%=\n\t"
+      // length: drop code, add extra bits
+      "s_lshr_b64 s[60:61], s[60:61], s77\n\t"
+      "s_sub_u32 s68, s68, s77\n\t"
+      "s_bfe_u32 s77, s76, 0x80008\n\t"
+      "s_bfm_b32 s78, s77, 0\n\t"
+      "s_and_b32 s78, s78, s60\n\t"
+      "s_lshr_b32 s76, s76, 16\n\t"
+      "s_add_u32 s80, s76, s78\n\t"
+      "s_lshr_b64 s[60:61], s[60:61], s77\n\t"
+      "s_sub_u32 s68, s68, s77\n\t"
+      "s_cmp_gt_u32 s68, 32\n\t"
+      "s_cbranch_scc1 L_dist_%=\n\t"
+      "s_lshl_b32 s77, s69, 2\n\t"
+      "s_load_dwordx2 s[62:63], s[64:65], s77\n\t"
+      "s_add_u32 s69, s69, 1\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_lshl_b64 s[62:63], s[62:63], s68\n\t"
+      "s_or_b64 s[60:61], s[60:61], s[62:63]\n\t"
+      "s_add_u32 s68, s68, 32\n"
+      "L_dist_%=:\n\t"
+      "s_and_b32 s77, s60, %[dmask]\n\t"
+      "s_lshl_b32 s77, s77, 2\n\t"
+      "s_add_u32 s77, s77, s75\n\t"
+      "v_mov_b32 %[va], s77\n\t"
+      "ds_read_b32 %[ve], %[va]\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_nop 0\n\t"
+      "v_readfirstlane_b32 s76, %[ve]\n\t"
+      "s_and_b32 s78, s76, 0xe0\n\t"
+      "s_cmp_eq_u32 s78, 0x80\n\t"
+      "s_cbranch_scc0 L_pend_%=\n\t"
+      "s_and_b32 s77, s76, 31\n\t"
+      "s_lshr_b64 s[60:61], s[60:61], s77\n\t"
+      "s_sub_u32 s68, s68, s77\n\t"
+      "s_bfe_u32 s77, s76, 0x80008\n\t"
+      "s_bfm_b32 s78, s77, 0\n\t"
+      "s_and_b32 s78, s78, s60\n\t"
+      "s_lshr_b32 s76, s76, 16\n\t"
+      "s_add_u32 s78, s76, s78\n\t"
+      "s_lshr_b64 s[60:61], s[60:61], s77\n\t"
+      "s_sub_u32 s68, s68, s77\n\t"
+      "s_cmp_gt_u32 s78, s71\n\t"
+      "s_cbranch_scc1 L_far_%=\n\t"
+      "s_lshl_b32 s77, s80, 16\n\t"
+      "s_or_b32 s77, s77, s78\n\t"
+      "s_bitset1_b32 s77, 31\n\t"
+      "v_writelane_b32 %[batch], s77, m0\n\t"
+      "s_add_u32 s71, s71, s80\n\t"
+      "s_add_u32 m0, m0, 1\n\t"
+      "s_cmp_eq_u32 m0, 64\n\t"
+      "s_cbranch_scc0 L_top_%=\n\t"
+      "s_branch L_store_%=\n"
+      "L_pend_%=:\n\t"
+      "s_mov_b32 s79, 2\n\t"
+      "s_branch L_exit_%=\n"
+      "L_far_%=:\n\t"
+      "s_mov_b32 s79, 3\n"
+      "L_exit_%=:\n\t"
+      "s_mov_b64 %[buf], s[60:61]\n\t"
+      "s_mov_b64 %[dst], s[66:67]\n\t"
+      "s_mov_b32 %[cnt], s68\n\t"
+      "s_mov_b32 %[idx], s69\n\t"
+      "s_mov_b32 %[out], s71\n\t"
+      "s_mov_b32 %[pend], m0\n\t"
+      "s_mov_b32 m0, s81\n\t"
+      "s_mov_b32 %[reason], s79\n\t"
+      "s_mov_b32 %[plen], s80\n\t"
+      : [buf] "+s"(buf), [dst] "+s"(dst), [cnt] "+s"(cnt), [idx] "+s"(idx), [out] "+s"(out),
+        [pend] "+s"(to.pend), [reason] "=s"(reason), [plen] "=s"(plen), [batch] "+v"(to.batch),
+        [va] "=&v"(va), [ve] "=&v"(ve)
+      : [c32] "s"(c32), [hot] "s"(hot), [olim] "s"(olim), [litb] "s"(litb), [distb] "s"(distb),
+        [lane4] "v"(lane4), [lmask] "i"((1 << LIT_FAST) - 1), [dmask] "i"((1 << DIST_FAST) - 1)
+      : "memory", "scc", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71",
+        "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81");
+  to.dst = reinterpret_cast<uint32_t *>(dst);
+}
 
 __global__ __launch_bounds__(WAVES *WAVE) void k_huff(const uint8_t *__restrict__ comp, DevBlocks bl,
                                                        uint64_t nblocks, uint32_t *__restrict__ tok) {
@@ -292,8 +452,10 @@ __global__ __launch_bounds__(WAVES *WAVE) void k_huff(const uint8_t *__restrict_
   TokOut to;
   to.dst = tok + G;
   to.batch = 0;
-  to.nt = 0;
-  to.bst = 0;
+  to.pend = 0;
+  const uint32_t lit_lds = (uint32_t)reinterpret_cast<uintptr_t>(sm.lit);
+  const uint32_t dist_lds = (uint32_t)reinterpret_cast<uintptr_t>(sm.dist);
+  const uint32_t olim = usize >= 258 ? usize - 258 : 0;
 
   uint32_t out = 0;  // bytes produced
   uint32_t status = INF_OK;
@@ -320,9 +482,8 @@ __global__ __launch_bounds__(WAVES *WAVE) void k_huff(const uint8_t *__restrict_
       if (n > usize - out) n = usize - out;
       const uint8_t *src = comp + (uint64_t)br.a0 * 4 + (p0 >> 3);
       to.drain(lane);
-      for (uint32_t i = lane; i < n; i += WAVE) to.dst[to.nt + i] = src[i];
-      to.nt += n;
-      to.bst = to.nt;
+      for (uint32_t i = lane; i < n; i += WAVE) to.dst[i] = src[i];
+      to.dst += n;
       out += n;
       if (n < len) break;  // output full or input exhausted
       br.seek(p0 + len * 8);
@@ -414,9 +575,22 @@ __global__ __launch_bounds__(WAVES *WAVE) void k_huff(const uint8_t *__restrict_
 
     // ---- symbols ----
     for (;;) {
-      // Hot loop: no input/output bound checks while a whole symbol is available and
-      // a whole match fits; rare events (EOB, long codes, bad codes) fall through to
-      // the careful single-symbol path below.
+      uint32_t mlen = 0;
+      bool have_len = false;
+#if SBH_HOT_ASM
+      if (usize >= 258 && br.idx <= hot_idx) {
+        uint32_t reason, plen;
+        hot_loop(br.buf, br.cnt, br.idx, out, to, reason, plen, br.c32, uni(hot_idx), uni(olim), uni(lit_lds), uni(dist_lds),
+                 lane * 4);
+        if (reason == 3) { status = INF_DATA; done = true; break; }  // too far back
+        if (reason == 2) {
+          mlen = plen;
+          have_len = true;
+        }
+      }
+#else
+      // C++ hot loop (A/B reference for the asm one): no input/output bound checks
+      // while a whole symbol is available and a whole match fits
       while (br.idx <= hot_idx && out + 258 <= usize) {
         br.refill();
         const uint32_t e = uni(sm.lit[(uint32_t)br.buf & ((1u << LIT_FAST) - 1)]);
@@ -428,72 +602,77 @@ __global__ __launch_bounds__(WAVES *WAVE) void k_huff(const uint8_t *__restrict_
         } else if (kind == K_LEN) {
           br.drop(e & 31);
           const uint32_t lx = (e >> 8) & 0xff;
-          const uint32_t mlen = (e >> 16) + br.take(lx);
+          const uint32_t ml = (e >> 16) + br.take(lx);
           br.refill();
           uint32_t d = uni(sm.dist[(uint32_t)br.buf & ((1u << DIST_FAST) - 1)]);
-          if (((d >> 5) & 7) == K_SLOW) d = uni(slow_decode(sm, br.buf, 1));
-          if (((d >> 5) & 7) != K_DIST) { status = INF_DATA; done = true; break; }
+          if (((d >> 5) & 7) != K_DIST) {
+            mlen = ml;
+            have_len = true;
+            break;
+          }
           br.drop(d & 31);
           const uint32_t dist = (d >> 16) + br.take((d >> 8) & 0xff);
           if (dist > out) { status = INF_DATA; done = true; break; }  // too far back
-          to.emit(TOK_MATCH | (mlen << 16) | dist, lane);
-          out += mlen;
+          to.emit(TOK_MATCH | (ml << 16) | dist, lane);
+          out += ml;
         } else {
           break;
         }
       }
       if (done) break;
+#endif
       // careful path: one symbol with every bound checked (zlib semantics at the edges)
-      br.refill();
-      uint32_t e = uni(sm.lit[br.peek(LIT_FAST)]);
-      uint32_t kind = (e >> 5) & 7;
-      if (kind == K_SLOW) {
-        e = uni(slow_decode(sm, br.buf, 0));
-        kind = (e >> 5) & 7;
-      }
-      const uint32_t L = e & 31;
-      if (kind == K_BAD) {
-        if (br.avail(1)) status = INF_DATA;
-        done = true;
-        break;
-      }
-      if (!br.avail(L)) { done = true; break; }
-      br.drop(L);
-      if (kind == K_LIT) {
-        if (out == usize) { done = true; break; }
-        to.emit((e >> 8) & 0xff, lane);
-        ++out;
-      } else if (kind == K_EOB) {
-        break;
-      } else {  // length
-        const uint32_t lx = (e >> 8) & 0xff;
-        if (!br.avail(lx)) { done = true; break; }
-        const uint32_t mlen = (e >> 16) + br.take(lx);
+      if (!have_len) {
         br.refill();
-        uint32_t d = uni(sm.dist[br.peek(DIST_FAST)]);
-        uint32_t dk = (d >> 5) & 7;
-        if (dk == K_SLOW) {
-          d = uni(slow_decode(sm, br.buf, 1));
-          dk = (d >> 5) & 7;
+        uint32_t e = uni(sm.lit[br.peek(LIT_FAST)]);
+        uint32_t kind = (e >> 5) & 7;
+        if (kind == K_SLOW) {
+          e = uni(slow_decode(sm, br.buf, 0));
+          kind = (e >> 5) & 7;
         }
-        if (dk == K_BAD) {
+        const uint32_t L = e & 31;
+        if (kind == K_BAD) {
           if (br.avail(1)) status = INF_DATA;
           done = true;
           break;
         }
-        const uint32_t DL = d & 31;
-        if (!br.avail(DL)) { done = true; break; }
-        br.drop(DL);
-        const uint32_t dx = (d >> 8) & 0xff;
-        if (!br.avail(dx)) { done = true; break; }
-        const uint32_t dist = (d >> 16) + br.take(dx);
-        if (out == usize) { done = true; break; }  // zlib stops at MATCH when full
-        if (dist > out) { status = INF_DATA; done = true; break; }  // too far back
-        const uint32_t n = mlen < usize - out ? mlen : usize - out;
-        to.emit(TOK_MATCH | (n << 16) | dist, lane);
-        out += n;
-        if (n < mlen) { done = true; break; }  // output full mid-match
+        if (!br.avail(L)) { done = true; break; }
+        br.drop(L);
+        if (kind == K_LIT) {
+          if (out == usize) { done = true; break; }
+          to.emit((e >> 8) & 0xff, lane);
+          ++out;
+          continue;
+        }
+        if (kind == K_EOB) break;
+        const uint32_t lx = (e >> 8) & 0xff;
+        if (!br.avail(lx)) { done = true; break; }
+        mlen = (e >> 16) + br.take(lx);
       }
+      br.refill();
+      uint32_t d = uni(sm.dist[br.peek(DIST_FAST)]);
+      uint32_t dk = (d >> 5) & 7;
+      if (dk == K_SLOW) {
+        d = uni(slow_decode(sm, br.buf, 1));
+        dk = (d >> 5) & 7;
+      }
+      if (dk == K_BAD) {
+        if (br.avail(1)) status = INF_DATA;
+        done = true;
+        break;
+      }
+      const uint32_t DL = d & 31;
+      if (!br.avail(DL)) { done = true; break; }
+      br.drop(DL);
+      const uint32_t dx = (d >> 8) & 0xff;
+      if (!br.avail(dx)) { done = true; break; }
+      const uint32_t dist = (d >> 16) + br.take(dx);
+      if (out == usize) { done = true; break; }  // zlib stops at MATCH when full
+      if (dist > out) { status = INF_DATA; done = true; break; }  // too far back
+      const uint32_t n = mlen < usize - out ? mlen : usize - out;
+      to.emit(TOK_MATCH | (n << 16) | dist, lane);
+      out += n;
+      if (n < mlen) { done = true; break; }  // output full mid-match
     }
     if (done || last) break;
   }
@@ -501,7 +680,7 @@ __global__ __launch_bounds__(WAVES *WAVE) void k_huff(const uint8_t *__restrict_
   if (status == INF_OK && out != usize) status = INF_SIZE;
   if (lane == 0) {
     bl.status[b] = status;
-    bl.ntok[b] = to.nt;
+    bl.ntok[b] = (uint32_t)(to.dst - (tok + G));
   }
 }
 
