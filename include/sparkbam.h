@@ -195,8 +195,9 @@ int sbh_run_shard(sbh_shard *sh, uint64_t index_start, uint64_t own_end_file,
                   int32_t reads_to_check, int32_t max_read_size, sbh_shard_result *res);
 
 /* Device time (ms, HIP events on the context stream) of the stages of the last
- * sbh_run_shard: [0] index, [1] inflate (k_inflate), [2] eager check (k_eager),
- * [3] record split/count.  Returns the number of stages written (<= cap). */
+ * sbh_run_shard: [0] index, [1] inflate (k_huff + k_lz), [2] eager check (k_eager),
+ * [3] record split/count, [4] k_huff alone, [5] k_lz alone.  Returns the number of
+ * stages written (<= cap, at most 6). */
 int sbh_stage_times(sbh_shard *sh, double *ms, int32_t cap);
 
 #ifdef __cplusplus

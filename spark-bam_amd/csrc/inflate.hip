@@ -834,15 +834,17 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
 
 }  // namespace
 
-hipError_t launch_inflate(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, uint32_t *tok, uint8_t *U,
-                          hipStream_t stream) {
+hipError_t launch_huff(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, uint32_t *tok,
+                       hipStream_t stream) {
   if (nblocks == 0) return hipSuccess;
   const uint64_t grid = (nblocks + WAVES - 1) / WAVES;
   hipLaunchKernelGGL(k_huff, dim3((uint32_t)grid), dim3(WAVES * WAVE), 0, stream, comp, blocks, nblocks, tok);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_lz, dim3((uint32_t)nblocks), dim3(LZ_THREADS), 0, stream, blocks, nblocks,
-                     (const uint32_t *)tok, U);
+  return hipGetLastError();
+}
+
+hipError_t launch_lz(DevBlocks blocks, uint64_t nblocks, const uint32_t *tok, uint8_t *U, hipStream_t stream) {
+  if (nblocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_lz, dim3((uint32_t)nblocks), dim3(LZ_THREADS), 0, stream, blocks, nblocks, tok, U);
   return hipGetLastError();
 }
 

@@ -107,9 +107,9 @@ struct sbh_shard {
   DBuf<unsigned long long> ctr;  // scratch counters
   unsigned long long *h_ctr = nullptr;  // pinned mirror
   uint64_t pad = 4096;
-  hipEvent_t ev[8] = {};
+  hipEvent_t ev[9] = {};
   bool ev_ok = false, timing = false;
-  double stage_ms[4] = {0, 0, 0, 0};
+  double stage_ms[6] = {0, 0, 0, 0, 0, 0};
 
   DevBlocks dev_blocks() {
     return DevBlocks{b_cstart.p, b_csize.p, b_hsize.p, b_usize.p, b_ustart.p, b_flags.p, b_status.p, b_ntok.p};
@@ -404,7 +404,9 @@ int sbh_inflate(sbh_shard *sh, uint64_t *bad_block) {
   HIPCHK(ctx, sh->tok.ensure(sh->utotal + 64));
   HIPCHK(ctx, hipMemsetAsync(sh->U.p + sh->utotal, 0, sh->pad, st));
   mark(sh, 2);
-  HIPCHK(ctx, launch_inflate(sh->comp.p, sh->dev_blocks(), sh->nblocks, sh->tok.p, sh->U.p, st));
+  HIPCHK(ctx, launch_huff(sh->comp.p, sh->dev_blocks(), sh->nblocks, sh->tok.p, st));
+  mark(sh, 7);
+  HIPCHK(ctx, launch_lz(sh->dev_blocks(), sh->nblocks, sh->tok.p, sh->U.p, st));
   mark(sh, 3);
   std::vector<uint32_t> status(sh->nblocks);
   if (sh->nblocks) HIPCHK(ctx, hipMemcpyAsync(status.data(), sh->b_status.p, sh->nblocks * 4, hipMemcpyDeviceToHost, st));
@@ -797,8 +799,8 @@ int sbh_run_shard(sbh_shard *sh, uint64_t index_start, uint64_t own_end_file, in
   res->exit_flat = E;
   if (sh->ev_ok) {
     (void)hipEventSynchronize(sh->ev[6]);
-    const int from[4] = {0, 2, 4, 5}, to[4] = {1, 3, 5, 6};
-    for (int i = 0; i < 4; ++i) {
+    const int from[6] = {0, 2, 4, 5, 2, 7}, to[6] = {1, 3, 5, 6, 7, 3};
+    for (int i = 0; i < 6; ++i) {
       float ms = 0;
       (void)hipEventElapsedTime(&ms, sh->ev[from[i]], sh->ev[to[i]]);
       sh->stage_ms[i] = ms;
@@ -809,7 +811,7 @@ int sbh_run_shard(sbh_shard *sh, uint64_t index_start, uint64_t own_end_file, in
 
 int sbh_stage_times(sbh_shard *sh, double *ms, int32_t cap) {
   if (!sh || !ms || cap < 0) return 0;
-  int n = cap < 4 ? cap : 4;
+  int n = cap < 6 ? cap : 6;
   for (int i = 0; i < n; ++i) ms[i] = sh->stage_ms[i];
   return n;
 }

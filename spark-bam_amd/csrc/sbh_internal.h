@@ -34,8 +34,11 @@ constexpr uint32_t INF_DATA = 2;      // DataFormatException (zlib Z_DATA_ERROR)
 constexpr uint32_t INF_BAD_ISIZE = 3; // ISIZE outside [0, 65536]
 
 // Launchers (defined in the .hip files, called from sbh_api.hip).
-// tok: scratch of >= 4 B per flat byte (block b's tokens at tok[ustart_b ...]).
-hipError_t launch_inflate(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks,
-                          uint32_t *tok, uint8_t *U, hipStream_t stream);
+// Inflate = k_huff (Huffman decode -> LZ77 tokens, block status) then k_lz (tokens ->
+// flat bytes).  tok: scratch of >= 4 B per flat byte (block b's tokens at tok[ustart_b ...]).
+hipError_t launch_huff(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, uint32_t *tok,
+                       hipStream_t stream);
+hipError_t launch_lz(DevBlocks blocks, uint64_t nblocks, const uint32_t *tok, uint8_t *U,
+                     hipStream_t stream);
 
 }  // namespace sbh

@@ -201,7 +201,8 @@ class Shard:
         return {f: getattr(r, f) for f, _ in SbhShardResult._fields_}
 
     def stage_times(self):
-        """[index, inflate, eager, records] device ms of the last run() (HIP events)."""
-        ms = (C.c_double * 4)()
-        n = lib().sbh_stage_times(self.h, ms, 4)
+        """[index, inflate, eager, records, k_huff, k_lz] device ms of the last run()
+        (HIP events on the context stream)."""
+        ms = (C.c_double * 6)()
+        n = lib().sbh_stage_times(self.h, ms, 6)
         return list(ms[:n])
