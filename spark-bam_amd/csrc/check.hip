@@ -203,12 +203,24 @@ struct Segs {
   uint32_t open_last;  // last segment ends at the resident end, not at a stream end
 };
 
-// Stage [s0, s0 + STAGE) of U into LDS (dword loads, zero past u_total).
-__device__ __forceinline__ void stage(uint32_t *lds32, const uint8_t *U, uint64_t s0, uint64_t u_pad) {
-  const uint32_t *g = reinterpret_cast<const uint32_t *>(U + s0);
-  for (uint32_t i = threadIdx.x; i < STAGE / 4; i += T) {
-    const uint64_t q = s0 + 4ull * i;
-    lds32[i] = q + 4 <= u_pad ? g[i] : 0u;
+// Stage NV 16-byte vectors of U from s0 (16-aligned) into LDS: every load is issued
+// before any LDS store (one HBM latency per workgroup, not one per iteration).
+// Vectors not wholly below u_pad stage as zeros (u_pad - u_total >= 16: only pad).
+template <uint32_t NV>
+__device__ __forceinline__ void stage_vec(uint4 *lds, const uint8_t *U, uint64_t s0, uint64_t u_pad) {
+  constexpr uint32_t R = (NV + T - 1) / T;
+  const uint4 *g = reinterpret_cast<const uint4 *>(U + s0);
+  uint4 v[R];
+#pragma unroll
+  for (uint32_t r = 0; r < R; ++r) {
+    const uint32_t i = threadIdx.x + r * T;
+    v[r] = make_uint4(0, 0, 0, 0);
+    if (i < NV && s0 + 16ull * i + 16 <= u_pad) v[r] = g[i];
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < R; ++r) {
+    const uint32_t i = threadIdx.x + r * T;
+    if (i < NV) lds[i] = v[r];
   }
 }
 
@@ -234,8 +246,13 @@ struct EagerOut {
   unsigned long long *min_unknown;
 };
 
-constexpr uint32_t EW = 8192;          // eager window: TILE positions + look-ahead
-constexpr uint32_t ESTAGE = EW + 512;  // staged bytes (records near the end fit)
+#ifndef SBH_ETILE
+#define SBH_ETILE 16384
+#endif
+constexpr uint32_t ETILE = SBH_ETILE;     // eager tile: positions per workgroup
+constexpr uint32_t ELA = 4096;            // look-ahead: chains of short reads stay inside
+constexpr uint32_t EW = ETILE + ELA;      // eager window: single-record predicate evaluated here
+constexpr uint32_t ESTAGE = EW + 512;     // staged bytes (records near the end fit)
 
 // Single-record eager predicate at q, with cur == start == q, reading only the
 // staged window: 0 fail, 1 pass, 2 cannot decide from the window (or EOF edge).
@@ -280,86 +297,109 @@ __device__ __forceinline__ uint32_t one_record(const Src &s, uint64_t q, uint64_
 //     HBM/L2.  Semantics are exactly eager.Checker.apply's.
 __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint64_t u_pad, uint64_t begin,
                                              uint64_t end, Segs sg, Ctg c, int32_t rtc, EagerOut o) {
-  __shared__ uint32_t lds32[ESTAGE / 4 + 2];
-  __shared__ uint32_t ok[EW / 32], nrm[EW / 32], und[EW / 32], bits[TILE / 32];
+  constexpr uint32_t NV = (ESTAGE + 32) / 16;
+  __shared__ uint4 ldsv[NV];
+  __shared__ uint32_t ok[EW / 32], nrm[EW / 32], und[EW / 32];
   __shared__ uint32_t seg0, ntrue;
-  const uint64_t t0 = begin + (uint64_t)blockIdx.x * TILE;
-  const uint64_t s0 = t0 & ~3ull;
-  {
-    const uint32_t *g = reinterpret_cast<const uint32_t *>(U + s0);
-    for (uint32_t i = threadIdx.x; i < ESTAGE / 4 + 2; i += T) {
-      const uint64_t q = s0 + 4ull * i;
-      lds32[i] = q + 4 <= u_pad ? g[i] : 0u;
-    }
-  }
+  __shared__ uint64_t seg_end0;
+  const uint32_t *lds32 = reinterpret_cast<const uint32_t *>(ldsv);
+  const uint64_t t0 = begin + (uint64_t)blockIdx.x * ETILE;
+  const uint64_t s0 = t0 & ~15ull;
+  stage_vec<NV>(ldsv, U, s0, u_pad);
   for (uint32_t i = threadIdx.x; i < EW / 32; i += T) { ok[i] = 0; nrm[i] = 0; und[i] = 0; }
-  for (uint32_t i = threadIdx.x; i < TILE / 32; i += T) bits[i] = 0;
-  if (threadIdx.x == 0) { seg0 = seg_first(sg, t0); ntrue = 0; }
+  if (threadIdx.x == 0) {
+    const uint32_t k = seg_first(sg, t0);
+    seg0 = k;
+    seg_end0 = sg.end[k];
+    ntrue = 0;
+  }
   __syncthreads();
-  Src s{U, lds32, s0, ESTAGE};
-  // ---- phase A ----
-  for (uint32_t i = threadIdx.x; i < EW; i += T) {
-    const uint64_t q = t0 + i;
-    const uint32_t k = seg_index(sg, q, seg0);
-    uint64_t succ;
-    bool normal;
-    uint32_t r = one_record(s, q, sg.end[k], c, &succ, &normal);
-    if (r == 1) {
-      atomicOr(&ok[i >> 5], 1u << (i & 31));
-      if (normal) atomicOr(&nrm[i >> 5], 1u << (i & 31));
-    } else if (r == 2) {
-      atomicOr(&und[i >> 5], 1u << (i & 31));
+  Src s{U, lds32, s0, ESTAGE};  // >= EW + 15 + 44: every phase-A read is staged
+  const uint32_t k0 = seg0;
+  const uint64_t e0 = seg_end0;  // positions below e0 are in segment k0 (nearly all)
+  // window-relative end of the positions whose first record is wholly inside segment k0
+  const uint32_t fast_end = e0 - t0 >= 36 + (uint64_t)EW ? EW : e0 - t0 >= 36 ? (uint32_t)(e0 - t0 - 36) + 1 : 0;
+  const uint32_t sa = (uint32_t)(t0 - s0);
+  const uint32_t nref1 = (uint32_t)c.n + 1u;
+  // ---- phase A: refID filter on 4 positions per staged dword pair; survivors get the
+  // whole single-record predicate ----
+  for (uint32_t j = threadIdx.x; 4 * j < EW + sa; j += T) {
+    const uint32_t a = lds32[j + 1], b = lds32[j + 2];  // bytes s0 + 4j + 4 .. + 11
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      const int32_t ii = (int32_t)(4 * j + k) - (int32_t)sa;
+      if (ii < 0 || ii >= (int32_t)EW) continue;
+      const uint32_t i = (uint32_t)ii;
+      if (i < fast_end) {
+        const uint32_t ref = __builtin_amdgcn_alignbyte(b, a, k);
+        if (ref + 1u >= nref1) continue;  // refID outside [-1, nContigs): fails first
+      }
+      const uint64_t q = t0 + i;
+      const uint64_t total = q < e0 ? e0 : sg.end[seg_index(sg, q, k0)];
+      uint64_t succ;
+      bool normal;
+      const uint32_t r = one_record(s, q, total, c, &succ, &normal);
+      if (r == 1) {
+        atomicOr(&ok[i >> 5], 1u << (i & 31));
+        if (normal) atomicOr(&nrm[i >> 5], 1u << (i & 31));
+      } else if (r == 2) {
+        atomicOr(&und[i >> 5], 1u << (i & 31));
+      }
     }
   }
   __syncthreads();
-  // ---- phase B ----
+  // ---- phase B: one 32-position word per thread; walk only candidate positions ----
   uint32_t mytrue = 0;
-  for (uint32_t i = threadIdx.x; i < TILE; i += T) {
-    const uint64_t p = t0 + i;
-    if (p >= end) break;
-    const uint32_t k = seg_index(sg, p, seg0);
-    const uint64_t total = sg.end[k];
-    const bool open = sg.open_last && k == sg.n - 1;
-    uint32_t r;
-    const bool ok_p = (ok[i >> 5] >> (i & 31)) & 1;
-    const bool und_p = (und[i >> 5] >> (i & 31)) & 1;
-    if (rtc <= 0 || und_p) {
-      r = eager_at(s, p, total, open, c, rtc);  // exact path (HBM/L2 reads)
-    } else if (!ok_p) {
-      r = 0;  // the first record already fails
-    } else {
-      // walk the chain through the window's ok bits (next record read at nominal)
-      uint64_t q = p;
-      int32_t n = 1;
-      r = 3;  // undecided
-      for (;;) {
-        if (n == rtc) { r = 1; break; }
-        const uint32_t iq = (uint32_t)(q - t0);
-        if (!((nrm[iq >> 5] >> (iq & 31)) & 1)) break;  // cursor past nominal: exact path
-        const uint64_t nxt = q + 4 + (int64_t)(int32_t)s.word_at(q);
-        if (nxt + 36 > total || nxt < t0 || nxt - t0 >= EW) break;  // EOF edge / outside window
-        const uint32_t j = (uint32_t)(nxt - t0);
-        if ((und[j >> 5] >> (j & 31)) & 1) break;
-        if (!((ok[j >> 5] >> (j & 31)) & 1)) { r = 0; break; }
-        q = nxt;
-        ++n;
+  const uint64_t wbase = (uint64_t)blockIdx.x * (ETILE / 32);
+  const uint64_t nwords = (end - begin + 31) / 32;
+  for (uint32_t w = threadIdx.x; w < ETILE / 32; w += T) {
+    if (wbase + w >= nwords) break;
+    uint32_t cand = rtc <= 0 ? ~0u : (ok[w] | und[w]);
+    uint32_t res = 0;
+    while (cand) {
+      const uint32_t bit = __builtin_ctz(cand);
+      cand &= cand - 1;
+      const uint32_t i = 32 * w + bit;
+      const uint64_t p = t0 + i;
+      if (p >= end) break;
+      const uint32_t k = p < e0 ? k0 : seg_index(sg, p, k0);
+      const uint64_t total = sg.end[k];
+      const bool open = sg.open_last && k == sg.n - 1;
+      const bool und_p = (und[w] >> bit) & 1;
+      uint32_t r;
+      if (rtc <= 0 || und_p) {
+        r = eager_at(s, p, total, open, c, rtc);  // exact path (HBM/L2 reads)
+      } else {
+        // walk the chain through the window's ok bits (next record read at nominal)
+        uint64_t q = p;
+        int32_t n = 1;
+        r = 3;  // undecided
+        for (;;) {
+          if (n == rtc) { r = 1; break; }
+          const uint32_t iq = (uint32_t)(q - t0);
+          if (!((nrm[iq >> 5] >> (iq & 31)) & 1)) break;  // cursor past nominal: exact path
+          const uint64_t nxt = q + 4 + (int64_t)(int32_t)s.word_at(q);
+          if (nxt + 36 > total || nxt < t0 || nxt - t0 >= EW) break;  // EOF edge / outside window
+          const uint32_t jn = (uint32_t)(nxt - t0);
+          if ((und[jn >> 5] >> (jn & 31)) & 1) break;
+          if (!((ok[jn >> 5] >> (jn & 31)) & 1)) { r = 0; break; }
+          q = nxt;
+          ++n;
+        }
+        if (r == 3) r = eager_at(s, p, total, open, c, rtc);
       }
-      if (r == 3) r = eager_at(s, p, total, open, c, rtc);
+      if (r == 1) {
+        res |= 1u << bit;
+      } else if (r == 2) {
+        atomicAdd(o.n_unknown, 1ull);
+        atomicMin(o.min_unknown, (unsigned long long)p);
+      }
     }
-    if (r == 1) {
-      atomicOr(&bits[i >> 5], 1u << (i & 31));
-      ++mytrue;
-    } else if (r == 2) {
-      atomicAdd(o.n_unknown, 1ull);
-      atomicMin(o.min_unknown, (unsigned long long)p);
-    }
+    o.bits[wbase + w] = res;
+    mytrue += __popc(res);
   }
   if (mytrue) atomicAdd(&ntrue, mytrue);
   __syncthreads();
-  const uint64_t wbase = (uint64_t)blockIdx.x * (TILE / 32);
-  const uint64_t nwords = (end - begin + 31) / 32;
-  for (uint32_t i = threadIdx.x; i < TILE / 32; i += T)
-    if (wbase + i < nwords) o.bits[wbase + i] = bits[i];
   if (threadIdx.x == 0 && ntrue) atomicAdd(o.n_true, (unsigned long long)ntrue);
 }
 
@@ -378,12 +418,14 @@ struct FullOut {
 
 __global__ __launch_bounds__(T) void k_full(const uint8_t *__restrict__ U, uint64_t u_pad, uint64_t begin,
                                             uint64_t end, Segs sg, Ctg c, int32_t rtc, FullOut o) {
-  __shared__ uint32_t lds32[STAGE / 4];
+  constexpr uint32_t NV = (STAGE + 16 + 15) / 16;
+  __shared__ uint4 ldsv[NV];
   __shared__ uint32_t hist[21 * 19 + 21 * 64];
   __shared__ uint32_t seg0, nsucc;
+  const uint32_t *lds32 = reinterpret_cast<const uint32_t *>(ldsv);
   const uint64_t t0 = begin + (uint64_t)blockIdx.x * TILE;
-  const uint64_t s0 = t0 & ~3ull;
-  stage(lds32, U, s0, u_pad);
+  const uint64_t s0 = t0 & ~15ull;
+  stage_vec<NV>(ldsv, U, s0, u_pad);
   for (uint32_t i = threadIdx.x; i < 21 * 19 + 21 * 64; i += T) hist[i] = 0;
   if (threadIdx.x == 0) { seg0 = seg_first(sg, t0); nsucc = 0; }
   __syncthreads();
@@ -540,7 +582,7 @@ hipError_t launch_eager(const uint8_t *U, uint64_t u_pad, uint64_t begin, uint64
   Segs sg{seg_end, nseg, open_last};
   Ctg c{ctg, nctg};
   EagerOut o{bits, counters, counters + 1, counters + 2};
-  hipLaunchKernelGGL(k_eager, dim3(ngrid(end - begin, TILE)), dim3(T), 0, st, U, u_pad, begin, end, sg, c,
+  hipLaunchKernelGGL(k_eager, dim3(ngrid(end - begin, ETILE)), dim3(T), 0, st, U, u_pad, begin, end, sg, c,
                      rtc, o);
   return hipGetLastError();
 }
