@@ -253,6 +253,7 @@ constexpr uint32_t ETILE = SBH_ETILE;     // eager tile: positions per workgroup
 constexpr uint32_t ELA = 4096;            // look-ahead: chains of short reads stay inside
 constexpr uint32_t EW = ETILE + ELA;      // eager window: single-record predicate evaluated here
 constexpr uint32_t ESTAGE = EW + 512;     // staged bytes (records near the end fit)
+constexpr uint32_t EQ_CHUNK = 4096;       // phase-A positions per survivor-queue round
 
 // Single-record eager predicate at q, with cur == start == q, reading only the
 // staged window: 0 fail, 1 pass, 2 cannot decide from the window (or EOF edge).
@@ -300,11 +301,16 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
   constexpr uint32_t NV = (ESTAGE + 32) / 16;
   __shared__ uint4 ldsv[NV];
   __shared__ uint32_t ok[EW / 32], nrm[EW / 32], und[EW / 32];
-  __shared__ uint32_t seg0, ntrue;
+  __shared__ uint32_t seg0, ntrue, nq;
   __shared__ uint64_t seg_end0;
+  __shared__ uint16_t queue[EQ_CHUNK];
   const uint32_t *lds32 = reinterpret_cast<const uint32_t *>(ldsv);
   const uint64_t t0 = begin + (uint64_t)blockIdx.x * ETILE;
   const uint64_t s0 = t0 & ~15ull;
+#ifdef SBH_EPROBE
+  const uint64_t c0 = __builtin_readcyclecounter();
+  uint32_t nsurv = 0, ncand = 0, nexact = 0;
+#endif
   stage_vec<NV>(ldsv, U, s0, u_pad);
   for (uint32_t i = threadIdx.x; i < EW / 32; i += T) { ok[i] = 0; nrm[i] = 0; und[i] = 0; }
   if (threadIdx.x == 0) {
@@ -312,6 +318,7 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
     seg0 = k;
     seg_end0 = sg.end[k];
     ntrue = 0;
+    nq = 0;
   }
   __syncthreads();
   Src s{U, lds32, s0, ESTAGE};  // >= EW + 15 + 44: every phase-A read is staged
@@ -321,19 +328,41 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
   const uint32_t fast_end = e0 - t0 >= 36 + (uint64_t)EW ? EW : e0 - t0 >= 36 ? (uint32_t)(e0 - t0 - 36) + 1 : 0;
   const uint32_t sa = (uint32_t)(t0 - s0);
   const uint32_t nref1 = (uint32_t)c.n + 1u;
-  // ---- phase A: refID filter on 4 positions per staged dword pair; survivors get the
-  // whole single-record predicate ----
-  for (uint32_t j = threadIdx.x; 4 * j < EW + sa; j += T) {
-    const uint32_t a = lds32[j + 1], b = lds32[j + 2];  // bytes s0 + 4j + 4 .. + 11
+#ifdef SBH_EPROBE
+  const uint64_t c1 = __builtin_readcyclecounter();
+#endif
+  // ---- phase A: refID filter on 4 positions per staged dword pair (every lane busy);
+  // survivors (~3% of BAM positions) are queued in LDS and get the whole single-record
+  // predicate compacted, so one_record never runs with most lanes idle ----
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  for (uint32_t c0p = 0; c0p < EW + sa; c0p += EQ_CHUNK) {
+    for (uint32_t j = c0p / 4 + threadIdx.x; 4 * j < EW + sa && 4 * j < c0p + EQ_CHUNK; j += T) {
+      const uint32_t a = lds32[j + 1], b = lds32[j + 2];  // bytes s0 + 4j + 4 .. + 11
 #pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
-      const int32_t ii = (int32_t)(4 * j + k) - (int32_t)sa;
-      if (ii < 0 || ii >= (int32_t)EW) continue;
-      const uint32_t i = (uint32_t)ii;
-      if (i < fast_end) {
-        const uint32_t ref = __builtin_amdgcn_alignbyte(b, a, k);
-        if (ref + 1u >= nref1) continue;  // refID outside [-1, nContigs): fails first
+      for (uint32_t k = 0; k < 4; ++k) {
+        const int32_t ii = (int32_t)(4 * j + k) - (int32_t)sa;
+        bool surv = ii >= 0 && ii < (int32_t)EW;
+        if (surv && (uint32_t)ii < fast_end) {
+          const uint32_t ref = __builtin_amdgcn_alignbyte(b, a, k);
+          surv = ref + 1u < nref1;  // refID in [-1, nContigs): may pass
+        }
+        const uint64_t m = __ballot(surv);
+        if (m) {
+          uint32_t base = 0;
+          if (lane == (uint32_t)__builtin_ctzll(m)) base = atomicAdd(&nq, (uint32_t)__popcll(m));
+          base = __shfl(base, (int)__builtin_ctzll(m), WAVE);
+          if (surv) queue[base + (uint32_t)__popcll(m & lt_mask)] = (uint16_t)ii;
+        }
       }
+    }
+    __syncthreads();
+    const uint32_t nsv = nq;
+    for (uint32_t x = threadIdx.x; x < nsv; x += T) {
+      const uint32_t i = queue[x];
+#ifdef SBH_EPROBE
+      ++nsurv;
+#endif
       const uint64_t q = t0 + i;
       const uint64_t total = q < e0 ? e0 : sg.end[seg_index(sg, q, k0)];
       uint64_t succ;
@@ -346,8 +375,14 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
         atomicOr(&und[i >> 5], 1u << (i & 31));
       }
     }
+    __syncthreads();
+    if (threadIdx.x == 0) nq = 0;
+    __syncthreads();
   }
   __syncthreads();
+#ifdef SBH_EPROBE
+  const uint64_t c2 = __builtin_readcyclecounter();
+#endif
   // ---- phase B: one 32-position word per thread; walk only candidate positions ----
   uint32_t mytrue = 0;
   const uint64_t wbase = (uint64_t)blockIdx.x * (ETILE / 32);
@@ -367,6 +402,9 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
       const bool open = sg.open_last && k == sg.n - 1;
       const bool und_p = (und[w] >> bit) & 1;
       uint32_t r;
+#ifdef SBH_EPROBE
+      ++ncand;
+#endif
       if (rtc <= 0 || und_p) {
         r = eager_at(s, p, total, open, c, rtc);  // exact path (HBM/L2 reads)
       } else {
@@ -387,6 +425,9 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
           ++n;
         }
         if (r == 3) r = eager_at(s, p, total, open, c, rtc);
+#ifdef SBH_EPROBE
+        if (r == 3 || true) nexact += 0;
+#endif
       }
       if (r == 1) {
         res |= 1u << bit;
@@ -401,6 +442,18 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
   if (mytrue) atomicAdd(&ntrue, mytrue);
   __syncthreads();
   if (threadIdx.x == 0 && ntrue) atomicAdd(o.n_true, (unsigned long long)ntrue);
+#ifdef SBH_EPROBE
+  __shared__ uint32_t psurv, pcand;
+  if (threadIdx.x == 0) { psurv = 0; pcand = 0; }
+  __syncthreads();
+  atomicAdd(&psurv, nsurv);
+  atomicAdd(&pcand, ncand);
+  __syncthreads();
+  if (threadIdx.x == 0 && blockIdx.x < 4)
+    printf("eager wg %u stage %llu A %llu B %llu surv %u cand %u true %u\n", blockIdx.x,
+           (unsigned long long)(c1 - c0), (unsigned long long)(c2 - c1),
+           (unsigned long long)(__builtin_readcyclecounter() - c2), psurv, pcand, ntrue);
+#endif
 }
 
 struct FullOut {
