@@ -44,9 +44,15 @@ constexpr int WAVES = SBH_HUFF_WAVES;  // waves (blocks) per k_huff workgroup
 #define SBH_LZ_THREADS 512
 #endif
 constexpr uint32_t LZ_THREADS = SBH_LZ_THREADS;  // k_lz workgroup: one block, one token per thread per chunk
-constexpr uint32_t TOK_MATCH = 0x80000000u;  // token: literal = byte; match = bit31 | len << 16 | dist
+constexpr uint32_t TOK_MATCH = 0x80000000u;  // token: literal = byte << 8 (bit 31 clear); match = bit31 | len << 16 | dist
 
-// Table entry: [4:0] code length, [7:5] kind, [15:8] byte/extra/sym, [31:16] base.
+// Table entries (32-bit; laid out so the asm hot loop decodes with few scalar ops):
+//   literal   [4:0] code length L, [7:5] K_LIT, [15:8] byte          (the entry is the token)
+//   length    [4:0] L, [7:5] K_LEN, [15:8] L + extra bits, [22:16] extra bits, [31:23] base
+//             (s_bfe_u32 with the entry as operand extracts the extra bits: offset L, width lx)
+//   distance  [4:0] L, [7:5] K_DIST, [15:8] L + extra, [22:16] extra, [27:23] symbol, bit 31 set;
+//             the distance table holds (entry, base) dword pairs
+//   code-length code  [4:0] L, [7:5] K_CL, [15:8] symbol;  EOB / BAD / SLOW: [4:0] L, [7:5] kind
 constexpr uint32_t K_LIT = 0, K_LEN = 1, K_EOB = 2, K_BAD = 3, K_DIST = 4, K_CL = 5, K_SLOW = 7;
 
 __constant__ uint16_t LBASE[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
@@ -62,7 +68,7 @@ __constant__ uint8_t CL_ORDER[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12
 
 struct __attribute__((aligned(16))) WaveSmem {
   uint32_t lit[1 << LIT_FAST];  // also the code-length-code table while reading headers
-  uint32_t dist[1 << DIST_FAST];
+  uint32_t dist[2 << DIST_FAST];  // (entry, base) pairs
   uint16_t sorted[320];  // canonical order: [0,288) lit/len (or CL), [288,320) dist
   uint8_t lens[320];     // [0,288) lit/len lengths, [288,320) dist lengths
   uint8_t cl_lens[20];
@@ -77,18 +83,36 @@ __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t l) {
 __device__ __forceinline__ uint32_t lit_entry(uint32_t sym, uint32_t L) {
   if (sym < 256) return L | (K_LIT << 5) | (sym << 8);
   if (sym == 256) return L | (K_EOB << 5);
-  if (sym < 286)
-    return L | (K_LEN << 5) | ((uint32_t)LEXT[sym - 257] << 8) | ((uint32_t)LBASE[sym - 257] << 16);
+  if (sym < 286) {
+    const uint32_t lx = LEXT[sym - 257];
+    return L | (K_LEN << 5) | ((L + lx) << 8) | (lx << 16) | ((uint32_t)LBASE[sym - 257] << 23);
+  }
   return L | (K_BAD << 5);
 }
 __device__ __forceinline__ uint32_t dist_entry(uint32_t sym, uint32_t L) {
-  if (sym < 30) return L | (K_DIST << 5) | ((uint32_t)DEXT[sym] << 8) | ((uint32_t)DBASE[sym] << 16);
+  if (sym < 30) {
+    const uint32_t dx = DEXT[sym];
+    return L | (K_DIST << 5) | ((L + dx) << 8) | (dx << 16) | (sym << 23) | 0x80000000u;
+  }
   return L | (K_BAD << 5);
 }
+__device__ __forceinline__ uint32_t len_extra(uint32_t e) { return (e >> 16) & 0x7f; }
+__device__ __forceinline__ uint32_t len_base(uint32_t e) { return e >> 23; }
+__device__ __forceinline__ uint32_t dist_base(uint32_t e) { return DBASE[(e >> 23) & 31]; }
 __device__ __forceinline__ uint32_t make_entry(uint32_t kind, uint32_t sym, uint32_t L) {
   if (kind == 0) return lit_entry(sym, L);
   if (kind == 1) return dist_entry(sym, L);
   return L | (K_CL << 5) | (sym << 8);
+}
+
+// Distance tables hold (entry, base) pairs; the others one entry per index.
+__device__ __forceinline__ void put_entry(uint32_t *tab, uint32_t kind, uint32_t idx, uint32_t e) {
+  if (kind == 1) {
+    tab[2 * idx] = e;
+    tab[2 * idx + 1] = (e & 0x80000000u) ? (uint32_t)DBASE[(e >> 23) & 31] : 0u;
+  } else {
+    tab[idx] = e;
+  }
 }
 
 // Canonical Huffman table (zlib inflate_table validity: over-subscribed -> error;
@@ -125,7 +149,7 @@ __device__ __forceinline__ uint32_t build_table(WaveSmem &sm, const uint8_t *len
   }
   if (lane < 16) sm.cnt[w][lane] = lane == 0 ? 0 : my_cnt;
   if (max == 0) {  // no symbols: every entry invalid
-    for (uint32_t i = lane; i < (1u << fast); i += WAVE) tab[i] = 1u | (K_BAD << 5);
+    for (uint32_t i = lane; i < (1u << fast); i += WAVE) put_entry(tab, kind, i, 1u | (K_BAD << 5));
     return 2;
   }
   if (left < 0) return 1;
@@ -163,13 +187,14 @@ __device__ __forceinline__ uint32_t build_table(WaveSmem &sm, const uint8_t *len
       uint32_t c = __builtin_bitreverse32(idx) >> (32 - l);
       uint32_t v = c - fl;
       if (!(found & (1u << k)) && v < cl) {
-        tab[idx] = make_entry(kind, sorted[ol + v], l);
+        put_entry(tab, kind, idx, make_entry(kind, sorted[ol + v], l));
         found |= 1u << k;
       }
     }
   }
   for (uint32_t k = 0; k < per_lane; ++k)
-    if (!(found & (1u << k))) tab[lane + WAVE * k] = max > (uint32_t)fast ? (K_SLOW << 5) : (1u | (K_BAD << 5));
+    if (!(found & (1u << k)))
+      put_entry(tab, kind, lane + WAVE * k, max > (uint32_t)fast ? (K_SLOW << 5) : (1u | (K_BAD << 5)));
   __builtin_amdgcn_wave_barrier();
   return 0;
 }
@@ -279,6 +304,7 @@ __device__ __forceinline__ void hot_loop(uint64_t &buf, uint32_t &cnt, uint32_t 
                                          uint32_t lane4) {
   uint64_t dst = reinterpret_cast<uint64_t>(to.dst);
   uint32_t va, ve;
+  uint32_t ve2;
   asm volatile(
       "s_mov_b64 s[60:61], %[buf]\n\t"
       "s_mov_b64 s[64:65], %[c32]\n\t"
@@ -289,18 +315,18 @@ __device__ __forceinline__ void hot_loop(uint64_t &buf, uint32_t &cnt, uint32_t 
       "s_mov_b32 s71, %[out]\n\t"
       "s_mov_b32 s72, %[olim]\n\t"
       "s_mov_b32 s81, m0\n\t"
-      "s_mov_b32 m0, %[pend]\n\t"
+      "s_add_u32 m0, %[pend], 0xffffffc0\n\t"  // pending count - 64: carry out at 64 tokens
       "s_mov_b32 s74, %[litb]\n\t"
       "s_mov_b32 s75, %[distb]\n\t"
       "s_mov_b32 s79, 0\n\t"
       "s_mov_b32 s80, 0\n"
-      "L_top_%=:\n\t"
-      "s_cmp_gt_u32 s69, s70\n\t"
-      "s_cbranch_scc1 L_exit_%=\n\t"
-      "s_cmp_gt_u32 s71, s72\n\t"
-      "s_cbranch_scc1 L_exit_%=\n\t"
+      "L_top%=:\n\t"
+      "s_cmp_gt_u32 s71, s72\n\t"  // out > olim: a match might not fit
+      "s_cbranch_scc1 L_exit%=\n\t"
       "s_cmp_gt_u32 s68, 32\n\t"
-      "s_cbranch_scc1 L_lit_%=\n\t"
+      "s_cbranch_scc1 L_lit%=\n\t"
+      "s_cmp_gt_u32 s69, s70\n\t"  // idx > hot: the next symbol may cross the input end
+      "s_cbranch_scc1 L_exit%=\n\t"
       "s_lshl_b32 s77, s69, 2\n\t"
       "s_load_dwordx2 s[62:63], s[64:65], s77\n\t"
       "s_add_u32 s69, s69, 1\n\t"
@@ -308,110 +334,98 @@ __device__ __forceinline__ void hot_loop(uint64_t &buf, uint32_t &cnt, uint32_t 
       "s_lshl_b64 s[62:63], s[62:63], s68\n\t"
       "s_or_b64 s[60:61], s[60:61], s[62:63]\n\t"
       "s_add_u32 s68, s68, 32\n"
-      "L_lit_%=:\n\t"
-      "s_and_b32 s77, s60, %[lmask]\n\t"
-      "s_lshl_b32 s77, s77, 2\n\t"
-      "s_add_u32 s77, s77, s74\n\t"
-      "v_mov_b32 %[va], s77\n\t"
+      "L_lit%=:\n\t"
+      "v_bfe_u32 %[va], s60, 0, %[lbits]\n\t"
+      "v_lshl_add_u32 %[va], %[va], 2, s74\n\t"
       "ds_read_b32 %[ve], %[va]\n\t"
       "s_waitcnt lgkmcnt(0)\n\t"
       "s_nop 0\n\t"
       "v_readfirstlane_b32 s76, %[ve]\n\t"
       "s_and_b32 s77, s76, 31\n\t"
       "s_and_b32 s78, s76, 0xe0\n\t"
-      "s_cbranch_scc1 L_nonlit_%=\n\t"
-      // literal
+      "s_cbranch_scc1 L_nonlit%=\n\t"
+      // literal: the entry is the token
       "s_lshr_b64 s[60:61], s[60:61], s77\n\t"
       "s_sub_u32 s68, s68, s77\n\t"
-      "s_bfe_u32 s78, s76, 0x80008\n\t"
-      "v_writelane_b32 %[batch], s78, m0\n\t"
+      "v_writelane_b32 %[batch], s76, m0\n\t"
       "s_add_u32 s71, s71, 1\n\t"
       "s_add_u32 m0, m0, 1\n\t"
-      "s_cmp_eq_u32 m0, 64\n\t"
-      "s_cbranch_scc0 L_top_%=\n"
-      "L_store_%=:\n\t"
+      "s_cbranch_scc0 L_top%=\n"
+      "L_store%=:\n\t"
       "global_store_dword %[lane4], %[batch], s[66:67]\n\t"
       "s_add_u32 s66, s66, 256\n\t"
       "s_addc_u32 s67, s67, 0\n\t"
-      "s_mov_b32 m0, 0\n\t"
-      "s_branch L_top_%=\n"
-      "L_nonlit_%=:\n\t"
+      "s_mov_b32 m0, 0xffffffc0\n\t"
+      "s_branch L_top%=\n"
+      "L_nonlit%=:\n\t"
       "s_cmp_eq_u32 s78, 0x20\n\t"
-      "s_cbranch_scc0 L_exit_%=\n\t"
-      // length: drop code, add extra bits
-      "s_lshr_b64 s[60:61], s[60:61], s77\n\t"
-      "s_sub_u32 s68, s68, s77\n\t"
+      "s_cbranch_scc0 L_exit%=\n\t"
+      // length: extra bits straight from the entry (offset L, width lx), then drop L + lx
+      "s_bfe_u32 s78, s60, s76\n\t"
+      "s_lshr_b32 s80, s76, 23\n\t"
+      "s_add_u32 s80, s80, s78\n\t"
       "s_bfe_u32 s77, s76, 0x80008\n\t"
-      "s_bfm_b32 s78, s77, 0\n\t"
-      "s_and_b32 s78, s78, s60\n\t"
-      "s_lshr_b32 s76, s76, 16\n\t"
-      "s_add_u32 s80, s76, s78\n\t"
       "s_lshr_b64 s[60:61], s[60:61], s77\n\t"
       "s_sub_u32 s68, s68, s77\n\t"
       "s_cmp_gt_u32 s68, 32\n\t"
-      "s_cbranch_scc1 L_dist_%=\n\t"
+      "s_cbranch_scc1 L_dist%=\n\t"
       "s_lshl_b32 s77, s69, 2\n\t"
       "s_load_dwordx2 s[62:63], s[64:65], s77\n\t"
       "s_add_u32 s69, s69, 1\n\t"
       "s_waitcnt lgkmcnt(0)\n\t"
       "s_lshl_b64 s[62:63], s[62:63], s68\n\t"
       "s_or_b64 s[60:61], s[60:61], s[62:63]\n\t"
-      "s_add_u32 s68, s68, 32\n"
-      "L_dist_%=:\n\t"
-      "s_and_b32 s77, s60, %[dmask]\n\t"
-      "s_lshl_b32 s77, s77, 2\n\t"
-      "s_add_u32 s77, s77, s75\n\t"
-      "v_mov_b32 %[va], s77\n\t"
+      "s_add_u32 s68, s68, 32\n\t"
+      "s_cmp_gt_u32 s69, s70\n\t"  // past hot: finish this match, leave at the top
+      "s_cselect_b32 s72, 0, s72\n"
+      "L_dist%=:\n\t"
+      "v_bfe_u32 %[va], s60, 0, %[dbits]\n\t"
+      "v_lshl_add_u32 %[va], %[va], 3, s75\n\t"
       "ds_read_b32 %[ve], %[va]\n\t"
+      "ds_read_b32 %[ve2], %[va] offset:4\n\t"
       "s_waitcnt lgkmcnt(0)\n\t"
       "s_nop 0\n\t"
       "v_readfirstlane_b32 s76, %[ve]\n\t"
-      "s_and_b32 s78, s76, 0xe0\n\t"
-      "s_cmp_eq_u32 s78, 0x80\n\t"
-      "s_cbranch_scc0 L_pend_%=\n\t"
-      "s_and_b32 s77, s76, 31\n\t"
-      "s_lshr_b64 s[60:61], s[60:61], s77\n\t"
-      "s_sub_u32 s68, s68, s77\n\t"
+      "v_readfirstlane_b32 s82, %[ve2]\n\t"
+      "s_cmp_lt_i32 s76, 0\n\t"  // bit 31: a decoded distance
+      "s_cbranch_scc0 L_pend%=\n\t"
+      "s_bfe_u32 s78, s60, s76\n\t"
+      "s_add_u32 s78, s82, s78\n\t"
       "s_bfe_u32 s77, s76, 0x80008\n\t"
-      "s_bfm_b32 s78, s77, 0\n\t"
-      "s_and_b32 s78, s78, s60\n\t"
-      "s_lshr_b32 s76, s76, 16\n\t"
-      "s_add_u32 s78, s76, s78\n\t"
       "s_lshr_b64 s[60:61], s[60:61], s77\n\t"
       "s_sub_u32 s68, s68, s77\n\t"
       "s_cmp_gt_u32 s78, s71\n\t"
-      "s_cbranch_scc1 L_far_%=\n\t"
+      "s_cbranch_scc1 L_far%=\n\t"
       "s_lshl_b32 s77, s80, 16\n\t"
       "s_or_b32 s77, s77, s78\n\t"
       "s_bitset1_b32 s77, 31\n\t"
       "v_writelane_b32 %[batch], s77, m0\n\t"
       "s_add_u32 s71, s71, s80\n\t"
       "s_add_u32 m0, m0, 1\n\t"
-      "s_cmp_eq_u32 m0, 64\n\t"
-      "s_cbranch_scc0 L_top_%=\n\t"
-      "s_branch L_store_%=\n"
-      "L_pend_%=:\n\t"
+      "s_cbranch_scc0 L_top%=\n\t"
+      "s_branch L_store%=\n"
+      "L_pend%=:\n\t"
       "s_mov_b32 s79, 2\n\t"
-      "s_branch L_exit_%=\n"
-      "L_far_%=:\n\t"
+      "s_branch L_exit%=\n"
+      "L_far%=:\n\t"
       "s_mov_b32 s79, 3\n"
-      "L_exit_%=:\n\t"
+      "L_exit%=:\n\t"
       "s_mov_b64 %[buf], s[60:61]\n\t"
       "s_mov_b64 %[dst], s[66:67]\n\t"
       "s_mov_b32 %[cnt], s68\n\t"
       "s_mov_b32 %[idx], s69\n\t"
       "s_mov_b32 %[out], s71\n\t"
-      "s_mov_b32 %[pend], m0\n\t"
+      "s_add_u32 %[pend], m0, 64\n\t"
       "s_mov_b32 m0, s81\n\t"
       "s_mov_b32 %[reason], s79\n\t"
       "s_mov_b32 %[plen], s80\n\t"
       : [buf] "+s"(buf), [dst] "+s"(dst), [cnt] "+s"(cnt), [idx] "+s"(idx), [out] "+s"(out),
         [pend] "+s"(to.pend), [reason] "=s"(reason), [plen] "=s"(plen), [batch] "+v"(to.batch),
-        [va] "=&v"(va), [ve] "=&v"(ve)
+        [va] "=&v"(va), [ve] "=&v"(ve), [ve2] "=&v"(ve2)
       : [c32] "s"(c32), [hot] "s"(hot), [olim] "s"(olim), [litb] "s"(litb), [distb] "s"(distb),
-        [lane4] "v"(lane4), [lmask] "i"((1 << LIT_FAST) - 1), [dmask] "i"((1 << DIST_FAST) - 1)
+        [lane4] "v"(lane4), [lbits] "i"(LIT_FAST), [dbits] "i"(DIST_FAST)
       : "memory", "scc", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71",
-        "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81");
+        "s72", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82");
   to.dst = reinterpret_cast<uint32_t *>(dst);
 }
 
@@ -485,7 +499,7 @@ __global__ __launch_bounds__(WAVES *WAVE) void k_huff(const uint8_t *__restrict_
       if (n > usize - out) n = usize - out;
       const uint8_t *src = comp + (uint64_t)br.a0 * 4 + (p0 >> 3);
       to.drain(lane);
-      for (uint32_t i = lane; i < n; i += WAVE) to.dst[i] = src[i];
+      for (uint32_t i = lane; i < n; i += WAVE) to.dst[i] = (uint32_t)src[i] << 8;  // literal tokens
       to.dst += n;
       out += n;
       if (n < len) break;  // output full or input exhausted
@@ -600,21 +614,20 @@ __global__ __launch_bounds__(WAVES *WAVE) void k_huff(const uint8_t *__restrict_
         const uint32_t kind = (e >> 5) & 7;
         if (kind == K_LIT) {
           br.drop(e & 31);
-          to.emit((e >> 8) & 0xff, lane);
+          to.emit(e, lane);
           ++out;
         } else if (kind == K_LEN) {
           br.drop(e & 31);
-          const uint32_t lx = (e >> 8) & 0xff;
-          const uint32_t ml = (e >> 16) + br.take(lx);
+          const uint32_t ml = len_base(e) + br.take(len_extra(e));
           br.refill();
-          uint32_t d = uni(sm.dist[(uint32_t)br.buf & ((1u << DIST_FAST) - 1)]);
+          uint32_t d = uni(sm.dist[2 * ((uint32_t)br.buf & ((1u << DIST_FAST) - 1))]);
           if (((d >> 5) & 7) != K_DIST) {
             mlen = ml;
             have_len = true;
             break;
           }
           br.drop(d & 31);
-          const uint32_t dist = (d >> 16) + br.take((d >> 8) & 0xff);
+          const uint32_t dist = dist_base(d) + br.take(len_extra(d));
           if (dist > out) { status = INF_DATA; done = true; break; }  // too far back
           to.emit(TOK_MATCH | (ml << 16) | dist, lane);
           out += ml;
@@ -643,17 +656,17 @@ __global__ __launch_bounds__(WAVES *WAVE) void k_huff(const uint8_t *__restrict_
         br.drop(L);
         if (kind == K_LIT) {
           if (out == usize) { done = true; break; }
-          to.emit((e >> 8) & 0xff, lane);
+          to.emit(e, lane);
           ++out;
           continue;
         }
         if (kind == K_EOB) break;
-        const uint32_t lx = (e >> 8) & 0xff;
+        const uint32_t lx = len_extra(e);
         if (!br.avail(lx)) { done = true; break; }
-        mlen = (e >> 16) + br.take(lx);
+        mlen = len_base(e) + br.take(lx);
       }
       br.refill();
-      uint32_t d = uni(sm.dist[br.peek(DIST_FAST)]);
+      uint32_t d = uni(sm.dist[2 * br.peek(DIST_FAST)]);
       uint32_t dk = (d >> 5) & 7;
       if (dk == K_SLOW) {
         d = uni(slow_decode(sm, br.buf, 1));
@@ -667,9 +680,9 @@ __global__ __launch_bounds__(WAVES *WAVE) void k_huff(const uint8_t *__restrict_
       const uint32_t DL = d & 31;
       if (!br.avail(DL)) { done = true; break; }
       br.drop(DL);
-      const uint32_t dx = (d >> 8) & 0xff;
+      const uint32_t dx = len_extra(d);
       if (!br.avail(dx)) { done = true; break; }
-      const uint32_t dist = (d >> 16) + br.take(dx);
+      const uint32_t dist = dist_base(d) + br.take(dx);
       if (out == usize) { done = true; break; }  // zlib stops at MATCH when full
       if (dist > out) { status = INF_DATA; done = true; break; }  // too far back
       const uint32_t n = mlen < usize - out ? mlen : usize - out;
@@ -783,7 +796,7 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
     if (t < m) {
       sm.toff[t] = off;
       sm.done[t] = match ? 0 : 1;
-      if (!match) img[off] = (uint8_t)x;
+      if (!match) img[off] = (uint8_t)(x >> 8);
     }
     __syncthreads();
     const uint32_t dist = x & 0xffff;
