@@ -43,7 +43,8 @@ constexpr int WAVES = SBH_HUFF_WAVES;  // waves (blocks) per k_huff workgroup
 #ifndef SBH_LZ_THREADS
 #define SBH_LZ_THREADS 512
 #endif
-constexpr uint32_t LZ_THREADS = SBH_LZ_THREADS;  // k_lz workgroup: one block, one token per thread per chunk
+constexpr uint32_t LZ_THREADS = SBH_LZ_THREADS;
+constexpr uint32_t LZ_LONG = 24;  // longer matches are copied by the whole wave
 constexpr uint32_t TOK_MATCH = 0x80000000u;  // token: literal = byte << 8 (bit 31 clear); match = bit31 | len << 16 | dist
 
 // Table entries (32-bit; laid out so the asm hot loop decodes with few scalar ops):
@@ -725,6 +726,7 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t *wsum, uint3
 struct LzSmem {
   uint8_t img[65536 + 16];    // block image, placed at (ustart & 15) so granules align with HBM
   uint32_t toff[LZ_THREADS];  // chunk tokens: output offsets (ascending)
+  uint32_t tokv[LZ_THREADS];  // chunk tokens
   uint32_t done[LZ_THREADS];  // round after which the token's bytes are final (0: pending)
   uint32_t wsum[LZ_THREADS / WAVE];
 };
@@ -740,26 +742,34 @@ __device__ __forceinline__ uint32_t cover(const uint32_t *toff, uint32_t m, uint
   return lo;
 }
 
-// One match into the image.  Every byte reads from below `off` (an overlapping match
-// repeats its period: out[k] = out[k mod dist - dist]), so a piece's loads are
-// independent of its stores.
-__device__ __forceinline__ void lz_match(uint8_t *img, uint32_t off, uint32_t dist, uint32_t len) {
-  const uint8_t *src = img + off - dist;
-  uint8_t *dst = img + off;
-  uint32_t k = 0;
+// One match into the image: out[off + k] = img[src + (k mod dist)] (src holds bytes
+// equal to out[off - dist ...], already final).  Loads never touch the match's own
+// output.  Non-overlapping matches copy by aligned destination dwords, each assembled
+// from two aligned source dwords with v_alignbyte; the ragged ends go by bytes.
+// `base` is the image's byte offset inside the 16-aligned LDS buffer `img0`.
+__device__ __forceinline__ void lz_match(uint8_t *img0, uint32_t base, uint32_t off, uint32_t src,
+                                         uint32_t dist, uint32_t len) {
+  uint8_t *img = img0 + base;
   if (dist >= len) {
-    for (; k + 4 <= len; k += 4) {
-      const uint8_t a = src[k], b = src[k + 1], c = src[k + 2], d = src[k + 3];
-      dst[k] = a;
-      dst[k + 1] = b;
-      dst[k + 2] = c;
-      dst[k + 3] = d;
+    uint32_t k = 0;
+    const uint32_t head = (4u - ((base + off) & 3u)) & 3u;
+    for (; k < len && k < head; ++k) img[off + k] = img[src + k];
+    uint32_t *d32 = reinterpret_cast<uint32_t *>(img0 + base + off + k);
+    const uint32_t *s32 = reinterpret_cast<const uint32_t *>(img0 + ((base + src + k) & ~3u));
+    const uint32_t sh = (base + src + k) & 3u;
+    if (k + 4 <= len) {
+      uint32_t lo = s32[0];
+      for (uint32_t w = 0; k + 4 <= len; k += 4, ++w) {
+        const uint32_t hi = s32[w + 1];
+        d32[w] = __builtin_amdgcn_alignbyte(hi, lo, sh);
+        lo = hi;
+      }
     }
-    for (; k < len; ++k) dst[k] = src[k];
+    for (; k < len; ++k) img[off + k] = img[src + k];
   } else {
     uint32_t s = 0;
-    for (; k < len; ++k) {
-      dst[k] = src[s];
+    for (uint32_t k = 0; k < len; ++k) {
+      img[off + k] = img[src + s];
       s = s + 1 == dist ? 0 : s + 1;
     }
   }
@@ -784,7 +794,14 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
 
   uint32_t base = 0;  // output offset of the chunk's first token
   uint32_t x_next = t < n ? tk[t] : 0;
+#ifdef SBH_LZ_PROBE
+  uint64_t tp0 = __builtin_readcyclecounter(), t_pre = 0, t_rounds = 0;
+  uint32_t nrounds = 0;
+#endif
   for (uint32_t c0 = 0; c0 < n; c0 += LZ_THREADS) {
+#ifdef SBH_LZ_PROBE
+    uint64_t ta = __builtin_readcyclecounter();
+#endif
     const uint32_t i = c0 + t;
     const uint32_t m = n - c0 < LZ_THREADS ? n - c0 : LZ_THREADS;  // tokens in this chunk
     const uint32_t x = x_next;
@@ -795,39 +812,85 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
     const uint32_t off = base + block_scan(len, sm.wsum, &chunk_len);
     if (t < m) {
       sm.toff[t] = off;
+      sm.tokv[t] = x;
       sm.done[t] = match ? 0 : 1;
       if (!match) img[off] = (uint8_t)(x >> 8);
     }
     __syncthreads();
     const uint32_t dist = x & 0xffff;
-    uint32_t jl = 1, jh = 0;  // chunk tokens the source overlaps (empty: none)
+    uint32_t src = off - dist;  // where the (final-equivalent) source bytes start
+    uint32_t jl = 1, jh = 0;    // chunk tokens the source overlaps (empty: none)
     if (match) {
-      const uint32_t q0 = off - dist;
-      const uint32_t q1 = off < q0 + len ? off : q0 + len;  // external source end
-      if (q1 > base) {
-        jl = q0 < base ? 0 : cover(sm.toff, m, q0);
-        jh = cover(sm.toff, m, q1 - 1);
+      // external source bytes: [src, src + min(len, dist)) (an overlapping match
+      // re-reads its own output only through the period)
+      const uint32_t ext = len < dist ? len : dist;
+      // Redirect through the chunk's own matches: a source wholly inside one
+      // non-overlapping match M' equals the bytes M' copied, dist' earlier.  This
+      // collapses chains (read names copying the previous read's name ...) so most
+      // matches copy in the first round.
+      for (int hop = 0; hop < 16 && src >= base; ++hop) {
+        const uint32_t j = cover(sm.toff, m, src);
+        const uint32_t y = sm.tokv[j];
+        if (!(y & TOK_MATCH)) break;
+        const uint32_t oj = sm.toff[j], lj = (y >> 16) & 0x1ff, dj = y & 0xffff;
+        if (dj < lj || src + ext > oj + lj) break;  // overlapping M' or source spans tokens
+        src -= dj;
+      }
+      if (src + ext > base) {
+        jl = src < base ? 0 : cover(sm.toff, m, src);
+        jh = cover(sm.toff, m, src + ext - 1);
       }
     }
     bool pending = match;
+#ifdef SBH_LZ_PROBE
+    uint64_t tb = __builtin_readcyclecounter();
+    t_pre += tb - ta;
+#endif
     for (uint32_t r = 1;; ++r) {
+#ifdef SBH_LZ_PROBE
+      ++nrounds;
+#endif
+      bool go = false;
       if (pending) {
-        bool ready = true;
-        for (uint32_t j = jl; j <= jh && ready; ++j) {
+        go = true;
+        for (uint32_t j = jl; j <= jh && go; ++j) {
           const uint32_t dj = sm.done[j];
-          ready = dj != 0 && dj <= r;
+          go = dj != 0 && dj <= r;
         }
-        if (ready) {
-          lz_match(img, off, dist, len);
-          sm.done[t] = r + 1;
-          pending = false;
+      }
+      // long matches: the whole wave copies each one (byte k by lane k mod 64)
+      uint64_t lm = __ballot(go && len > LZ_LONG);
+      while (lm) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(lm);
+        lm &= lm - 1;
+        const uint32_t o = __builtin_amdgcn_readlane(off, l), sr = __builtin_amdgcn_readlane(src, l);
+        const uint32_t d = __builtin_amdgcn_readlane(dist, l), L = __builtin_amdgcn_readlane(len, l);
+        const uint32_t lane = t & (WAVE - 1);
+        if (d >= L) {
+          for (uint32_t k = lane; k < L; k += WAVE) img[o + k] = img[sr + k];
+        } else {
+          for (uint32_t k = lane; k < L; k += WAVE) img[o + k] = img[sr + k % d];
         }
+      }
+      if (go && len <= LZ_LONG) lz_match(sm.img, sh, off, src, dist, len);
+      if (go) {
+        sm.done[t] = r + 1;
+        pending = false;
       }
       if (!__syncthreads_or(pending)) break;
     }
     base += chunk_len;
     __syncthreads();  // toff/done/wsum are reused by the next chunk
+#ifdef SBH_LZ_PROBE
+    t_rounds += __builtin_readcyclecounter() - tb;
+#endif
   }
+#ifdef SBH_LZ_PROBE
+  if (t == 0 && b < 4)
+    printf("lz blk %llu ntok %u cyc %llu pre %llu rounds %llu nrounds %u\n", (unsigned long long)b, n,
+           (unsigned long long)(__builtin_readcyclecounter() - tp0), (unsigned long long)t_pre,
+           (unsigned long long)t_rounds, nrounds);
+#endif
   const uint32_t usize = base;
   // write the image: 16-byte granules aligned to the flat address
   const uint64_t g0 = G & ~15ull;
