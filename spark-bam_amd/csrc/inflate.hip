@@ -39,6 +39,7 @@ namespace {
 constexpr int LIT_FAST = SBH_LIT_FAST;
 constexpr int DIST_FAST = 8;
 constexpr int CL_FAST = 7;
+constexpr int PDIST_FAST = DIST_FAST + 1;  // PAR-format distance table: one dword per entry
 constexpr int WAVES = SBH_HUFF_WAVES;  // waves (blocks) per k_huff workgroup
 #ifndef SBH_LZ_THREADS
 #define SBH_LZ_THREADS 512
@@ -68,12 +69,20 @@ __constant__ uint8_t DEXT[30] = {0, 0, 0, 0, 1, 1, 2, 2,  3,  3,  4,  4,  5,  5,
 __constant__ uint8_t CL_ORDER[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
 struct __attribute__((aligned(16))) WaveSmem {
-  uint32_t lit[1 << LIT_FAST];  // also the code-length-code table while reading headers
-  uint32_t dist[2 << DIST_FAST];  // (entry, base) pairs
+  union {
+    struct {
+      uint32_t lit[1 << LIT_FAST];    // also the code-length-code table while reading headers
+      uint32_t dist[2 << DIST_FAST];  // (entry, base) pairs; PAR format: 1 << PDIST_FAST entries
+    };
+    uint32_t tab[(1 << LIT_FAST) + (2 << DIST_FAST)];
+  };
   uint16_t sorted[320];  // canonical order: [0,288) lit/len (or CL), [288,320) dist
   uint8_t lens[320];     // [0,288) lit/len lengths, [288,320) dist lengths
   uint8_t cl_lens[20];
   uint32_t cnt[2][16];  // per-length counts (slow path)
+  uint32_t pk[2][16];   // PAR format, per length: left-justified (15-bit) code limit << 16 |
+                        // sorted index of the length's code 0 (offs - first, mod 2^16)
+  uint32_t sent[320];   // PAR format: entry of each sorted symbol ([0,288) lit/len, [288,320) dist)
 };
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -198,6 +207,108 @@ __device__ __forceinline__ uint32_t build_table(WaveSmem &sm, const uint8_t *len
       put_entry(tab, kind, lane + WAVE * k, max > (uint32_t)fast ? (K_SLOW << 5) : (1u | (K_BAD << 5)));
   __builtin_amdgcn_wave_barrier();
   return 0;
+}
+
+// PAR-format entries (the lane-parallel decoder): [4:0] code length L, [7:5] kind,
+// [11:8] extra bits, [31:16] base (a literal's byte; a length or distance base), so a
+// code decodes as base + bits(L, extra) whatever its kind.  A distance is kind K_LIT
+// too: kind 0 means "this code completes a token" in either table.
+__device__ __forceinline__ uint32_t pentry(uint32_t kind, uint32_t sym, uint32_t L) {
+  if (kind == 0) {
+    if (sym < 256) return L | (K_LIT << 5) | (sym << 16);
+    if (sym == 256) return L | (K_EOB << 5);
+    if (sym < 286) return L | (K_LEN << 5) | ((uint32_t)LEXT[sym - 257] << 8) | ((uint32_t)LBASE[sym - 257] << 16);
+    return L | (K_BAD << 5);
+  }
+  if (sym < 30) return L | (K_LIT << 5) | ((uint32_t)DEXT[sym] << 8) | ((uint32_t)DBASE[sym] << 16);
+  return L | (K_BAD << 5);
+}
+
+// Canonical table in the PAR format (kind 0 lit/len, 1 dist), same validity rules as
+// build_table.  Codes are located by their left-justified limits: the codes of length
+// v occupy [lj[v-1], lj[v]) of the 15-bit left-justified code space, so a reversed
+// index's length is 1 + #{v : lj[v] <= code}.  Entries whose code is longer than
+// `fast` bits are K_SLOW (slow_lane finishes them); prefixes of no code are K_BAD.
+__device__ __forceinline__ uint32_t build_ptable(WaveSmem &sm, const uint8_t *lens, uint32_t nsym, uint32_t kind,
+                                                 uint32_t *tab, uint32_t fast, uint32_t lane) {
+  uint16_t *sorted = sm.sorted + (kind ? 288 : 0);
+  uint32_t my_cnt = 0;  // lane v (1..15): count of length v
+  for (uint32_t base = 0; base < nsym; base += WAVE) {
+    const uint32_t s = base + lane;
+    const uint32_t l = s < nsym ? lens[s] : 0;
+#pragma unroll
+    for (uint32_t v = 1; v <= 15; ++v) {
+      const uint32_t c = (uint32_t)__popcll(__ballot(l == v));
+      my_cnt += lane == v ? c : 0;
+    }
+  }
+  int32_t left = 1;
+  uint32_t max = 0, acc = 0, code = 0, prev = 0, my_offs = 0;
+  uint32_t ljv[16];
+#pragma unroll
+  for (uint32_t v = 1; v <= 15; ++v) {
+    const uint32_t c = uni(rdlane(my_cnt, v));
+    left = 2 * left - (int32_t)c;
+    if (c) max = v;
+    code = (code + prev) << 1;
+    prev = c;
+    ljv[v] = (code + c) << (15 - v);
+    if (lane == v) {
+      sm.pk[kind][v] = (ljv[v] << 16) | ((acc - code) & 0xffffu);
+      my_offs = acc;
+    }
+    acc += c;
+  }
+  const uint32_t n_ent = 1u << fast;
+  if (max == 0) {  // no symbols: every entry invalid
+    for (uint32_t i = lane; i < n_ent; i += WAVE) tab[i] = 1u | (K_BAD << 5);
+    if (lane < 16) sm.pk[kind][lane] = 0;
+    return 2;
+  }
+  if (left < 0) return 1;
+  if (left > 0 && max != 1) return 1;
+  uint32_t my_run = 0;
+  for (uint32_t base = 0; base < nsym; base += WAVE) {
+    const uint32_t s = base + lane;
+    const uint32_t l = s < nsym ? lens[s] : 0;
+    uint32_t rank = 0;
+    for (uint32_t v = 1; v <= max; ++v) {
+      const uint64_t m = __ballot(l == v);
+      if (m == 0) continue;
+      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+      const uint32_t ov = uni(rdlane(my_offs, v)), rv = uni(rdlane(my_run, v));
+      if (l == v) rank = ov + rv + below;
+      my_run += lane == v ? (uint32_t)__popcll(m) : 0;
+    }
+    if (l) {
+      sorted[rank] = (uint16_t)s;
+      sm.sent[(kind ? 288 : 0) + rank] = pentry(kind, s, l);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  for (uint32_t i = lane; i < n_ent; i += WAVE) {
+    const uint32_t c15 = (__builtin_bitreverse32(i) >> (32 - fast)) << (15 - fast);
+    uint32_t len = 1;
+#pragma unroll
+    for (uint32_t v = 1; v <= 15; ++v) len += ljv[v] <= c15 ? 1u : 0u;
+    uint32_t e;
+    if (len > 15) e = 1u | (K_BAD << 5);
+    else if (len > fast) e = K_SLOW << 5;
+    else e = pentry(kind, sorted[((sm.pk[kind][len] & 0xffffu) + (c15 >> (15 - len))) & 0xffffu], len);
+    tab[i] = e;
+  }
+  __builtin_amdgcn_wave_barrier();
+  return 0;
+}
+
+template <bool PAR>
+__device__ __forceinline__ uint32_t build_lit(WaveSmem &sm, const uint8_t *lens, uint32_t nsym, uint32_t lane) {
+  return PAR ? build_ptable(sm, lens, nsym, 0, sm.lit, LIT_FAST, lane) : build_table(sm, lens, nsym, 0, sm.lit, LIT_FAST, lane);
+}
+template <bool PAR>
+__device__ __forceinline__ uint32_t build_dist(WaveSmem &sm, const uint8_t *lens, uint32_t nsym, uint32_t lane) {
+  return PAR ? build_ptable(sm, lens, nsym, 1, sm.dist, PDIST_FAST, lane)
+             : build_table(sm, lens, nsym, 1, sm.dist, DIST_FAST, lane);
 }
 
 // Canonical slow-path decode (codes longer than the primary table): returns the
@@ -430,15 +541,97 @@ __device__ __forceinline__ void hot_loop(uint64_t &buf, uint32_t &cnt, uint32_t 
   to.dst = reinterpret_cast<uint32_t *>(dst);
 }
 
-__global__ __launch_bounds__(WAVES *WAVE) void k_huff(const uint8_t *__restrict__ comp, DevBlocks bl,
-                                                       uint64_t nblocks, uint32_t *__restrict__ tok) {
-  __shared__ WaveSmem smem[WAVES];
-  const uint32_t lane = threadIdx.x & (WAVE - 1);
-  const uint32_t wid = uni(threadIdx.x / WAVE);
-  const uint64_t b = (uint64_t)blockIdx.x * WAVES + wid;
-  if (b >= nblocks) return;
-  WaveSmem &sm = smem[wid];
+// Tables of a fixed (type 1) or dynamic (type 2) deflate block, read at br (just after
+// the 3 block-header bits) and built in sm.  Wave-uniform; follows zlib inflate's
+// TABLE / LENLENS / CODELENS states.  RT_STOP: the input ends inside the header (zlib
+// waits for more input, so the block ends short); RT_ERR: DataFormatException.
+constexpr uint32_t RT_OK = 0, RT_STOP = 1, RT_ERR = 2;
 
+template <bool PAR>
+__device__ __forceinline__ uint32_t read_tables(WaveSmem &sm, Bits &br, uint32_t type, bool &fixed_built,
+                                                uint32_t lane) {
+  if (type == 1) {
+    if (!fixed_built) {
+      for (uint32_t s = lane; s < 288; s += WAVE) sm.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
+      if (lane < 32) sm.lens[288 + lane] = 5;
+      __builtin_amdgcn_wave_barrier();
+      build_lit<PAR>(sm, sm.lens, 288, lane);
+      build_dist<PAR>(sm, sm.lens + 288, 32, lane);
+      fixed_built = true;
+    }
+    return RT_OK;
+  }
+  fixed_built = false;
+  br.refill();
+  if (!br.avail(14)) return RT_STOP;
+  const uint32_t nlen = br.take(5) + 257, ndist = br.take(5) + 1, ncode = br.take(4) + 4;
+  if (nlen > 286 || ndist > 30) return RT_ERR;
+  if (!br.avail(ncode * 3)) return RT_STOP;
+  if (lane < 20) sm.cl_lens[lane] = 0;
+  __builtin_amdgcn_wave_barrier();
+  for (uint32_t i = 0; i < ncode; ++i) {
+    br.refill();
+    const uint32_t v = br.take(3);
+    if (lane == 0) sm.cl_lens[CL_ORDER[i]] = (uint8_t)v;
+  }
+  __builtin_amdgcn_wave_barrier();
+  const uint32_t rc = uni(build_table(sm, sm.cl_lens, 19, 2, sm.lit, CL_FAST, lane));
+  if (rc == 1) return RT_ERR;
+  const uint32_t total = nlen + ndist;
+  if (rc == 2) return br.avail(total) ? RT_ERR : RT_STOP;  // no code-length codes: each decodes as 0 (1 bit), then fails
+  uint32_t i = 0, prevlen = 0;
+  while (i < total) {
+    br.refill();
+    const uint32_t e = uni(sm.lit[br.peek(CL_FAST)]);
+    const uint32_t L = e & 31;
+    if (!br.avail(L)) return RT_STOP;
+    br.drop(L);
+    const uint32_t sym = (e >> 8) & 0xff;
+    if (sym < 16) {
+      if (lane == 0) sm.lens[i] = (uint8_t)sym;
+      prevlen = sym;
+      ++i;
+      continue;
+    }
+    uint32_t rep, val;
+    if (sym == 16) {
+      if (i == 0) return RT_ERR;
+      if (!br.avail(2)) return RT_STOP;
+      rep = 3 + br.take(2);
+      val = prevlen;
+    } else if (sym == 17) {
+      if (!br.avail(3)) return RT_STOP;
+      rep = 3 + br.take(3);
+      val = 0;
+    } else {
+      if (!br.avail(7)) return RT_STOP;
+      rep = 11 + br.take(7);
+      val = 0;
+    }
+    if (i + rep > total) return RT_ERR;
+    for (uint32_t k = lane; k < rep; k += WAVE) sm.lens[i + k] = (uint8_t)val;
+    prevlen = val;
+    i += rep;
+  }
+  __builtin_amdgcn_wave_barrier();
+  // split: lit lens [0,nlen) (+zeros to 288); dist lens -> [288, 288+ndist)
+  const uint32_t dv = lane < ndist ? sm.lens[nlen + lane] : 0;
+  __builtin_amdgcn_wave_barrier();
+  for (uint32_t s = nlen + lane; s < 288; s += WAVE) sm.lens[s] = 0;
+  __builtin_amdgcn_wave_barrier();
+  if (lane < 32) sm.lens[288 + lane] = (uint8_t)dv;
+  __builtin_amdgcn_wave_barrier();
+  if (uni(sm.lens[256]) == 0) return RT_ERR;  // missing end-of-block
+  if (uni(build_lit<PAR>(sm, sm.lens, nlen, lane)) == 1) return RT_ERR;
+  if (uni(build_dist<PAR>(sm, sm.lens + 288, ndist, lane)) == 1) return RT_ERR;
+  return RT_OK;
+}
+
+// Exact serial decode of block b by one wave (zlib semantics everywhere: stored blocks,
+// long codes, every input/output edge, every error).  The lane-parallel k_huff falls
+// back to it for any block its fast path does not prove well-formed.
+__device__ __forceinline__ void inflate_serial(const uint8_t *__restrict__ comp, const DevBlocks &bl, uint64_t b,
+                                            uint32_t *__restrict__ tok, WaveSmem &sm, uint32_t lane) {
   const uint64_t cstart = bl.cstart[b];
   const uint32_t csize = bl.csize[b], hsize = bl.hsize[b], usize = bl.usize[b];
   const uint64_t G = bl.ustart[b];
@@ -509,87 +702,9 @@ __global__ __launch_bounds__(WAVES *WAVE) void k_huff(const uint8_t *__restrict_
       continue;
     }
     if (type == 3) { status = INF_DATA; break; }  // invalid block type
-    if (type == 1) {
-      if (!fixed_built) {
-        for (uint32_t s = lane; s < 288; s += WAVE) sm.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
-        if (lane < 32) sm.lens[288 + lane] = 5;
-        __builtin_amdgcn_wave_barrier();
-        build_table(sm, sm.lens, 288, 0, sm.lit, LIT_FAST, lane);
-        build_table(sm, sm.lens + 288, 32, 1, sm.dist, DIST_FAST, lane);
-        fixed_built = true;
-      }
-    } else {
-      fixed_built = false;
-      br.refill();
-      if (!br.avail(14)) break;
-      const uint32_t nlen = br.take(5) + 257, ndist = br.take(5) + 1, ncode = br.take(4) + 4;
-      if (nlen > 286 || ndist > 30) { status = INF_DATA; break; }
-      if (!br.avail(ncode * 3)) break;
-      if (lane < 20) sm.cl_lens[lane] = 0;
-      __builtin_amdgcn_wave_barrier();
-      for (uint32_t i = 0; i < ncode; ++i) {
-        br.refill();
-        const uint32_t v = br.take(3);
-        if (lane == 0) sm.cl_lens[CL_ORDER[i]] = (uint8_t)v;
-      }
-      __builtin_amdgcn_wave_barrier();
-      const uint32_t rc = uni(build_table(sm, sm.cl_lens, 19, 2, sm.lit, CL_FAST, lane));
-      if (rc == 1) { status = INF_DATA; break; }
-      const uint32_t total = nlen + ndist;
-      if (rc == 2) {  // no code-length codes: zlib decodes each as 0 (1 bit) then fails
-        if (!br.avail(total)) break;
-        status = INF_DATA;
-        break;
-      }
-      uint32_t i = 0, prevlen = 0;
-      bool hdr_ok = true, starved = false;
-      while (i < total) {
-        br.refill();
-        const uint32_t e = uni(sm.lit[br.peek(CL_FAST)]);
-        const uint32_t L = e & 31;
-        if (!br.avail(L)) { starved = true; break; }
-        br.drop(L);
-        const uint32_t sym = (e >> 8) & 0xff;
-        if (sym < 16) {
-          if (lane == 0) sm.lens[i] = (uint8_t)sym;
-          prevlen = sym;
-          ++i;
-          continue;
-        }
-        uint32_t rep, val;
-        if (sym == 16) {
-          if (i == 0) { hdr_ok = false; break; }
-          if (!br.avail(2)) { starved = true; break; }
-          rep = 3 + br.take(2);
-          val = prevlen;
-        } else if (sym == 17) {
-          if (!br.avail(3)) { starved = true; break; }
-          rep = 3 + br.take(3);
-          val = 0;
-        } else {
-          if (!br.avail(7)) { starved = true; break; }
-          rep = 11 + br.take(7);
-          val = 0;
-        }
-        if (i + rep > total) { hdr_ok = false; break; }
-        for (uint32_t k = lane; k < rep; k += WAVE) sm.lens[i + k] = (uint8_t)val;
-        prevlen = val;
-        i += rep;
-      }
-      if (starved) break;
-      if (!hdr_ok) { status = INF_DATA; break; }
-      __builtin_amdgcn_wave_barrier();
-      // split: lit lens [0,nlen) (+zeros to 288); dist lens -> [288, 288+ndist)
-      const uint32_t dv = lane < ndist ? sm.lens[nlen + lane] : 0;
-      __builtin_amdgcn_wave_barrier();
-      for (uint32_t s = nlen + lane; s < 288; s += WAVE) sm.lens[s] = 0;
-      __builtin_amdgcn_wave_barrier();
-      if (lane < 32) sm.lens[288 + lane] = (uint8_t)dv;
-      __builtin_amdgcn_wave_barrier();
-      if (uni(sm.lens[256]) == 0) { status = INF_DATA; break; }  // missing end-of-block
-      if (uni(build_table(sm, sm.lens, nlen, 0, sm.lit, LIT_FAST, lane)) == 1) { status = INF_DATA; break; }
-      if (uni(build_table(sm, sm.lens + 288, ndist, 1, sm.dist, DIST_FAST, lane)) == 1) { status = INF_DATA; break; }
-    }
+    const uint32_t rt = read_tables<false>(sm, br, type, fixed_built, lane);
+    if (rt == RT_STOP) break;
+    if (rt == RT_ERR) { status = INF_DATA; break; }
 
     // ---- symbols ----
     for (;;) {
@@ -701,7 +816,23 @@ __global__ __launch_bounds__(WAVES *WAVE) void k_huff(const uint8_t *__restrict_
   }
 }
 
-// Block-wide exclusive prefix sum over LZ_THREADS threads; *total gets the sum.
+// Serial decoder kernel: one wave per block.  As the A/B baseline it decodes every block
+// (SBH_HUFF_SERIAL); behind the lane-parallel k_huff it decodes only the blocks k_huff
+// marked INF_SERIAL.
+template <bool ONLY_MARKED>
+__global__ __launch_bounds__(WAVES *WAVE) void k_huff_serial(const uint8_t *__restrict__ comp, DevBlocks bl,
+                                                              uint64_t nblocks, uint32_t *__restrict__ tok) {
+  __shared__ WaveSmem smem[WAVES];
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  const uint32_t wid = uni(threadIdx.x / WAVE);
+  const uint64_t b = (uint64_t)blockIdx.x * WAVES + wid;
+  if (b >= nblocks) return;
+  if (ONLY_MARKED && uni(bl.status[b]) != INF_SERIAL) return;
+  inflate_serial(comp, bl, b, tok, smem[wid], lane);
+}
+
+// Block-wide exclusive prefix sum over NT threads; *total gets the sum.  wsum: NT/64 words.
+template <uint32_t NT>
 __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t *wsum, uint32_t *total) {
   const uint32_t lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
   uint32_t x = v;
@@ -714,13 +845,331 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t *wsum, uint3
   __syncthreads();
   uint32_t before = 0, all = 0;
 #pragma unroll
-  for (uint32_t k = 0; k < LZ_THREADS / WAVE; ++k) {
+  for (uint32_t k = 0; k < NT / WAVE; ++k) {
     const uint32_t s = wsum[k];
     before += k < w ? s : 0;
     all += s;
   }
   *total = all;
   return before + x - v;
+}
+
+// ---------------------------------------------------------------------------------
+// Lane-parallel Huffman decode (the k_huff fast path).
+//
+// A deflate block's symbol stream is serial only through its bit positions: decoding
+// from a codeword boundary is deterministic, and Huffman/DEFLATE decoding
+// self-synchronises -- a decode started at an arbitrary bit soon falls onto the true
+// codeword boundaries.  So the HT lanes of the workgroup each take an equal slice of
+// the bits, decode speculatively from the slice start to the first token boundary at or
+// past the next slice (its exit), and then repair: a lane whose start differs from its
+// left neighbour's exit redoes its slice from that exit, until no exit changes (round r
+// fixes lane r at the latest; in practice one or two rounds).  The first lane whose
+// chain ends (EOB, invalid code, input end) decides the deflate block; a prefix sum over
+// the lanes' token/byte counts places every lane's tokens, and a third pass emits them
+// and checks distances against the bytes produced so far.  Anything the fast path does
+// not prove well-formed (stored blocks, an invalid code or too-far-back distance on the
+// true chain, a stream that ends short/long, input end inside a symbol) falls back to
+// the exact serial decoder above, so block status and tokens always equal zlib's.
+// ---------------------------------------------------------------------------------
+#ifndef SBH_HT
+#define SBH_HT 256
+#endif
+#ifndef SBH_STAGE_DW
+#define SBH_STAGE_DW 7168
+#endif
+#ifndef SBH_HUFF_OCC
+#define SBH_HUFF_OCC 4  // waves per SIMD the register budget must allow
+#endif
+constexpr uint32_t HT = SBH_HT;              // k_huff lanes per BGZF block
+constexpr uint32_t STAGE_DW = SBH_STAGE_DW;  // deflate bytes staged in LDS (28 KiB)
+constexpr uint32_t PAR_MIN_USIZE = 4096;     // smaller blocks decode serially
+#ifndef SBH_MIN_SLICE
+#define SBH_MIN_SLICE 256
+#endif
+constexpr uint32_t MIN_SLICE = SBH_MIN_SLICE;  // bits per lane at least
+constexpr uint32_t NOPOS = 0xffffffffu;
+constexpr uint32_t LR_RUN = 0, LR_EOB = 1, LR_DEAD = 2, LR_PAST = 3;
+
+struct HuffSmem {
+  WaveSmem t;                    // tables (built by wave 0; the serial fallback's too)
+  uint32_t stage[STAGE_DW + 8];  // the block's deflate dwords, from dword a0
+  uint32_t exitv[HT];            // lane exits (NOPOS: the chain ended in the lane)
+  uint32_t wsum[HT / WAVE];
+  uint32_t ctl[8];
+};
+
+// Bit source of a lane: the LDS stage or (blocks too large to stage) global memory.
+template <bool LDS>
+struct Src {
+  const uint32_t *p;
+  __device__ __forceinline__ uint32_t operator()(uint32_t i) const {
+    if (LDS) return p[i < STAGE_DW + 7 ? i : STAGE_DW + 7];
+    return p[i];
+  }
+  // 32 stream bits starting at bit position `pos`
+  __device__ __forceinline__ uint32_t bits32(uint32_t pos) const {
+    uint32_t i = pos >> 5;
+    if (LDS) i = i < STAGE_DW + 6 ? i : STAGE_DW + 6;
+    return __builtin_amdgcn_alignbit(p[i + 1], p[i], pos & 31);
+  }
+};
+
+// Long codes (> the table's bits) in the PAR format, decoded by left-justified limits:
+// the length is one more than the number of lengths whose limit lies at or below the
+// code, and the entry sits at sent[dl[len] + code].  lj/dl of lengths 10..15 are read
+// together as packed (lj << 16 | dl) words, so a long code costs two LDS round trips.
+__device__ __forceinline__ uint32_t slow_lane(const WaveSmem &sm, uint32_t bits, bool dist) {
+  const uint32_t rev15 = __builtin_bitreverse32(bits) >> 17;
+  const uint32_t *pk = sm.pk[dist ? 1 : 0];
+  const uint32_t first = dist ? PDIST_FAST + 1 : LIT_FAST + 1;  // shortest long code
+  uint32_t len = first, d = pk[first] & 0xffffu;
+#pragma unroll
+  for (uint32_t v = PDIST_FAST + 2; v <= 15; ++v) {
+    const uint32_t below = pk[v - 1], here = pk[v];
+    if (v > first && (below >> 16) <= rev15) {
+      len = v;
+      d = here & 0xffffu;
+    }
+  }
+  if (rev15 >= (pk[15] >> 16)) return 1u | (K_BAD << 5);
+  return sm.sent[(dist ? 288 : 0) + ((d + (rev15 >> (15 - len))) & 0xffffu)];
+}
+
+struct LaneRun {
+  uint32_t st;    // LR_*
+  uint32_t exit;  // RUN: first token boundary >= stop; EOB: bit after the EOB code
+  uint32_t ntok;  // tokens (EOB excluded)
+  uint32_t nout;  // bytes
+};
+
+// Checkpoints of a lane's pass-1 chain: the boundaries after CK1 and CK2 tokens and
+// the bytes produced up to them.  A repair run that lands on one of them has joined
+// that chain, so the rest of the pass-1 result holds.
+struct Ckpt {
+  uint32_t p1, o1, p2, o2;
+};
+constexpr uint32_t CK1 = 6, CK2 = 24;
+constexpr int RUN_SPEC = 0, RUN_REDO = 1, RUN_EMIT = 2;
+
+// Decode tokens from bit A while the position is below `stop`, as a two-state machine
+// (literal/length code, then distance code) so every lane runs the same instructions:
+// one table lookup per code, the extra bits taken straight from the entry.
+//   RUN_SPEC: record checkpoints in ck.
+//   RUN_REDO: stop early on reaching one of ck's boundaries (sp: that chain's result).
+//   RUN_EMIT: store tokens at dst, flag a distance reaching before the block's first
+//             byte (out0: bytes before A).
+template <bool LDS, int MODE>
+__device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, Src<LDS> src, uint32_t A, uint32_t stop,
+                                            uint32_t limit, Ckpt &ck, const LaneRun &sp,
+                                            uint32_t *__restrict__ dst, uint32_t out0, uint32_t &bad) {
+  // The only decode state is the bit position: every code reads its 32 bits afresh
+  // (two LDS dwords, one v_alignbit), which is enough for any code plus its extra bits
+  // (<= 28), and the extra bits come out with one v_bfe.  One loop exit, at the end of
+  // the body; everything else is selects (apart from the rare long code).
+  const uint32_t stop2 = stop < limit ? stop : limit;
+  uint32_t pos = A;
+  uint32_t ml = 0;  // pending match length: the next code is a distance
+  uint32_t ntok = 0, nout = 0;
+  uint32_t c1p = NOPOS, c1o = 0, c2p = NOPOS, c2o = 0;
+  uint32_t e, L;
+  bool atb, cut;
+  for (;;) {
+    const uint32_t bits = src.bits32(pos);
+    atb = ml == 0;  // token boundary
+    e = t.tab[atb ? (bits & ((1u << LIT_FAST) - 1)) : (1u << LIT_FAST) | (bits & ((1u << PDIST_FAST) - 1))];
+    if (((e >> 5) & 7) == K_SLOW) e = slow_lane(t, bits, !atb);
+    const uint32_t k = (e >> 5) & 7, x = (e >> 8) & 15;
+    L = e & 31;
+    const uint32_t val = (e >> 16) + __builtin_amdgcn_ubfe(bits, L, x);
+    const bool is_tok = k == K_LIT;  // a literal, or the distance completing a match
+    const bool is_len = atb && k == K_LEN;
+    if (MODE == RUN_SPEC) {
+      const bool h1 = atb && ntok == CK1, h2 = atb && ntok == CK2;
+      c1p = h1 ? pos : c1p;
+      c1o = h1 ? nout : c1o;
+      c2p = h2 ? pos : c2p;
+      c2o = h2 ? nout : c2o;
+    }
+    cut = atb && (pos >= stop2 || (MODE == RUN_REDO && (pos == ck.p1 || pos == ck.p2)));
+    if (cut || !(is_tok || is_len)) break;
+    pos += L + x;
+    if (MODE == RUN_EMIT) {
+      if (is_tok) dst[ntok] = atb ? val << 8 : TOK_MATCH | (ml << 16) | val;
+      bad |= (!atb && val > out0 + nout) ? 1u : 0u;
+    }
+    ntok += is_tok ? 1u : 0u;
+    nout += is_tok ? (atb ? 1u : ml) : 0u;
+    ml = is_len ? val : 0u;
+  }
+  if (MODE == RUN_SPEC) ck = Ckpt{c1p, c1o, c2p, c2o};
+  LaneRun r{LR_RUN, pos, ntok, nout};
+  if (cut) {
+    if (MODE == RUN_REDO && pos < stop2) {  // joined the pass-1 chain at a checkpoint
+      const bool one = pos == ck.p1;
+      r.ntok += sp.ntok - (one ? CK1 : CK2);
+      r.nout += sp.nout - (one ? ck.o1 : ck.o2);
+      r.st = sp.st;
+      r.exit = sp.exit;
+    } else if (pos >= limit) {
+      r.st = LR_PAST;
+    }
+  } else {  // end of block, or an invalid code
+    r.st = (atb && ((e >> 5) & 7) == K_EOB) ? LR_EOB : LR_DEAD;
+    r.exit = pos + L;
+  }
+  return r;
+}
+
+// The deflate blocks of one BGZF block, lane-parallel.  Returns false (uniformly) when
+// the block must be decoded by the serial path instead.
+template <bool LDS>
+__device__ __forceinline__ bool inflate_par(HuffSmem &sm, const uint8_t *__restrict__ comp, uint32_t a0, uint32_t skip,
+                            uint32_t limit, uint32_t usize, uint32_t *__restrict__ tk, uint32_t tid, uint32_t lane,
+                            uint32_t wid, uint32_t &ntok_out) {
+  const Src<LDS> src{LDS ? sm.stage : reinterpret_cast<const uint32_t *>(comp) + a0};
+  uint32_t p = skip, out = 0, ntok = 0;
+  bool fixed_built = false;  // wave 0: the tables in sm.t are the fixed code's
+  for (;;) {
+#ifdef SBH_HUFF_PROBE
+    const uint64_t tp0 = __builtin_readcyclecounter();
+#endif
+    if (wid == 0) {
+      Bits br;
+      br.c32 = reinterpret_cast<const uint32_t *>(comp);
+      br.a0 = a0;
+      br.limit = limit;
+      br.seek(p);
+      br.refill();
+      uint32_t ok = 0, last = 0, psym = 0;
+      if (br.avail(3)) {
+        last = br.take(1);
+        const uint32_t type = br.take(2);
+        if (type == 1 || type == 2) ok = read_tables<true>(sm.t, br, type, fixed_built, lane) == RT_OK;
+        psym = br.pos();
+      }
+      if (lane == 0) {
+        sm.ctl[0] = ok;
+        sm.ctl[1] = psym;
+        sm.ctl[2] = last;
+        sm.ctl[3] = HT;
+      }
+    }
+    __syncthreads();
+    const uint32_t ok = uni(sm.ctl[0]), p0 = uni(sm.ctl[1]), last = uni(sm.ctl[2]);
+    if (!ok) return false;
+
+#ifdef SBH_HUFF_PROBE
+    const uint64_t tph = __builtin_readcyclecounter();
+#endif
+    // pass 1: speculative decode of every lane's slice
+    uint32_t S = (limit > p0 ? limit - p0 : 0) / HT + 1;
+    if (S < MIN_SLICE) S = MIN_SLICE;  // short streams: fewer, longer slices (sync needs bits)
+    const uint32_t s = p0 + tid * S, stop = s + S;
+    uint32_t A = s, nobad = 0;
+    Ckpt ck;
+    const LaneRun none{};
+    LaneRun r = lane_run<LDS, RUN_SPEC>(sm.t, src, A, stop, limit, ck, none, nullptr, 0, nobad);
+    sm.exitv[tid] = r.st == LR_RUN ? r.exit : NOPOS;
+    // pass 2: repair rounds until every lane starts where its left neighbour exits.
+    // A repair run stops as soon as it joins the lane's pass-1 chain (first round only).
+#ifdef SBH_HUFF_PROBE
+    uint32_t nrounds = 0;
+    __syncthreads();
+    const uint64_t tp1 = __builtin_readcyclecounter();
+#endif
+    for (;;) {
+#ifdef SBH_HUFF_PROBE
+      ++nrounds;
+#endif
+      __syncthreads();
+      // a lane keeps its speculation while its left neighbour's chain has ended (that
+      // neighbour is then past the true end, or itself speculating and not yet repaired)
+      const uint32_t nA = tid == 0 ? p0 : sm.exitv[tid - 1];
+      const bool changed = nA != NOPOS && nA != A;
+      __syncthreads();
+      if (changed) {
+        A = nA;
+        r = lane_run<LDS, RUN_REDO>(sm.t, src, A, stop, limit, ck, r, nullptr, 0, nobad);
+        sm.exitv[tid] = r.st == LR_RUN ? r.exit : NOPOS;
+      }
+      ck = Ckpt{NOPOS, 0, NOPOS, 0};  // later rounds: the chain changed, run fully
+      if (!__syncthreads_or(changed)) break;
+    }
+    // the first lane whose chain ends decides the deflate block
+    if (r.st != LR_RUN) atomicMin(&sm.ctl[3], tid);
+    __syncthreads();
+    const uint32_t k = uni(sm.ctl[3]);
+    if (tid == k) sm.ctl[4] = (r.st == LR_EOB && r.exit <= limit) ? r.exit : NOPOS;
+    uint32_t ttot, otot;
+    const uint32_t tpre = block_scan<HT>(tid <= k ? r.ntok : 0, sm.wsum, &ttot);  // (syncs: ctl[4] visible)
+    __syncthreads();
+    const uint32_t opre = block_scan<HT>(tid <= k ? r.nout : 0, sm.wsum, &otot);
+    const uint32_t eob_end = uni(sm.ctl[4]);
+    ttot = uni(ttot);
+    otot = uni(otot);
+#ifdef SBH_HUFF_PROBE
+    if (tid == 0 && blockIdx.x < 6)
+      printf("huff blk %u S %u rounds %u k %u ttot %u otot %u last %u hdr %llu p1 %llu p2 %llu\n",
+             blockIdx.x, S, nrounds, k, ttot, otot, last, (unsigned long long)(tph - tp0),
+             (unsigned long long)(tp1 - tph), (unsigned long long)(__builtin_readcyclecounter() - tp1));
+    const uint64_t tp3 = __builtin_readcyclecounter();
+#endif
+    if (k >= HT || eob_end == NOPOS || otot > usize - out) return false;
+    // pass 3: emit
+    uint32_t bad = 0;
+    if (tid <= k) lane_run<LDS, RUN_EMIT>(sm.t, src, A, stop, limit, ck, none, tk + ntok + tpre, out + opre, bad);
+    if (__syncthreads_or(bad)) return false;
+#ifdef SBH_HUFF_PROBE
+    if (tid == 0 && blockIdx.x < 6) printf("huff blk %u p3 %llu\n", blockIdx.x, (unsigned long long)(__builtin_readcyclecounter() - tp3));
+#endif
+    ntok += ttot;
+    out += otot;
+    p = eob_end;
+    if (last) break;
+  }
+  if (out != usize) return false;
+  ntok_out = ntok;
+  return true;
+}
+
+__global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__restrict__ comp, DevBlocks bl, uint64_t nblocks,
+                                              uint32_t *__restrict__ tok) {
+  __shared__ HuffSmem sm;
+  const uint32_t tid = threadIdx.x, lane = tid & (WAVE - 1), wid = uni(tid / WAVE);
+  const uint64_t b = blockIdx.x;
+  if (b >= nblocks) return;
+  const uint64_t cstart = bl.cstart[b];
+  const uint32_t csize = bl.csize[b], hsize = bl.hsize[b], usize = bl.usize[b];
+  const uint64_t G = bl.ustart[b];
+  const bool serial = (bl.flags[b] & BLK_TRUNCATED) || usize > 65536u || usize < PAR_MIN_USIZE ||
+                (int32_t)csize - (int32_t)hsize - 8 < 0;
+  if (!serial) {
+    const uint32_t data_len = csize - hsize - 8;
+    const uint64_t dbyte = cstart + hsize;
+    const uint32_t a0 = (uint32_t)(dbyte >> 2);
+    const uint32_t skip = (uint32_t)(dbyte & 3) * 8;
+    const uint32_t limit = skip + data_len * 8;
+    const uint32_t ndw = (limit + 31) / 32 + 2;
+    uint32_t ntok = 0;
+    bool ok;
+    if (ndw <= STAGE_DW) {
+      const uint32_t *g = reinterpret_cast<const uint32_t *>(comp) + a0;
+      for (uint32_t i = tid; i < ndw; i += HT) sm.stage[i] = g[i];
+      __syncthreads();
+      ok = inflate_par<true>(sm, comp, a0, skip, limit, usize, tok + G, tid, lane, wid, ntok);
+    } else {
+      ok = inflate_par<false>(sm, comp, a0, skip, limit, usize, tok + G, tid, lane, wid, ntok);
+    }
+    if (uni(ok)) {
+      if (tid == 0) {
+        bl.status[b] = INF_OK;
+        bl.ntok[b] = ntok;
+      }
+      return;
+    }
+  }
+  if (tid == 0) bl.status[b] = INF_SERIAL;  // k_huff_serial<true> decodes it
 }
 
 struct LzSmem {
@@ -809,7 +1258,7 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
     const bool match = i < n && (x & TOK_MATCH) != 0;
     const uint32_t len = i >= n ? 0 : match ? (x >> 16) & 0x1ff : 1;
     uint32_t chunk_len;
-    const uint32_t off = base + block_scan(len, sm.wsum, &chunk_len);
+    const uint32_t off = base + block_scan<LZ_THREADS>(len, sm.wsum, &chunk_len);
     if (t < m) {
       sm.toff[t] = off;
       sm.tokv[t] = x;
@@ -913,8 +1362,16 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
 hipError_t launch_huff(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, uint32_t *tok,
                        hipStream_t stream) {
   if (nblocks == 0) return hipSuccess;
+#ifdef SBH_HUFF_SERIAL
   const uint64_t grid = (nblocks + WAVES - 1) / WAVES;
-  hipLaunchKernelGGL(k_huff, dim3((uint32_t)grid), dim3(WAVES * WAVE), 0, stream, comp, blocks, nblocks, tok);
+  hipLaunchKernelGGL(k_huff_serial<false>, dim3((uint32_t)grid), dim3(WAVES * WAVE), 0, stream, comp, blocks, nblocks,
+                     tok);
+#else
+  hipLaunchKernelGGL(k_huff, dim3((uint32_t)nblocks), dim3(HT), 0, stream, comp, blocks, nblocks, tok);
+  const uint64_t grid = (nblocks + WAVES - 1) / WAVES;
+  hipLaunchKernelGGL(k_huff_serial<true>, dim3((uint32_t)grid), dim3(WAVES * WAVE), 0, stream, comp, blocks, nblocks,
+                     tok);
+#endif
   return hipGetLastError();
 }
 

@@ -32,6 +32,7 @@ constexpr uint32_t INF_OK = 0;
 constexpr uint32_t INF_SIZE = 1;      // fewer than ISIZE bytes produced
 constexpr uint32_t INF_DATA = 2;      // DataFormatException (zlib Z_DATA_ERROR)
 constexpr uint32_t INF_BAD_ISIZE = 3; // ISIZE outside [0, 65536]
+constexpr uint32_t INF_SERIAL = 0xffu; // (inside inflate only) left to the serial decoder
 
 // Launchers (defined in the .hip files, called from sbh_api.hip).
 // Inflate = k_huff (Huffman decode -> LZ77 tokens, block status) then k_lz (tokens ->
