@@ -1021,6 +1021,132 @@ __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, Src<LDS> src, uin
   return r;
 }
 
+// Deflate block header and tables for the lane-parallel path, read from the bit source
+// (sm.ctl[5..6] carry wave 0's result to the workgroup).  The code-length symbols are
+// decoded 64 bit positions at a time -- lane i decodes the symbol that would start at
+// q + i -- and wave 0 walks the chain through those with v_readlane, writing each run
+// of lengths with one vector store.  Then wave 0 builds the literal/length table and
+// wave 1 the distance table, concurrently.  Returns false (uniformly) for anything
+// the serial decoder must judge: stored/invalid block types, invalid or incomplete
+// codes, a header running past the input.
+template <bool LDS>
+__device__ __forceinline__ bool par_header(HuffSmem &sm, Src<LDS> src, uint32_t p, uint32_t limit, bool &fixed_built,
+                                           uint32_t wid, uint32_t lane, uint32_t &psym, uint32_t &last) {
+  WaveSmem &t = sm.t;
+  const uint32_t hb = uni(src.bits32(p));
+  last = hb & 1;
+  const uint32_t type = (hb >> 1) & 3;
+  if (p + 3 > limit || type == 0 || type == 3) return false;
+  if (type == 1) {
+    psym = p + 3;
+    if (!fixed_built) {
+      if (wid == 0) {
+        for (uint32_t s = lane; s < 288; s += WAVE) t.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
+        __builtin_amdgcn_wave_barrier();
+        build_ptable(t, t.lens, 288, 0, t.lit, LIT_FAST, lane);
+      } else if (wid == 1) {
+        if (lane < 32) t.lens[288 + lane] = 5;
+        __builtin_amdgcn_wave_barrier();
+        build_ptable(t, t.lens + 288, 32, 1, t.dist, PDIST_FAST, lane);
+      }
+      __syncthreads();
+      fixed_built = true;
+    }
+    return true;
+  }
+  fixed_built = false;
+  const uint32_t nlen = ((hb >> 3) & 31) + 257, ndist = ((hb >> 8) & 31) + 1, ncode = ((hb >> 13) & 15) + 4;
+  if (nlen > 286 || ndist > 30) return false;
+#ifdef SBH_HUFF_PROBE
+  const uint64_t h0 = __builtin_readcyclecounter();
+  uint64_t h1 = 0, h2 = 0;
+#endif
+  if (wid == 0) {
+    if (lane < 19) t.cl_lens[CL_ORDER[lane]] = lane < ncode ? (uint8_t)(src.bits32(p + 17 + 3 * lane) & 7) : 0;
+    __builtin_amdgcn_wave_barrier();
+    bool ok = uni(build_table(t, t.cl_lens, 19, 2, t.lit, CL_FAST, lane)) == 0;
+#ifdef SBH_HUFF_PROBE
+    h1 = __builtin_readcyclecounter();
+#endif
+    const uint32_t total = nlen + ndist;
+    uint32_t i = 0, prev = 0, q = p + 17 + 3 * ncode;
+    const uint64_t below = (1ull << lane) - 1;  // lanes under this one
+    while (ok && i < total) {
+      // every lane decodes the symbol that would start at q + lane
+      const uint32_t b = src.bits32(q + lane);
+      const uint32_t e = t.lit[b & ((1u << CL_FAST) - 1)];
+      const uint32_t L = e & 31, sym = (e >> 8) & 31;
+      const uint32_t xb = sym < 16 ? 0 : sym == 16 ? 2 : sym == 17 ? 3 : 7;
+      const uint32_t xv = __builtin_amdgcn_ubfe(b, L, xb);
+      const uint32_t rep = sym < 16 ? 1 : sym == 16 ? 3 + xv : sym == 17 ? 3 + xv : 11 + xv;
+      const uint32_t pack = (L + xb) | (rep << 8);
+      // serial part: the chain of symbol starts through this window
+      uint64_t M = 0;
+      uint32_t o = 0, i0 = i;
+      while (o < WAVE && i < total) {
+        const uint32_t inf = __builtin_amdgcn_readlane(pack, o);
+        M |= 1ull << o;
+        o += inf & 255;
+        i += inf >> 8;
+      }
+      // parallel part: output index and value of each symbol, then its run of lengths
+      const bool mine = (M >> lane) & 1;
+      uint32_t ex;  // exclusive prefix of rep over the window's symbols
+      {
+        uint32_t x = mine ? rep : 0;
+#pragma unroll
+        for (uint32_t d = 1; d < WAVE; d <<= 1) {
+          const uint32_t y = __shfl_up(x, d, WAVE);
+          if (lane >= d) x += y;
+        }
+        ex = x - (mine ? rep : 0);
+      }
+      const uint32_t start = i0 + ex;
+      const uint64_t N = M & __ballot(sym != 16);  // symbols with a value of their own
+      const uint64_t lowN = N & below;
+      const uint32_t own = sym < 16 ? sym : 0;
+      const uint32_t src_lane = lowN ? 63 - (uint32_t)__builtin_clzll(lowN) : 0;
+      const uint32_t from = __shfl(own, src_lane, WAVE);
+      const uint32_t val = sym == 16 ? (lowN ? from : prev) : own;
+      if (M & 1 && __builtin_amdgcn_readfirstlane(sym) == 16 && i0 == 0) ok = false;  // repeat with no previous length
+      if (mine) {
+        for (uint32_t k = 0; k < rep; ++k) {
+          const uint32_t j = start + k;
+          if (j < total) t.lens[j < nlen ? j : 288 + j - nlen] = (uint8_t)val;
+        }
+      }
+      const uint32_t top = 63 - (uint32_t)__builtin_clzll(M);
+      prev = __builtin_amdgcn_readlane(val, top);
+      q += o;
+    }
+    if (i != total || q > limit) ok = false;  // a repeat past the end, or input ran out
+    __builtin_amdgcn_wave_barrier();
+#ifdef SBH_HUFF_PROBE
+    h2 = __builtin_readcyclecounter();
+#endif
+    if (ok && uni(t.lens[256]) == 0) ok = false;  // no end-of-block code
+    if (lane == 0) {
+      sm.ctl[5] = ok;
+      sm.ctl[6] = q;
+    }
+  }
+  __syncthreads();
+  if (!uni(sm.ctl[5])) return false;
+  psym = uni(sm.ctl[6]);
+  uint32_t rc = 0;
+  if (wid == 0) rc = build_ptable(t, t.lens, nlen, 0, t.lit, LIT_FAST, lane);
+  else if (wid == 1) rc = build_ptable(t, t.lens + 288, ndist, 1, t.dist, PDIST_FAST, lane);
+#ifdef SBH_HUFF_PROBE
+  const bool res = !__syncthreads_or(rc == 1);
+  if (threadIdx.x == 0 && blockIdx.x < 3)
+    printf("hdr blk %u cl %llu walk %llu build %llu\n", blockIdx.x, (unsigned long long)(h1 - h0),
+           (unsigned long long)(h2 - h1), (unsigned long long)(__builtin_readcyclecounter() - h2));
+  return res;
+#else
+  return !__syncthreads_or(rc == 1);
+#endif
+}
+
 // The deflate blocks of one BGZF block, lane-parallel.  Returns false (uniformly) when
 // the block must be decoded by the serial path instead.
 template <bool LDS>
@@ -1029,35 +1155,14 @@ __device__ __forceinline__ bool inflate_par(HuffSmem &sm, const uint8_t *__restr
                             uint32_t wid, uint32_t &ntok_out) {
   const Src<LDS> src{LDS ? sm.stage : reinterpret_cast<const uint32_t *>(comp) + a0};
   uint32_t p = skip, out = 0, ntok = 0;
-  bool fixed_built = false;  // wave 0: the tables in sm.t are the fixed code's
+  bool fixed_built = false;  // the tables in sm.t are the fixed code's
   for (;;) {
 #ifdef SBH_HUFF_PROBE
     const uint64_t tp0 = __builtin_readcyclecounter();
 #endif
-    if (wid == 0) {
-      Bits br;
-      br.c32 = reinterpret_cast<const uint32_t *>(comp);
-      br.a0 = a0;
-      br.limit = limit;
-      br.seek(p);
-      br.refill();
-      uint32_t ok = 0, last = 0, psym = 0;
-      if (br.avail(3)) {
-        last = br.take(1);
-        const uint32_t type = br.take(2);
-        if (type == 1 || type == 2) ok = read_tables<true>(sm.t, br, type, fixed_built, lane) == RT_OK;
-        psym = br.pos();
-      }
-      if (lane == 0) {
-        sm.ctl[0] = ok;
-        sm.ctl[1] = psym;
-        sm.ctl[2] = last;
-        sm.ctl[3] = HT;
-      }
-    }
-    __syncthreads();
-    const uint32_t ok = uni(sm.ctl[0]), p0 = uni(sm.ctl[1]), last = uni(sm.ctl[2]);
-    if (!ok) return false;
+    uint32_t p0, last;
+    if (!par_header(sm, src, p, limit, fixed_built, wid, lane, p0, last)) return false;
+    if (tid == 0) sm.ctl[3] = HT;
 
 #ifdef SBH_HUFF_PROBE
     const uint64_t tph = __builtin_readcyclecounter();
