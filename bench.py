@@ -190,7 +190,7 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBPS, 5),
                 "traffic": args.traffic,
                 "alg_bytes_per_launch": int(alg_bytes),
-                "limiter": "k_huff: scalar-unit issue of the serial Huffman decode, not HBM",
+                "limiter": "k_lz (LDS-resident LZ77 resolve rounds) then k_huff (VALU issue of the lane-parallel decode passes); neither is HBM-bound",
                 "per_kernel_GBps": {"k_huff (C in)": gbps(comp_bytes, stage_ms[4]),
                                     "k_lz (U out)": gbps(flat_bytes, stage_ms[5]),
                                     "k_eager (U in + U/8 out)": gbps(flat_bytes * 1.125, stage_ms[2])},
