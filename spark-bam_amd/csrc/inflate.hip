@@ -1277,13 +1277,49 @@ __global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__rest
   if (tid == 0) bl.status[b] = INF_SERIAL;  // k_huff_serial<true> decodes it
 }
 
+constexpr uint32_t PTR_CAP = 4096;                 // chunk bytes resolved by pointer jumping
+constexpr uint32_t PTR_PER = PTR_CAP / LZ_THREADS;  // slots per thread
+static_assert(PTR_PER == 8, "one uint4 of u16 slots per thread");
+
 struct LzSmem {
   uint8_t img[65536 + 16];    // block image, placed at (ustart & 15) so granules align with HBM
   uint32_t toff[LZ_THREADS];  // chunk tokens: output offsets (ascending)
   uint32_t tokv[LZ_THREADS];  // chunk tokens
   uint32_t done[LZ_THREADS];  // round after which the token's bytes are final (0: pending)
   uint32_t wsum[LZ_THREADS / WAVE];
+  uint4 ptr[LZ_THREADS];      // u16 per chunk byte: owning token, then source pointer
 };
+
+// Block-wide exclusive prefix max over NT threads (0 for thread 0).
+template <uint32_t NT>
+__device__ __forceinline__ uint32_t block_scan_max(uint32_t v, uint32_t *wsum) {
+  const uint32_t lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+  uint32_t x = v;
+#pragma unroll
+  for (uint32_t d = 1; d < WAVE; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, WAVE);
+    if (lane >= d) x = x > y ? x : y;
+  }
+  const uint32_t ex_w = __shfl_up(x, 1, WAVE);
+  if (lane == WAVE - 1) wsum[w] = x;
+  __syncthreads();
+  uint32_t before = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < NT / WAVE; ++k) {
+    const uint32_t s = wsum[k];
+    before = (k < w && s > before) ? s : before;
+  }
+  const uint32_t in_w = lane ? ex_w : 0;
+  return before > in_w ? before : in_w;
+}
+
+// k mod d for k < 2^17, d >= 1 (one reciprocal, one correction).
+__device__ __forceinline__ uint32_t mod_small(uint32_t k, uint32_t d) {
+  const uint32_t q = (uint32_t)((float)k * __builtin_amdgcn_rcpf((float)d));
+  int32_t r = (int32_t)(k - q * d);
+  r = r < 0 ? r + (int32_t)d : r;
+  return (uint32_t)(r >= (int32_t)d ? r - (int32_t)d : r);
+}
 
 // Token of the chunk covering output offset q (toff[0] <= q).
 __device__ __forceinline__ uint32_t cover(const uint32_t *toff, uint32_t m, uint32_t q) {
@@ -1329,11 +1365,14 @@ __device__ __forceinline__ void lz_match(uint8_t *img0, uint32_t base, uint32_t 
   }
 }
 
-// LZ77 resolution of one block per workgroup, LZ_THREADS tokens per chunk.  Within a
-// chunk, a match waits only for the chunk's matches its source bytes overlap (the
-// token range found once by binary search over the chunk's output offsets); on
-// synthetic and real BAM data that dependency depth is <= 4 at 256 tokens, so a
-// chunk resolves in a few barrier rounds.  Bytes before the chunk are final.
+// LZ77 resolution of one block per workgroup, LZ_THREADS tokens per chunk; bytes before
+// the chunk are final.  A chunk whose output fits PTR_CAP bytes (the common case) is
+// resolved by pointer chasing: every byte gets the position it copies from (itself for a
+// literal), each thread follows its 8 bytes' pointers to final bytes -- rewriting its
+// slots with the results, which shortens other threads' chases -- and gathers.  Longer
+// chunks (long matches) fall back to dependency rounds: a match waits only for the
+// chunk's matches its (redirected) source overlaps, found by binary search over the
+// chunk's output offsets.
 __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblocks,
                                                     const uint32_t *__restrict__ tok, uint8_t *__restrict__ U) {
   __shared__ LzSmem sm;
@@ -1349,8 +1388,8 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
   uint32_t base = 0;  // output offset of the chunk's first token
   uint32_t x_next = t < n ? tk[t] : 0;
 #ifdef SBH_LZ_PROBE
-  uint64_t tp0 = __builtin_readcyclecounter(), t_pre = 0, t_rounds = 0;
-  uint32_t nrounds = 0;
+  uint64_t tp0 = __builtin_readcyclecounter(), t_pre = 0, t_rounds = 0, t_init = 0;
+  uint32_t nrounds = 0, njumps = 0;
 #endif
   for (uint32_t c0 = 0; c0 < n; c0 += LZ_THREADS) {
 #ifdef SBH_LZ_PROBE
@@ -1370,68 +1409,134 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
       sm.done[t] = match ? 0 : 1;
       if (!match) img[off] = (uint8_t)(x >> 8);
     }
-    __syncthreads();
-    const uint32_t dist = x & 0xffff;
-    uint32_t src = off - dist;  // where the (final-equivalent) source bytes start
-    uint32_t jl = 1, jh = 0;    // chunk tokens the source overlaps (empty: none)
-    if (match) {
-      // external source bytes: [src, src + min(len, dist)) (an overlapping match
-      // re-reads its own output only through the period)
-      const uint32_t ext = len < dist ? len : dist;
-      // Redirect through the chunk's own matches: a source wholly inside one
-      // non-overlapping match M' equals the bytes M' copied, dist' earlier.  This
-      // collapses chains (read names copying the previous read's name ...) so most
-      // matches copy in the first round.
-      for (int hop = 0; hop < 16 && src >= base; ++hop) {
-        const uint32_t j = cover(sm.toff, m, src);
-        const uint32_t y = sm.tokv[j];
-        if (!(y & TOK_MATCH)) break;
-        const uint32_t oj = sm.toff[j], lj = (y >> 16) & 0x1ff, dj = y & 0xffff;
-        if (dj < lj || src + ext > oj + lj) break;  // overlapping M' or source spans tokens
-        src -= dj;
-      }
-      if (src + ext > base) {
-        jl = src < base ? 0 : cover(sm.toff, m, src);
-        jh = cover(sm.toff, m, src + ext - 1);
-      }
-    }
-    bool pending = match;
 #ifdef SBH_LZ_PROBE
-    uint64_t tb = __builtin_readcyclecounter();
+    const uint64_t tb = __builtin_readcyclecounter();
     t_pre += tb - ta;
+    nrounds += chunk_len > PTR_CAP;
 #endif
-    for (uint32_t r = 1;; ++r) {
+    if (chunk_len <= PTR_CAP) sm.ptr[t] = make_uint4(0, 0, 0, 0);  // free since the last chunk's barrier
+    __syncthreads();  // toff/tokv, the literal bytes and the cleared slots are visible
+    if (chunk_len <= PTR_CAP) {
+      // Pointer jumping over the chunk's bytes.  Every byte gets a source pointer: a
+      // literal byte points at itself, match byte k at the byte it copies
+      // (off - dist + k mod dist, always earlier); bytes before the chunk are final.
+      // Rounds of ptr = ptr[ptr] end when every pointer reaches a final byte, then
+      // one gather fills all match bytes at once.
+      // owner token of each slot: token start marks, then a block-wide max-scan
+      if (t < m) reinterpret_cast<uint16_t *>(sm.ptr)[off - base] = (uint16_t)t;
+      __syncthreads();
+      uint32_t own[PTR_PER];
+      {
+        const uint4 mk = sm.ptr[t];
+        own[0] = mk.x & 0xffff; own[1] = mk.x >> 16; own[2] = mk.y & 0xffff; own[3] = mk.y >> 16;
+        own[4] = mk.z & 0xffff; own[5] = mk.z >> 16; own[6] = mk.w & 0xffff; own[7] = mk.w >> 16;
+#pragma unroll
+        for (uint32_t k = 1; k < PTR_PER; ++k) own[k] = own[k] > own[k - 1] ? own[k] : own[k - 1];
+        const uint32_t before = block_scan_max<LZ_THREADS>(own[PTR_PER - 1], sm.wsum);
+#pragma unroll
+        for (uint32_t k = 0; k < PTR_PER; ++k) own[k] = own[k] > before ? own[k] : before;
+      }
+      uint32_t q[PTR_PER];
+#pragma unroll
+      for (uint32_t k = 0; k < PTR_PER; ++k) {
+        const uint32_t slot = t * PTR_PER + k, pos = base + slot;
+        uint32_t ptr = pos;
+        if (slot < chunk_len) {
+          const uint32_t j = own[k];
+          const uint32_t y = sm.tokv[j];
+          if (y & TOK_MATCH) {
+            const uint32_t oj = sm.toff[j], dj = y & 0xffff;
+            uint32_t kk = pos - oj;
+            if (kk >= dj) kk = mod_small(kk, dj);
+            ptr = oj - dj + kk;
+          }
+        }
+        q[k] = ptr;
+      }
+      sm.ptr[t] = make_uint4(q[0] | q[1] << 16, q[2] | q[3] << 16, q[4] | q[5] << 16, q[6] | q[7] << 16);
+      uint16_t *p16 = reinterpret_cast<uint16_t *>(sm.ptr);
 #ifdef SBH_LZ_PROBE
-      ++nrounds;
+      const uint64_t tc = __builtin_readcyclecounter();
+      t_init += tc - tb;
 #endif
-      bool go = false;
-      if (pending) {
-        go = true;
-        for (uint32_t j = jl; j <= jh && go; ++j) {
-          const uint32_t dj = sm.done[j];
-          go = dj != 0 && dj <= r;
+      __syncthreads();
+      // chase every pointer to a final byte (before the chunk, or a literal: a slot
+      // pointing at itself).  Slots are rewritten with their final pointers as threads
+      // finish, which only shortens other threads' chases; no rounds, no barriers.
+#pragma unroll
+      for (uint32_t k = 0; k < PTR_PER; ++k) {
+        const uint32_t pos = base + t * PTR_PER + k;
+        uint32_t c = q[k];
+        if (c != pos) {
+          while (c >= base) {
+            const uint32_t v = __hip_atomic_load(&p16[c - base], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef SBH_LZ_PROBE
+            ++njumps;
+#endif
+            if (v == c) break;
+            c = v;
+          }
+          __hip_atomic_store(&p16[pos - base], (uint16_t)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          img[pos] = img[c];
         }
       }
-      // long matches: the whole wave copies each one (byte k by lane k mod 64)
-      uint64_t lm = __ballot(go && len > LZ_LONG);
-      while (lm) {
-        const uint32_t l = (uint32_t)__builtin_ctzll(lm);
-        lm &= lm - 1;
-        const uint32_t o = __builtin_amdgcn_readlane(off, l), sr = __builtin_amdgcn_readlane(src, l);
-        const uint32_t d = __builtin_amdgcn_readlane(dist, l), L = __builtin_amdgcn_readlane(len, l);
-        const uint32_t lane = t & (WAVE - 1);
-        if (d >= L) {
-          for (uint32_t k = lane; k < L; k += WAVE) img[o + k] = img[sr + k];
-        } else {
-          for (uint32_t k = lane; k < L; k += WAVE) img[o + k] = img[sr + k % d];
+    } else {
+      const uint32_t dist = x & 0xffff;
+      uint32_t src = off - dist;  // where the (final-equivalent) source bytes start
+      uint32_t jl = 1, jh = 0;    // chunk tokens the source overlaps (empty: none)
+      if (match) {
+        // external source bytes: [src, src + min(len, dist)) (an overlapping match
+        // re-reads its own output only through the period)
+        const uint32_t ext = len < dist ? len : dist;
+        // Redirect through the chunk's own matches: a source wholly inside one
+        // non-overlapping match M' equals the bytes M' copied, dist' earlier.  This
+        // collapses chains (read names copying the previous read's name ...) so most
+        // matches copy in the first round.
+        for (int hop = 0; hop < 16 && src >= base; ++hop) {
+          const uint32_t j = cover(sm.toff, m, src);
+          const uint32_t y = sm.tokv[j];
+          if (!(y & TOK_MATCH)) break;
+          const uint32_t oj = sm.toff[j], lj = (y >> 16) & 0x1ff, dj = y & 0xffff;
+          if (dj < lj || src + ext > oj + lj) break;  // overlapping M' or source spans tokens
+          src -= dj;
+        }
+        if (src + ext > base) {
+          jl = src < base ? 0 : cover(sm.toff, m, src);
+          jh = cover(sm.toff, m, src + ext - 1);
         }
       }
-      if (go && len <= LZ_LONG) lz_match(sm.img, sh, off, src, dist, len);
-      if (go) {
-        sm.done[t] = r + 1;
-        pending = false;
+      bool pending = match;
+      for (uint32_t r = 1;; ++r) {
+        bool go = false;
+        if (pending) {
+          go = true;
+          for (uint32_t j = jl; j <= jh && go; ++j) {
+            const uint32_t dj = sm.done[j];
+            go = dj != 0 && dj <= r;
+          }
+        }
+        // long matches: the whole wave copies each one (byte k by lane k mod 64)
+        uint64_t lm = __ballot(go && len > LZ_LONG);
+        while (lm) {
+          const uint32_t l = (uint32_t)__builtin_ctzll(lm);
+          lm &= lm - 1;
+          const uint32_t o = __builtin_amdgcn_readlane(off, l), sr = __builtin_amdgcn_readlane(src, l);
+          const uint32_t d = __builtin_amdgcn_readlane(dist, l), L = __builtin_amdgcn_readlane(len, l);
+          const uint32_t lane = t & (WAVE - 1);
+          if (d >= L) {
+            for (uint32_t k = lane; k < L; k += WAVE) img[o + k] = img[sr + k];
+          } else {
+            for (uint32_t k = lane; k < L; k += WAVE) img[o + k] = img[sr + k % d];
+          }
+        }
+        if (go && len <= LZ_LONG) lz_match(sm.img, sh, off, src, dist, len);
+        if (go) {
+          sm.done[t] = r + 1;
+          pending = false;
+        }
+        if (!__syncthreads_or(pending)) break;
       }
-      if (!__syncthreads_or(pending)) break;
+
     }
     base += chunk_len;
     __syncthreads();  // toff/done/wsum are reused by the next chunk
@@ -1441,9 +1546,9 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
   }
 #ifdef SBH_LZ_PROBE
   if (t == 0 && b < 4)
-    printf("lz blk %llu ntok %u cyc %llu pre %llu rounds %llu nrounds %u\n", (unsigned long long)b, n,
+    printf("lz blk %llu ntok %u cyc %llu pre %llu init %llu resolve %llu fallback_chunks %u jump_rounds %u\n", (unsigned long long)b, n,
            (unsigned long long)(__builtin_readcyclecounter() - tp0), (unsigned long long)t_pre,
-           (unsigned long long)t_rounds, nrounds);
+           (unsigned long long)t_init, (unsigned long long)t_rounds, nrounds, njumps);
 #endif
   const uint32_t usize = base;
   // write the image: 16-byte granules aligned to the flat address
