@@ -300,7 +300,7 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
                                              uint64_t end, Segs sg, Ctg c, int32_t rtc, EagerOut o) {
   constexpr uint32_t NV = (ESTAGE + 32) / 16;
   __shared__ uint4 ldsv[NV];
-  __shared__ uint32_t ok[EW / 32], nrm[EW / 32], und[EW / 32];
+  __shared__ uint32_t ok[EW / 32], nrm[EW / 32], und[EW / 32], res[ETILE / 32];
   __shared__ uint32_t seg0, ntrue, nq;
   __shared__ uint64_t seg_end0;
   __shared__ uint16_t queue[EQ_CHUNK];
@@ -313,6 +313,7 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
 #endif
   stage_vec<NV>(ldsv, U, s0, u_pad);
   for (uint32_t i = threadIdx.x; i < EW / 32; i += T) { ok[i] = 0; nrm[i] = 0; und[i] = 0; }
+  for (uint32_t i = threadIdx.x; i < ETILE / 32; i += T) res[i] = 0;
   if (threadIdx.x == 0) {
     const uint32_t k = seg_first(sg, t0);
     seg0 = k;
@@ -331,128 +332,189 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
 #ifdef SBH_EPROBE
   const uint64_t c1 = __builtin_readcyclecounter();
 #endif
-  // ---- phase A: refID filter on 4 positions per staged dword pair (every lane busy);
-  // survivors (~3% of BAM positions) are queued in LDS and get the whole single-record
-  // predicate compacted, so one_record never runs with most lanes idle ----
-  const uint32_t lane = threadIdx.x & (WAVE - 1);
-  const uint64_t lt_mask = (1ull << lane) - 1ull;
-  for (uint32_t c0p = 0; c0p < EW + sa; c0p += EQ_CHUNK) {
-    for (uint32_t j = c0p / 4 + threadIdx.x; 4 * j < EW + sa && 4 * j < c0p + EQ_CHUNK; j += T) {
-      const uint32_t a = lds32[j + 1], b = lds32[j + 2];  // bytes s0 + 4j + 4 .. + 11
+  // ---- phase A: every position of the window gets the fixed-field part of the
+  // single-record predicate (refID / next refID in [-1, n), pos / next pos >= -1,
+  // l_read_name >= 2, the empty-mapped rule, remaining-length floor), 4 positions per
+  // thread from 9 staged dwords with v_alignbyte.  Only true record starts and rare
+  // look-alikes survive (~0.5% of BAM positions); they are queued in LDS and get the
+  // whole single-record predicate compacted.  A position failing a fixed-field test
+  // would fail one_record too, so the filter is exact. ----
+  auto eval_one = [&](uint32_t i) {
+    const uint64_t q = t0 + i;
+    const uint64_t total = q < e0 ? e0 : sg.end[seg_index(sg, q, k0)];
+    uint64_t succ;
+    bool normal;
+    const uint32_t r = one_record(s, q, total, c, &succ, &normal);
+    if (r == 1) {
+      atomicOr(&ok[i >> 5], 1u << (i & 31));
+      if (normal) atomicOr(&nrm[i >> 5], 1u << (i & 31));
+    } else if (r == 2) {
+      atomicOr(&und[i >> 5], 1u << (i & 31));
+    }
+  };
+  {
+    // this thread's groups of 4 positions: [g0, g0 + EG); group g covers staged bytes 4g..4g+3
+    constexpr uint32_t EG = (EW / 4 + 4 + T - 1) / T;
+    constexpr uint32_t EMW = (EG * 4 + 31) / 32;
+    const uint32_t ngroups = (EW + sa + 3) / 4;
+    const uint32_t g0 = threadIdx.x * EG;
+    // stage 1: refID in [-1, n) (the most selective field; ~3% pass), ~3 VALU per position
+    uint32_t msk[EMW];
+#pragma unroll
+    for (uint32_t w = 0; w < EMW; ++w) msk[w] = 0;
+    uint32_t a = lds32[g0 + 1];
+#pragma unroll
+    for (uint32_t gi = 0; gi < EG; ++gi) {
+      const uint32_t g = g0 + gi;
+      const uint32_t b = lds32[g + 2];
+      uint32_t m4 = 0;
 #pragma unroll
       for (uint32_t k = 0; k < 4; ++k) {
-        const int32_t ii = (int32_t)(4 * j + k) - (int32_t)sa;
-        bool surv = ii >= 0 && ii < (int32_t)EW;
-        if (surv && (uint32_t)ii < fast_end) {
-          const uint32_t ref = __builtin_amdgcn_alignbyte(b, a, k);
-          surv = ref + 1u < nref1;  // refID in [-1, nContigs): may pass
-        }
-        const uint64_t m = __ballot(surv);
-        if (m) {
-          uint32_t base = 0;
-          if (lane == (uint32_t)__builtin_ctzll(m)) base = atomicAdd(&nq, (uint32_t)__popcll(m));
-          base = __shfl(base, (int)__builtin_ctzll(m), WAVE);
-          if (surv) queue[base + (uint32_t)__popcll(m & lt_mask)] = (uint16_t)ii;
-        }
+        const uint32_t ref = __builtin_amdgcn_alignbyte(b, a, k);
+        const uint32_t ii = 4 * g + k - sa;  // wraps for positions before the window
+        const bool in = ii < EW && g < ngroups;
+        m4 |= (in && (ref + 1u < nref1 || ii >= fast_end)) ? 1u << k : 0u;
       }
+      msk[(gi * 4) / 32] |= m4 << ((gi * 4) % 32);
+      a = b;
     }
-    __syncthreads();
-    const uint32_t nsv = nq;
-    for (uint32_t x = threadIdx.x; x < nsv; x += T) {
-      const uint32_t i = queue[x];
+    // stage 2: the other fixed fields for the refID survivors; survivors of those are queued
+#pragma unroll
+    for (uint32_t w = 0; w < EMW; ++w) {
+      uint32_t mw = msk[w];
+      while (mw) {
+        const uint32_t bit = __builtin_ctz(mw);
+        mw &= mw - 1;
+        const uint32_t gk = w * 32 + bit, g = g0 + gk / 4, k = gk % 4;
+        const uint32_t i = 4 * g + k - sa;
+        bool pass = true;
+        if (i < fast_end) {
+          const uint32_t *dw = lds32 + g;
+          const uint32_t rem = __builtin_amdgcn_alignbyte(dw[1], dw[0], k);
+          const uint32_t pos = __builtin_amdgcn_alignbyte(dw[3], dw[2], k);
+          const uint32_t bmn = __builtin_amdgcn_alignbyte(dw[4], dw[3], k);
+          const uint32_t fnc = __builtin_amdgcn_alignbyte(dw[5], dw[4], k);
+          const uint32_t lsq = __builtin_amdgcn_alignbyte(dw[6], dw[5], k);
+          const uint32_t nrf = __builtin_amdgcn_alignbyte(dw[7], dw[6], k);
+          const uint32_t nps = __builtin_amdgcn_alignbyte(dw[8], dw[7], k);
+          const int32_t rnl = (int32_t)(bmn & 0xff), nc = (int32_t)(fnc & 0xffff);
+          pass = nrf + 1u < nref1 && (int32_t)pos >= -1 && (int32_t)nps >= -1 && rnl >= 2 &&
+                 (((fnc >> 16) & 4) != 0 || ((int32_t)lsq != 0 && nc != 0)) &&
+                 (int32_t)rem >= implied_min_remaining(rnl, nc, (int32_t)lsq);
+        }
+        if (pass) {
 #ifdef SBH_EPROBE
-      ++nsurv;
+          ++nsurv;
 #endif
-      const uint64_t q = t0 + i;
-      const uint64_t total = q < e0 ? e0 : sg.end[seg_index(sg, q, k0)];
-      uint64_t succ;
-      bool normal;
-      const uint32_t r = one_record(s, q, total, c, &succ, &normal);
-      if (r == 1) {
-        atomicOr(&ok[i >> 5], 1u << (i & 31));
-        if (normal) atomicOr(&nrm[i >> 5], 1u << (i & 31));
-      } else if (r == 2) {
-        atomicOr(&und[i >> 5], 1u << (i & 31));
+          const uint32_t x = atomicAdd(&nq, 1u);
+          if (x < EQ_CHUNK) queue[x] = (uint16_t)i;
+          else eval_one(i);  // queue full: evaluate in place
+        }
       }
     }
-    __syncthreads();
-    if (threadIdx.x == 0) nq = 0;
-    __syncthreads();
+  }
+  __syncthreads();
+  {
+    const uint32_t nsv = nq < EQ_CHUNK ? nq : EQ_CHUNK;
+    for (uint32_t x = threadIdx.x; x < nsv; x += T) eval_one(queue[x]);
   }
   __syncthreads();
 #ifdef SBH_EPROBE
   const uint64_t c2 = __builtin_readcyclecounter();
 #endif
-  // ---- phase B: one 32-position word per thread; walk only candidate positions ----
+  // ---- phase B: the eager call at each candidate (a tile position whose single-record
+  // predicate passed or could not be decided in the window) ----
   uint32_t mytrue = 0;
   const uint64_t wbase = (uint64_t)blockIdx.x * (ETILE / 32);
   const uint64_t nwords = (end - begin + 31) / 32;
-  for (uint32_t w = threadIdx.x; w < ETILE / 32; w += T) {
-    if (wbase + w >= nwords) break;
-    uint32_t cand = rtc <= 0 ? ~0u : (ok[w] | und[w]);
-    uint32_t res = 0;
-    while (cand) {
-      const uint32_t bit = __builtin_ctz(cand);
-      cand &= cand - 1;
-      const uint32_t i = 32 * w + bit;
-      const uint64_t p = t0 + i;
-      if (p >= end) break;
-      const uint32_t k = p < e0 ? k0 : seg_index(sg, p, k0);
-      const uint64_t total = sg.end[k];
-      const bool open = sg.open_last && k == sg.n - 1;
-      const bool und_p = (und[w] >> bit) & 1;
-      uint32_t r;
+  // r: 1 true, 0 false, 2 unknown (needs bytes past an open end)
+  auto call_at = [&](uint32_t i) -> uint32_t {
+    const uint64_t p = t0 + i;
+    const uint32_t k = p < e0 ? k0 : seg_index(sg, p, k0);
+    const uint64_t total = sg.end[k];
+    const bool open = sg.open_last && k == sg.n - 1;
+    const bool und_p = (und[i >> 5] >> (i & 31)) & 1;
 #ifdef SBH_EPROBE
-      ++ncand;
+    ++ncand;
 #endif
-      if (rtc <= 0 || und_p) {
-        r = eager_at(s, p, total, open, c, rtc);  // exact path (HBM/L2 reads)
-      } else {
-        // walk the chain through the window's ok bits (next record read at nominal)
-        uint64_t q = p;
-        int32_t n = 1;
-        r = 3;  // undecided
-        for (;;) {
-          if (n == rtc) { r = 1; break; }
-          const uint32_t iq = (uint32_t)(q - t0);
-          if (!((nrm[iq >> 5] >> (iq & 31)) & 1)) break;  // cursor past nominal: exact path
-          const uint64_t nxt = q + 4 + (int64_t)(int32_t)s.word_at(q);
-          if (nxt + 36 > total || nxt < t0 || nxt - t0 >= EW) break;  // EOF edge / outside window
-          const uint32_t jn = (uint32_t)(nxt - t0);
-          if ((und[jn >> 5] >> (jn & 31)) & 1) break;
-          if (!((ok[jn >> 5] >> (jn & 31)) & 1)) { r = 0; break; }
-          q = nxt;
-          ++n;
-        }
-        if (r == 3) r = eager_at(s, p, total, open, c, rtc);
+    if (rtc <= 0 || und_p) return eager_at(s, p, total, open, c, rtc);  // exact path (HBM/L2 reads)
+    // walk the chain through the window's ok bits (next record read at nominal)
+    uint64_t q = p;
+    int32_t n = 1;
+    for (;;) {
+      if (n == rtc) return 1;
+      const uint32_t iq = (uint32_t)(q - t0);
+      if (!((nrm[iq >> 5] >> (iq & 31)) & 1)) break;  // cursor past nominal: exact path
+      const uint64_t nxt = q + 4 + (int64_t)(int32_t)s.word_at(q);
+      if (nxt + 36 > total || nxt < t0 || nxt - t0 >= EW) break;  // EOF edge / outside window
+      const uint32_t jn = (uint32_t)(nxt - t0);
+      if ((und[jn >> 5] >> (jn & 31)) & 1) break;
+      if (!((ok[jn >> 5] >> (jn & 31)) & 1)) return 0;
+      q = nxt;
+      ++n;
+    }
 #ifdef SBH_EPROBE
-        if (r == 3 || true) nexact += 0;
+    ++nexact;
 #endif
-      }
+    return eager_at(s, p, total, open, c, rtc);
+  };
+  if (rtc > 0 && nq <= EQ_CHUNK) {
+    // every candidate is in the survivor queue: one candidate per thread, balanced
+    for (uint32_t x = threadIdx.x; x < nq; x += T) {
+      const uint32_t i = queue[x];
+      if (i >= ETILE || t0 + i >= end) continue;
+      if (!(((ok[i >> 5] | und[i >> 5]) >> (i & 31)) & 1)) continue;
+      const uint32_t r = call_at(i);
       if (r == 1) {
-        res |= 1u << bit;
+        atomicOr(&res[i >> 5], 1u << (i & 31));
       } else if (r == 2) {
         atomicAdd(o.n_unknown, 1ull);
-        atomicMin(o.min_unknown, (unsigned long long)p);
+        atomicMin(o.min_unknown, (unsigned long long)(t0 + i));
       }
     }
-    o.bits[wbase + w] = res;
-    mytrue += __popc(res);
+    __syncthreads();
+    for (uint32_t w = threadIdx.x; w < ETILE / 32; w += T) {
+      if (wbase + w >= nwords) break;
+      o.bits[wbase + w] = res[w];
+      mytrue += __popc(res[w]);
+    }
+  } else {
+    for (uint32_t w = threadIdx.x; w < ETILE / 32; w += T) {
+      if (wbase + w >= nwords) break;
+      uint32_t cand = rtc <= 0 ? ~0u : (ok[w] | und[w]);
+      uint32_t rw = 0;
+      while (cand) {
+        const uint32_t bit = __builtin_ctz(cand);
+        cand &= cand - 1;
+        const uint32_t i = 32 * w + bit;
+        if (t0 + i >= end) break;
+        const uint32_t r = call_at(i);
+        if (r == 1) {
+          rw |= 1u << bit;
+        } else if (r == 2) {
+          atomicAdd(o.n_unknown, 1ull);
+          atomicMin(o.min_unknown, (unsigned long long)(t0 + i));
+        }
+      }
+      o.bits[wbase + w] = rw;
+      mytrue += __popc(rw);
+    }
   }
   if (mytrue) atomicAdd(&ntrue, mytrue);
   __syncthreads();
   if (threadIdx.x == 0 && ntrue) atomicAdd(o.n_true, (unsigned long long)ntrue);
 #ifdef SBH_EPROBE
-  __shared__ uint32_t psurv, pcand;
-  if (threadIdx.x == 0) { psurv = 0; pcand = 0; }
+  __shared__ uint32_t psurv, pcand, pexact;
+  if (threadIdx.x == 0) { psurv = 0; pcand = 0; pexact = 0; }
   __syncthreads();
   atomicAdd(&psurv, nsurv);
   atomicAdd(&pcand, ncand);
+  atomicAdd(&pexact, nexact);
   __syncthreads();
   if (threadIdx.x == 0 && blockIdx.x < 4)
-    printf("eager wg %u stage %llu A %llu B %llu surv %u cand %u true %u\n", blockIdx.x,
+    printf("eager wg %u stage %llu A %llu B %llu surv %u cand %u true %u exact %u\n", blockIdx.x,
            (unsigned long long)(c1 - c0), (unsigned long long)(c2 - c1),
-           (unsigned long long)(__builtin_readcyclecounter() - c2), psurv, pcand, ntrue);
+           (unsigned long long)(__builtin_readcyclecounter() - c2), psurv, pcand, ntrue, pexact);
 #endif
 }
 

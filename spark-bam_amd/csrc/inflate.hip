@@ -45,7 +45,8 @@ constexpr int WAVES = SBH_HUFF_WAVES;  // waves (blocks) per k_huff workgroup
 #define SBH_LZ_THREADS 512
 #endif
 constexpr uint32_t LZ_THREADS = SBH_LZ_THREADS;
-constexpr uint32_t LZ_LONG = 24;  // longer matches are copied by the whole wave
+constexpr uint32_t LZ_LONG = 24;  // longer matches are copied by the whole wave (rounds path)
+constexpr uint32_t LZ_SHORT = 16;  // longer matches get their pointers from the whole wave
 constexpr uint32_t TOK_MATCH = 0x80000000u;  // token: literal = byte << 8 (bit 31 clear); match = bit31 | len << 16 | dist
 
 // Table entries (32-bit; laid out so the asm hot loop decodes with few scalar ops):
@@ -214,13 +215,24 @@ __device__ __forceinline__ uint32_t build_table(WaveSmem &sm, const uint8_t *len
 // code decodes as base + bits(L, extra) whatever its kind.  A distance is kind K_LIT
 // too: kind 0 means "this code completes a token" in either table.
 __device__ __forceinline__ uint32_t pentry(uint32_t kind, uint32_t sym, uint32_t L) {
+  // base / extra bits of length symbols 257 + i and distance symbols i, computed
+  // (RFC 1951 3.2.5) rather than looked up: no constant-memory loads in the table build
   if (kind == 0) {
     if (sym < 256) return L | (K_LIT << 5) | (sym << 16);
     if (sym == 256) return L | (K_EOB << 5);
-    if (sym < 286) return L | (K_LEN << 5) | ((uint32_t)LEXT[sym - 257] << 8) | ((uint32_t)LBASE[sym - 257] << 16);
+    if (sym < 286) {
+      const uint32_t i = sym - 257;
+      const uint32_t x = (i < 8 || i == 28) ? 0u : (i - 4) >> 2;
+      const uint32_t base = i < 8 ? 3 + i : i == 28 ? 258u : ((4 + (i & 3)) << x) + 3;
+      return L | (K_LEN << 5) | (x << 8) | (base << 16);
+    }
     return L | (K_BAD << 5);
   }
-  if (sym < 30) return L | (K_LIT << 5) | ((uint32_t)DEXT[sym] << 8) | ((uint32_t)DBASE[sym] << 16);
+  if (sym < 30) {
+    const uint32_t x = sym < 4 ? 0u : (sym - 2) >> 1;
+    const uint32_t base = sym < 4 ? sym + 1 : ((2 + (sym & 1)) << x) + 1;
+    return L | (K_LIT << 5) | (x << 8) | (base << 16);
+  }
   return L | (K_BAD << 5);
 }
 
@@ -294,7 +306,7 @@ __device__ __forceinline__ uint32_t build_ptable(WaveSmem &sm, const uint8_t *le
     uint32_t e;
     if (len > 15) e = 1u | (K_BAD << 5);
     else if (len > fast) e = K_SLOW << 5;
-    else e = pentry(kind, sorted[((sm.pk[kind][len] & 0xffffu) + (c15 >> (15 - len))) & 0xffffu], len);
+    else e = sm.sent[(kind ? 288 : 0) + (((sm.pk[kind][len] & 0xffffu) + (c15 >> (15 - len))) & 0xffffu)];
     tab[i] = e;
   }
   __builtin_amdgcn_wave_barrier();
@@ -1403,71 +1415,67 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
     const uint32_t len = i >= n ? 0 : match ? (x >> 16) & 0x1ff : 1;
     uint32_t chunk_len;
     const uint32_t off = base + block_scan<LZ_THREADS>(len, sm.wsum, &chunk_len);
-    if (t < m) {
-      sm.toff[t] = off;
-      sm.tokv[t] = x;
-      sm.done[t] = match ? 0 : 1;
-      if (!match) img[off] = (uint8_t)(x >> 8);
-    }
+    const uint32_t dist = x & 0xffff;
 #ifdef SBH_LZ_PROBE
     const uint64_t tb = __builtin_readcyclecounter();
     t_pre += tb - ta;
     nrounds += chunk_len > PTR_CAP;
 #endif
-    if (chunk_len <= PTR_CAP) sm.ptr[t] = make_uint4(0, 0, 0, 0);  // free since the last chunk's barrier
-    __syncthreads();  // toff/tokv, the literal bytes and the cleared slots are visible
     if (chunk_len <= PTR_CAP) {
-      // Pointer jumping over the chunk's bytes.  Every byte gets a source pointer: a
-      // literal byte points at itself, match byte k at the byte it copies
-      // (off - dist + k mod dist, always earlier); bytes before the chunk are final.
-      // Rounds of ptr = ptr[ptr] end when every pointer reaches a final byte, then
-      // one gather fills all match bytes at once.
-      // owner token of each slot: token start marks, then a block-wide max-scan
-      if (t < m) reinterpret_cast<uint16_t *>(sm.ptr)[off - base] = (uint16_t)t;
-      __syncthreads();
-      uint32_t own[PTR_PER];
-      {
-        const uint4 mk = sm.ptr[t];
-        own[0] = mk.x & 0xffff; own[1] = mk.x >> 16; own[2] = mk.y & 0xffff; own[3] = mk.y >> 16;
-        own[4] = mk.z & 0xffff; own[5] = mk.z >> 16; own[6] = mk.w & 0xffff; own[7] = mk.w >> 16;
-#pragma unroll
-        for (uint32_t k = 1; k < PTR_PER; ++k) own[k] = own[k] > own[k - 1] ? own[k] : own[k - 1];
-        const uint32_t before = block_scan_max<LZ_THREADS>(own[PTR_PER - 1], sm.wsum);
-#pragma unroll
-        for (uint32_t k = 0; k < PTR_PER; ++k) own[k] = own[k] > before ? own[k] : before;
-      }
-      uint32_t q[PTR_PER];
-#pragma unroll
-      for (uint32_t k = 0; k < PTR_PER; ++k) {
-        const uint32_t slot = t * PTR_PER + k, pos = base + slot;
-        uint32_t ptr = pos;
-        if (slot < chunk_len) {
-          const uint32_t j = own[k];
-          const uint32_t y = sm.tokv[j];
-          if (y & TOK_MATCH) {
-            const uint32_t oj = sm.toff[j], dj = y & 0xffff;
-            uint32_t kk = pos - oj;
-            if (kk >= dj) kk = mod_small(kk, dj);
-            ptr = oj - dj + kk;
+      // Every byte of the chunk gets a source pointer, written by its own token: a
+      // literal points at itself, match byte k at off - dist + (k mod dist) (always
+      // earlier); bytes before the chunk are final.  Each thread then follows its 8
+      // bytes' pointers to final bytes -- rewriting its slots with the results, which
+      // shortens other threads' chases -- and gathers.  (Slots are 16-bit positions in
+      // the block image.)
+      uint16_t *p16 = reinterpret_cast<uint16_t *>(sm.ptr);
+      if (t < m) {
+        if (!match) {
+          img[off] = (uint8_t)(x >> 8);
+          p16[off - base] = (uint16_t)off;
+        } else if (len <= LZ_SHORT) {
+          uint32_t s = 0;
+          for (uint32_t k = 0; k < len; ++k) {
+            p16[off - base + k] = (uint16_t)(off - dist + s);
+            s = s + 1 == dist ? 0 : s + 1;
           }
         }
-        q[k] = ptr;
       }
-      sm.ptr[t] = make_uint4(q[0] | q[1] << 16, q[2] | q[3] << 16, q[4] | q[5] << 16, q[6] | q[7] << 16);
-      uint16_t *p16 = reinterpret_cast<uint16_t *>(sm.ptr);
+      {  // long matches: the wave writes each one's pointers, 64 per step
+        const uint32_t lane = t & (WAVE - 1);
+        uint64_t lm = __ballot(t < m && match && len > LZ_SHORT);
+        while (lm) {
+          const uint32_t l = (uint32_t)__builtin_ctzll(lm);
+          lm &= lm - 1;
+          const uint32_t o = __builtin_amdgcn_readlane(off, l), d = __builtin_amdgcn_readlane(dist, l);
+          const uint32_t L = __builtin_amdgcn_readlane(len, l);
+          uint32_t s = lane < d ? lane : mod_small(lane, d);
+          const uint32_t step = WAVE < d ? WAVE : mod_small(WAVE, d);
+          for (uint32_t k = lane; k < L; k += WAVE) {
+            p16[o - base + k] = (uint16_t)(o - d + s);
+            s += step;
+            s = s >= d ? s - d : s;
+          }
+        }
+      }
+      __syncthreads();
+      uint32_t q[PTR_PER];
+      {
+        const uint4 pv = sm.ptr[t];
+        q[0] = pv.x & 0xffff; q[1] = pv.x >> 16; q[2] = pv.y & 0xffff; q[3] = pv.y >> 16;
+        q[4] = pv.z & 0xffff; q[5] = pv.z >> 16; q[6] = pv.w & 0xffff; q[7] = pv.w >> 16;
+      }
 #ifdef SBH_LZ_PROBE
       const uint64_t tc = __builtin_readcyclecounter();
       t_init += tc - tb;
 #endif
-      __syncthreads();
       // chase every pointer to a final byte (before the chunk, or a literal: a slot
-      // pointing at itself).  Slots are rewritten with their final pointers as threads
-      // finish, which only shortens other threads' chases; no rounds, no barriers.
+      // pointing at itself); no rounds, no barriers
 #pragma unroll
       for (uint32_t k = 0; k < PTR_PER; ++k) {
-        const uint32_t pos = base + t * PTR_PER + k;
+        const uint32_t slot = t * PTR_PER + k, pos = base + slot;
         uint32_t c = q[k];
-        if (c != pos) {
+        if (slot < chunk_len && c != pos) {
           while (c >= base) {
             const uint32_t v = __hip_atomic_load(&p16[c - base], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #ifdef SBH_LZ_PROBE
@@ -1476,12 +1484,18 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
             if (v == c) break;
             c = v;
           }
-          __hip_atomic_store(&p16[pos - base], (uint16_t)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_store(&p16[slot], (uint16_t)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           img[pos] = img[c];
         }
       }
     } else {
-      const uint32_t dist = x & 0xffff;
+      if (t < m) {
+        sm.toff[t] = off;
+        sm.tokv[t] = x;
+        sm.done[t] = match ? 0 : 1;
+        if (!match) img[off] = (uint8_t)(x >> 8);
+      }
+      __syncthreads();
       uint32_t src = off - dist;  // where the (final-equivalent) source bytes start
       uint32_t jl = 1, jh = 0;    // chunk tokens the source overlaps (empty: none)
       if (match) {
