@@ -39,7 +39,7 @@ namespace {
 constexpr int LIT_FAST = SBH_LIT_FAST;
 constexpr int DIST_FAST = 8;
 constexpr int CL_FAST = 7;
-constexpr int PDIST_FAST = DIST_FAST + 1;  // PAR-format distance table: one dword per entry
+constexpr int PDIST_FAST = 10;  // PAR-format distance table: one dword per entry, as wide as the literal one
 constexpr int WAVES = SBH_HUFF_WAVES;  // waves (blocks) per k_huff workgroup
 #ifndef SBH_LZ_THREADS
 #define SBH_LZ_THREADS 512
@@ -69,13 +69,21 @@ __constant__ uint8_t DEXT[30] = {0, 0, 0, 0, 1, 1, 2, 2,  3,  3,  4,  4,  5,  5,
                                  6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
 __constant__ uint8_t CL_ORDER[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
+static_assert((1 << PDIST_FAST) >= (2 << DIST_FAST), "the serial distance table fits the PAR one");
+
+// PAR-format entry flags (see pentry)
+constexpr uint32_t PE_LEN = 1u << 5;      // a length code: a distance code follows
+constexpr uint32_t PE_SPECIAL = 1u << 6;  // not a token: end of block, invalid, or long code
+constexpr uint32_t PE_SLOW = 1u << 7;     // (with PE_SPECIAL) code longer than the table: slow_lane
+constexpr uint32_t PE_EOB = 1u << 12;     // (with PE_SPECIAL) end of block
+
 struct __attribute__((aligned(16))) WaveSmem {
   union {
     struct {
       uint32_t lit[1 << LIT_FAST];    // also the code-length-code table while reading headers
-      uint32_t dist[2 << DIST_FAST];  // (entry, base) pairs; PAR format: 1 << PDIST_FAST entries
+      uint32_t dist[1 << PDIST_FAST];  // serial format: (entry, base) pairs in the first 2 << DIST_FAST
     };
-    uint32_t tab[(1 << LIT_FAST) + (2 << DIST_FAST)];
+    uint32_t tab[(1 << LIT_FAST) + (1 << PDIST_FAST)];
   };
   uint16_t sorted[320];  // canonical order: [0,288) lit/len (or CL), [288,320) dist
   uint8_t lens[320];     // [0,288) lit/len lengths, [288,320) dist lengths
@@ -210,30 +218,30 @@ __device__ __forceinline__ uint32_t build_table(WaveSmem &sm, const uint8_t *len
   return 0;
 }
 
-// PAR-format entries (the lane-parallel decoder): [4:0] code length L, [7:5] kind,
-// [11:8] extra bits, [31:16] base (a literal's byte; a length or distance base), so a
-// code decodes as base + bits(L, extra) whatever its kind.  A distance is kind K_LIT
-// too: kind 0 means "this code completes a token" in either table.
+// PAR-format entries (the lane-parallel decoder): [4:0] code length L, [5] PE_LEN,
+// [6] PE_SPECIAL, [7] PE_SLOW, [11:8] extra bits, [12] PE_EOB, [31:16] base (a literal's
+// byte; a length or distance base), so any token code decodes as base + bits(L, extra)
+// and "completes a token" is simply "neither PE_LEN nor PE_SPECIAL" in either table.
 __device__ __forceinline__ uint32_t pentry(uint32_t kind, uint32_t sym, uint32_t L) {
   // base / extra bits of length symbols 257 + i and distance symbols i, computed
   // (RFC 1951 3.2.5) rather than looked up: no constant-memory loads in the table build
   if (kind == 0) {
-    if (sym < 256) return L | (K_LIT << 5) | (sym << 16);
-    if (sym == 256) return L | (K_EOB << 5);
+    if (sym < 256) return L | (sym << 16);
+    if (sym == 256) return L | PE_SPECIAL | PE_EOB;
     if (sym < 286) {
       const uint32_t i = sym - 257;
       const uint32_t x = (i < 8 || i == 28) ? 0u : (i - 4) >> 2;
       const uint32_t base = i < 8 ? 3 + i : i == 28 ? 258u : ((4 + (i & 3)) << x) + 3;
-      return L | (K_LEN << 5) | (x << 8) | (base << 16);
+      return L | PE_LEN | (x << 8) | (base << 16);
     }
-    return L | (K_BAD << 5);
+    return L | PE_SPECIAL;
   }
   if (sym < 30) {
     const uint32_t x = sym < 4 ? 0u : (sym - 2) >> 1;
     const uint32_t base = sym < 4 ? sym + 1 : ((2 + (sym & 1)) << x) + 1;
-    return L | (K_LIT << 5) | (x << 8) | (base << 16);
+    return L | (x << 8) | (base << 16);
   }
-  return L | (K_BAD << 5);
+  return L | PE_SPECIAL;
 }
 
 // Canonical table in the PAR format (kind 0 lit/len, 1 dist), same validity rules as
@@ -273,7 +281,7 @@ __device__ __forceinline__ uint32_t build_ptable(WaveSmem &sm, const uint8_t *le
   }
   const uint32_t n_ent = 1u << fast;
   if (max == 0) {  // no symbols: every entry invalid
-    for (uint32_t i = lane; i < n_ent; i += WAVE) tab[i] = 1u | (K_BAD << 5);
+    for (uint32_t i = lane; i < n_ent; i += WAVE) tab[i] = 1u | PE_SPECIAL;
     if (lane < 16) sm.pk[kind][lane] = 0;
     return 2;
   }
@@ -304,8 +312,8 @@ __device__ __forceinline__ uint32_t build_ptable(WaveSmem &sm, const uint8_t *le
 #pragma unroll
     for (uint32_t v = 1; v <= 15; ++v) len += ljv[v] <= c15 ? 1u : 0u;
     uint32_t e;
-    if (len > 15) e = 1u | (K_BAD << 5);
-    else if (len > fast) e = K_SLOW << 5;
+    if (len > 15) e = 1u | PE_SPECIAL;
+    else if (len > fast) e = PE_SPECIAL | PE_SLOW;
     else e = sm.sent[(kind ? 288 : 0) + (((sm.pk[kind][len] & 0xffffu) + (c15 >> (15 - len))) & 0xffffu)];
     tab[i] = e;
   }
@@ -888,21 +896,21 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t *wsum, uint3
 #define SBH_HT 256
 #endif
 #ifndef SBH_STAGE_DW
-#define SBH_STAGE_DW 7168
+#define SBH_STAGE_DW 6144
 #endif
 #ifndef SBH_HUFF_OCC
 #define SBH_HUFF_OCC 4  // waves per SIMD the register budget must allow
 #endif
 constexpr uint32_t HT = SBH_HT;              // k_huff lanes per BGZF block
-constexpr uint32_t STAGE_DW = SBH_STAGE_DW;  // deflate bytes staged in LDS (28 KiB)
+constexpr uint32_t STAGE_DW = SBH_STAGE_DW;  // deflate bytes staged in LDS (24 KiB)
 constexpr uint32_t PAR_MIN_USIZE = 4096;     // smaller blocks decode serially
 #ifndef SBH_MIN_SLICE
 #define SBH_MIN_SLICE 256
 #endif
 constexpr uint32_t MIN_SLICE = SBH_MIN_SLICE;  // bits per lane at least
 constexpr uint32_t NOPOS = 0xffffffffu;
+constexpr uint32_t CK1 = 6, CK2 = 24;  // pass-1 checkpoints (tokens)
 constexpr uint32_t LR_RUN = 0, LR_EOB = 1, LR_DEAD = 2, LR_PAST = 3;
-
 struct HuffSmem {
   WaveSmem t;                    // tables (built by wave 0; the serial fallback's too)
   uint32_t stage[STAGE_DW + 8];  // the block's deflate dwords, from dword a0
@@ -920,9 +928,10 @@ struct Src {
     return p[i];
   }
   // 32 stream bits starting at bit position `pos`
+  // (no clamp: a lane never reads past dword (limit + 48) / 32 + 1, and staged blocks
+  // leave that much of the STAGE_DW + 8 array)
   __device__ __forceinline__ uint32_t bits32(uint32_t pos) const {
-    uint32_t i = pos >> 5;
-    if (LDS) i = i < STAGE_DW + 6 ? i : STAGE_DW + 6;
+    const uint32_t i = pos >> 5;
     return __builtin_amdgcn_alignbit(p[i + 1], p[i], pos & 31);
   }
 };
@@ -932,19 +941,19 @@ struct Src {
 // code, and the entry sits at sent[dl[len] + code].  lj/dl of lengths 10..15 are read
 // together as packed (lj << 16 | dl) words, so a long code costs two LDS round trips.
 __device__ __forceinline__ uint32_t slow_lane(const WaveSmem &sm, uint32_t bits, bool dist) {
+  static_assert(LIT_FAST == 10 && PDIST_FAST == 10, "long codes are lengths 11..15");
   const uint32_t rev15 = __builtin_bitreverse32(bits) >> 17;
   const uint32_t *pk = sm.pk[dist ? 1 : 0];
-  const uint32_t first = dist ? PDIST_FAST + 1 : LIT_FAST + 1;  // shortest long code
-  uint32_t len = first, d = pk[first] & 0xffffu;
+  uint32_t len = 11, d = pk[11] & 0xffffu;
 #pragma unroll
-  for (uint32_t v = PDIST_FAST + 2; v <= 15; ++v) {
+  for (uint32_t v = 12; v <= 15; ++v) {
     const uint32_t below = pk[v - 1], here = pk[v];
-    if (v > first && (below >> 16) <= rev15) {
+    if ((below >> 16) <= rev15) {
       len = v;
       d = here & 0xffffu;
     }
   }
-  if (rev15 >= (pk[15] >> 16)) return 1u | (K_BAD << 5);
+  if (rev15 >= (pk[15] >> 16)) return 1u | PE_SPECIAL;
   return sm.sent[(dist ? 288 : 0) + ((d + (rev15 >> (15 - len))) & 0xffffu)];
 }
 
@@ -961,7 +970,6 @@ struct LaneRun {
 struct Ckpt {
   uint32_t p1, o1, p2, o2;
 };
-constexpr uint32_t CK1 = 6, CK2 = 24;
 constexpr int RUN_SPEC = 0, RUN_REDO = 1, RUN_EMIT = 2;
 
 // Decode tokens from bit A while the position is below `stop`, as a two-state machine
@@ -984,18 +992,13 @@ __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, Src<LDS> src, uin
   uint32_t ml = 0;  // pending match length: the next code is a distance
   uint32_t ntok = 0, nout = 0;
   uint32_t c1p = NOPOS, c1o = 0, c2p = NOPOS, c2o = 0;
-  uint32_t e, L;
-  bool atb, cut;
+  uint32_t e;
+  bool cut;
   for (;;) {
     const uint32_t bits = src.bits32(pos);
-    atb = ml == 0;  // token boundary
-    e = t.tab[atb ? (bits & ((1u << LIT_FAST) - 1)) : (1u << LIT_FAST) | (bits & ((1u << PDIST_FAST) - 1))];
-    if (((e >> 5) & 7) == K_SLOW) e = slow_lane(t, bits, !atb);
-    const uint32_t k = (e >> 5) & 7, x = (e >> 8) & 15;
-    L = e & 31;
-    const uint32_t val = (e >> 16) + __builtin_amdgcn_ubfe(bits, L, x);
-    const bool is_tok = k == K_LIT;  // a literal, or the distance completing a match
-    const bool is_len = atb && k == K_LEN;
+    const bool atb = ml == 0;  // token boundary
+    e = t.tab[(bits & ((1u << LIT_FAST) - 1)) | (atb ? 0u : 1u << LIT_FAST)];
+    if (e & PE_SLOW) e = slow_lane(t, bits, !atb);
     if (MODE == RUN_SPEC) {
       const bool h1 = atb && ntok == CK1, h2 = atb && ntok == CK2;
       c1p = h1 ? pos : c1p;
@@ -1004,15 +1007,18 @@ __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, Src<LDS> src, uin
       c2o = h2 ? nout : c2o;
     }
     cut = atb && (pos >= stop2 || (MODE == RUN_REDO && (pos == ck.p1 || pos == ck.p2)));
-    if (cut || !(is_tok || is_len)) break;
+    if (cut || (e & PE_SPECIAL)) break;
+    const uint32_t L = e & 31, x = (e >> 8) & 15;
+    const uint32_t val = (e >> 16) + __builtin_amdgcn_ubfe(bits, L, x);
     pos += L + x;
+    const bool is_tok = (e & PE_LEN) == 0;  // a literal, or the distance completing a match
     if (MODE == RUN_EMIT) {
       if (is_tok) dst[ntok] = atb ? val << 8 : TOK_MATCH | (ml << 16) | val;
       bad |= (!atb && val > out0 + nout) ? 1u : 0u;
     }
     ntok += is_tok ? 1u : 0u;
-    nout += is_tok ? (atb ? 1u : ml) : 0u;
-    ml = is_len ? val : 0u;
+    nout += is_tok ? (ml > 1u ? ml : 1u) : 0u;
+    ml = is_tok ? 0u : val;
   }
   if (MODE == RUN_SPEC) ck = Ckpt{c1p, c1o, c2p, c2o};
   LaneRun r{LR_RUN, pos, ntok, nout};
@@ -1027,8 +1033,8 @@ __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, Src<LDS> src, uin
       r.st = LR_PAST;
     }
   } else {  // end of block, or an invalid code
-    r.st = (atb && ((e >> 5) & 7) == K_EOB) ? LR_EOB : LR_DEAD;
-    r.exit = pos + L;
+    r.st = (ml == 0 && (e & PE_EOB)) ? LR_EOB : LR_DEAD;
+    r.exit = pos + (e & 31);
   }
   return r;
 }
