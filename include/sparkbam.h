@@ -142,6 +142,12 @@ int sbh_set_contigs(sbh_shard *sh, const int32_t *lens, int32_t n);
 int sbh_check_eager(sbh_shard *sh, uint64_t begin, uint64_t end, int32_t reads_to_check,
                     uint8_t *out_bits, uint64_t *n_true);
 
+/* Copy [begin, end) of the eager bitmap the last sbh_check_eager / sbh_run_shard left on
+ * the device (the batch behind Checker.apply(pos) answers).  begin must lie in the
+ * bitmap's range at a multiple of 8 positions from its start; SBH_E_STATE if there is
+ * no bitmap. */
+int sbh_eager_bits(sbh_shard *sh, uint64_t begin, uint64_t end, uint8_t *out_bits);
+
 /* full.Checker.apply at every flat position of [begin, end)
  * (check/.../full/Checker.scala:22-184) with the FullCheck aggregation
  * (cli/.../check/full/FullCheck.scala:142-192).  Optional outputs: out_words
@@ -194,9 +200,10 @@ typedef struct {
 int sbh_run_shard(sbh_shard *sh, uint64_t index_start, uint64_t own_end_file,
                   int32_t reads_to_check, int32_t max_read_size, sbh_shard_result *res);
 
-/* Device time (ms, HIP events on the context stream) of the stages of the last
- * sbh_run_shard: [0] index, [1] inflate (k_huff + k_lz), [2] eager check (k_eager),
- * [3] record split/count, [4] k_huff alone, [5] k_lz alone.  Returns the number of
+/* Device time (ms, HIP events) of the stages of the last sbh_run_shard: [0] index,
+ * [1] inflate + eager check (one pipeline over block batches on three streams),
+ * [2] k_eager, [3] record split/count, [4] k_huff, [5] k_lz -- [2], [4], [5] summed
+ * over the pipeline's launches, each timed on its own stream.  Returns the number of
  * stages written (<= cap, at most 6). */
 int sbh_stage_times(sbh_shard *sh, double *ms, int32_t cap);
 

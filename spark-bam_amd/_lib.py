@@ -33,7 +33,7 @@ EXPORTS = [
     "sbh_ctx_synchronize", "sbh_version", "sbh_header_make", "sbh_shard_create",
     "sbh_shard_destroy", "sbh_shard_comp_device_ptr", "sbh_find_block_start", "sbh_index",
     "sbh_get_blocks", "sbh_inflate", "sbh_read_flat", "sbh_flat_device_ptr", "sbh_flat_of",
-    "sbh_pos_of", "sbh_flat_bound", "sbh_set_contigs", "sbh_check_eager", "sbh_check_full",
+    "sbh_pos_of", "sbh_flat_bound", "sbh_set_contigs", "sbh_check_eager", "sbh_eager_bits", "sbh_check_full",
     "sbh_find_record_start", "sbh_count_records", "sbh_split", "sbh_run_shard",
     "sbh_stage_times",
 ]
@@ -89,6 +89,7 @@ def lib():
         "sbh_flat_bound": [P, U64, PU64],
         "sbh_set_contigs": [P, P, I32],
         "sbh_check_eager": [P, U64, U64, I32, P, PU64],
+        "sbh_eager_bits": [P, U64, U64, P],
         "sbh_check_full": [P, U64, U64, I32, P, P, P, PU64, P, P, U64, PU64],
         "sbh_find_record_start": [P, U64, I32, I32, PU64, PI32],
         "sbh_count_records": [P, U64, U64, PU64],

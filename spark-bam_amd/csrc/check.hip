@@ -77,9 +77,12 @@ __device__ __forceinline__ int32_t implied_min_remaining(int32_t rnl, int32_t nc
   return (int32_t)(32u + (uint32_t)rnl + 4u * (uint32_t)nc + (uint32_t)nsq);
 }
 
-// Eager check at p: 0 false, 1 true, 2 unknown (needs bytes past an open end).
+// Eager check at p: 0 false, 1 true, 2 unknown (needs bytes past an open end), 3 deferred
+// (needs flat bytes at or past `front`, which are not inflated yet: the pipelined run
+// re-checks the position once they are).
+constexpr uint32_t EAGER_DEFER = 3;
 __device__ uint32_t eager_at(const Src &s, uint64_t p, uint64_t total, bool open, const Ctg &c,
-                             int32_t rtc) {
+                             int32_t rtc, uint64_t front = ~0ull) {
   uint64_t cur = p, start = p;
   for (int32_t n = 0;; ++n) {
     if (n == rtc) return 1;
@@ -87,6 +90,7 @@ __device__ uint32_t eager_at(const Src &s, uint64_t p, uint64_t total, bool open
       if (open) return 2;
       return (total == start && n > 0) ? 1 : 0;
     }
+    if (cur + 36 > front) return EAGER_DEFER;
     const int32_t rem = (int32_t)s.word_at(cur);
     const uint64_t nominal = start + 4 + (int64_t)rem;
     if (ref_pos_error((int32_t)s.word_at(cur + 4), (int32_t)s.word_at(cur + 8), c)) return 0;
@@ -101,12 +105,14 @@ __device__ uint32_t eager_at(const Src &s, uint64_t p, uint64_t total, bool open
     if (ref_pos_error((int32_t)s.word_at(cur + 24), (int32_t)s.word_at(cur + 28), c)) return 0;
     cur += 36;
     if (cur + (uint64_t)rnl > total) return open ? 2 : 0;
+    if (cur + (uint64_t)rnl > front) return EAGER_DEFER;
     if (s.byte_at(cur + rnl - 1) != 0) return 0;
     for (int32_t i = 0; i < rnl - 1; ++i)
       if (!name_char_ok(s.byte_at(cur + i))) return 0;
     cur += rnl;
     for (int32_t k = 0; k < nc; ++k) {
       if (cur + 4 > total) return open ? 2 : 0;
+      if (cur + 4 > front) return EAGER_DEFER;
       if ((s.byte_at(cur) & 0xf) > 8) return 0;
       cur += 4;
     }
@@ -244,16 +250,18 @@ struct EagerOut {
   unsigned long long *n_true;
   unsigned long long *n_unknown;
   unsigned long long *min_unknown;
+  uint64_t front;                 // flat bytes at/after front are not inflated yet (pipelined run)
+  uint64_t *defer_pos;            // positions whose exact check needs them (re-checked later)
+  unsigned long long *defer_n;
+  uint64_t defer_cap;
 };
 
-#ifndef SBH_ETILE
-#define SBH_ETILE 16384
-#endif
 constexpr uint32_t ETILE = SBH_ETILE;     // eager tile: positions per workgroup
 constexpr uint32_t ELA = 4096;            // look-ahead: chains of short reads stay inside
 constexpr uint32_t EW = ETILE + ELA;      // eager window: single-record predicate evaluated here
 constexpr uint32_t ESTAGE = EW + 512;     // staged bytes (records near the end fit)
-constexpr uint32_t EQ_CHUNK = 4096;       // phase-A positions per survivor-queue round
+constexpr uint32_t EQ_CHUNK = 4096;       // survivor-queue capacity
+static_assert(EAGER_REACH >= ESTAGE + 32 + 16, "EAGER_REACH covers the staged window");
 
 // Single-record eager predicate at q, with cur == start == q, reading only the
 // staged window: 0 fail, 1 pass, 2 cannot decide from the window (or EOF edge).
@@ -437,7 +445,7 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
 #ifdef SBH_EPROBE
     ++ncand;
 #endif
-    if (rtc <= 0 || und_p) return eager_at(s, p, total, open, c, rtc);  // exact path (HBM/L2 reads)
+    if (rtc <= 0 || und_p) return eager_at(s, p, total, open, c, rtc, o.front);  // exact path (HBM/L2 reads)
     // walk the chain through the window's ok bits (next record read at nominal)
     uint64_t q = p;
     int32_t n = 1;
@@ -456,7 +464,11 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
 #ifdef SBH_EPROBE
     ++nexact;
 #endif
-    return eager_at(s, p, total, open, c, rtc);
+    return eager_at(s, p, total, open, c, rtc, o.front);
+  };
+  auto defer = [&](uint32_t i) {
+    const unsigned long long x = atomicAdd(o.defer_n, 1ull);
+    if (x < o.defer_cap) o.defer_pos[x] = t0 + i;
   };
   if (rtc > 0 && nq <= EQ_CHUNK) {
     // every candidate is in the survivor queue: one candidate per thread, balanced
@@ -467,6 +479,8 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
       const uint32_t r = call_at(i);
       if (r == 1) {
         atomicOr(&res[i >> 5], 1u << (i & 31));
+      } else if (r == EAGER_DEFER) {
+        defer(i);
       } else if (r == 2) {
         atomicAdd(o.n_unknown, 1ull);
         atomicMin(o.min_unknown, (unsigned long long)(t0 + i));
@@ -491,6 +505,8 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
         const uint32_t r = call_at(i);
         if (r == 1) {
           rw |= 1u << bit;
+        } else if (r == EAGER_DEFER) {
+          defer(i);
         } else if (r == 2) {
           atomicAdd(o.n_unknown, 1ull);
           atomicMin(o.min_unknown, (unsigned long long)(t0 + i));
@@ -686,19 +702,57 @@ __global__ void k_chain_walk(const uint8_t *U, uint64_t first, uint64_t E, uint6
   *last = prev;
 }
 
+// Positions the pipelined eager pass deferred (their exact check reached flat bytes that
+// were not inflated yet), re-checked once everything is: bit set atomically over the
+// tile's word, counters as in k_eager.
+__global__ void k_eager_defer(const uint8_t *__restrict__ U, uint64_t begin, Segs sg, Ctg c, int32_t rtc,
+                              const uint64_t *pos, const unsigned long long *n, EagerOut o) {
+  const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= *n) return;
+  const uint64_t p = pos[x];
+  const uint32_t k = seg_first(sg, p);
+  const uint64_t total = sg.end[k];
+  const bool open = sg.open_last && k == sg.n - 1;
+  Src s{U, nullptr, 0, 0};
+  const uint32_t r = eager_at(s, p, total, open, c, rtc);
+  if (r == 1) {
+    atomicOr(&o.bits[(p - begin) >> 5], 1u << ((p - begin) & 31));
+    atomicAdd(o.n_true, 1ull);
+  } else if (r == 2) {
+    atomicAdd(o.n_unknown, 1ull);
+    atomicMin(o.min_unknown, (unsigned long long)p);
+  }
+}
+
 }  // namespace
 
 static inline uint32_t ngrid(uint64_t n, uint32_t t) { return (uint32_t)((n + t - 1) / t); }
 
 hipError_t launch_eager(const uint8_t *U, uint64_t u_pad, uint64_t begin, uint64_t end, const uint64_t *seg_end,
                         uint32_t nseg, uint32_t open_last, const int32_t *ctg, int32_t nctg, int32_t rtc,
-                        uint32_t *bits, unsigned long long *counters, hipStream_t st) {
+                        uint32_t *bits, unsigned long long *counters, hipStream_t st, uint64_t front,
+                        uint64_t *defer_pos, uint64_t defer_cap) {
   if (end <= begin) return hipSuccess;
   Segs sg{seg_end, nseg, open_last};
   Ctg c{ctg, nctg};
-  EagerOut o{bits, counters, counters + 1, counters + 2};
+  EagerOut o{bits, counters, counters + 1, counters + 2, front, defer_pos, counters + 3, defer_cap};
   hipLaunchKernelGGL(k_eager, dim3(ngrid(end - begin, ETILE)), dim3(T), 0, st, U, u_pad, begin, end, sg, c,
                      rtc, o);
+  return hipGetLastError();
+}
+
+// Re-check of deferred positions (launched with a grid for `cap` entries; threads past
+// the device-side count exit).  bits is the bitmap of the whole range from `begin`.
+hipError_t launch_eager_defer(const uint8_t *U, uint64_t begin, const uint64_t *seg_end, uint32_t nseg,
+                              uint32_t open_last, const int32_t *ctg, int32_t nctg, int32_t rtc, uint32_t *bits,
+                              unsigned long long *counters, const uint64_t *defer_pos, uint64_t cap,
+                              hipStream_t st) {
+  if (cap == 0) return hipSuccess;
+  Segs sg{seg_end, nseg, open_last};
+  Ctg c{ctg, nctg};
+  EagerOut o{bits, counters, counters + 1, counters + 2, ~0ull, nullptr, nullptr, 0};
+  hipLaunchKernelGGL(k_eager_defer, dim3(ngrid(cap, 256)), dim3(256), 0, st, U, begin, sg, c, rtc, defer_pos,
+                     counters + 3, o);
   return hipGetLastError();
 }
 

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -24,7 +25,12 @@ hipError_t build_chain(const uint8_t *comp, uint64_t n, const uint64_t *cand, ui
                        uint64_t *nchain, hipStream_t st);
 hipError_t launch_eager(const uint8_t *U, uint64_t u_pad, uint64_t begin, uint64_t end, const uint64_t *seg_end,
                         uint32_t nseg, uint32_t open_last, const int32_t *ctg, int32_t nctg, int32_t rtc,
-                        uint32_t *bits, unsigned long long *counters, hipStream_t st);
+                        uint32_t *bits, unsigned long long *counters, hipStream_t st, uint64_t front,
+                        uint64_t *defer_pos, uint64_t defer_cap);
+hipError_t launch_eager_defer(const uint8_t *U, uint64_t begin, const uint64_t *seg_end, uint32_t nseg,
+                              uint32_t open_last, const int32_t *ctg, int32_t nctg, int32_t rtc, uint32_t *bits,
+                              unsigned long long *counters, const uint64_t *defer_pos, uint64_t cap,
+                              hipStream_t st);
 hipError_t launch_full(const uint8_t *U, uint64_t u_pad, uint64_t begin, uint64_t end, const uint64_t *seg_end,
                        uint32_t nseg, uint32_t open_last, const int32_t *ctg, int32_t nctg, int32_t rtc,
                        uint32_t *words, unsigned long long *counters, uint64_t *close_pos, uint32_t *close_word,
@@ -107,9 +113,14 @@ struct sbh_shard {
   DBuf<unsigned long long> ctr;  // scratch counters
   unsigned long long *h_ctr = nullptr;  // pinned mirror
   uint64_t pad = 4096;
+  // pipelined run (run_pipelined): extra streams, per-batch events, deferred positions
+  hipStream_t s_lz = nullptr, s_eg = nullptr;
+  std::vector<hipEvent_t> pev;
+  DBuf<uint64_t> defer;
   hipEvent_t ev[9] = {};
   bool ev_ok = false, timing = false;
   double stage_ms[6] = {0, 0, 0, 0, 0, 0};
+  double pipe_ms[3] = {0, 0, 0};  // k_huff, k_lz, k_eager summed over the pipelined launches
 
   DevBlocks dev_blocks() {
     return DevBlocks{b_cstart.p, b_csize.p, b_hsize.p, b_usize.p, b_ustart.p, b_flags.p, b_status.p, b_ntok.p};
@@ -249,6 +260,11 @@ int sbh_shard_destroy(sbh_shard *sh) {
   sh->close_word.release(); sh->ctr.release();
   for (hipEvent_t &e : sh->ev)
     if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t &e : sh->pev)
+    if (e) (void)hipEventDestroy(e);
+  if (sh->s_lz) (void)hipStreamDestroy(sh->s_lz);
+  if (sh->s_eg) (void)hipStreamDestroy(sh->s_eg);
+  sh->defer.release();
   if (sh->h_ctr) (void)hipHostFree(sh->h_ctr);
   delete sh;
   return SBH_OK;
@@ -518,11 +534,11 @@ static int eager_range(sbh_shard *sh, uint64_t begin, uint64_t end, int32_t rtc,
   const uint64_t nwords = (end - begin + 31) / 32;
   HIPCHK(ctx, sh->bits.ensure(nwords + 1));
   unsigned long long *c = sh->ctr.p;
-  HIPCHK(ctx, hipMemsetAsync(c, 0, 16, st));
+  HIPCHK(ctx, hipMemsetAsync(c, 0, 32, st));
   HIPCHK(ctx, hipMemsetAsync(c + 2, 0xff, 8, st));
   mark(sh, 4);
   HIPCHK(ctx, launch_eager(sh->U.p, sh->utotal + sh->pad, begin, end, sh->d_seg.p, (uint32_t)sh->seg_end.size(),
-                           sh->open_last ? 1 : 0, sh->ctg.p, sh->nctg, rtc, sh->bits.p, c, st));
+                           sh->open_last ? 1 : 0, sh->ctg.p, sh->nctg, rtc, sh->bits.p, c, st, ~0ull, nullptr, 0));
   mark(sh, 5);
   HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr, c, 24, hipMemcpyDeviceToHost, st));
   HIPCHK(ctx, hipStreamSynchronize(st));
@@ -551,6 +567,22 @@ int sbh_check_eager(sbh_shard *sh, uint64_t begin, uint64_t end, int32_t rtc, ui
     HIPCHK(sh->ctx, hipMemcpyAsync(out_bits, sh->bits.p, (end - begin + 7) / 8, hipMemcpyDeviceToHost, sh->ctx->stream));
     HIPCHK(sh->ctx, hipStreamSynchronize(sh->ctx->stream));
   }
+  return SBH_OK;
+}
+
+int sbh_eager_bits(sbh_shard *sh, uint64_t begin, uint64_t end, uint8_t *out_bits) {
+  if (!sh || (!out_bits && end > begin)) return SBH_E_ARG;
+  if (!sh->bits_valid) return fail(sh->ctx, SBH_E_STATE, "no eager bitmap");
+  if (begin > end || begin < sh->bits_begin || end > sh->bits_end || (begin - sh->bits_begin) % 8)
+    return fail(sh->ctx, SBH_E_ARG, "range [%llu,%llu) outside the bitmap [%llu,%llu) or unaligned",
+                (unsigned long long)begin, (unsigned long long)end, (unsigned long long)sh->bits_begin,
+                (unsigned long long)sh->bits_end);
+  if (end == begin) return SBH_OK;
+  int rc = set_device(sh->ctx);
+  if (rc) return rc;
+  const uint8_t *src = reinterpret_cast<const uint8_t *>(sh->bits.p) + (begin - sh->bits_begin) / 8;
+  HIPCHK(sh->ctx, hipMemcpyAsync(out_bits, src, (end - begin + 7) / 8, hipMemcpyDeviceToHost, sh->ctx->stream));
+  HIPCHK(sh->ctx, hipStreamSynchronize(sh->ctx->stream));
   return SBH_OK;
 }
 
@@ -758,6 +790,141 @@ int sbh_split(sbh_shard *sh, uint64_t start, uint64_t end, int32_t k, int32_t rt
   return SBH_OK;
 }
 
+// Inflate + eager check of flat [0, E) as one pipeline over batches of blocks, on three
+// streams: k_huff of batch i+1 runs beside k_lz of batch i and beside the eager tiles
+// whose staged windows batch i completed (k_huff is latency-bound on LDS and VALU, k_lz on
+// barriers, k_eager on its chain walks: side by side they fill each other's idle issue
+// slots).  An eager position whose exact check needs bytes past the inflated frontier is
+// deferred and re-checked at the end.  Same results as sbh_inflate + sbh_check_eager.
+static constexpr uint64_t PIPE_MAX_BATCHES = 16;
+static constexpr uint64_t PIPE_MIN_BLOCKS = 1024;
+static constexpr uint64_t DEFER_CAP = 1 << 20;
+
+// SBH_PIPE_MIN_BLOCKS (tests): smaller batches, to exercise many frontiers on small inputs
+static uint64_t pipe_min_blocks() {
+  const char *e = std::getenv("SBH_PIPE_MIN_BLOCKS");
+  const long long v = e ? std::atoll(e) : 0;
+  return v > 0 ? (uint64_t)v : PIPE_MIN_BLOCKS;
+}
+
+static hipEvent_t pev(sbh_shard *sh, size_t i) {
+  while (sh->pev.size() <= i) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    sh->pev.push_back(e);
+  }
+  return sh->pev[i];
+}
+
+static DevBlocks blocks_from(DevBlocks d, uint64_t b) {
+  return DevBlocks{d.cstart + b, d.csize + b, d.hsize + b, d.usize + b, d.ustart + b, d.flags + b, d.status + b, d.ntok + b};
+}
+
+static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_true) {
+  sbh_ctx *ctx = sh->ctx;
+  if (!sh->indexed) return fail(ctx, SBH_E_STATE, "inflate before index");
+  if (sh->nctg < 0) return fail(ctx, SBH_E_STATE, "contig lengths not set");
+  if (rtc < 0 || rtc > 1023) return fail(ctx, SBH_E_ARG, "readsToCheck must be in [0, 1023]");
+  hipStream_t sa = ctx->stream;
+  if (!sh->s_lz) HIPCHK(ctx, hipStreamCreateWithFlags(&sh->s_lz, hipStreamNonBlocking));
+  if (!sh->s_eg) HIPCHK(ctx, hipStreamCreateWithFlags(&sh->s_eg, hipStreamNonBlocking));
+  hipStream_t sl = sh->s_lz, se = sh->s_eg;
+  HIPCHK(ctx, sh->U.ensure(sh->utotal + sh->pad));
+  HIPCHK(ctx, sh->tok.ensure(sh->utotal + 64));
+  HIPCHK(ctx, sh->bits.ensure((E + 31) / 32 + 1));
+  HIPCHK(ctx, sh->defer.ensure(DEFER_CAP));
+  HIPCHK(ctx, hipMemsetAsync(sh->U.p + sh->utotal, 0, sh->pad, sa));
+  unsigned long long *c = sh->ctr.p;
+  HIPCHK(ctx, hipMemsetAsync(c, 0, 32, sa));
+  HIPCHK(ctx, hipMemsetAsync(c + 2, 0xff, 8, sa));
+  sh->inflated = sh->bits_valid = false;
+  const uint64_t nb = sh->nblocks;
+  const uint64_t nbat = std::max<uint64_t>(1, std::min<uint64_t>(PIPE_MAX_BATCHES, nb / pipe_min_blocks()));
+  // events: per batch [huff start, huff end, lz start, lz end, eager start, eager end]
+  for (size_t i = 0; i < 6 * nbat + 2; ++i)
+    if (!pev(sh, i)) return fail(ctx, SBH_E_HIP, "hipEventCreate failed");
+  hipEvent_t *ev = sh->pev.data();
+  HIPCHK(ctx, hipEventRecord(ev[6 * nbat], sa));  // setup done: the other streams start after it
+  HIPCHK(ctx, hipStreamWaitEvent(sl, ev[6 * nbat], 0));
+  HIPCHK(ctx, hipStreamWaitEvent(se, ev[6 * nbat], 0));
+  const DevBlocks all = sh->dev_blocks();
+  uint64_t e_done = 0;
+  std::vector<int> eager_launched(nbat, 0);
+  for (uint64_t i = 0; i < nbat; ++i) {
+    const uint64_t b0 = nb * i / nbat, b1 = nb * (i + 1) / nbat;
+    hipEvent_t *e = ev + 6 * i;
+    const DevBlocks d = blocks_from(all, b0);
+    HIPCHK(ctx, hipEventRecord(e[0], sa));
+    HIPCHK(ctx, launch_huff(sh->comp.p, d, b1 - b0, sh->tok.p, sa));
+    HIPCHK(ctx, hipEventRecord(e[1], sa));
+    HIPCHK(ctx, hipStreamWaitEvent(sl, e[1], 0));
+    HIPCHK(ctx, hipEventRecord(e[2], sl));
+    HIPCHK(ctx, launch_lz(d, b1 - b0, sh->tok.p, sh->U.p, sl));
+    HIPCHK(ctx, hipEventRecord(e[3], sl));
+    // eager tiles whose staged windows lie below the inflated frontier
+    const bool last = i + 1 == nbat;
+    const uint64_t front = last ? ~0ull : sh->hb[b1].ustart;
+    uint64_t hi = E;
+    if (!last) {
+      hi = front + EAGER_TILE >= EAGER_REACH ? (front + EAGER_TILE - EAGER_REACH) / EAGER_TILE * EAGER_TILE : 0;
+      hi = std::min(hi, E);
+    }
+    if (hi > e_done) {
+      HIPCHK(ctx, hipStreamWaitEvent(se, e[3], 0));
+      HIPCHK(ctx, hipEventRecord(e[4], se));
+      HIPCHK(ctx, launch_eager(sh->U.p, sh->utotal + sh->pad, e_done, hi, sh->d_seg.p, (uint32_t)sh->seg_end.size(),
+                               sh->open_last ? 1 : 0, sh->ctg.p, sh->nctg, rtc, sh->bits.p + e_done / 32, c, se,
+                               front, sh->defer.p, DEFER_CAP));
+      HIPCHK(ctx, hipEventRecord(e[5], se));
+      eager_launched[i] = 1;
+      e_done = hi;
+    }
+  }
+  HIPCHK(ctx, hipStreamWaitEvent(se, ev[6 * (nbat - 1) + 3], 0));
+  HIPCHK(ctx, launch_eager_defer(sh->U.p, 0, sh->d_seg.p, (uint32_t)sh->seg_end.size(), sh->open_last ? 1 : 0,
+                                 sh->ctg.p, sh->nctg, rtc, sh->bits.p, c, sh->defer.p, DEFER_CAP, se));
+  HIPCHK(ctx, hipEventRecord(ev[6 * nbat + 1], se));
+  HIPCHK(ctx, hipStreamWaitEvent(sa, ev[6 * nbat + 1], 0));
+  std::vector<uint32_t> status(nb);
+  if (nb) HIPCHK(ctx, hipMemcpyAsync(status.data(), sh->b_status.p, nb * 4, hipMemcpyDeviceToHost, sa));
+  HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr, c, 32, hipMemcpyDeviceToHost, sa));
+  HIPCHK(ctx, hipStreamSynchronize(sa));
+  for (uint64_t i = 0; i < nb; ++i) {
+    if (status[i] == INF_OK) continue;
+    const sbh_block &b = sh->hb[i];
+    if (status[i] == INF_SIZE)
+      return fail(ctx, SBH_E_INFLATE_SIZE, "block %llu: expected %u decompressed bytes", (unsigned long long)b.start,
+                  b.usize);
+    if (status[i] == INF_BAD_ISIZE) return fail(ctx, SBH_E_BAD_ISIZE, "block %llu: ISIZE %u", (unsigned long long)b.start, b.usize);
+    return fail(ctx, SBH_E_INFLATE_DATA, "block %llu: invalid deflate data", (unsigned long long)b.start);
+  }
+  sh->inflated = true;
+  if (sh->timing) {
+    double hs = 0, ls = 0, es = 0;
+    for (uint64_t i = 0; i < nbat; ++i) {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, ev[6 * i], ev[6 * i + 1]) == hipSuccess) hs += ms;
+      if (hipEventElapsedTime(&ms, ev[6 * i + 2], ev[6 * i + 3]) == hipSuccess) ls += ms;
+      if (eager_launched[i] && hipEventElapsedTime(&ms, ev[6 * i + 4], ev[6 * i + 5]) == hipSuccess) es += ms;
+    }
+    sh->pipe_ms[0] = hs;
+    sh->pipe_ms[1] = ls;
+    sh->pipe_ms[2] = es;
+  }
+  if (sh->h_ctr[3] > DEFER_CAP) return eager_range(sh, 0, E, rtc, n_true);  // deferral overflow: plain pass
+  sh->bits_valid = true;
+  sh->bits_begin = 0;
+  sh->bits_end = E;
+  sh->bits_rtc = rtc;
+  if (n_true) *n_true = sh->h_ctr[0];
+  if (sh->h_ctr[1]) {
+    sh->bits_valid = false;
+    return fail(ctx, SBH_E_NEED_HALO, "%llu positions (first %llu) need bytes past the shard", sh->h_ctr[1],
+                sh->h_ctr[2]);
+  }
+  return SBH_OK;
+}
+
 int sbh_run_shard(sbh_shard *sh, uint64_t index_start, uint64_t own_end_file, int32_t rtc, int32_t mrs,
                   sbh_shard_result *res) {
   if (!sh || !res) return SBH_E_ARG;
@@ -768,19 +935,22 @@ int sbh_run_shard(sbh_shard *sh, uint64_t index_start, uint64_t own_end_file, in
   mark(sh, 0);
   int rc = sbh_index(sh, index_start, &res->n_blocks, nullptr);
   mark(sh, 1);
-  if (!rc) rc = sbh_inflate(sh, nullptr);
   if (rc) { sh->timing = false; return res->status = rc; }
   uint64_t E = 0;
   (void)sbh_flat_bound(sh, own_end_file, &E);
-  if (!sh->at_eof && E == sh->utotal)
+  if (!sh->at_eof && E == sh->utotal) {
+    sh->timing = false;
     return res->status = fail(ctx, SBH_E_NEED_HALO, "no halo past %llu", (unsigned long long)own_end_file);
+  }
   uint64_t owned_blocks = 0, cbytes = 0;
   for (const sbh_block &b : sh->hb)
     if (b.start < own_end_file) { ++owned_blocks; cbytes += b.csize; }
   res->n_blocks = owned_blocks;
   res->comp_bytes = cbytes;
   res->flat_bytes = E;
-  rc = sbh_check_eager(sh, 0, E, rtc, nullptr, &res->n_true);
+  mark(sh, 2);
+  rc = run_pipelined(sh, E, rtc, &res->n_true);
+  mark(sh, 5);
   if (rc) { sh->timing = false; return res->status = rc; }
   uint64_t first = 0;
   int32_t delta = 0;
@@ -799,12 +969,19 @@ int sbh_run_shard(sbh_shard *sh, uint64_t index_start, uint64_t own_end_file, in
   res->exit_flat = E;
   if (sh->ev_ok) {
     (void)hipEventSynchronize(sh->ev[6]);
-    const int from[6] = {0, 2, 4, 5, 2, 7}, to[6] = {1, 3, 5, 6, 7, 3};
-    for (int i = 0; i < 6; ++i) {
+    // [index, inflate + eager pipeline, eager (sum of launches), split/count, k_huff, k_lz]
+    const int from[2] = {0, 5}, to[2] = {1, 6};
+    for (int i = 0; i < 2; ++i) {
       float ms = 0;
       (void)hipEventElapsedTime(&ms, sh->ev[from[i]], sh->ev[to[i]]);
-      sh->stage_ms[i] = ms;
+      sh->stage_ms[i == 0 ? 0 : 3] = ms;
     }
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, sh->ev[2], sh->ev[5]);
+    sh->stage_ms[1] = ms;
+    sh->stage_ms[2] = sh->pipe_ms[2];
+    sh->stage_ms[4] = sh->pipe_ms[0];
+    sh->stage_ms[5] = sh->pipe_ms[1];
   }
   return res->status = rc;
 }

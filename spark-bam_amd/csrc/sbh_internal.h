@@ -34,6 +34,16 @@ constexpr uint32_t INF_DATA = 2;      // DataFormatException (zlib Z_DATA_ERROR)
 constexpr uint32_t INF_BAD_ISIZE = 3; // ISIZE outside [0, 65536]
 constexpr uint32_t INF_SERIAL = 0xffu; // (inside inflate only) left to the serial decoder
 
+// Eager tile geometry (check.hip): a workgroup decides ETILE positions and stages those
+// plus a look-ahead; EAGER_REACH bounds the flat bytes past a tile's first position
+// that its staged window touches (the pipelined run launches a tile only once they are
+// inflated; reads beyond, by the exact path, defer the position instead).
+#ifndef SBH_ETILE
+#define SBH_ETILE 16384
+#endif
+constexpr uint64_t EAGER_TILE = SBH_ETILE;
+constexpr uint64_t EAGER_REACH = SBH_ETILE + 4096 + 512 + 64;
+
 // Launchers (defined in the .hip files, called from sbh_api.hip).
 // Inflate = k_huff (Huffman decode -> LZ77 tokens, block status) then k_lz (tokens ->
 // flat bytes).  tok: scratch of >= 4 B per flat byte (block b's tokens at tok[ustart_b ...]).

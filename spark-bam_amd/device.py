@@ -157,6 +157,13 @@ class Shard:
         self._c(lib().sbh_check_eager(self.h, begin, end, reads_to_check, _ptr(bits), C.byref(n)))
         return n.value, bits
 
+    def eager_bits(self, begin=0, end=None):
+        """The eager bitmap the last check_eager()/run() left on the device, [begin, end)."""
+        end = self.flat_size if end is None else end
+        bits = np.zeros((end - begin + 7) // 8, dtype=np.uint8)
+        self._c(lib().sbh_eager_bits(self.h, begin, end, _ptr(bits)))
+        return bits
+
     def check_full(self, begin=0, end=None, reads_to_check=10, want_words=False, close_cap=1 << 20):
         end = self.flat_size if end is None else end
         words = np.zeros(end - begin, dtype=np.uint32) if want_words else None
@@ -201,8 +208,9 @@ class Shard:
         return {f: getattr(r, f) for f, _ in SbhShardResult._fields_}
 
     def stage_times(self):
-        """[index, inflate, eager, records, k_huff, k_lz] device ms of the last run()
-        (HIP events on the context stream)."""
+        """[index, inflate+eager pipeline, eager (sum of launches), records, k_huff
+        (sum), k_lz (sum)] device ms of the last run() (HIP events on each kernel's
+        stream)."""
         ms = (C.c_double * 6)()
         n = lib().sbh_stage_times(self.h, ms, 6)
         return list(ms[:n])

@@ -345,3 +345,42 @@ def test_shard_with_halo_matches_whole_file(ctx, synth_files):
         sh.close()
     finally:
         whole.close()
+
+
+@pytest.mark.parametrize("name,batch_blocks", [("short_l6", 4), ("long", 2), ("adversarial", 3)])
+def test_pipelined_run_matches_separate_calls(ctx, synth_files, name, batch_blocks):
+    """run() inflates and checks in a pipeline over block batches (eager tiles launched
+    behind the inflate frontier, positions whose exact check crosses it deferred).  With
+    tiny batches (many frontiers; long reads cross them) it must equal inflate() +
+    check_eager() + the record walk."""
+    data = synth_files[name]
+    of = OracleFile(data)
+    sh = ctx.shard(data)
+    sh.set_contigs(of.contig_len)
+    old = os.environ.get("SBH_PIPE_MIN_BLOCKS")
+    os.environ["SBH_PIPE_MIN_BLOCKS"] = str(batch_blocks)
+    try:
+        r = sh.run(0, data.size)
+        got = sh.read_flat(0, of.flat_size)
+        i = first_diff(got, of.uncompressed())
+        assert i < 0, f"inflate differs at flat {i}"
+        E = r["flat_bytes"]
+        bits_pipe = sh.eager_bits(0, E)
+    finally:
+        if old is None:
+            del os.environ["SBH_PIPE_MIN_BLOCKS"]
+        else:
+            os.environ["SBH_PIPE_MIN_BLOCKS"] = old
+    assert r["status"] == 0
+    # the same shard, unpipelined, over the same range
+    sh.index(0)
+    sh.inflate()
+    n, bits = sh.check_eager(0, E)
+    assert r["n_true"] == n
+    i = first_diff(np.unpackbits(bits_pipe, bitorder="little"), np.unpackbits(bits, bitorder="little"))
+    assert i < 0, f"pipelined eager differs at {i}"
+    # and the first stream segment against the oracle
+    n_ref, bits_ref = of.eager_range(0, of.flat_size)
+    k = of.flat_size
+    assert np.array_equal(np.unpackbits(bits_pipe, bitorder="little")[:k], np.unpackbits(bits_ref, bitorder="little")[:k])
+    sh.close()
