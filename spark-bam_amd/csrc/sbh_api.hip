@@ -797,14 +797,17 @@ int sbh_split(sbh_shard *sh, uint64_t start, uint64_t end, int32_t k, int32_t rt
 // slots).  An eager position whose exact check needs bytes past the inflated frontier is
 // deferred and re-checked at the end.  Same results as sbh_inflate + sbh_check_eager.
 static constexpr uint64_t PIPE_MAX_BATCHES = 16;
-static constexpr uint64_t PIPE_MIN_BLOCKS = 1024;
 static constexpr uint64_t DEFER_CAP = 1 << 20;
 
-// SBH_PIPE_MIN_BLOCKS (tests): smaller batches, to exercise many frontiers on small inputs
+// Batches of at least SBH_PIPE_MIN_BLOCKS blocks (tests: small batches exercise many
+// frontiers on small inputs).  Default: one batch.  Measured on MI355X (1 GiB shard,
+// this design): 1 batch 34.7 ms/step, 3 batches 35.2, 16 batches 38.2 -- side by side
+// the three kernels contend for the same LDS and issue slots, and k_lz (two 80 KiB
+// workgroups per CU) loses the most; the pipeline stays for inputs where it pays.
 static uint64_t pipe_min_blocks() {
   const char *e = std::getenv("SBH_PIPE_MIN_BLOCKS");
   const long long v = e ? std::atoll(e) : 0;
-  return v > 0 ? (uint64_t)v : PIPE_MIN_BLOCKS;
+  return v > 0 ? (uint64_t)v : ~0ull;
 }
 
 static hipEvent_t pev(sbh_shard *sh, size_t i) {
