@@ -1295,18 +1295,25 @@ __global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__rest
   if (tid == 0) bl.status[b] = INF_SERIAL;  // k_huff_serial<true> decodes it
 }
 
-constexpr uint32_t PTR_CAP = 4096;                 // chunk bytes resolved by pointer jumping
-constexpr uint32_t PTR_PER = PTR_CAP / LZ_THREADS;  // slots per thread
-static_assert(PTR_PER == 8, "one uint4 of u16 slots per thread");
+constexpr uint32_t LZ_TPT = 2;                         // tokens per thread per chunk
+constexpr uint32_t LZ_CHUNK = LZ_THREADS * LZ_TPT;      // tokens per chunk
+constexpr uint32_t PTR_PER = 16;                        // pointer slots per thread
+constexpr uint32_t PTR_AREA = 16384 - 32 - 256;         // bytes: slots + wsum (2 WGs/CU incl. 256 B of compiler LDS)
+constexpr uint32_t PTR_CAP = (PTR_AREA - 32) / 2;       // chunk bytes resolved by pointer chasing
 
 struct LzSmem {
-  uint8_t img[65536 + 16];    // block image, placed at (ustart & 15) so granules align with HBM
-  uint32_t toff[LZ_THREADS];  // chunk tokens: output offsets (ascending)
-  uint32_t tokv[LZ_THREADS];  // chunk tokens
-  uint32_t done[LZ_THREADS];  // round after which the token's bytes are final (0: pending)
-  uint32_t wsum[LZ_THREADS / WAVE];
-  uint4 ptr[LZ_THREADS];      // u16 per chunk byte: owning token, then source pointer
+  uint8_t img[65536 + 16];  // block image, placed at (ustart & 15) so granules align with HBM
+  union {
+    uint16_t p16[PTR_AREA / 2];  // u16 per chunk byte: its source pointer
+    struct {                     // dependency-rounds path, per half chunk
+      uint32_t toff[LZ_THREADS];  // tokens: output offsets (ascending)
+      uint32_t tokv[LZ_THREADS];  // tokens
+      uint32_t done[LZ_THREADS];  // round after which the token's bytes are final (0: pending)
+    } fb;
+  };
 };
+static_assert(sizeof(LzSmem) * 2 <= 160 * 1024, "two k_lz workgroups per CU");
+static_assert(3 * LZ_THREADS * 4 <= PTR_CAP * 2, "the rounds path's arrays fit below wsum");
 
 // Block-wide exclusive prefix max over NT threads (0 for thread 0).
 template <uint32_t NT>
@@ -1383,20 +1390,22 @@ __device__ __forceinline__ void lz_match(uint8_t *img0, uint32_t base, uint32_t 
   }
 }
 
-// LZ77 resolution of one block per workgroup, LZ_THREADS tokens per chunk; bytes before
-// the chunk are final.  A chunk whose output fits PTR_CAP bytes (the common case) is
-// resolved by pointer chasing: every byte gets the position it copies from (itself for a
-// literal), each thread follows its 8 bytes' pointers to final bytes -- rewriting its
-// slots with the results, which shortens other threads' chases -- and gathers.  Longer
-// chunks (long matches) fall back to dependency rounds: a match waits only for the
-// chunk's matches its (redirected) source overlaps, found by binary search over the
-// chunk's output offsets.
+// LZ77 resolution of one block per workgroup, LZ_CHUNK tokens per chunk (two consecutive
+// tokens per thread); bytes before the chunk are final.  A chunk whose output fits PTR_CAP
+// bytes (the common case) is resolved by pointer chasing: every byte gets the position it
+// copies from (itself for a literal; match byte k: off - dist + k mod dist, always
+// earlier), written by its own token; then each thread follows its 16 bytes' pointers to
+// final bytes -- rewriting its slots with the results, which shortens other threads'
+// chases -- and gathers.  Longer chunks (long matches) fall back, per half chunk, to
+// dependency rounds: a match waits only for the matches its (redirected) source overlaps,
+// found by binary search over the half chunk's output offsets.
 __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblocks,
                                                     const uint32_t *__restrict__ tok, uint8_t *__restrict__ U) {
   __shared__ LzSmem sm;
+  uint32_t *wsum = reinterpret_cast<uint32_t *>(sm.p16 + PTR_CAP);  // 8 words after the slots
   const uint64_t b = blockIdx.x;
   if (b >= nblocks) return;
-  const uint32_t t = threadIdx.x;
+  const uint32_t t = threadIdx.x, lane = t & (WAVE - 1);
   const uint32_t n = bl.ntok[b];
   const uint64_t G = bl.ustart[b];
   const uint32_t sh = (uint32_t)(G & 15);
@@ -1404,104 +1413,167 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
   const uint32_t *tk = tok + G;
 
   uint32_t base = 0;  // output offset of the chunk's first token
-  uint32_t x_next = t < n ? tk[t] : 0;
 #ifdef SBH_LZ_PROBE
-  uint64_t tp0 = __builtin_readcyclecounter(), t_pre = 0, t_rounds = 0, t_init = 0;
+  uint64_t tp0 = __builtin_readcyclecounter(), t_pre = 0, t_rounds = 0, t_init = 0, t_w = 0, t_ch = 0;
   uint32_t nrounds = 0, njumps = 0;
 #endif
-  for (uint32_t c0 = 0; c0 < n; c0 += LZ_THREADS) {
+  uint32_t xn[LZ_TPT];  // next chunk's tokens, loaded one chunk ahead
+#pragma unroll
+  for (uint32_t k = 0; k < LZ_TPT; ++k) xn[k] = LZ_TPT * t + k < n ? tk[LZ_TPT * t + k] : 0;
+  for (uint32_t c0 = 0; c0 < n; c0 += LZ_CHUNK) {
 #ifdef SBH_LZ_PROBE
     uint64_t ta = __builtin_readcyclecounter();
 #endif
-    const uint32_t i = c0 + t;
-    const uint32_t m = n - c0 < LZ_THREADS ? n - c0 : LZ_THREADS;  // tokens in this chunk
-    const uint32_t x = x_next;
-    x_next = i + LZ_THREADS < n ? tk[i + LZ_THREADS] : 0;  // prefetch the next chunk
-    const bool match = i < n && (x & TOK_MATCH) != 0;
-    const uint32_t len = i >= n ? 0 : match ? (x >> 16) & 0x1ff : 1;
+    // this thread's two tokens
+    const uint32_t i0 = c0 + LZ_TPT * t;
+    uint32_t x[LZ_TPT], len[LZ_TPT], dist[LZ_TPT], off[LZ_TPT];
+    bool match[LZ_TPT];
+    uint32_t mysum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < LZ_TPT; ++k) {
+      x[k] = xn[k];
+      xn[k] = i0 + LZ_CHUNK + k < n ? tk[i0 + LZ_CHUNK + k] : 0;
+      match[k] = i0 + k < n && (x[k] & TOK_MATCH) != 0;
+      len[k] = i0 + k >= n ? 0 : match[k] ? (x[k] >> 16) & 0x1ff : 1;
+      dist[k] = x[k] & 0xffff;
+      mysum += len[k];
+    }
     uint32_t chunk_len;
-    const uint32_t off = base + block_scan<LZ_THREADS>(len, sm.wsum, &chunk_len);
-    const uint32_t dist = x & 0xffff;
+    off[0] = base + block_scan<LZ_THREADS>(mysum, wsum, &chunk_len);
+#pragma unroll
+    for (uint32_t k = 1; k < LZ_TPT; ++k) off[k] = off[k - 1] + len[k - 1];
+    // slots start at the 16-byte LDS granule holding `base`, so that each thread's 16
+    // slots are one granule of the image
+    const uint32_t lead = (sh + base) & 15, abase = base - lead;
 #ifdef SBH_LZ_PROBE
     const uint64_t tb = __builtin_readcyclecounter();
     t_pre += tb - ta;
-    nrounds += chunk_len > PTR_CAP;
+    nrounds += chunk_len + lead > PTR_CAP;
 #endif
-    if (chunk_len <= PTR_CAP) {
-      // Every byte of the chunk gets a source pointer, written by its own token: a
-      // literal points at itself, match byte k at off - dist + (k mod dist) (always
-      // earlier); bytes before the chunk are final.  Each thread then follows its 8
-      // bytes' pointers to final bytes -- rewriting its slots with the results, which
-      // shortens other threads' chases -- and gathers.  (Slots are 16-bit positions in
-      // the block image.)
-      uint16_t *p16 = reinterpret_cast<uint16_t *>(sm.ptr);
-      if (t < m) {
-        if (!match) {
-          img[off] = (uint8_t)(x >> 8);
-          p16[off - base] = (uint16_t)off;
-        } else if (len <= LZ_SHORT) {
+    if (chunk_len + lead <= PTR_CAP) {
+      uint16_t *p16 = sm.p16;
+#pragma unroll
+      for (uint32_t k = 0; k < LZ_TPT; ++k) {
+        if (i0 + k >= n) continue;
+        const uint32_t d = off[k] - abase;
+        if (!match[k]) {
+          img[off[k]] = (uint8_t)(x[k] >> 8);
+          p16[d] = (uint16_t)off[k];
+        } else if (len[k] <= LZ_SHORT) {
+          const uint32_t src = off[k] - dist[k];
           uint32_t s = 0;
-          for (uint32_t k = 0; k < len; ++k) {
-            p16[off - base + k] = (uint16_t)(off - dist + s);
-            s = s + 1 == dist ? 0 : s + 1;
+          for (uint32_t j = 0; j < len[k]; ++j) {
+            p16[d + j] = (uint16_t)(src + s);
+            s = s + 1 == dist[k] ? 0 : s + 1;
           }
         }
       }
-      {  // long matches: the wave writes each one's pointers, 64 per step
-        const uint32_t lane = t & (WAVE - 1);
-        uint64_t lm = __ballot(t < m && match && len > LZ_SHORT);
+#pragma unroll
+      for (uint32_t k = 0; k < LZ_TPT; ++k) {  // long matches: the wave writes each one's pointers
+        uint64_t lm = __ballot(i0 + k < n && match[k] && len[k] > LZ_SHORT);
         while (lm) {
           const uint32_t l = (uint32_t)__builtin_ctzll(lm);
           lm &= lm - 1;
-          const uint32_t o = __builtin_amdgcn_readlane(off, l), d = __builtin_amdgcn_readlane(dist, l);
-          const uint32_t L = __builtin_amdgcn_readlane(len, l);
+          const uint32_t o = __builtin_amdgcn_readlane(off[k], l), d = __builtin_amdgcn_readlane(dist[k], l);
+          const uint32_t L = __builtin_amdgcn_readlane(len[k], l);
           uint32_t s = lane < d ? lane : mod_small(lane, d);
           const uint32_t step = WAVE < d ? WAVE : mod_small(WAVE, d);
-          for (uint32_t k = lane; k < L; k += WAVE) {
-            p16[o - base + k] = (uint16_t)(o - d + s);
+          for (uint32_t j = lane; j < L; j += WAVE) {
+            p16[o - abase + j] = (uint16_t)(o - d + s);
             s += step;
             s = s >= d ? s - d : s;
           }
         }
       }
+#ifdef SBH_LZ_PROBE
+      t_w += __builtin_readcyclecounter() - tb;
+#endif
       __syncthreads();
-      uint32_t q[PTR_PER];
-      {
-        const uint4 pv = sm.ptr[t];
-        q[0] = pv.x & 0xffff; q[1] = pv.x >> 16; q[2] = pv.y & 0xffff; q[3] = pv.y >> 16;
-        q[4] = pv.z & 0xffff; q[5] = pv.z >> 16; q[6] = pv.w & 0xffff; q[7] = pv.w >> 16;
-      }
 #ifdef SBH_LZ_PROBE
       const uint64_t tc = __builtin_readcyclecounter();
       t_init += tc - tb;
 #endif
-      // chase every pointer to a final byte (before the chunk, or a literal: a slot
-      // pointing at itself); no rounds, no barriers
-#pragma unroll
-      for (uint32_t k = 0; k < PTR_PER; ++k) {
-        const uint32_t slot = t * PTR_PER + k, pos = base + slot;
-        uint32_t c = q[k];
-        if (slot < chunk_len && c != pos) {
-          while (c >= base) {
-            const uint32_t v = __hip_atomic_load(&p16[c - base], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#ifdef SBH_LZ_PROBE
-            ++njumps;
-#endif
-            if (v == c) break;
-            c = v;
-          }
-          __hip_atomic_store(&p16[slot], (uint16_t)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          img[pos] = img[c];
+      // chase all 16 pointers of this thread's granule together, one LDS round trip per
+      // round, writing shortened pointers back (other threads' chains pass through them);
+      // no barriers.  A pointer is final when it is before the chunk or names a literal
+      // (a slot pointing at itself).  Then gather the bytes and store the granule.
+      const uint32_t g0 = abase + PTR_PER * t;  // image position of the granule
+      if (PTR_PER * t < chunk_len + lead) {
+        uint32_t c[PTR_PER];
+        {
+          const uint4 *pv = reinterpret_cast<const uint4 *>(p16) + 2 * t;
+          const uint4 a = pv[0], e = pv[1];
+          c[0] = a.x & 0xffff; c[1] = a.x >> 16; c[2] = a.y & 0xffff; c[3] = a.y >> 16;
+          c[4] = a.z & 0xffff; c[5] = a.z >> 16; c[6] = a.w & 0xffff; c[7] = a.w >> 16;
+          c[8] = e.x & 0xffff; c[9] = e.x >> 16; c[10] = e.y & 0xffff; c[11] = e.y >> 16;
+          c[12] = e.z & 0xffff; c[13] = e.z >> 16; c[14] = e.w & 0xffff; c[15] = e.w >> 16;
         }
+        uint32_t pend = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < PTR_PER; ++k) {
+          const uint32_t pos = g0 + k;
+          const bool in = pos >= base && pos < base + chunk_len;
+          c[k] = in ? c[k] : pos;
+          pend |= (in && c[k] != pos && c[k] >= base) ? 1u << k : 0u;
+        }
+        // Plain loads: another thread may rewrite a slot concurrently, and either value
+        // (u16 LDS accesses are single-copy atomic) is a valid pointer.  Rounds are
+        // branch-free; settled slots reread their own final pointer's slot harmlessly.
+        uint32_t *p32 = reinterpret_cast<uint32_t *>(p16);
+        while (__builtin_expect(pend != 0, 0)) {
+          uint32_t v[PTR_PER];
+#pragma unroll
+          for (uint32_t k = 0; k < PTR_PER; ++k) v[k] = p16[(c[k] >= base ? c[k] : base) - abase];
+#ifdef SBH_LZ_PROBE
+          ++njumps;
+#endif
+          uint32_t np = 0;
+#pragma unroll
+          for (uint32_t k = 0; k < PTR_PER; ++k) {
+            const bool go = ((pend >> k) & 1) && v[k] != c[k];
+            c[k] = go ? v[k] : c[k];
+            np |= (go && v[k] >= base) ? 1u << k : 0u;
+          }
+          pend = np;
+          // write back: settled and shortened pointers alike (literal and out-of-chunk
+          // slots keep pointing at themselves)
+          uint4 *pw = reinterpret_cast<uint4 *>(p32) + 2 * t;
+          pw[0] = make_uint4(c[0] | c[1] << 16, c[2] | c[3] << 16, c[4] | c[5] << 16, c[6] | c[7] << 16);
+          pw[1] = make_uint4(c[8] | c[9] << 16, c[10] | c[11] << 16, c[12] | c[13] << 16, c[14] | c[15] << 16);
+        }
+        uint32_t w[4];
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+          w[q] = (uint32_t)img[c[4 * q]] | (uint32_t)img[c[4 * q + 1]] << 8 |
+                 (uint32_t)img[c[4 * q + 2]] << 16 | (uint32_t)img[c[4 * q + 3]] << 24;
+        }
+        *reinterpret_cast<uint4 *>(img + g0) = make_uint4(w[0], w[1], w[2], w[3]);
       }
+#ifdef SBH_LZ_PROBE
+      t_ch += __builtin_readcyclecounter() - tc;
+#endif
     } else {
-      if (t < m) {
-        sm.toff[t] = off;
-        sm.tokv[t] = x;
-        sm.done[t] = match ? 0 : 1;
-        if (!match) img[off] = (uint8_t)(x >> 8);
-      }
-      __syncthreads();
+      // dependency rounds, one half chunk (one token per thread) at a time
+      uint32_t hbase = base;
+      for (uint32_t h = 0; h < LZ_TPT; ++h) {
+        const uint32_t ih = c0 + h * LZ_THREADS + t;
+        const uint32_t m = n > c0 + h * LZ_THREADS ? min(n - (c0 + h * LZ_THREADS), LZ_THREADS) : 0u;
+        const uint32_t xh = ih < n ? tk[ih] : 0;
+        const bool match = ih < n && (xh & TOK_MATCH) != 0;
+        const uint32_t len = ih >= n ? 0 : match ? (xh >> 16) & 0x1ff : 1;
+        const uint32_t dist = xh & 0xffff;
+        uint32_t half_len;
+        __syncthreads();  // wsum / fb arrays free
+        const uint32_t off = hbase + block_scan<LZ_THREADS>(len, wsum, &half_len);
+        const uint32_t base = hbase;
+        if (t < m) {
+          sm.fb.toff[t] = off;
+          sm.fb.tokv[t] = xh;
+          sm.fb.done[t] = match ? 0 : 1;
+          if (!match) img[off] = (uint8_t)(xh >> 8);
+        }
+        __syncthreads();
+        if (m) {
       uint32_t src = off - dist;  // where the (final-equivalent) source bytes start
       uint32_t jl = 1, jh = 0;    // chunk tokens the source overlaps (empty: none)
       if (match) {
@@ -1513,16 +1585,16 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
         // collapses chains (read names copying the previous read's name ...) so most
         // matches copy in the first round.
         for (int hop = 0; hop < 16 && src >= base; ++hop) {
-          const uint32_t j = cover(sm.toff, m, src);
-          const uint32_t y = sm.tokv[j];
+          const uint32_t j = cover(sm.fb.toff, m, src);
+          const uint32_t y = sm.fb.tokv[j];
           if (!(y & TOK_MATCH)) break;
-          const uint32_t oj = sm.toff[j], lj = (y >> 16) & 0x1ff, dj = y & 0xffff;
+          const uint32_t oj = sm.fb.toff[j], lj = (y >> 16) & 0x1ff, dj = y & 0xffff;
           if (dj < lj || src + ext > oj + lj) break;  // overlapping M' or source spans tokens
           src -= dj;
         }
         if (src + ext > base) {
-          jl = src < base ? 0 : cover(sm.toff, m, src);
-          jh = cover(sm.toff, m, src + ext - 1);
+          jl = src < base ? 0 : cover(sm.fb.toff, m, src);
+          jh = cover(sm.fb.toff, m, src + ext - 1);
         }
       }
       bool pending = match;
@@ -1531,7 +1603,7 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
         if (pending) {
           go = true;
           for (uint32_t j = jl; j <= jh && go; ++j) {
-            const uint32_t dj = sm.done[j];
+            const uint32_t dj = sm.fb.done[j];
             go = dj != 0 && dj <= r;
           }
         }
@@ -1551,24 +1623,27 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
         }
         if (go && len <= LZ_LONG) lz_match(sm.img, sh, off, src, dist, len);
         if (go) {
-          sm.done[t] = r + 1;
+          sm.fb.done[t] = r + 1;
           pending = false;
         }
         if (!__syncthreads_or(pending)) break;
       }
-
+        }
+        hbase += half_len;
+      }
     }
     base += chunk_len;
-    __syncthreads();  // toff/done/wsum are reused by the next chunk
+    __syncthreads();  // slots / wsum are reused by the next chunk
 #ifdef SBH_LZ_PROBE
     t_rounds += __builtin_readcyclecounter() - tb;
 #endif
   }
 #ifdef SBH_LZ_PROBE
-  if (t == 0 && b < 4)
-    printf("lz blk %llu ntok %u cyc %llu pre %llu init %llu resolve %llu fallback_chunks %u jump_rounds %u\n", (unsigned long long)b, n,
-           (unsigned long long)(__builtin_readcyclecounter() - tp0), (unsigned long long)t_pre,
-           (unsigned long long)t_init, (unsigned long long)t_rounds, nrounds, njumps);
+  if (lane == 0 && b < 2)
+    printf("lz blk %llu wave %u ntok %u cyc %llu pre %llu writes %llu init+bar %llu chase %llu resolve+bar %llu fallback %u chase_rounds %u\n",
+           (unsigned long long)b, t / WAVE, n, (unsigned long long)(__builtin_readcyclecounter() - tp0),
+           (unsigned long long)t_pre, (unsigned long long)t_w, (unsigned long long)t_init,
+           (unsigned long long)t_ch, (unsigned long long)t_rounds, nrounds, njumps);
 #endif
   const uint32_t usize = base;
   // write the image: 16-byte granules aligned to the flat address
