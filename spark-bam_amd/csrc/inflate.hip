@@ -1297,7 +1297,7 @@ __global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__rest
 
 constexpr uint32_t LZ_TPT = 2;                         // tokens per thread per chunk
 constexpr uint32_t LZ_CHUNK = LZ_THREADS * LZ_TPT;      // tokens per chunk
-constexpr uint32_t PTR_PER = 16;                        // pointer slots per thread
+constexpr uint32_t PTR_HALF = 8;                        // pointer slots per thread and pass
 constexpr uint32_t PTR_AREA = 16384 - 32 - 256;         // bytes: slots + wsum (2 WGs/CU incl. 256 B of compiler LDS)
 constexpr uint32_t PTR_CAP = (PTR_AREA - 32) / 2;       // chunk bytes resolved by pointer chasing
 
@@ -1493,24 +1493,22 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
       const uint64_t tc = __builtin_readcyclecounter();
       t_init += tc - tb;
 #endif
-      // chase all 16 pointers of this thread's granule together, one LDS round trip per
+      // chase the pointers of 8 consecutive slots together, one LDS round trip per
       // round, writing shortened pointers back (other threads' chains pass through them);
       // no barriers.  A pointer is final when it is before the chunk or names a literal
-      // (a slot pointing at itself).  Then gather the bytes and store the granule.
-      const uint32_t g0 = abase + PTR_PER * t;  // image position of the granule
-      if (PTR_PER * t < chunk_len + lead) {
-        uint32_t c[PTR_PER];
+      // (a slot pointing at itself).  Then gather the bytes and store them (8 per thread
+      // and pass, so that all waves share the work).
+      for (uint32_t h = t; PTR_HALF * h < chunk_len + lead; h += LZ_THREADS) {
+        const uint32_t g0 = abase + PTR_HALF * h;  // image position of the half granule
+        uint32_t c[PTR_HALF];
         {
-          const uint4 *pv = reinterpret_cast<const uint4 *>(p16) + 2 * t;
-          const uint4 a = pv[0], e = pv[1];
+          const uint4 a = reinterpret_cast<const uint4 *>(p16)[h];
           c[0] = a.x & 0xffff; c[1] = a.x >> 16; c[2] = a.y & 0xffff; c[3] = a.y >> 16;
           c[4] = a.z & 0xffff; c[5] = a.z >> 16; c[6] = a.w & 0xffff; c[7] = a.w >> 16;
-          c[8] = e.x & 0xffff; c[9] = e.x >> 16; c[10] = e.y & 0xffff; c[11] = e.y >> 16;
-          c[12] = e.z & 0xffff; c[13] = e.z >> 16; c[14] = e.w & 0xffff; c[15] = e.w >> 16;
         }
         uint32_t pend = 0;
 #pragma unroll
-        for (uint32_t k = 0; k < PTR_PER; ++k) {
+        for (uint32_t k = 0; k < PTR_HALF; ++k) {
           const uint32_t pos = g0 + k;
           const bool in = pos >= base && pos < base + chunk_len;
           c[k] = in ? c[k] : pos;
@@ -1519,17 +1517,16 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
         // Plain loads: another thread may rewrite a slot concurrently, and either value
         // (u16 LDS accesses are single-copy atomic) is a valid pointer.  Rounds are
         // branch-free; settled slots reread their own final pointer's slot harmlessly.
-        uint32_t *p32 = reinterpret_cast<uint32_t *>(p16);
         while (__builtin_expect(pend != 0, 0)) {
-          uint32_t v[PTR_PER];
+          uint32_t v[PTR_HALF];
 #pragma unroll
-          for (uint32_t k = 0; k < PTR_PER; ++k) v[k] = p16[(c[k] >= base ? c[k] : base) - abase];
+          for (uint32_t k = 0; k < PTR_HALF; ++k) v[k] = p16[(c[k] >= base ? c[k] : base) - abase];
 #ifdef SBH_LZ_PROBE
           ++njumps;
 #endif
           uint32_t np = 0;
 #pragma unroll
-          for (uint32_t k = 0; k < PTR_PER; ++k) {
+          for (uint32_t k = 0; k < PTR_HALF; ++k) {
             const bool go = ((pend >> k) & 1) && v[k] != c[k];
             c[k] = go ? v[k] : c[k];
             np |= (go && v[k] >= base) ? 1u << k : 0u;
@@ -1537,17 +1534,16 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
           pend = np;
           // write back: settled and shortened pointers alike (literal and out-of-chunk
           // slots keep pointing at themselves)
-          uint4 *pw = reinterpret_cast<uint4 *>(p32) + 2 * t;
-          pw[0] = make_uint4(c[0] | c[1] << 16, c[2] | c[3] << 16, c[4] | c[5] << 16, c[6] | c[7] << 16);
-          pw[1] = make_uint4(c[8] | c[9] << 16, c[10] | c[11] << 16, c[12] | c[13] << 16, c[14] | c[15] << 16);
+          reinterpret_cast<uint4 *>(p16)[h] =
+              make_uint4(c[0] | c[1] << 16, c[2] | c[3] << 16, c[4] | c[5] << 16, c[6] | c[7] << 16);
         }
-        uint32_t w[4];
+        uint32_t w[2];
 #pragma unroll
-        for (uint32_t q = 0; q < 4; ++q) {
+        for (uint32_t q = 0; q < 2; ++q) {
           w[q] = (uint32_t)img[c[4 * q]] | (uint32_t)img[c[4 * q + 1]] << 8 |
                  (uint32_t)img[c[4 * q + 2]] << 16 | (uint32_t)img[c[4 * q + 3]] << 24;
         }
-        *reinterpret_cast<uint4 *>(img + g0) = make_uint4(w[0], w[1], w[2], w[3]);
+        *reinterpret_cast<uint2 *>(img + g0) = make_uint2(w[0], w[1]);
       }
 #ifdef SBH_LZ_PROBE
       t_ch += __builtin_readcyclecounter() - tc;
