@@ -46,7 +46,11 @@ constexpr int WAVES = SBH_HUFF_WAVES;  // waves (blocks) per k_huff workgroup
 #endif
 constexpr uint32_t LZ_THREADS = SBH_LZ_THREADS;
 constexpr uint32_t LZ_LONG = 24;  // longer matches are copied by the whole wave (rounds path)
-constexpr uint32_t LZ_SHORT = 16;  // longer matches get their pointers from the whole wave
+#ifndef SBH_LZ_SHORT
+#define SBH_LZ_SHORT 32
+#endif
+constexpr uint32_t LZ_SHORT = SBH_LZ_SHORT;  // longer matches get their pointers from the whole wave
+static_assert(LZ_SHORT <= 33, "k_lz finds a short match's start within 32 slots back");
 constexpr uint32_t TOK_MATCH = 0x80000000u;  // token: literal = byte << 8 (bit 31 clear); match = bit31 | len << 16 | dist
 
 // Table entries (32-bit; laid out so the asm hot loop decodes with few scalar ops):
@@ -1298,22 +1302,27 @@ __global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__rest
 constexpr uint32_t LZ_TPT = 2;                         // tokens per thread per chunk
 constexpr uint32_t LZ_CHUNK = LZ_THREADS * LZ_TPT;      // tokens per chunk
 constexpr uint32_t PTR_HALF = 8;                        // pointer slots per thread and pass
-constexpr uint32_t PTR_AREA = 16384 - 32 - 256;         // bytes: slots + wsum (2 WGs/CU incl. 256 B of compiler LDS)
-constexpr uint32_t PTR_CAP = (PTR_AREA - 32) / 2;       // chunk bytes resolved by pointer chasing
+constexpr uint32_t PTR_CAP = 7552;                      // chunk bytes resolved by pointer chasing
+constexpr uint32_t SB_WORDS = PTR_CAP / 32;             // token-start bitmap words
 
 struct LzSmem {
   uint8_t img[65536 + 16];  // block image, placed at (ustart & 15) so granules align with HBM
   union {
-    uint16_t p16[PTR_AREA / 2];  // u16 per chunk byte: its source pointer
-    struct {                     // dependency-rounds path, per half chunk
+    struct {
+      uint16_t p16[PTR_CAP];     // per chunk byte: its source pointer (token starts first)
+      uint32_t sbits[SB_WORDS];  // per chunk byte: starts a token (every byte of a long match)
+      uint32_t wsum[8];          // block_scan scratch (both paths)
+    } pp;
+    struct {                      // dependency-rounds path, per half chunk
       uint32_t toff[LZ_THREADS];  // tokens: output offsets (ascending)
       uint32_t tokv[LZ_THREADS];  // tokens
       uint32_t done[LZ_THREADS];  // round after which the token's bytes are final (0: pending)
     } fb;
   };
 };
-static_assert(sizeof(LzSmem) * 2 <= 160 * 1024, "two k_lz workgroups per CU");
-static_assert(3 * LZ_THREADS * 4 <= PTR_CAP * 2, "the rounds path's arrays fit below wsum");
+// two workgroups per CU, counting the 256 B of LDS the compiler adds
+static_assert(sizeof(LzSmem) * 2 + 512 <= 160 * 1024, "two k_lz workgroups per CU");
+static_assert(sizeof(LzSmem::fb) <= offsetof(decltype(LzSmem::pp), wsum), "the rounds path keeps wsum");
 
 // Block-wide exclusive prefix max over NT threads (0 for thread 0).
 template <uint32_t NT>
@@ -1390,6 +1399,12 @@ __device__ __forceinline__ void lz_match(uint8_t *img0, uint32_t base, uint32_t 
   }
 }
 
+// Eight u16 slot values (positions; ones before the block may have wrapped) as a uint4.
+__device__ __forceinline__ uint4 pack8_u16(const uint32_t *c) {
+  return make_uint4(__builtin_amdgcn_perm(c[1], c[0], 0x05040100u), __builtin_amdgcn_perm(c[3], c[2], 0x05040100u),
+                    __builtin_amdgcn_perm(c[5], c[4], 0x05040100u), __builtin_amdgcn_perm(c[7], c[6], 0x05040100u));
+}
+
 // LZ77 resolution of one block per workgroup, LZ_CHUNK tokens per chunk (two consecutive
 // tokens per thread); bytes before the chunk are final.  A chunk whose output fits PTR_CAP
 // bytes (the common case) is resolved by pointer chasing: every byte gets the position it
@@ -1402,7 +1417,7 @@ __device__ __forceinline__ void lz_match(uint8_t *img0, uint32_t base, uint32_t 
 __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblocks,
                                                     const uint32_t *__restrict__ tok, uint8_t *__restrict__ U) {
   __shared__ LzSmem sm;
-  uint32_t *wsum = reinterpret_cast<uint32_t *>(sm.p16 + PTR_CAP);  // 8 words after the slots
+  uint32_t *wsum = sm.pp.wsum;
   const uint64_t b = blockIdx.x;
   if (b >= nblocks) return;
   const uint32_t t = threadIdx.x, lane = t & (WAVE - 1);
@@ -1414,8 +1429,8 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
 
   uint32_t base = 0;  // output offset of the chunk's first token
 #ifdef SBH_LZ_PROBE
-  uint64_t tp0 = __builtin_readcyclecounter(), t_pre = 0, t_rounds = 0, t_init = 0, t_w = 0, t_ch = 0;
-  uint32_t nrounds = 0, njumps = 0;
+  uint64_t tp0 = __builtin_readcyclecounter(), t_pre = 0, t_rounds = 0, t_init = 0, t_w = 0, t_ch = 0, t_mk = 0;
+  uint32_t nrounds = 0, njumps = 0, nlong = 0;
 #endif
   uint32_t xn[LZ_TPT];  // next chunk's tokens, loaded one chunk ahead
 #pragma unroll
@@ -1438,6 +1453,7 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
       dist[k] = x[k] & 0xffff;
       mysum += len[k];
     }
+    for (uint32_t w = t; w < SB_WORDS; w += LZ_THREADS) sm.pp.sbits[w] = 0;  // ordered by the scan's barrier
     uint32_t chunk_len;
     off[0] = base + block_scan<LZ_THREADS>(mysum, wsum, &chunk_len);
 #pragma unroll
@@ -1451,26 +1467,25 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
     nrounds += chunk_len + lead > PTR_CAP;
 #endif
     if (chunk_len + lead <= PTR_CAP) {
-      uint16_t *p16 = sm.p16;
+      uint16_t *p16 = sm.pp.p16;
+      uint32_t *sbits = sm.pp.sbits;
+      // Tokens mark their starts: one slot write (a literal points at itself, a short
+      // match at its source) and one start bit each; the bytes inside a short match get
+      // their pointers in the slot pass below, from the nearest start.
 #pragma unroll
       for (uint32_t k = 0; k < LZ_TPT; ++k) {
-        if (i0 + k >= n) continue;
+        if (i0 + k >= n || len[k] > LZ_SHORT) continue;
         const uint32_t d = off[k] - abase;
-        if (!match[k]) {
-          img[off[k]] = (uint8_t)(x[k] >> 8);
-          p16[d] = (uint16_t)off[k];
-        } else if (len[k] <= LZ_SHORT) {
-          const uint32_t src = off[k] - dist[k];
-          uint32_t s = 0;
-          for (uint32_t j = 0; j < len[k]; ++j) {
-            p16[d + j] = (uint16_t)(src + s);
-            s = s + 1 == dist[k] ? 0 : s + 1;
-          }
-        }
+        p16[d] = (uint16_t)(match[k] ? off[k] - dist[k] : off[k]);
+        if (!match[k]) img[off[k]] = (uint8_t)(x[k] >> 8);
+        __hip_atomic_fetch_or(&sbits[d >> 5], 1u << (d & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
 #pragma unroll
-      for (uint32_t k = 0; k < LZ_TPT; ++k) {  // long matches: the wave writes each one's pointers
+      for (uint32_t k = 0; k < LZ_TPT; ++k) {  // long matches: the wave writes every byte's pointer
         uint64_t lm = __ballot(i0 + k < n && match[k] && len[k] > LZ_SHORT);
+#ifdef SBH_LZ_PROBE
+        nlong += __builtin_popcountll(lm);
+#endif
         while (lm) {
           const uint32_t l = (uint32_t)__builtin_ctzll(lm);
           lm &= lm - 1;
@@ -1483,7 +1498,48 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
             s += step;
             s = s >= d ? s - d : s;
           }
+          const uint32_t sa = o - abase, se = sa + L;  // every byte is a start
+          for (uint32_t wi = (sa >> 5) + lane; wi <= ((se - 1) >> 5); wi += WAVE) {
+            const uint32_t lo = max(sa, wi * 32), hi = min(se, wi * 32 + 32);
+            const uint32_t m = (hi - lo == 32 ? ~0u : (1u << (hi - lo)) - 1) << (lo & 31);
+            __hip_atomic_fetch_or(&sbits[wi], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
         }
+      }
+#ifdef SBH_LZ_PROBE
+      t_mk += __builtin_readcyclecounter() - tb;
+#endif
+      __syncthreads();
+      // slot pass: every byte's pointer from its token's start (at most LZ_SHORT - 1
+      // back, inside this 64-bit window of start bits): byte j of a match that starts at
+      // s and copies from v points at v + (j mod (s - v)); starts keep their value
+      for (uint32_t h = t; PTR_HALF * h < chunk_len + lead; h += LZ_THREADS) {
+        const uint32_t wi = h >> 2, g0 = abase + PTR_HALF * h;
+        const uint64_t W = (uint64_t)sbits[wi] << 32 | (wi ? sbits[wi - 1] : 0u);
+        uint32_t sidx[PTR_HALF], jj[PTR_HALF], v[PTR_HALF];
+#pragma unroll
+        for (uint32_t k = 0; k < PTR_HALF; ++k) {
+          const uint32_t pos = g0 + k, bit = 32 + ((PTR_HALF * h + k) & 31);
+          const bool in = pos >= base && pos < base + chunk_len;
+          const uint64_t m = W & (~0ull >> (63 - bit));
+          const uint32_t sb = 63 - (uint32_t)__builtin_clzll(m | 1);
+          sidx[k] = in ? wi * 32 + sb - 32 : PTR_HALF * h + k;
+          jj[k] = in ? bit - sb : 0;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < PTR_HALF; ++k) v[k] = p16[sidx[k]];
+        uint32_t c[PTR_HALF];
+#pragma unroll
+        for (uint32_t k = 0; k < PTR_HALF; ++k) {
+          const uint32_t pos = g0 + k;
+          const bool in = pos >= base && pos < base + chunk_len;
+          const uint32_t dd = abase + sidx[k] - v[k];  // the match's distance
+          const uint32_t j = jj[k];
+          const uint32_t pj = v[k] + (j < dd ? j : mod_small(j, dd));
+          c[k] = !in ? pos : j == 0 ? v[k] : pj;
+        }
+        reinterpret_cast<uint4 *>(p16)[h] =
+            pack8_u16(c);
       }
 #ifdef SBH_LZ_PROBE
       t_w += __builtin_readcyclecounter() - tb;
@@ -1517,7 +1573,19 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
         // Plain loads: another thread may rewrite a slot concurrently, and either value
         // (u16 LDS accesses are single-copy atomic) is a valid pointer.  Rounds are
         // branch-free; settled slots reread their own final pointer's slot harmlessly.
+#ifdef SBH_LZ_DEBUG
+        uint32_t guard = 0;
+#endif
         while (__builtin_expect(pend != 0, 0)) {
+#ifdef SBH_LZ_DEBUG
+          if (++guard > 300) {
+            for (uint32_t k = 0; k < PTR_HALF; ++k)
+              if ((pend >> k) & 1)
+                printf("lz chase stuck blk %llu pos %u c %u base %u chunk_len %u lead %u\n", (unsigned long long)b,
+                       g0 + k, c[k], base, chunk_len, lead);
+            break;
+          }
+#endif
           uint32_t v[PTR_HALF];
 #pragma unroll
           for (uint32_t k = 0; k < PTR_HALF; ++k) v[k] = p16[(c[k] >= base ? c[k] : base) - abase];
@@ -1535,7 +1603,7 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
           // write back: settled and shortened pointers alike (literal and out-of-chunk
           // slots keep pointing at themselves)
           reinterpret_cast<uint4 *>(p16)[h] =
-              make_uint4(c[0] | c[1] << 16, c[2] | c[3] << 16, c[4] | c[5] << 16, c[6] | c[7] << 16);
+              pack8_u16(c);
         }
         uint32_t w[2];
 #pragma unroll
@@ -1636,10 +1704,10 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
   }
 #ifdef SBH_LZ_PROBE
   if (lane == 0 && b < 2)
-    printf("lz blk %llu wave %u ntok %u cyc %llu pre %llu writes %llu init+bar %llu chase %llu resolve+bar %llu fallback %u chase_rounds %u\n",
+    printf("lz blk %llu wave %u ntok %u cyc %llu pre %llu marks %llu marks+slots %llu init+bar %llu chase %llu resolve+bar %llu fallback %u chase_rounds %u long %u\n",
            (unsigned long long)b, t / WAVE, n, (unsigned long long)(__builtin_readcyclecounter() - tp0),
-           (unsigned long long)t_pre, (unsigned long long)t_w, (unsigned long long)t_init,
-           (unsigned long long)t_ch, (unsigned long long)t_rounds, nrounds, njumps);
+           (unsigned long long)t_pre, (unsigned long long)t_mk, (unsigned long long)t_w, (unsigned long long)t_init,
+           (unsigned long long)t_ch, (unsigned long long)t_rounds, nrounds, njumps, nlong);
 #endif
   const uint32_t usize = base;
   // write the image: 16-byte granules aligned to the flat address
