@@ -15,7 +15,8 @@ namespace {
 
 constexpr int SCAN_T = 256;       // threads per workgroup
 constexpr int SCAN_PER = 8;       // elements per thread in the scans
-constexpr uint64_t CHUNK = 4096;  // bytes per candidate-count workgroup (256 x 16)
+constexpr uint64_t CHUNK = 16384;  // bytes per candidate-scan workgroup (256 x 4 x 16)
+static_assert(CHUNK % 4096 == 0 && CHUNK / 256 <= 64, "chunk layout");
 
 __device__ __forceinline__ bool header_at(const uint8_t *c, uint64_t p) {
   // gzip magic 31 139 8 4 and 'B' 'C' 2 (Header.scala:61-75; byte 15 unchecked)
@@ -96,32 +97,88 @@ __global__ void k_find_block_start(const uint8_t *comp, uint64_t n, uint64_t sta
 }
 
 // ---------------------------------------------------------------- candidate scan
-__global__ __launch_bounds__(256) void k_cand_count(const uint8_t *comp, uint64_t n, uint64_t from,
-                                                     uint64_t *counts) {
-  __shared__ uint32_t c;
-  if (threadIdx.x == 0) c = 0;
-  __syncthreads();
-  const uint64_t p0 = (uint64_t)blockIdx.x * CHUNK + threadIdx.x * 16;
-  uint32_t mine = 0;
-  for (uint32_t k = 0; k < 16; ++k) {
-    const uint64_t p = p0 + k;
-    if (p >= from && p + 18 <= n && comp[p] == 31 && header_at(comp, p)) ++mine;
-  }
-  if (mine) atomicAdd(&c, mine);
-  __syncthreads();
-  if (threadIdx.x == 0) counts[blockIdx.x] = c;
+// Pass 1 streams every byte once with coalesced 16 B loads (lane t of segment i reads
+// chunk + i*4096 + 16t) and finds the bytes equal to 31 with a SWAR zero-byte test;
+// only those get the full header check.  Per chunk it records the candidate count and
+// the first candidate's offset.  Pass 2 then needs the bytes again only for the rare
+// chunks holding two or more candidates (blocks are ~20-65 KB apart).
+
+// Bytes of w equal to 31, as bit 7 of each byte (may over-report above a true hit;
+// every reported byte is re-checked exactly).
+__device__ __forceinline__ uint32_t bytes_eq31(uint32_t w) {
+  const uint32_t x = w ^ 0x1f1f1f1fu;
+  return (x - 0x01010101u) & ~x & 0x80808080u;
 }
 
-__global__ __launch_bounds__(256) void k_cand_write(const uint8_t *comp, uint64_t n, uint64_t from,
-                                                     const uint64_t *offs, uint64_t *cand) {
-  __shared__ uint32_t pre[256];
-  const uint64_t p0 = (uint64_t)blockIdx.x * CHUNK + threadIdx.x * 16;
-  uint32_t mask = 0;
-  for (uint32_t k = 0; k < 16; ++k) {
-    const uint64_t p = p0 + k;
-    if (p >= from && p + 18 <= n && comp[p] == 31 && header_at(comp, p)) mask |= 1u << k;
+__device__ __forceinline__ bool cand_at(const uint8_t *comp, uint64_t n, uint64_t from, uint64_t p) {
+  return p >= from && p + 18 <= n && header_at(comp, p);
+}
+
+__global__ __launch_bounds__(256) void k_cand_count(const uint8_t *comp, uint64_t n, uint64_t from,
+                                                     uint64_t *counts, uint32_t *first) {
+  __shared__ uint32_t c, f;
+  if (threadIdx.x == 0) { c = 0; f = ~0u; }
+  __syncthreads();
+  const uint64_t cbase = (uint64_t)blockIdx.x * CHUNK;
+  uint32_t mine = 0, myfirst = ~0u;
+#pragma unroll
+  for (uint32_t i = 0; i < CHUNK / 4096; ++i) {
+    const uint32_t o0 = i * 4096 + threadIdx.x * 16;
+    const uint64_t p0 = cbase + o0;
+    uint4 v;
+    if (p0 + 16 <= n) {
+      v = *reinterpret_cast<const uint4 *>(comp + p0);
+    } else {  // ragged end of the shard
+      uint32_t w[4] = {0, 0, 0, 0};
+      for (uint32_t k = 0; k < 16 && p0 + k < n; ++k) w[k >> 2] |= (uint32_t)comp[p0 + k] << (8 * (k & 3));
+      v = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    const uint32_t m[4] = {bytes_eq31(v.x), bytes_eq31(v.y), bytes_eq31(v.z), bytes_eq31(v.w)};
+    if (m[0] | m[1] | m[2] | m[3]) {
+      for (uint32_t q = 0; q < 4; ++q) {
+        uint32_t mq = m[q];
+        while (mq) {
+          const uint32_t k = 4 * q + (__builtin_ctz(mq) >> 3);
+          mq &= mq - 1;
+          if (cand_at(comp, n, from, p0 + k)) {
+            ++mine;
+            myfirst = min(myfirst, o0 + k);
+          }
+        }
+      }
+    }
   }
-  pre[threadIdx.x] = __popc(mask);
+  if (mine) {
+    atomicAdd(&c, mine);
+    atomicMin(&f, myfirst);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    counts[blockIdx.x] = c;
+    first[blockIdx.x] = f;
+  }
+}
+
+// Pass 2: chunk candidates in position order; only multi-candidate chunks rescan (each
+// thread a contiguous CHUNK/256 bytes).
+__global__ __launch_bounds__(256) void k_cand_write(const uint8_t *comp, uint64_t n, uint64_t from,
+                                                     const uint64_t *counts, const uint32_t *first,
+                                                     const uint64_t *offs, uint64_t *cand) {
+  const uint64_t cnt = counts[blockIdx.x];
+  if (cnt == 0) return;
+  const uint64_t cbase = (uint64_t)blockIdx.x * CHUNK;
+  if (cnt == 1) {
+    if (threadIdx.x == 0) cand[offs[blockIdx.x]] = cbase + first[blockIdx.x];
+    return;
+  }
+  constexpr uint32_t PER = CHUNK / 256;
+  __shared__ uint32_t pre[256];
+  const uint64_t p0 = cbase + (uint64_t)threadIdx.x * PER;
+  uint64_t mask = 0;
+  for (uint32_t k = 0; k < PER; ++k)
+    if (comp[p0 + k < n ? p0 + k : 0] == 31 && cand_at(comp, n, from, p0 + k)) mask |= 1ull << k;
+  const uint32_t mc = (uint32_t)__popcll(mask);
+  pre[threadIdx.x] = mc;
   __syncthreads();
   for (int off = 1; off < 256; off <<= 1) {
     uint32_t x = threadIdx.x >= (unsigned)off ? pre[threadIdx.x - off] : 0;
@@ -129,9 +186,11 @@ __global__ __launch_bounds__(256) void k_cand_write(const uint8_t *comp, uint64_
     pre[threadIdx.x] += x;
     __syncthreads();
   }
-  uint64_t o = offs[blockIdx.x] + pre[threadIdx.x] - __popc(mask);
-  for (uint32_t k = 0; k < 16; ++k)
-    if (mask & (1u << k)) cand[o++] = p0 + k;
+  uint64_t o = offs[blockIdx.x] + pre[threadIdx.x] - mc;
+  while (mask) {
+    cand[o++] = p0 + __builtin_ctzll(mask);
+    mask &= mask - 1;
+  }
 }
 
 constexpr int64_t TERM_END = -2;     // chain reaches the end of the resident bytes exactly
@@ -254,14 +313,18 @@ hipError_t launch_find_block_start(const uint8_t *comp, uint64_t n, uint64_t sta
   return hipGetLastError();
 }
 
-hipError_t launch_cand_count(const uint8_t *comp, uint64_t n, uint64_t from, uint64_t *counts,
+uint64_t cand_chunks(uint64_t n) { return (n + CHUNK - 1) / CHUNK; }
+
+hipError_t launch_cand_count(const uint8_t *comp, uint64_t n, uint64_t from, uint64_t *counts, uint32_t *first,
                              uint64_t nchunks, hipStream_t st) {
-  hipLaunchKernelGGL(k_cand_count, dim3((uint32_t)nchunks), dim3(256), 0, st, comp, n, from, counts);
+  hipLaunchKernelGGL(k_cand_count, dim3((uint32_t)nchunks), dim3(256), 0, st, comp, n, from, counts, first);
   return hipGetLastError();
 }
-hipError_t launch_cand_write(const uint8_t *comp, uint64_t n, uint64_t from, const uint64_t *offs,
-                             uint64_t *cand, uint64_t nchunks, hipStream_t st) {
-  hipLaunchKernelGGL(k_cand_write, dim3((uint32_t)nchunks), dim3(256), 0, st, comp, n, from, offs, cand);
+hipError_t launch_cand_write(const uint8_t *comp, uint64_t n, uint64_t from, const uint64_t *counts,
+                             const uint32_t *first, const uint64_t *offs, uint64_t *cand, uint64_t nchunks,
+                             hipStream_t st) {
+  hipLaunchKernelGGL(k_cand_write, dim3((uint32_t)nchunks), dim3(256), 0, st, comp, n, from, counts, first,
+                     offs, cand);
   return hipGetLastError();
 }
 

@@ -16,10 +16,12 @@ uint64_t scan_tmp_words(uint64_t n);
 hipError_t scan_exclusive_u64(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *tmp, hipStream_t st);
 hipError_t launch_find_block_start(const uint8_t *comp, uint64_t n, uint64_t start, int32_t k, int at_eof,
                                    unsigned long long *best, hipStream_t st);
-hipError_t launch_cand_count(const uint8_t *comp, uint64_t n, uint64_t from, uint64_t *counts, uint64_t nchunks,
-                             hipStream_t st);
-hipError_t launch_cand_write(const uint8_t *comp, uint64_t n, uint64_t from, const uint64_t *offs, uint64_t *cand,
+uint64_t cand_chunks(uint64_t n);
+hipError_t launch_cand_count(const uint8_t *comp, uint64_t n, uint64_t from, uint64_t *counts, uint32_t *first,
                              uint64_t nchunks, hipStream_t st);
+hipError_t launch_cand_write(const uint8_t *comp, uint64_t n, uint64_t from, const uint64_t *counts,
+                             const uint32_t *first, const uint64_t *offs, uint64_t *cand, uint64_t nchunks,
+                             hipStream_t st);
 hipError_t build_chain(const uint8_t *comp, uint64_t n, const uint64_t *cand, uint64_t nc, int64_t *J0, int64_t *J1,
                        uint8_t *on, uint64_t *v, uint64_t *rank, uint64_t *tmp, DevBlocks bl, uint64_t *usz,
                        uint64_t *nchain, hipStream_t st);
@@ -90,6 +92,7 @@ struct sbh_shard {
   DBuf<uint64_t> b_cstart, b_ustart, usz;
   DBuf<uint32_t> b_csize, b_hsize, b_usize, b_flags, b_status, b_ntok;
   DBuf<uint64_t> counts, offs, cand, v, rank, tmp;
+  DBuf<uint32_t> cfirst;  // per scan chunk: offset of its first candidate
   DBuf<int64_t> J0, J1;
   DBuf<uint8_t> on;
   std::vector<sbh_block> hb;
@@ -254,7 +257,7 @@ int sbh_shard_destroy(sbh_shard *sh) {
   sh->b_status.release();
   sh->b_ntok.release();
   sh->tok.release();
-  sh->counts.release(); sh->offs.release(); sh->cand.release(); sh->v.release(); sh->rank.release();
+  sh->counts.release(); sh->cfirst.release(); sh->offs.release(); sh->cand.release(); sh->v.release(); sh->rank.release();
   sh->tmp.release(); sh->J0.release(); sh->J1.release(); sh->on.release(); sh->d_seg.release();
   sh->U.release(); sh->ctg.release(); sh->bits.release(); sh->words.release(); sh->close_pos.release();
   sh->close_word.release(); sh->ctr.release();
@@ -313,13 +316,14 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
     if (sbh_header_make(h18, 18, nullptr, nullptr) != SBH_OK)
       return fail(ctx, SBH_E_HEADER_PARSE, "no BGZF header at %llu", (unsigned long long)start);
   }
-  const uint64_t nchunks = (n + 4095) / 4096;
+  const uint64_t nchunks = cand_chunks(n);
   uint64_t nc = 0;
   if (nchunks && rel + 18 <= n) {
     HIPCHK(ctx, sh->counts.ensure(nchunks));
+    HIPCHK(ctx, sh->cfirst.ensure(nchunks));
     HIPCHK(ctx, sh->offs.ensure(nchunks));
     HIPCHK(ctx, sh->tmp.ensure(scan_tmp_words(nchunks) + scan_tmp_words(1 << 24)));
-    HIPCHK(ctx, launch_cand_count(sh->comp.p, n, rel, sh->counts.p, nchunks, st));
+    HIPCHK(ctx, launch_cand_count(sh->comp.p, n, rel, sh->counts.p, sh->cfirst.p, nchunks, st));
     HIPCHK(ctx, scan_exclusive_u64(sh->counts.p, sh->offs.p, nchunks, sh->tmp.p, st));
     HIPCHK(ctx, hipMemcpyAsync(&sh->h_ctr[0], sh->offs.p + nchunks - 1, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipMemcpyAsync(&sh->h_ctr[1], sh->counts.p + nchunks - 1, 8, hipMemcpyDeviceToHost, st));
@@ -335,7 +339,7 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
     HIPCHK(ctx, sh->v.ensure(nc));
     HIPCHK(ctx, sh->rank.ensure(nc));
     HIPCHK(ctx, sh->tmp.ensure(scan_tmp_words(nc) + scan_tmp_words(nchunks)));
-    HIPCHK(ctx, launch_cand_write(sh->comp.p, n, rel, sh->offs.p, sh->cand.p, nchunks, st));
+    HIPCHK(ctx, launch_cand_write(sh->comp.p, n, rel, sh->counts.p, sh->cfirst.p, sh->offs.p, sh->cand.p, nchunks, st));
     HIPCHK(ctx, sh->b_cstart.ensure(nc));
     HIPCHK(ctx, sh->b_ustart.ensure(nc));
     HIPCHK(ctx, sh->usz.ensure(nc));
