@@ -599,16 +599,36 @@ __global__ __launch_bounds__(T) void k_full(const uint8_t *__restrict__ U, uint6
 
 // ---------------------------------------------------------------- bitmap utilities
 // First set bit at or after `from` and before `to` (positions; bit i <-> begin + i).
-__global__ void k_first_set(const uint32_t *bits, uint64_t begin, uint64_t from, uint64_t to,
-                            unsigned long long *best) {
-  const uint64_t w = (from - begin) / 32 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t w_end = (to - begin + 31) / 32;
-  if (w >= w_end) return;
-  uint32_t v = bits[w];
-  const uint64_t p0 = begin + 32 * w;
-  if (p0 < from) v &= ~0u << (uint32_t)(from - p0);
-  if (p0 + 32 > to) v &= (to - p0) >= 32 ? ~0u : ((1u << (uint32_t)(to - p0)) - 1u);
-  if (v) atomicMin(best, (unsigned long long)(p0 + __builtin_ctz(v)));
+// A persistent grid walks FS_SPAN-word chunks in order (chunk i by workgroup i mod grid)
+// and stops as soon as a hit before its next chunk is known: records start every few
+// hundred bytes, so the search normally ends within the first round of chunks.
+constexpr uint32_t FS_SPAN = 1024;  // words per chunk (4 per thread)
+__global__ __launch_bounds__(256) void k_first_set(const uint32_t *bits, uint64_t begin, uint64_t from,
+                                                   uint64_t to, unsigned long long *best) {
+  const uint64_t w0 = (from - begin) / 32, w_end = (to - begin + 31) / 32;
+  for (uint64_t c = blockIdx.x;; c += gridDim.x) {
+    const uint64_t cw = w0 + c * FS_SPAN;
+    if (cw >= w_end) return;
+    if (__hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < begin + 32 * cw) return;
+    const uint64_t w = cw + 4 * threadIdx.x;
+    uint32_t v[4];
+    if (w + 4 <= w_end && (w & 3) == 0) {
+      const uint4 q = *reinterpret_cast<const uint4 *>(bits + w);
+      v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+    } else {
+      for (uint32_t k = 0; k < 4; ++k) v[k] = w + k < w_end ? bits[w + k] : 0u;
+    }
+    for (uint32_t k = 0; k < 4; ++k) {
+      uint32_t x = v[k];
+      const uint64_t p0 = begin + 32 * (w + k);
+      if (p0 < from) x &= ~0u << (uint32_t)(from - p0);
+      if (p0 + 32 > to) x &= (to - p0) >= 32 ? ~0u : ((1u << (uint32_t)(to - p0)) - 1u);
+      if (x) {
+        atomicMin(best, (unsigned long long)(p0 + __builtin_ctz(x)));
+        break;
+      }
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void k_popcount(const uint32_t *bits, uint64_t begin, uint64_t from,
@@ -639,27 +659,43 @@ __global__ __launch_bounds__(256) void k_popcount(const uint32_t *bits, uint64_t
 // to the next true one (or leave [from, E) / reach the stream end).  Any other
 // step is an anomaly (a false positive inside the chain, or a chain record the
 // eager checker rejects); those ranges fall back to an exact sequential walk.
-__global__ void k_verify_chain(const uint8_t *U, const uint32_t *bits, uint64_t begin, uint64_t bits_end,
-                               uint64_t from, uint64_t E, uint64_t total, unsigned long long *n_anom,
-                               unsigned long long *first_anom) {
-  const uint64_t w = (from - begin) / 32 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void k_verify_chain(const uint8_t *U, const uint32_t *bits, uint64_t begin,
+                                                       uint64_t bits_end, uint64_t from, uint64_t E, uint64_t total,
+                                                       unsigned long long *n_anom, unsigned long long *first_anom) {
+  const uint64_t w = ((from - begin) / 32 & ~3ull) + 4 * ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x);
   const uint64_t w_end = (E - begin + 31) / 32;
   if (w >= w_end) return;
-  uint32_t v = bits[w];
-  const uint64_t p0 = begin + 32 * w;
-  if (p0 < from) v &= ~0u << (uint32_t)(from - p0);
-  if (p0 + 32 > E) v &= (E - p0) >= 32 ? ~0u : ((1u << (uint32_t)(E - p0)) - 1u);
   const uint64_t w_lim = (bits_end - begin + 31) / 32;
-  while (v) {
-    const uint32_t b = __builtin_ctz(v);
-    v &= v - 1;
-    const uint64_t s = p0 + b;
-    // next set bit after s (bounded by E)
+  uint32_t v[4];
+  if (w + 4 <= w_lim) {
+    const uint4 q = *reinterpret_cast<const uint4 *>(bits + w);
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  } else {
+    for (uint32_t k = 0; k < 4; ++k) v[k] = w + k < w_lim ? bits[w + k] : 0u;
+  }
+  for (uint32_t k = 0; k < 4; ++k) {  // positions outside [from, E)
+    const uint64_t p0 = begin + 32 * (w + k);
+    if (p0 + 32 <= from || p0 >= E) v[k] = 0;
+    else {
+      if (p0 < from) v[k] &= ~0u << (uint32_t)(from - p0);
+      if (p0 + 32 > E) v[k] &= (E - p0) >= 32 ? ~0u : ((1u << (uint32_t)(E - p0)) - 1u);
+    }
+  }
+  // walk the set bits of the 128-position group in order; each one's successor is the
+  // next set bit (in the group, else the first set word after it, bounded by E)
+  uint32_t k = 0;
+  while (k < 4 && !v[k]) ++k;
+  while (k < 4) {
+    const uint32_t b = __builtin_ctz(v[k]);
+    v[k] &= v[k] - 1;
+    const uint64_t s = begin + 32 * (w + k) + b;
+    uint32_t kn = k;
+    while (kn < 4 && !v[kn]) ++kn;
     uint64_t nxt_set = ~0ull;
-    if (v) {
-      nxt_set = p0 + __builtin_ctz(v);
+    if (kn < 4) {
+      nxt_set = begin + 32 * (w + kn) + __builtin_ctz(v[kn]);
     } else {
-      for (uint64_t ww = w + 1; ww < w_lim && begin + 32 * ww < E; ++ww) {
+      for (uint64_t ww = w + 4; ww < w_lim && begin + 32 * ww < E; ++ww) {
         const uint32_t x = bits[ww];
         if (x) { nxt_set = begin + 32 * ww + __builtin_ctz(x); break; }
       }
@@ -680,6 +716,7 @@ __global__ void k_verify_chain(const uint8_t *U, const uint32_t *bits, uint64_t 
       atomicAdd(n_anom, 1ull);
       atomicMin(first_anom, (unsigned long long)s);
     }
+    k = kn;
   }
 }
 
@@ -783,7 +820,8 @@ hipError_t launch_first_set(const uint32_t *bits, uint64_t begin, uint64_t from,
                             unsigned long long *best, hipStream_t st) {
   if (to <= from) return hipSuccess;
   const uint64_t nw = (to - begin + 31) / 32 - (from - begin) / 32;
-  hipLaunchKernelGGL(k_first_set, dim3(ngrid(nw, 256)), dim3(256), 0, st, bits, begin, from, to, best);
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(ngrid(nw, FS_SPAN), 1024);
+  hipLaunchKernelGGL(k_first_set, dim3(grid), dim3(256), 0, st, bits, begin, from, to, best);
   return hipGetLastError();
 }
 
@@ -800,8 +838,8 @@ hipError_t launch_verify_chain(const uint8_t *U, const uint32_t *bits, uint64_t 
                                uint64_t from, uint64_t E, uint64_t total, unsigned long long *n_anom,
                                unsigned long long *first_anom, hipStream_t st) {
   if (E <= from) return hipSuccess;
-  const uint64_t nw = (E - begin + 31) / 32 - (from - begin) / 32;
-  hipLaunchKernelGGL(k_verify_chain, dim3(ngrid(nw, 256)), dim3(256), 0, st, U, bits, begin, bits_end, from,
+  const uint64_t nw = (E - begin + 31) / 32 - ((from - begin) / 32 & ~3ull);
+  hipLaunchKernelGGL(k_verify_chain, dim3(ngrid(nw, 1024)), dim3(256), 0, st, U, bits, begin, bits_end, from,
                      E, total, n_anom, first_anom);
   return hipGetLastError();
 }
