@@ -43,7 +43,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", type=float, default=None,
-                    help="HBM bytes per inflate launch from a separate rocprofv3 --pmc pass (profiles/)")
+                    help="HBM bytes per launch of the dominant kernel (default: the committed "
+                         "rocprofv3 --pmc summary, profiles/*_pmc_traffic.json)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -147,6 +148,16 @@ def main():
     alg_bytes, dom_ms, dom_units = kern[dom]
     achieved = alg_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
 
+    traffic, traffic_src = args.traffic, "--traffic" if args.traffic is not None else None
+    if traffic is None:
+        import glob
+        files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+        if files:
+            with open(files[-1]) as fh:
+                kt = json.load(fh)["kernels"].get(dom)
+            if kt:
+                traffic, traffic_src = kt["hbm_bytes"], os.path.relpath(files[-1], ROOT)
+
     def gbps(nbytes, ms):
         return round(nbytes / (ms * 1e-3) / 1e9, 2) if ms > 0 else None
 
@@ -194,7 +205,9 @@ def main():
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 5),
-                "traffic": args.traffic,
+                "traffic": traffic,
+                "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                "traffic_source": traffic_src,
                 "alg_bytes_per_step": int(alg_bytes),
                 "alg_units": dom_units,
                 "limiter": "latency: LDS round trips of the per-lane Huffman chains (k_huff) and barrier-separated "
