@@ -10,19 +10,18 @@
 // reported.  No CRC is checked (the reference does not check it either).
 //
 // Design (MI355X-first):
-//  * k_huff -- the serial part.  One 64-lane wave per BGZF block runs a wave-uniform
-//    Huffman decoder: bit buffer, counters and symbol state in SGPRs, compressed bytes
-//    pulled in with scalar loads, decode tables in LDS (~6 KiB per wave, so many waves
-//    per SIMD hide the LDS/scalar-load latency of the serial symbol chain).  It emits
-//    LZ77 tokens (one u32 per literal or match, batched in a VGPR and stored 64 at a
-//    time) and does all of zlib's validation, so it alone decides the block status.
-//    It needs no window: a match is only checked against the bytes produced so far.
-//  * k_lz -- the parallel part.  One 256-thread workgroup per block resolves the
-//    tokens into a 64 KiB LDS image of the block: a prefix sum gives every token its
-//    output offset, literals land at once, and matches are resolved in rounds -- a
-//    match copies as soon as its source lies below the lowest unresolved output
-//    offset.  The image is then written to HBM with 16-byte stores aligned to the flat
-//    address (block images start at arbitrary flat offsets).
+//  * k_huff -- Huffman decode to LZ77 tokens.  One 256-lane workgroup per BGZF block
+//    stages the deflate bytes in LDS and decodes lane-parallel: each lane takes a slice
+//    of the bits, decodes speculatively (Huffman/DEFLATE self-synchronises), repairs
+//    from its left neighbour's exit until no exit changes, and after two prefix sums
+//    emits its tokens (see "Lane-parallel Huffman decode" below).  Anything it cannot
+//    prove well-formed goes to k_huff_serial, the exact one-wave zlib-semantics decoder
+//    (stored blocks, errors, short/long streams), so block status always equals zlib's.
+//  * k_lz -- LZ77 resolution.  One 512-thread workgroup per block builds the block's
+//    64 KiB image in LDS, 1024 tokens per chunk: token starts are marked (one slot
+//    value + one start bit each), a divergence-free slot pass gives every byte the
+//    position it copies from, and barrier-free pointer chasing settles them; the image
+//    goes to HBM with 16-byte stores aligned to the flat address.
 //  * Token buffer: tokens of block b live at tok[ustart_b ...]; a block has at most
 //    usize tokens (every token yields >= 1 byte), so the buffer is 4 B per flat byte.
 #include "sbh_internal.h"
