@@ -102,6 +102,19 @@ __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t l) {
   return __builtin_amdgcn_readlane(v, l);
 }
 
+// Inclusive prefix sum over the 64 lanes of a wave in DPP steps (no LDS round trips):
+// row_shr 1/2/4/8 within each 16-lane row, then row_bcast:15 and row_bcast:31 carry
+// the row totals across rows (gfx9 DPP).  Inactive lanes must contribute 0.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return x;
+}
+
 __device__ __forceinline__ uint32_t lit_entry(uint32_t sym, uint32_t L) {
   if (sym < 256) return L | (K_LIT << 5) | (sym << 8);
   if (sym == 256) return L | (K_EOB << 5);
@@ -309,6 +322,7 @@ __device__ __forceinline__ uint32_t build_ptable(WaveSmem &sm, const uint8_t *le
     }
   }
   __builtin_amdgcn_wave_barrier();
+#pragma unroll 4
   for (uint32_t i = lane; i < n_ent; i += WAVE) {
     const uint32_t c15 = (__builtin_bitreverse32(i) >> (32 - fast)) << (15 - fast);
     uint32_t len = 1;
@@ -858,12 +872,7 @@ __global__ __launch_bounds__(WAVES *WAVE) void k_huff_serial(const uint8_t *__re
 template <uint32_t NT>
 __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t *wsum, uint32_t *total) {
   const uint32_t lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
-  uint32_t x = v;
-#pragma unroll
-  for (uint32_t d = 1; d < WAVE; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d, WAVE);
-    if (lane >= d) x += y;
-  }
+  const uint32_t x = wave_incl_scan(v);
   if (lane == WAVE - 1) wsum[w] = x;
   __syncthreads();
   uint32_t before = 0, all = 0;
@@ -1114,12 +1123,7 @@ __device__ __forceinline__ bool par_header(HuffSmem &sm, Src<LDS> src, uint32_t 
       const bool mine = (M >> lane) & 1;
       uint32_t ex;  // exclusive prefix of rep over the window's symbols
       {
-        uint32_t x = mine ? rep : 0;
-#pragma unroll
-        for (uint32_t d = 1; d < WAVE; d <<= 1) {
-          const uint32_t y = __shfl_up(x, d, WAVE);
-          if (lane >= d) x += y;
-        }
+        const uint32_t x = wave_incl_scan(mine ? rep : 0);
         ex = x - (mine ? rep : 0);
       }
       const uint32_t start = i0 + ex;
@@ -1130,10 +1134,19 @@ __device__ __forceinline__ bool par_header(HuffSmem &sm, Src<LDS> src, uint32_t 
       const uint32_t from = __shfl(own, src_lane, WAVE);
       const uint32_t val = sym == 16 ? (lowN ? from : prev) : own;
       if (M & 1 && __builtin_amdgcn_readfirstlane(sym) == 16 && i0 == 0) ok = false;  // repeat with no previous length
-      if (mine) {
-        for (uint32_t k = 0; k < rep; ++k) {
-          const uint32_t j = start + k;
-          if (j < total) t.lens[j < nlen ? j : 288 + j - nlen] = (uint8_t)val;
+      if (mine) {  // the run [start, start + rep) of lengths; lens[] puts distances at 288
+        const uint32_t e = min(start + rep, total);
+        const uint32_t v4 = val * 0x01010101u;
+        for (uint32_t j = start; j < e;) {
+          const uint32_t d = j < nlen ? j : 288 + j - nlen;
+          const uint32_t seg_end = j < nlen ? min(e, nlen) : e;  // don't cross the lit/dist split
+          if ((d & 3) == 0 && j + 4 <= seg_end) {
+            *reinterpret_cast<uint32_t *>(&t.lens[d]) = v4;
+            j += 4;
+          } else {
+            t.lens[d] = (uint8_t)val;
+            ++j;
+          }
         }
       }
       const uint32_t top = 63 - (uint32_t)__builtin_clzll(M);
@@ -1159,7 +1172,7 @@ __device__ __forceinline__ bool par_header(HuffSmem &sm, Src<LDS> src, uint32_t 
   else if (wid == 1) rc = build_ptable(t, t.lens + 288, ndist, 1, t.dist, PDIST_FAST, lane);
 #ifdef SBH_HUFF_PROBE
   const bool res = !__syncthreads_or(rc == 1);
-  if (threadIdx.x == 0 && blockIdx.x < 3)
+  if (threadIdx.x == 0 && blockIdx.x >= 5000 && blockIdx.x < 5003)
     printf("hdr blk %u cl %llu walk %llu build %llu\n", blockIdx.x, (unsigned long long)(h1 - h0),
            (unsigned long long)(h2 - h1), (unsigned long long)(__builtin_readcyclecounter() - h2));
   return res;
@@ -1235,7 +1248,7 @@ __device__ __forceinline__ bool inflate_par(HuffSmem &sm, const uint8_t *__restr
     ttot = uni(ttot);
     otot = uni(otot);
 #ifdef SBH_HUFF_PROBE
-    if (tid == 0 && blockIdx.x < 6)
+    if (tid == 0 && blockIdx.x >= 5000 && blockIdx.x < 5004)
       printf("huff blk %u S %u rounds %u k %u ttot %u otot %u last %u hdr %llu p1 %llu p2 %llu\n",
              blockIdx.x, S, nrounds, k, ttot, otot, last, (unsigned long long)(tph - tp0),
              (unsigned long long)(tp1 - tph), (unsigned long long)(__builtin_readcyclecounter() - tp1));
@@ -1247,7 +1260,7 @@ __device__ __forceinline__ bool inflate_par(HuffSmem &sm, const uint8_t *__restr
     if (tid <= k) lane_run<LDS, RUN_EMIT>(sm.t, src, A, stop, limit, ck, none, tk + ntok + tpre, out + opre, bad);
     if (__syncthreads_or(bad)) return false;
 #ifdef SBH_HUFF_PROBE
-    if (tid == 0 && blockIdx.x < 6) printf("huff blk %u p3 %llu\n", blockIdx.x, (unsigned long long)(__builtin_readcyclecounter() - tp3));
+    if (tid == 0 && blockIdx.x >= 5000 && blockIdx.x < 5004) printf("huff blk %u p3 %llu\n", blockIdx.x, (unsigned long long)(__builtin_readcyclecounter() - tp3));
 #endif
     ntok += ttot;
     out += otot;
@@ -1322,29 +1335,6 @@ struct LzSmem {
 // two workgroups per CU, counting the 256 B of LDS the compiler adds
 static_assert(sizeof(LzSmem) * 2 + 512 <= 160 * 1024, "two k_lz workgroups per CU");
 static_assert(sizeof(LzSmem::fb) <= offsetof(decltype(LzSmem::pp), wsum), "the rounds path keeps wsum");
-
-// Block-wide exclusive prefix max over NT threads (0 for thread 0).
-template <uint32_t NT>
-__device__ __forceinline__ uint32_t block_scan_max(uint32_t v, uint32_t *wsum) {
-  const uint32_t lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
-  uint32_t x = v;
-#pragma unroll
-  for (uint32_t d = 1; d < WAVE; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d, WAVE);
-    if (lane >= d) x = x > y ? x : y;
-  }
-  const uint32_t ex_w = __shfl_up(x, 1, WAVE);
-  if (lane == WAVE - 1) wsum[w] = x;
-  __syncthreads();
-  uint32_t before = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < NT / WAVE; ++k) {
-    const uint32_t s = wsum[k];
-    before = (k < w && s > before) ? s : before;
-  }
-  const uint32_t in_w = lane ? ex_w : 0;
-  return before > in_w ? before : in_w;
-}
 
 // k mod d for k < 2^17, d >= 1 (one reciprocal, one correction).
 __device__ __forceinline__ uint32_t mod_small(uint32_t k, uint32_t d) {
