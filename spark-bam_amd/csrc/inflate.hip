@@ -1004,6 +1004,7 @@ __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, Src<LDS> src, uin
   uint32_t ml = 0;  // pending match length: the next code is a distance
   uint32_t ntok = 0, nout = 0;
   uint32_t c1p = NOPOS, c1o = 0, c2p = NOPOS, c2o = 0;
+  uint32_t ck_next = CK1;  // RUN_SPEC: token count of the next checkpoint
   uint32_t e;
   bool cut;
   for (;;) {
@@ -1011,12 +1012,16 @@ __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, Src<LDS> src, uin
     const bool atb = ml == 0;  // token boundary
     e = t.tab[(bits & ((1u << LIT_FAST) - 1)) | (atb ? 0u : 1u << LIT_FAST)];
     if (e & PE_SLOW) e = slow_lane(t, bits, !atb);
-    if (MODE == RUN_SPEC) {
-      const bool h1 = atb && ntok == CK1, h2 = atb && ntok == CK2;
-      c1p = h1 ? pos : c1p;
-      c1o = h1 ? nout : c1o;
-      c2p = h2 ? pos : c2p;
-      c2o = h2 ? nout : c2o;
+    if (MODE == RUN_SPEC && atb && ntok == ck_next) {  // rare: a branch, not per-code selects
+      if (ck_next == CK1) {
+        c1p = pos;
+        c1o = nout;
+        ck_next = CK2;
+      } else {
+        c2p = pos;
+        c2o = nout;
+        ck_next = ~0u;
+      }
     }
     cut = atb && (pos >= stop2 || (MODE == RUN_REDO && (pos == ck.p1 || pos == ck.p2)));
     if (cut || (e & PE_SPECIAL)) break;
