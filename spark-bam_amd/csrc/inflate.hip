@@ -1321,6 +1321,8 @@ constexpr uint32_t LZ_CHUNK = LZ_THREADS * LZ_TPT;      // tokens per chunk
 constexpr uint32_t PTR_HALF = 8;                        // pointer slots per thread and pass
 constexpr uint32_t PTR_CAP = 7552;                      // chunk bytes resolved by pointer chasing
 constexpr uint32_t SB_WORDS = PTR_CAP / 32;             // token-start bitmap words
+constexpr uint32_t NHP = 2;                             // half granules (8 slots) per k_lz thread, at most
+static_assert(PTR_CAP <= NHP * LZ_THREADS * PTR_HALF, "slot pass covers the slots");
 
 struct LzSmem {
   uint8_t img[65536 + 16];  // block image, placed at (ustart & 15) so granules align with HBM
@@ -1505,35 +1507,53 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
 #endif
       __syncthreads();
       // slot pass: every byte's pointer from its token's start (at most LZ_SHORT - 1
-      // back, inside this 64-bit window of start bits): byte j of a match that starts at
-      // s and copies from v points at v + (j mod (s - v)); starts keep their value
-      for (uint32_t h = t; PTR_HALF * h < chunk_len + lead; h += LZ_THREADS) {
-        const uint32_t wi = h >> 2, g0 = abase + PTR_HALF * h;
-        const uint64_t W = (uint64_t)sbits[wi] << 32 | (wi ? sbits[wi - 1] : 0u);
-        uint32_t sidx[PTR_HALF], jj[PTR_HALF], v[PTR_HALF];
+      // slots back): byte j of a match that starts at slot s and copies from v points at
+      // v + j, or v + (j mod (s - v)) when the match overlaps itself (rare); a literal
+      // start points at itself.  Each thread owns up to NHP half granules (8 slots) and
+      // keeps their pointers in registers for the chase below.
+      const uint32_t nh = (chunk_len + lead + PTR_HALF - 1) / PTR_HALF;
+      uint32_t c[NHP][PTR_HALF], pend[NHP];
+#pragma unroll
+      for (uint32_t hh = 0; hh < NHP; ++hh) {
+        const uint32_t h = t + hh * LZ_THREADS;
+        pend[hh] = 0;
+        if (h >= nh) continue;
+        const uint32_t s0 = PTR_HALF * h, g0 = abase + s0;  // first slot, its position
+        const uint32_t wi = h >> 2, sh8 = (h & 3) * PTR_HALF;
+        const uint32_t cur = sbits[wi], prev = wi ? sbits[wi - 1] : 0u;
+        // the window's slots inside the chunk: [klo, khi)
+        const int32_t rlo = (int32_t)lead - (int32_t)s0, rhi = rlo + (int32_t)chunk_len;
+        const uint32_t klo = (uint32_t)min(max(rlo, 0), (int32_t)PTR_HALF);
+        const uint32_t khi = (uint32_t)min(max(rhi, 0), (int32_t)PTR_HALF);
+        // nearest start before the window, then walk the window's start bits
+        const uint32_t low = cur & ((1u << sh8) - 1u);
+        uint32_t st = low ? wi * 32 + 31 - __builtin_clz(low) : prev ? wi * 32 - 1 - __builtin_clz(prev) : s0;
+        const uint32_t wb = cur >> sh8;
+        uint32_t sidx[PTR_HALF], v[PTR_HALF];
 #pragma unroll
         for (uint32_t k = 0; k < PTR_HALF; ++k) {
-          const uint32_t pos = g0 + k, bit = 32 + ((PTR_HALF * h + k) & 31);
-          const bool in = pos >= base && pos < base + chunk_len;
-          const uint64_t m = W & (~0ull >> (63 - bit));
-          const uint32_t sb = 63 - (uint32_t)__builtin_clzll(m | 1);
-          sidx[k] = in ? wi * 32 + sb - 32 : PTR_HALF * h + k;
-          jj[k] = in ? bit - sb : 0;
+          st = (wb >> k) & 1u ? s0 + k : st;
+          sidx[k] = st;
         }
 #pragma unroll
         for (uint32_t k = 0; k < PTR_HALF; ++k) v[k] = p16[sidx[k]];
-        uint32_t c[PTR_HALF];
+        uint32_t ovl = 0;  // slots of overlapping matches
 #pragma unroll
         for (uint32_t k = 0; k < PTR_HALF; ++k) {
-          const uint32_t pos = g0 + k;
-          const bool in = pos >= base && pos < base + chunk_len;
-          const uint32_t dd = abase + sidx[k] - v[k];  // the match's distance
-          const uint32_t j = jj[k];
-          const uint32_t pj = v[k] + (j < dd ? j : mod_small(j, dd));
-          c[k] = !in ? pos : j == 0 ? v[k] : pj;
+          const uint32_t j = s0 + k - sidx[k], dd = abase + sidx[k] - v[k];
+          const bool in = k - klo < khi - klo;
+          ovl |= (in && j != 0 && j >= dd) ? 1u << k : 0u;
+          c[hh][k] = in ? v[k] + j : g0 + k;
         }
-        reinterpret_cast<uint4 *>(p16)[h] =
-            pack8_u16(c);
+        if (ovl) {
+#pragma unroll
+          for (uint32_t k = 0; k < PTR_HALF; ++k)
+            if ((ovl >> k) & 1u) c[hh][k] = v[k] + mod_small(s0 + k - sidx[k], abase + sidx[k] - v[k]);
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < PTR_HALF; ++k)  // in the chunk, not a literal, not final yet
+          pend[hh] |= (c[hh][k] != g0 + k && c[hh][k] >= base) ? 1u << k : 0u;
+        reinterpret_cast<uint4 *>(p16)[h] = pack8_u16(c[hh]);
       }
 #ifdef SBH_LZ_PROBE
       t_w += __builtin_readcyclecounter() - tb;
@@ -1543,67 +1563,54 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
       const uint64_t tc = __builtin_readcyclecounter();
       t_init += tc - tb;
 #endif
-      // chase the pointers of 8 consecutive slots together, one LDS round trip per
-      // round, writing shortened pointers back (other threads' chains pass through them);
-      // no barriers.  A pointer is final when it is before the chunk or names a literal
-      // (a slot pointing at itself).  Then gather the bytes and store them (8 per thread
-      // and pass, so that all waves share the work).
-      for (uint32_t h = t; PTR_HALF * h < chunk_len + lead; h += LZ_THREADS) {
-        const uint32_t g0 = abase + PTR_HALF * h;  // image position of the half granule
-        uint32_t c[PTR_HALF];
-        {
-          const uint4 a = reinterpret_cast<const uint4 *>(p16)[h];
-          c[0] = a.x & 0xffff; c[1] = a.x >> 16; c[2] = a.y & 0xffff; c[3] = a.y >> 16;
-          c[4] = a.z & 0xffff; c[5] = a.z >> 16; c[6] = a.w & 0xffff; c[7] = a.w >> 16;
-        }
-        uint32_t pend = 0;
+      // chase the pointers of each half granule together, one LDS round trip per round,
+      // writing shortened pointers back (other threads' chains pass through them); no
+      // barriers.  A pointer is final when it is before the chunk or names a literal (a
+      // slot pointing at itself).  Then gather the bytes and store them.
 #pragma unroll
-        for (uint32_t k = 0; k < PTR_HALF; ++k) {
-          const uint32_t pos = g0 + k;
-          const bool in = pos >= base && pos < base + chunk_len;
-          c[k] = in ? c[k] : pos;
-          pend |= (in && c[k] != pos && c[k] >= base) ? 1u << k : 0u;
-        }
+      for (uint32_t hh = 0; hh < NHP; ++hh) {
+        const uint32_t h = t + hh * LZ_THREADS;
+        if (h >= nh) continue;
+        const uint32_t g0 = abase + PTR_HALF * h;  // image position of the half granule
         // Plain loads: another thread may rewrite a slot concurrently, and either value
         // (u16 LDS accesses are single-copy atomic) is a valid pointer.  Rounds are
         // branch-free; settled slots reread their own final pointer's slot harmlessly.
 #ifdef SBH_LZ_DEBUG
         uint32_t guard = 0;
 #endif
-        while (__builtin_expect(pend != 0, 0)) {
+        while (__builtin_expect(pend[hh] != 0, 0)) {
 #ifdef SBH_LZ_DEBUG
           if (++guard > 300) {
             for (uint32_t k = 0; k < PTR_HALF; ++k)
-              if ((pend >> k) & 1)
+              if ((pend[hh] >> k) & 1)
                 printf("lz chase stuck blk %llu pos %u c %u base %u chunk_len %u lead %u\n", (unsigned long long)b,
-                       g0 + k, c[k], base, chunk_len, lead);
+                       g0 + k, c[hh][k], base, chunk_len, lead);
             break;
           }
 #endif
           uint32_t v[PTR_HALF];
 #pragma unroll
-          for (uint32_t k = 0; k < PTR_HALF; ++k) v[k] = p16[(c[k] >= base ? c[k] : base) - abase];
+          for (uint32_t k = 0; k < PTR_HALF; ++k) v[k] = p16[(c[hh][k] >= base ? c[hh][k] : base) - abase];
 #ifdef SBH_LZ_PROBE
           ++njumps;
 #endif
           uint32_t np = 0;
 #pragma unroll
           for (uint32_t k = 0; k < PTR_HALF; ++k) {
-            const bool go = ((pend >> k) & 1) && v[k] != c[k];
-            c[k] = go ? v[k] : c[k];
+            const bool go = ((pend[hh] >> k) & 1) && v[k] != c[hh][k];
+            c[hh][k] = go ? v[k] : c[hh][k];
             np |= (go && v[k] >= base) ? 1u << k : 0u;
           }
-          pend = np;
+          pend[hh] = np;
           // write back: settled and shortened pointers alike (literal and out-of-chunk
           // slots keep pointing at themselves)
-          reinterpret_cast<uint4 *>(p16)[h] =
-              pack8_u16(c);
+          reinterpret_cast<uint4 *>(p16)[h] = pack8_u16(c[hh]);
         }
         uint32_t w[2];
 #pragma unroll
         for (uint32_t q = 0; q < 2; ++q) {
-          w[q] = (uint32_t)img[c[4 * q]] | (uint32_t)img[c[4 * q + 1]] << 8 |
-                 (uint32_t)img[c[4 * q + 2]] << 16 | (uint32_t)img[c[4 * q + 3]] << 24;
+          w[q] = (uint32_t)img[c[hh][4 * q]] | (uint32_t)img[c[hh][4 * q + 1]] << 8 |
+                 (uint32_t)img[c[hh][4 * q + 2]] << 16 | (uint32_t)img[c[hh][4 * q + 3]] << 24;
         }
         *reinterpret_cast<uint2 *>(img + g0) = make_uint2(w[0], w[1]);
       }
