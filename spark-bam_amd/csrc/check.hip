@@ -307,9 +307,11 @@ __device__ __forceinline__ uint32_t one_record(const Src &s, uint64_t q, uint64_
 __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint64_t u_pad, uint64_t begin,
                                              uint64_t end, Segs sg, Ctg c, int32_t rtc, EagerOut o) {
   constexpr uint32_t NV = (ESTAGE + 32) / 16;
+  constexpr uint32_t NWV = T / WAVE, SEGCAP = EQ_CHUNK / NWV;
   __shared__ uint4 ldsv[NV];
   __shared__ uint32_t ok[EW / 32], nrm[EW / 32], und[EW / 32], res[ETILE / 32];
-  __shared__ uint32_t seg0, ntrue, nq;
+  __shared__ uint32_t lnk[EQ_CHUNK / 32], lfail[EQ_CHUNK / 32];  // per sorted candidate: LINK / FAIL step
+  __shared__ uint32_t seg0, ntrue, nq, wcnt[NWV];
   __shared__ uint64_t seg_end0;
   __shared__ uint16_t queue[EQ_CHUNK];
   const uint32_t *lds32 = reinterpret_cast<const uint32_t *>(ldsv);
@@ -322,6 +324,7 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
   stage_vec<NV>(ldsv, U, s0, u_pad);
   for (uint32_t i = threadIdx.x; i < EW / 32; i += T) { ok[i] = 0; nrm[i] = 0; und[i] = 0; }
   for (uint32_t i = threadIdx.x; i < ETILE / 32; i += T) res[i] = 0;
+  for (uint32_t i = threadIdx.x; i < EQ_CHUNK / 32; i += T) { lnk[i] = 0; lfail[i] = 0; }
   if (threadIdx.x == 0) {
     const uint32_t k = seg_first(sg, t0);
     seg0 = k;
@@ -337,16 +340,12 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
   const uint32_t fast_end = e0 - t0 >= 36 + (uint64_t)EW ? EW : e0 - t0 >= 36 ? (uint32_t)(e0 - t0 - 36) + 1 : 0;
   const uint32_t sa = (uint32_t)(t0 - s0);
   const uint32_t nref1 = (uint32_t)c.n + 1u;
+  const uint32_t lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
 #ifdef SBH_EPROBE
   const uint64_t c1 = __builtin_readcyclecounter();
+  uint64_t c1a = 0, c1b = 0, c2 = 0;
 #endif
-  // ---- phase A: every position of the window gets the fixed-field part of the
-  // single-record predicate (refID / next refID in [-1, n), pos / next pos >= -1,
-  // l_read_name >= 2, the empty-mapped rule, remaining-length floor), 4 positions per
-  // thread from 9 staged dwords with v_alignbyte.  Only true record starts and rare
-  // look-alikes survive (~0.5% of BAM positions); they are queued in LDS and get the
-  // whole single-record predicate compacted.  A position failing a fixed-field test
-  // would fail one_record too, so the filter is exact. ----
+  // single-record predicate at window position i -> ok / nrm / und bits
   auto eval_one = [&](uint32_t i) {
     const uint64_t q = t0 + i;
     const uint64_t total = q < e0 ? e0 : sg.end[seg_index(sg, q, k0)];
@@ -360,82 +359,28 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
       atomicOr(&und[i >> 5], 1u << (i & 31));
     }
   };
-  {
-    // this thread's groups of 4 positions: [g0, g0 + EG); group g covers staged bytes 4g..4g+3
-    constexpr uint32_t EG = (EW / 4 + 4 + T - 1) / T;
-    constexpr uint32_t EMW = (EG * 4 + 31) / 32;
-    const uint32_t ngroups = (EW + sa + 3) / 4;
-    const uint32_t g0 = threadIdx.x * EG;
-    // stage 1: refID in [-1, n) (the most selective field; ~3% pass), ~3 VALU per position
-    uint32_t msk[EMW];
-#pragma unroll
-    for (uint32_t w = 0; w < EMW; ++w) msk[w] = 0;
-    uint32_t a = lds32[g0 + 1];
-#pragma unroll
-    for (uint32_t gi = 0; gi < EG; ++gi) {
-      const uint32_t g = g0 + gi;
-      const uint32_t b = lds32[g + 2];
-      uint32_t m4 = 0;
-#pragma unroll
-      for (uint32_t k = 0; k < 4; ++k) {
-        const uint32_t ref = __builtin_amdgcn_alignbyte(b, a, k);
-        const uint32_t ii = 4 * g + k - sa;  // wraps for positions before the window
-        const bool in = ii < EW && g < ngroups;
-        m4 |= (in && (ref + 1u < nref1 || ii >= fast_end)) ? 1u << k : 0u;
-      }
-      msk[(gi * 4) / 32] |= m4 << ((gi * 4) % 32);
-      a = b;
-    }
-    // stage 2: the other fixed fields for the refID survivors; survivors of those are queued
-#pragma unroll
-    for (uint32_t w = 0; w < EMW; ++w) {
-      uint32_t mw = msk[w];
-      while (mw) {
-        const uint32_t bit = __builtin_ctz(mw);
-        mw &= mw - 1;
-        const uint32_t gk = w * 32 + bit, g = g0 + gk / 4, k = gk % 4;
-        const uint32_t i = 4 * g + k - sa;
-        bool pass = true;
-        if (i < fast_end) {
-          const uint32_t *dw = lds32 + g;
-          const uint32_t rem = __builtin_amdgcn_alignbyte(dw[1], dw[0], k);
-          const uint32_t pos = __builtin_amdgcn_alignbyte(dw[3], dw[2], k);
-          const uint32_t bmn = __builtin_amdgcn_alignbyte(dw[4], dw[3], k);
-          const uint32_t fnc = __builtin_amdgcn_alignbyte(dw[5], dw[4], k);
-          const uint32_t lsq = __builtin_amdgcn_alignbyte(dw[6], dw[5], k);
-          const uint32_t nrf = __builtin_amdgcn_alignbyte(dw[7], dw[6], k);
-          const uint32_t nps = __builtin_amdgcn_alignbyte(dw[8], dw[7], k);
-          const int32_t rnl = (int32_t)(bmn & 0xff), nc = (int32_t)(fnc & 0xffff);
-          pass = nrf + 1u < nref1 && (int32_t)pos >= -1 && (int32_t)nps >= -1 && rnl >= 2 &&
-                 (((fnc >> 16) & 4) != 0 || ((int32_t)lsq != 0 && nc != 0)) &&
-                 (int32_t)rem >= implied_min_remaining(rnl, nc, (int32_t)lsq);
-        }
-        if (pass) {
-#ifdef SBH_EPROBE
-          ++nsurv;
-#endif
-          const uint32_t x = atomicAdd(&nq, 1u);
-          if (x < EQ_CHUNK) queue[x] = (uint16_t)i;
-          else eval_one(i);  // queue full: evaluate in place
-        }
-      }
-    }
-  }
-  __syncthreads();
-  {
-    const uint32_t nsv = nq < EQ_CHUNK ? nq : EQ_CHUNK;
-    for (uint32_t x = threadIdx.x; x < nsv; x += T) eval_one(queue[x]);
-  }
-  __syncthreads();
-#ifdef SBH_EPROBE
-  const uint64_t c2 = __builtin_readcyclecounter();
-#endif
-  // ---- phase B: the eager call at each candidate (a tile position whose single-record
-  // predicate passed or could not be decided in the window) ----
+  // the fixed fields other than refID at window position i < fast_end (refID / next
+  // refID in [-1, n), pos / next pos >= -1, l_read_name >= 2, the empty-mapped rule, the
+  // remaining-length floor); failing one implies one_record fails, so the filter is exact
+  auto fixed_ok = [&](uint32_t i) -> bool {
+    const uint32_t gb = i + sa, g = gb >> 2, k = gb & 3;
+    const uint32_t *dw = lds32 + g;
+    const uint32_t rem = __builtin_amdgcn_alignbyte(dw[1], dw[0], k);
+    const uint32_t pos = __builtin_amdgcn_alignbyte(dw[3], dw[2], k);
+    const uint32_t bmn = __builtin_amdgcn_alignbyte(dw[4], dw[3], k);
+    const uint32_t fnc = __builtin_amdgcn_alignbyte(dw[5], dw[4], k);
+    const uint32_t lsq = __builtin_amdgcn_alignbyte(dw[6], dw[5], k);
+    const uint32_t nrf = __builtin_amdgcn_alignbyte(dw[7], dw[6], k);
+    const uint32_t nps = __builtin_amdgcn_alignbyte(dw[8], dw[7], k);
+    const int32_t rnl = (int32_t)(bmn & 0xff), nc = (int32_t)(fnc & 0xffff);
+    return nrf + 1u < nref1 && (int32_t)pos >= -1 && (int32_t)nps >= -1 && rnl >= 2 &&
+           (((fnc >> 16) & 4) != 0 || ((int32_t)lsq != 0 && nc != 0)) &&
+           (int32_t)rem >= implied_min_remaining(rnl, nc, (int32_t)lsq);
+  };
+  // phase B helpers.  r: 1 true, 0 false, 2 unknown (needs bytes past an open end)
   uint32_t mytrue = 0;
   const uint64_t wbase = (uint64_t)blockIdx.x * (ETILE / 32);
   const uint64_t nwords = (end - begin + 31) / 32;
-  // r: 1 true, 0 false, 2 unknown (needs bytes past an open end)
   auto call_at = [&](uint32_t i) -> uint32_t {
     const uint64_t p = t0 + i;
     const uint32_t k = p < e0 ? k0 : seg_index(sg, p, k0);
@@ -470,50 +415,241 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
     const unsigned long long x = atomicAdd(o.defer_n, 1ull);
     if (x < o.defer_cap) o.defer_pos[x] = t0 + i;
   };
-  if (rtc > 0 && nq <= EQ_CHUNK) {
-    // every candidate is in the survivor queue: one candidate per thread, balanced
-    for (uint32_t x = threadIdx.x; x < nq; x += T) {
-      const uint32_t i = queue[x];
-      if (i >= ETILE || t0 + i >= end) continue;
-      if (!(((ok[i >> 5] | und[i >> 5]) >> (i & 31)) & 1)) continue;
-      const uint32_t r = call_at(i);
-      if (r == 1) {
-        atomicOr(&res[i >> 5], 1u << (i & 31));
-      } else if (r == EAGER_DEFER) {
-        defer(i);
-      } else if (r == 2) {
-        atomicAdd(o.n_unknown, 1ull);
-        atomicMin(o.min_unknown, (unsigned long long)(t0 + i));
-      }
+  auto settle = [&](uint32_t i, uint32_t r) {  // a candidate's result (queue-driven paths)
+    if (r == 1) {
+      atomicOr(&res[i >> 5], 1u << (i & 31));
+    } else if (r == EAGER_DEFER) {
+      defer(i);
+    } else if (r == 2) {
+      atomicAdd(o.n_unknown, 1ull);
+      atomicMin(o.min_unknown, (unsigned long long)(t0 + i));
     }
-    __syncthreads();
+  };
+  auto write_res = [&]() {
     for (uint32_t w = threadIdx.x; w < ETILE / 32; w += T) {
       if (wbase + w >= nwords) break;
       o.bits[wbase + w] = res[w];
       mytrue += __popc(res[w]);
     }
-  } else {
-    for (uint32_t w = threadIdx.x; w < ETILE / 32; w += T) {
-      if (wbase + w >= nwords) break;
-      uint32_t cand = rtc <= 0 ? ~0u : (ok[w] | und[w]);
-      uint32_t rw = 0;
-      while (cand) {
-        const uint32_t bit = __builtin_ctz(cand);
-        cand &= cand - 1;
-        const uint32_t i = 32 * w + bit;
-        if (t0 + i >= end) break;
-        const uint32_t r = call_at(i);
-        if (r == 1) {
-          rw |= 1u << bit;
-        } else if (r == EAGER_DEFER) {
-          defer(i);
-        } else if (r == 2) {
-          atomicAdd(o.n_unknown, 1ull);
-          atomicMin(o.min_unknown, (unsigned long long)(t0 + i));
-        }
+  };
+
+  // ---- phase A, stage 1: refID in [-1, n) (the most selective field; ~3% pass) for
+  // every position of the window, 4 positions per thread and step from staged dwords
+  // with v_alignbyte.  This thread's groups of 4 positions: [g0, g0 + EG); group g
+  // covers staged bytes 4g..4g+3. ----
+  constexpr uint32_t EG = (EW / 4 + 4 + T - 1) / T;
+  constexpr uint32_t EMW = (EG * 4 + 31) / 32;
+  const uint32_t ngroups = (EW + sa + 3) / 4;
+  const uint32_t g0 = threadIdx.x * EG;
+  uint32_t msk[EMW];
+#pragma unroll
+  for (uint32_t w = 0; w < EMW; ++w) msk[w] = 0;
+  {
+    uint32_t a = lds32[g0 + 1];
+#pragma unroll
+    for (uint32_t gi = 0; gi < EG; ++gi) {
+      const uint32_t g = g0 + gi;
+      const uint32_t b = lds32[g + 2];
+      uint32_t m4 = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t ref = __builtin_amdgcn_alignbyte(b, a, k);
+        const uint32_t ii = 4 * g + k - sa;  // wraps for positions before the window
+        const bool in = ii < EW && g < ngroups;
+        m4 |= (in && (ref + 1u < nref1 || ii >= fast_end)) ? 1u << k : 0u;
       }
-      o.bits[wbase + w] = rw;
-      mytrue += __popc(rw);
+      msk[(gi * 4) / 32] |= m4 << ((gi * 4) % 32);
+      a = b;
+    }
+  }
+  // ---- survivor lists: each wave compacts its refID survivors, in position order, into
+  // its own queue segment and filters them in place (fixed fields, then the whole
+  // single-record predicate), so every step runs one survivor per lane.  The candidate
+  // list comes out sorted, which lets phase B link each record to the next candidate. ----
+  uint16_t *wq = queue + wid * SEGCAP;
+  uint32_t n1 = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < EMW; ++w) n1 += __popc(msk[w]);
+  const uint32_t incl1 = wave_incl_scan(n1);
+  const uint32_t wtot1 = __builtin_amdgcn_readlane(incl1, WAVE - 1);
+  if (wtot1 <= SEGCAP) {
+    uint32_t o1 = incl1 - n1;
+#pragma unroll
+    for (uint32_t w = 0; w < EMW; ++w) {
+      uint32_t mw = msk[w];
+      while (mw) {
+        const uint32_t bit = __builtin_ctz(mw);
+        mw &= mw - 1;
+        const uint32_t gk = w * 32 + bit;
+        wq[o1++] = (uint16_t)(4 * (g0 + gk / 4) + gk % 4 - sa);
+      }
+    }
+  }
+  // in-place, order-keeping wave compaction of wq[0, n) by pred; returns the kept count
+  // (a lane's store never reaches an entry another lane has yet to load)
+  auto compact = [&](uint32_t n, auto pred) -> uint32_t {
+    uint32_t kept = 0;
+    for (uint32_t x = 0; x < n; x += WAVE) {
+      const bool has = x + lane < n;
+      const uint32_t i = has ? wq[x + lane] : 0u;
+      const bool keep = has && pred(i);
+      const uint64_t bal = __ballot(keep);
+      const uint32_t rank =
+          __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+      if (keep) wq[kept + rank] = (uint16_t)i;
+      kept += (uint32_t)__popcll(bal);
+    }
+    return kept;
+  };
+  uint32_t n2 = 0;
+  if (wtot1 <= SEGCAP) n2 = compact(wtot1, [&](uint32_t i) { return i >= fast_end || fixed_ok(i); });
+  if (lane == 0) wcnt[wid] = wtot1 <= SEGCAP ? n2 : ~0u;
+#ifdef SBH_EPROBE
+  c1a = __builtin_readcyclecounter();
+#endif
+  __syncthreads();
+  bool fast = rtc > 0;
+#pragma unroll
+  for (uint32_t w = 0; w < NWV; ++w) fast = fast && wcnt[w] != ~0u;
+  if (fast) {
+    // entries of the concatenated segment lists (sorted by position)
+    uint32_t pre[NWV + 1];
+    pre[0] = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < NWV; ++w) pre[w + 1] = pre[w] + wcnt[w];
+    auto entry = [&](uint32_t g) -> uint32_t {
+      uint32_t w = 0;
+#pragma unroll
+      for (uint32_t k = 1; k < NWV; ++k) w += g >= pre[k] ? 1u : 0u;
+      return queue[w * SEGCAP + g - pre[w]];
+    };
+#ifdef SBH_EPROBE
+    if (threadIdx.x == 0) nsurv = pre[NWV];
+#endif
+    for (uint32_t x = threadIdx.x; x < pre[NWV]; x += T) eval_one(entry(x));
+#ifdef SBH_EPROBE
+    c1b = __builtin_readcyclecounter();
+#endif
+    __syncthreads();
+    // candidates: ok or undecidable
+    const uint32_t n3 = compact(n2, [&](uint32_t i) { return (((ok[i >> 5] | und[i >> 5]) >> (i & 31)) & 1) != 0; });
+    __syncthreads();  // every thread has read wcnt
+    if (lane == 0) wcnt[wid] = n3;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t w = 0; w < NWV; ++w) pre[w + 1] = pre[w] + wcnt[w];
+    const uint32_t nc3 = pre[NWV];
+#ifdef SBH_EPROBE
+    c2 = __builtin_readcyclecounter();
+#endif
+    // ---- phase B.  One step of call_at's chain walk per candidate: from an ok, normal
+    // record whose successor lies in the window, is decidable and is ok, the step LINKs
+    // when that successor is the next candidate; it FAILs when the successor is not ok;
+    // anything else leaves the candidate to call_at.  A candidate is true when the
+    // rtc - 1 steps from it and its successors all LINK. ----
+    for (uint32_t g = threadIdx.x; g < nc3; g += T) {
+      const uint32_t i = entry(g);
+      if ((und[i >> 5] >> (i & 31)) & 1) continue;
+      if (!((nrm[i >> 5] >> (i & 31)) & 1)) continue;  // cursor past nominal
+      const uint64_t q = t0 + i;
+      const uint64_t total = q < e0 ? e0 : sg.end[seg_index(sg, q, k0)];
+      const uint64_t nxt = q + 4 + (int64_t)(int32_t)s.word_at(q);
+      if (nxt + 36 > total || nxt < t0 || nxt - t0 >= EW) continue;  // EOF edge / outside window
+      const uint32_t jn = (uint32_t)(nxt - t0);
+      if ((und[jn >> 5] >> (jn & 31)) & 1) continue;
+      if (!((ok[jn >> 5] >> (jn & 31)) & 1)) atomicOr(&lfail[g >> 5], 1u << (g & 31));
+      else if (g + 1 < nc3 && entry(g + 1) == jn) atomicOr(&lnk[g >> 5], 1u << (g & 31));
+    }
+    __syncthreads();
+    const uint32_t need = (uint32_t)rtc - 1;  // steps from a candidate to its rtc-th record
+    for (uint32_t g = threadIdx.x; g < nc3; g += T) {
+      const uint32_t i = entry(g);
+      if (i >= ETILE || t0 + i >= end) continue;
+      uint32_t r;
+      if ((und[i >> 5] >> (i & 31)) & 1) {
+        r = call_at(i);
+      } else {
+        uint32_t m = 0;  // first non-LINK step among [g, g + need)
+        bool all = true;
+        while (m < need) {
+          const uint32_t gg = g + m, b = gg & 31;
+          const uint32_t span = min(32u - b, need - m);
+          const uint32_t gap = ~(gg < EQ_CHUNK ? lnk[gg >> 5] : 0u) >> b;
+          const uint32_t mk = span == 32 ? ~0u : (1u << span) - 1u;
+          if (gap & mk) {
+            m += __builtin_ctz(gap & mk);
+            all = false;
+            break;
+          }
+          m += span;
+        }
+        if (all) r = 1;
+        else if (g + m < EQ_CHUNK && ((lfail[(g + m) >> 5] >> ((g + m) & 31)) & 1)) r = 0;
+        else r = call_at(i);
+      }
+      settle(i, r);
+    }
+    __syncthreads();
+    write_res();
+  } else {
+    // ---- fallback (a survivor list overflowed, or rtc <= 0): per-thread survivor loop
+    // (fixed fields), shared queue, word-wise phase B ----
+#pragma unroll
+    for (uint32_t w = 0; w < EMW; ++w) {
+      uint32_t mw = msk[w];
+      while (mw) {
+        const uint32_t bit = __builtin_ctz(mw);
+        mw &= mw - 1;
+        const uint32_t gk = w * 32 + bit;
+        const uint32_t i = 4 * (g0 + gk / 4) + gk % 4 - sa;
+        if (i < fast_end && !fixed_ok(i)) continue;
+#ifdef SBH_EPROBE
+        ++nsurv;
+#endif
+        const uint32_t x = atomicAdd(&nq, 1u);
+        if (x < EQ_CHUNK) queue[x] = (uint16_t)i;
+        else eval_one(i);  // queue full: evaluate in place
+      }
+    }
+    __syncthreads();
+    {
+      const uint32_t nsv = nq < EQ_CHUNK ? nq : EQ_CHUNK;
+      for (uint32_t x = threadIdx.x; x < nsv; x += T) eval_one(queue[x]);
+    }
+    __syncthreads();
+    if (rtc > 0 && nq <= EQ_CHUNK) {
+      // every candidate is in the survivor queue: one candidate per thread, balanced
+      for (uint32_t x = threadIdx.x; x < nq; x += T) {
+        const uint32_t i = queue[x];
+        if (i >= ETILE || t0 + i >= end) continue;
+        if (!(((ok[i >> 5] | und[i >> 5]) >> (i & 31)) & 1)) continue;
+        settle(i, call_at(i));
+      }
+      __syncthreads();
+      write_res();
+    } else {
+      for (uint32_t w = threadIdx.x; w < ETILE / 32; w += T) {
+        if (wbase + w >= nwords) break;
+        uint32_t cand = rtc <= 0 ? ~0u : (ok[w] | und[w]);
+        uint32_t rw = 0;
+        while (cand) {
+          const uint32_t bit = __builtin_ctz(cand);
+          cand &= cand - 1;
+          const uint32_t i = 32 * w + bit;
+          if (t0 + i >= end) break;
+          const uint32_t r = call_at(i);
+          if (r == 1) {
+            rw |= 1u << bit;
+          } else if (r == EAGER_DEFER) {
+            defer(i);
+          } else if (r == 2) {
+            atomicAdd(o.n_unknown, 1ull);
+            atomicMin(o.min_unknown, (unsigned long long)(t0 + i));
+          }
+        }
+        o.bits[wbase + w] = rw;
+        mytrue += __popc(rw);
+      }
     }
   }
   if (mytrue) atomicAdd(&ntrue, mytrue);
@@ -527,9 +663,10 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
   atomicAdd(&pcand, ncand);
   atomicAdd(&pexact, nexact);
   __syncthreads();
-  if (threadIdx.x == 0 && blockIdx.x < 4)
-    printf("eager wg %u stage %llu A %llu B %llu surv %u cand %u true %u exact %u\n", blockIdx.x,
-           (unsigned long long)(c1 - c0), (unsigned long long)(c2 - c1),
+  if (threadIdx.x == 0 && blockIdx.x >= 3000 && blockIdx.x < 3008)
+    printf("eager wg %u fast %d stage %llu A1+2 %llu eval %llu cand %llu B %llu surv %u exactcalls %u true %u exact %u\n",
+           blockIdx.x, (int)fast, (unsigned long long)(c1 - c0), (unsigned long long)(c1a - c1),
+           (unsigned long long)(c1b - c1a), (unsigned long long)(c2 - c1b),
            (unsigned long long)(__builtin_readcyclecounter() - c2), psurv, pcand, ntrue, pexact);
 #endif
 }

@@ -102,18 +102,6 @@ __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t l) {
   return __builtin_amdgcn_readlane(v, l);
 }
 
-// Inclusive prefix sum over the 64 lanes of a wave in DPP steps (no LDS round trips):
-// row_shr 1/2/4/8 within each 16-lane row, then row_bcast:15 and row_bcast:31 carry
-// the row totals across rows (gfx9 DPP).  Inactive lanes must contribute 0.
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
-  return x;
-}
 
 __device__ __forceinline__ uint32_t lit_entry(uint32_t sym, uint32_t L) {
   if (sym < 256) return L | (K_LIT << 5) | (sym << 8);
