@@ -1566,13 +1566,16 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
 #ifdef SBH_LZ_DEBUG
         uint32_t guard = 0;
 #endif
-        while (__builtin_expect(pend[hh] != 0, 0)) {
+        // Each round replaces every in-chunk pointer by the one stored at its target (a
+        // final slot -- a literal -- stores itself, so it stays); a lane stops once no
+        // pointer of its own moved to another in-chunk position.
+        bool more = pend[hh] != 0;
+        while (__builtin_expect(more, 0)) {
 #ifdef SBH_LZ_DEBUG
           if (++guard > 300) {
             for (uint32_t k = 0; k < PTR_HALF; ++k)
-              if ((pend[hh] >> k) & 1)
-                printf("lz chase stuck blk %llu pos %u c %u base %u chunk_len %u lead %u\n", (unsigned long long)b,
-                       g0 + k, c[hh][k], base, chunk_len, lead);
+              printf("lz chase stuck blk %llu pos %u c %u base %u chunk_len %u lead %u\n", (unsigned long long)b,
+                     g0 + k, c[hh][k], base, chunk_len, lead);
             break;
           }
 #endif
@@ -1580,16 +1583,15 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
 #pragma unroll
           for (uint32_t k = 0; k < PTR_HALF; ++k) v[k] = p16[(c[hh][k] >= base ? c[hh][k] : base) - abase];
 #ifdef SBH_LZ_PROBE
-          ++njumps;
+          if (__builtin_amdgcn_readfirstlane(lane) == lane) ++njumps;  // rounds this wave ran
 #endif
-          uint32_t np = 0;
+          more = false;
 #pragma unroll
           for (uint32_t k = 0; k < PTR_HALF; ++k) {
-            const bool go = ((pend[hh] >> k) & 1) && v[k] != c[hh][k];
-            c[hh][k] = go ? v[k] : c[hh][k];
-            np |= (go && v[k] >= base) ? 1u << k : 0u;
+            const uint32_t nc = c[hh][k] >= base ? v[k] : c[hh][k];
+            more = more || (nc != c[hh][k] && nc >= base);
+            c[hh][k] = nc;
           }
-          pend[hh] = np;
           // write back: settled and shortened pointers alike (literal and out-of-chunk
           // slots keep pointing at themselves)
           reinterpret_cast<uint4 *>(p16)[h] = pack8_u16(c[hh]);
@@ -1692,6 +1694,11 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
 #endif
   }
 #ifdef SBH_LZ_PROBE
+  {
+    uint32_t tot = 0;
+    for (uint32_t l = 0; l < WAVE; ++l) tot += __builtin_amdgcn_readlane(njumps, l);
+    njumps = tot;
+  }
   if (lane == 0 && b < 2)
     printf("lz blk %llu wave %u ntok %u cyc %llu pre %llu marks %llu marks+slots %llu init+bar %llu chase %llu resolve+bar %llu fallback %u chase_rounds %u long %u\n",
            (unsigned long long)b, t / WAVE, n, (unsigned long long)(__builtin_readcyclecounter() - tp0),
