@@ -253,8 +253,8 @@ __device__ __forceinline__ uint32_t pentry(uint32_t kind, uint32_t sym, uint32_t
 // v occupy [lj[v-1], lj[v]) of the 15-bit left-justified code space, so a reversed
 // index's length is 1 + #{v : lj[v] <= code}.  Entries whose code is longer than
 // `fast` bits are K_SLOW (slow_lane finishes them); prefixes of no code are K_BAD.
-__device__ __forceinline__ uint32_t build_ptable(WaveSmem &sm, const uint8_t *lens, uint32_t nsym, uint32_t kind,
-                                                 uint32_t *tab, uint32_t fast, uint32_t lane) {
+__device__ __forceinline__ uint32_t ptable_meta(WaveSmem &sm, const uint8_t *lens, uint32_t nsym, uint32_t kind,
+                                                uint32_t lane) {
   uint16_t *sorted = sm.sorted + (kind ? 288 : 0);
   uint32_t my_cnt = 0;  // lane v (1..15): count of length v
   for (uint32_t base = 0; base < nsym; base += WAVE) {
@@ -283,9 +283,7 @@ __device__ __forceinline__ uint32_t build_ptable(WaveSmem &sm, const uint8_t *le
     }
     acc += c;
   }
-  const uint32_t n_ent = 1u << fast;
-  if (max == 0) {  // no symbols: every entry invalid
-    for (uint32_t i = lane; i < n_ent; i += WAVE) tab[i] = 1u | PE_SPECIAL;
+  if (max == 0) {  // no symbols: all-zero limits make every entry invalid (ptable_entry)
     if (lane < 16) sm.pk[kind][lane] = 0;
     return 2;
   }
@@ -309,21 +307,36 @@ __device__ __forceinline__ uint32_t build_ptable(WaveSmem &sm, const uint8_t *le
       sm.sent[(kind ? 288 : 0) + rank] = pentry(kind, s, l);
     }
   }
-  __builtin_amdgcn_wave_barrier();
-#pragma unroll 4
-  for (uint32_t i = lane; i < n_ent; i += WAVE) {
-    const uint32_t c15 = (__builtin_bitreverse32(i) >> (32 - fast)) << (15 - fast);
-    uint32_t len = 1;
-#pragma unroll
-    for (uint32_t v = 1; v <= 15; ++v) len += ljv[v] <= c15 ? 1u : 0u;
-    uint32_t e;
-    if (len > 15) e = 1u | PE_SPECIAL;
-    else if (len > fast) e = PE_SPECIAL | PE_SLOW;
-    else e = sm.sent[(kind ? 288 : 0) + (((sm.pk[kind][len] & 0xffffu) + (c15 >> (15 - len))) & 0xffffu)];
-    tab[i] = e;
-  }
-  __builtin_amdgcn_wave_barrier();
   return 0;
+}
+
+// Entry i of the PAR table of `kind` from its limits lj[v] (= pk[kind][v] >> 16) and
+// ptable_meta's canonical order: the code's length is 1 + #{v : lj[v] <= code}.
+__device__ __forceinline__ uint32_t ptable_entry(const WaveSmem &sm, const uint32_t *lj, uint32_t kind, uint32_t fast,
+                                                 uint32_t i) {
+  const uint32_t c15 = (__builtin_bitreverse32(i) >> (32 - fast)) << (15 - fast);
+  uint32_t len = 1;
+#pragma unroll
+  for (uint32_t v = 1; v <= 15; ++v) len += lj[v] <= c15 ? 1u : 0u;
+  if (len > 15) return 1u | PE_SPECIAL;
+  if (len > fast) return PE_SPECIAL | PE_SLOW;
+  return sm.sent[(kind ? 288 : 0) + (((sm.pk[kind][len] & 0xffffu) + (c15 >> (15 - len))) & 0xffffu)];
+}
+
+// Canonical table in the PAR format (kind 0 lit/len, 1 dist), same validity rules as
+// build_table, built by one wave.  Returns 0 ok, 1 error, 2 empty.
+__device__ __forceinline__ uint32_t build_ptable(WaveSmem &sm, const uint8_t *lens, uint32_t nsym, uint32_t kind,
+                                                 uint32_t *tab, uint32_t fast, uint32_t lane) {
+  const uint32_t rc = ptable_meta(sm, lens, nsym, kind, lane);
+  if (rc == 1) return 1;
+  __builtin_amdgcn_wave_barrier();
+  uint32_t lj[16];
+#pragma unroll
+  for (uint32_t v = 1; v <= 15; ++v) lj[v] = sm.pk[kind][v] >> 16;
+#pragma unroll 4
+  for (uint32_t i = lane; i < (1u << fast); i += WAVE) tab[i] = ptable_entry(sm, lj, kind, fast, i);
+  __builtin_amdgcn_wave_barrier();
+  return rc;
 }
 
 template <bool PAR>
@@ -1056,6 +1069,20 @@ template <bool LDS>
 __device__ __forceinline__ bool par_header(HuffSmem &sm, Src<LDS> src, uint32_t p, uint32_t limit, bool &fixed_built,
                                            uint32_t wid, uint32_t lane, uint32_t &psym, uint32_t &last) {
   WaveSmem &t = sm.t;
+  // both decode tables from ptable_meta's limits and order, filled by the whole workgroup
+  auto fill_tables = [&]() {
+    const uint32_t tid = wid * WAVE + lane;
+    uint32_t lj0[16], lj1[16];
+#pragma unroll
+    for (uint32_t v = 1; v <= 15; ++v) {
+      lj0[v] = t.pk[0][v] >> 16;
+      lj1[v] = t.pk[1][v] >> 16;
+    }
+#pragma unroll
+    for (uint32_t i = tid; i < (1u << LIT_FAST); i += HT) t.lit[i] = ptable_entry(t, lj0, 0, LIT_FAST, i);
+#pragma unroll
+    for (uint32_t i = tid; i < (1u << PDIST_FAST); i += HT) t.dist[i] = ptable_entry(t, lj1, 1, PDIST_FAST, i);
+  };
   const uint32_t hb = uni(src.bits32(p));
   last = hb & 1;
   const uint32_t type = (hb >> 1) & 3;
@@ -1066,12 +1093,14 @@ __device__ __forceinline__ bool par_header(HuffSmem &sm, Src<LDS> src, uint32_t 
       if (wid == 0) {
         for (uint32_t s = lane; s < 288; s += WAVE) t.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
         __builtin_amdgcn_wave_barrier();
-        build_ptable(t, t.lens, 288, 0, t.lit, LIT_FAST, lane);
+        ptable_meta(t, t.lens, 288, 0, lane);
       } else if (wid == 1) {
         if (lane < 32) t.lens[288 + lane] = 5;
         __builtin_amdgcn_wave_barrier();
-        build_ptable(t, t.lens + 288, 32, 1, t.dist, PDIST_FAST, lane);
+        ptable_meta(t, t.lens + 288, 32, 1, lane);
       }
+      __syncthreads();
+      fill_tables();
       __syncthreads();
       fixed_built = true;
     }
@@ -1091,6 +1120,8 @@ __device__ __forceinline__ bool par_header(HuffSmem &sm, Src<LDS> src, uint32_t 
 #ifdef SBH_HUFF_PROBE
     h1 = __builtin_readcyclecounter();
 #endif
+    for (uint32_t w = lane; w < 320 / 4; w += WAVE) reinterpret_cast<uint32_t *>(t.lens)[w] = 0;
+    __builtin_amdgcn_wave_barrier();
     const uint32_t total = nlen + ndist;
     uint32_t i = 0, prev = 0, q = p + 17 + 3 * ncode;
     const uint64_t below = (1ull << lane) - 1;  // lanes under this one
@@ -1127,7 +1158,7 @@ __device__ __forceinline__ bool par_header(HuffSmem &sm, Src<LDS> src, uint32_t 
       const uint32_t from = __shfl(own, src_lane, WAVE);
       const uint32_t val = sym == 16 ? (lowN ? from : prev) : own;
       if (M & 1 && __builtin_amdgcn_readfirstlane(sym) == 16 && i0 == 0) ok = false;  // repeat with no previous length
-      if (mine) {  // the run [start, start + rep) of lengths; lens[] puts distances at 288
+      if (mine && val != 0) {  // the run [start, start + rep) of lengths (zeros: pre-set); distances at 288
         const uint32_t e = min(start + rep, total);
         const uint32_t v4 = val * 0x01010101u;
         for (uint32_t j = start; j < e;) {
@@ -1161,17 +1192,17 @@ __device__ __forceinline__ bool par_header(HuffSmem &sm, Src<LDS> src, uint32_t 
   if (!uni(sm.ctl[5])) return false;
   psym = uni(sm.ctl[6]);
   uint32_t rc = 0;
-  if (wid == 0) rc = build_ptable(t, t.lens, nlen, 0, t.lit, LIT_FAST, lane);
-  else if (wid == 1) rc = build_ptable(t, t.lens + 288, ndist, 1, t.dist, PDIST_FAST, lane);
+  if (wid == 0) rc = ptable_meta(t, t.lens, nlen, 0, lane);
+  else if (wid == 1) rc = ptable_meta(t, t.lens + 288, ndist, 1, lane);
+  if (__syncthreads_or(rc == 1)) return false;
+  fill_tables();
+  __syncthreads();
 #ifdef SBH_HUFF_PROBE
-  const bool res = !__syncthreads_or(rc == 1);
   if (threadIdx.x == 0 && blockIdx.x >= 5000 && blockIdx.x < 5003)
     printf("hdr blk %u cl %llu walk %llu build %llu\n", blockIdx.x, (unsigned long long)(h1 - h0),
            (unsigned long long)(h2 - h1), (unsigned long long)(__builtin_readcyclecounter() - h2));
-  return res;
-#else
-  return !__syncthreads_or(rc == 1);
 #endif
+  return true;
 }
 
 // The deflate blocks of one BGZF block, lane-parallel.  Returns false (uniformly) when
