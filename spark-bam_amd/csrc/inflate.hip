@@ -924,6 +924,12 @@ constexpr uint32_t MIN_SLICE = SBH_MIN_SLICE;  // bits per lane at least
 constexpr uint32_t NOPOS = 0xffffffffu;
 constexpr uint32_t CK1 = 6, CK2 = 24;  // pass-1 checkpoints (tokens)
 constexpr uint32_t LR_RUN = 0, LR_EOB = 1, LR_DEAD = 2, LR_PAST = 3;
+#ifdef SBH_HUFF_PROBE
+// whole-kernel phase sums (cycles): 0 stage, 1 header, 2 pass 1, 3 repair, 4 emit, 5 repair
+// rounds, 6 deflate blocks, 7 whole block, 8-10 header: CL table / walk / tables, 11 tokens
+__device__ unsigned long long hp_acc[16];
+__device__ unsigned int hp_done;
+#endif
 struct HuffSmem {
   WaveSmem t;                    // tables (built by wave 0; the serial fallback's too)
   uint32_t stage[STAGE_DW + 8];  // the block's deflate dwords, from dword a0
@@ -1198,9 +1204,11 @@ __device__ __forceinline__ bool par_header(HuffSmem &sm, Src<LDS> src, uint32_t 
   fill_tables();
   __syncthreads();
 #ifdef SBH_HUFF_PROBE
-  if (threadIdx.x == 0 && blockIdx.x >= 5000 && blockIdx.x < 5003)
-    printf("hdr blk %u cl %llu walk %llu build %llu\n", blockIdx.x, (unsigned long long)(h1 - h0),
-           (unsigned long long)(h2 - h1), (unsigned long long)(__builtin_readcyclecounter() - h2));
+  if (wid == 0 && lane == 0) {
+    atomicAdd(&hp_acc[8], h1 - h0);
+    atomicAdd(&hp_acc[9], h2 - h1);
+    atomicAdd(&hp_acc[10], __builtin_readcyclecounter() - h2);
+  }
 #endif
   return true;
 }
@@ -1257,7 +1265,12 @@ __device__ __forceinline__ bool inflate_par(HuffSmem &sm, const uint8_t *__restr
         sm.exitv[tid] = r.st == LR_RUN ? r.exit : NOPOS;
       }
       ck = Ckpt{NOPOS, 0, NOPOS, 0};  // later rounds: the chain changed, run fully
-      if (!__syncthreads_or(changed)) break;
+      const bool again = __syncthreads_or(changed);
+#ifdef SBH_HUFF_PROBE
+      if (tid == 0 && nrounds == 1) atomicAdd(&hp_acc[12], __builtin_readcyclecounter() - tp1);
+      if (tid == 0 && nrounds == 2) atomicAdd(&hp_acc[13], __builtin_readcyclecounter() - tp1);
+#endif
+      if (!again) break;
     }
     // the first lane whose chain ends decides the deflate block
     if (r.st != LR_RUN) atomicMin(&sm.ctl[3], tid);
@@ -1272,11 +1285,15 @@ __device__ __forceinline__ bool inflate_par(HuffSmem &sm, const uint8_t *__restr
     ttot = uni(ttot);
     otot = uni(otot);
 #ifdef SBH_HUFF_PROBE
-    if (tid == 0 && blockIdx.x >= 5000 && blockIdx.x < 5004)
-      printf("huff blk %u S %u rounds %u k %u ttot %u otot %u last %u hdr %llu p1 %llu p2 %llu\n",
-             blockIdx.x, S, nrounds, k, ttot, otot, last, (unsigned long long)(tph - tp0),
-             (unsigned long long)(tp1 - tph), (unsigned long long)(__builtin_readcyclecounter() - tp1));
     const uint64_t tp3 = __builtin_readcyclecounter();
+    if (tid == 0) {
+      atomicAdd(&hp_acc[1], tph - tp0);
+      atomicAdd(&hp_acc[2], tp1 - tph);
+      atomicAdd(&hp_acc[3], tp3 - tp1);
+      atomicAdd(&hp_acc[5], (unsigned long long)nrounds);
+      atomicAdd(&hp_acc[6], 1ull);
+      atomicAdd(&hp_acc[11], (unsigned long long)ttot);
+    }
 #endif
     if (k >= HT || eob_end == NOPOS || otot > usize - out) return false;
     // pass 3: emit
@@ -1284,7 +1301,7 @@ __device__ __forceinline__ bool inflate_par(HuffSmem &sm, const uint8_t *__restr
     if (tid <= k) lane_run<LDS, RUN_EMIT>(sm.t, src, A, stop, limit, ck, none, tk + ntok + tpre, out + opre, bad);
     if (__syncthreads_or(bad)) return false;
 #ifdef SBH_HUFF_PROBE
-    if (tid == 0 && blockIdx.x >= 5000 && blockIdx.x < 5004) printf("huff blk %u p3 %llu\n", blockIdx.x, (unsigned long long)(__builtin_readcyclecounter() - tp3));
+    if (tid == 0) atomicAdd(&hp_acc[4], __builtin_readcyclecounter() - tp3);
 #endif
     ntok += ttot;
     out += otot;
@@ -1307,6 +1324,9 @@ __global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__rest
   const uint64_t G = bl.ustart[b];
   const bool serial = (bl.flags[b] & BLK_TRUNCATED) || usize > 65536u || usize < PAR_MIN_USIZE ||
                 (int32_t)csize - (int32_t)hsize - 8 < 0;
+#ifdef SBH_HUFF_PROBE
+  const uint64_t hk0 = __builtin_readcyclecounter();
+#endif
   if (!serial) {
     const uint32_t data_len = csize - hsize - 8;
     const uint64_t dbyte = cstart + hsize;
@@ -1320,6 +1340,9 @@ __global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__rest
       const uint32_t *g = reinterpret_cast<const uint32_t *>(comp) + a0;
       for (uint32_t i = tid; i < ndw; i += HT) sm.stage[i] = g[i];
       __syncthreads();
+#ifdef SBH_HUFF_PROBE
+      if (tid == 0) atomicAdd(&hp_acc[0], __builtin_readcyclecounter() - hk0);
+#endif
       ok = inflate_par<true>(sm, comp, a0, skip, limit, usize, tok + G, tid, lane, wid, ntok);
     } else {
       ok = inflate_par<false>(sm, comp, a0, skip, limit, usize, tok + G, tid, lane, wid, ntok);
@@ -1329,6 +1352,21 @@ __global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__rest
         bl.status[b] = INF_OK;
         bl.ntok[b] = ntok;
       }
+#ifdef SBH_HUFF_PROBE
+      if (tid == 0) {
+        atomicAdd(&hp_acc[7], __builtin_readcyclecounter() - hk0);
+        __threadfence();
+        if (atomicAdd(&hp_done, 1u) == (uint32_t)nblocks - 1) {  // (serial blocks not counted)
+          unsigned long long a[14];
+          for (int k = 0; k < 14; ++k) a[k] = atomicExch(&hp_acc[k], 0ull);
+          hp_done = 0;
+          const double n = (double)nblocks, d = (double)a[6];
+          printf("huffprobe blocks %.0f deflate %.0f per-BGZF-block cycles: stage %.0f hdr %.0f (cl %.0f walk %.0f tables %.0f) p1 %.0f p2 %.0f (rounds/defl %.2f) p3 %.0f whole %.0f tokens/defl %.0f | p2 to end of round1 %.0f round2 %.0f\n",
+                 n, d, a[0] / n, a[1] / n, a[8] / n, a[9] / n, a[10] / n, a[2] / n, a[3] / n, a[5] / d, a[4] / n,
+                 a[7] / n, a[11] / d, a[12] / n, a[13] / n);
+        }
+      }
+#endif
       return;
     }
   }
