@@ -210,8 +210,15 @@ def main():
                 "traffic_source": traffic_src,
                 "alg_bytes_per_step": int(alg_bytes),
                 "alg_units": dom_units,
-                "limiter": "latency: LDS round trips of the per-lane Huffman chains (k_huff) and barrier-separated "
-                           "pointer chasing (k_lz); neither kernel is HBM-bound",
+                "limiter": "not HBM: k_huff ~57% VALU-issue busy, the rest LDS latency of the per-lane decode "
+                           "chains and the repair round (max sync distance over 256 lanes); k_lz ~80% VALU-issue "
+                           "bound (pointer slot pass + chase); PMC in profiles/",
+                "path": {  # B_alg = C + U (inflate write) + U (checker read) + U/8 (bitmap) per step
+                    "alg_bytes_per_step": int(sum(own_sizes) / world + 2.125 * flat_bytes),
+                    "achieved": round((sum(own_sizes) / world + 2.125 * flat_bytes) * args.steps / elapsed / 1e9, 2),
+                    "frac": round((sum(own_sizes) / world + 2.125 * flat_bytes) * args.steps / elapsed / 1e9
+                                  / HBM_PEAK_GBPS, 5),
+                },
                 "per_kernel_GBps": {k: gbps(v[0], v[1]) for k, v in kern.items()},
             },
             "cpu_baseline": cpu,
