@@ -8,6 +8,7 @@
 //   spark-bam full-check    [-m SIZE] [-i RANGES] [-l N] BAM       (check/full/FullCheck.scala)
 //   spark-bam index-blocks  BAM [OUT]                        (bgzf/index/IndexBlocks.scala)
 //   spark-bam index-records BAM [OUT]                        (check/index/IndexRecords.scala)
+//   spark-bam check-blocks -s [-r RECORDS] [-l N] BAM        (cli/.../check/blocks/CheckBlocks.scala)
 //
 // The hadoop-bam ("seqdoop", -u) comparisons are out of scope: hadoop-bam's
 // BAMSplitGuesser is a competitor's algorithm, not part of spark-bam's path.
@@ -607,6 +608,143 @@ int index_records(const Args &a) {
   return 0;
 }
 
+
+// hammerlab Stats.fromHist rendered with the truncating Show[Double] CheckBlocks installs
+// (CheckBlocks.scala:123-131): N, mean / population sigma, median / MAD, the histogram's
+// first and last 10 runs ("v" or "v×n", "…" between), and the percentiles whose
+// interpolation index (N + 1) p - 1 lies inside [0, N - 1].
+std::string stats_hist(const std::map<long long, uint64_t> &hist) {
+  std::vector<double> v;
+  for (auto &kv : hist) v.insert(v.end(), kv.second, (double)kv.first);
+  const size_t n = v.size();
+  if (!n) return "(empty)\n";
+  auto rnd = [](double x) { return std::to_string((long long)std::floor(x + 0.5)); };
+  auto pct = [&](const std::vector<double> &s, double p) {  // s sorted
+    const double idx = (double)(s.size() + 1) * p - 1;
+    const size_t lo = (size_t)std::floor(idx);
+    const double f = idx - (double)lo;
+    return lo + 1 < s.size() ? s[lo] + f * (s[lo + 1] - s[lo]) : s[lo];
+  };
+  double mean = 0, var = 0;
+  for (double x : v) mean += x;
+  mean /= (double)n;
+  for (double x : v) var += (x - mean) * (x - mean);
+  const double sd = std::sqrt(var / (double)n), med = pct(v, 0.5);
+  std::vector<double> dev;
+  for (double x : v) dev.push_back(std::fabs(x - med));
+  std::sort(dev.begin(), dev.end());
+  std::string out = "N: " + std::to_string(n) + ", μ/σ: " + rnd(mean) + "/" + rnd(sd) + ", med/mad: " + rnd(med) +
+                    "/" + rnd(pct(dev, 0.5)) + "\n";
+  std::vector<std::string> runs;
+  for (auto &kv : hist)
+    runs.push_back(std::to_string(kv.first) + (kv.second > 1 ? "×" + std::to_string(kv.second) : ""));
+  out += " elems:";
+  for (size_t i = 0; i < runs.size(); ++i) {
+    if (runs.size() > 20 && i == 10) {
+      out += " …";
+      i = runs.size() - 10;
+    }
+    out += " " + runs[i];
+  }
+  out += "\n";
+  const double ps[] = {0.01, 0.05, 0.10, 0.25, 0.50, 0.75, 0.90, 0.95, 0.99};
+  for (double p : ps) {
+    const double idx = (double)(n + 1) * p - 1;
+    if (idx < 0 || idx > (double)(n - 1)) continue;
+    char lab[16];
+    snprintf(lab, sizeof lab, "%.2f", p);
+    out += std::string("  ") + (lab + 1) + ":\t" + rnd(pct(v, p)) + "\n";
+  }
+  return out;
+}
+
+// java.lang.Double.toString for 1e-3 <= |x| < 1e7: the shortest digits that read back
+std::string jdouble(double x) {
+  char b[64];
+  for (int p = 1; p <= 17; ++p) {
+    snprintf(b, sizeof b, "%.*g", p, x);
+    if (std::strtod(b, nullptr) == x) break;
+  }
+  std::string s(b);
+  if (s.find('.') == std::string::npos && s.find('e') == std::string::npos) s += ".0";
+  return s;
+}
+
+// CheckBlocks (cli/.../check/blocks/CheckBlocks.scala:30-195), -s mode: for every BGZF
+// block, the next read start from Pos(start, 0) by the indexed checker (the .records
+// ground truth) and by the eager checker; blocks where they differ are reported with the
+// compressed positions whose splits they would break.
+int check_blocks(const Args &a) {
+  if (!a.s || a.u) no_hadoop_bam();
+  Loaded L(a.path);
+  std::vector<uint64_t> truth;
+  for (auto &r : read_records_file(a.records.empty() ? a.path + ".records" : a.records)) {
+    uint64_t f = 0;
+    chk(sbh_flat_of(L.sh, r.block, r.off, &f), "records file position");
+    truth.push_back(f);
+  }
+  std::sort(truth.begin(), truth.end());
+  uint64_t seg_end = L.flat;
+  std::vector<const sbh_block *> blocks;
+  for (const sbh_block &b : L.blocks) {
+    if (b.flags & SBH_BLOCK_EMPTY) { seg_end = b.ustart; break; }  // the stream (and the block list) ends
+    blocks.push_back(&b);
+  }
+  std::vector<uint8_t> bits((seg_end + 7) / 8);
+  uint64_t ncalled = 0;
+  if (seg_end) chk(sbh_check_eager(L.sh, 0, seg_end, a.reads_to_check, bits.data(), &ncalled), "eager");
+  auto next_set = [&](uint64_t f) -> int64_t {  // eager nextReadStart: first call in [f, f + maxReadSize)
+    const uint64_t lim = std::min<uint64_t>(seg_end, f + (uint64_t)a.max_read_size);
+    for (uint64_t i = f; i < lim; ++i)
+      if (bits[i >> 3] & (1u << (i & 7))) return (int64_t)i;
+    return -1;
+  };
+  auto show = [&](int64_t f) { return f < 0 ? std::string("-") : L.pos((uint64_t)f).str(); };
+  std::map<long long, uint64_t> offsets;  // first read's offset in its block -> blocks
+  uint64_t no_read = 0, wrong_pos = 0;
+  std::vector<std::string> bad;
+  for (size_t i = 0; i < blocks.size(); ++i) {
+    const sbh_block &b = *blocks[i];
+    auto it = std::lower_bound(truth.begin(), truth.end(), b.ustart);
+    const int64_t p1 = it == truth.end() ? -1 : (int64_t)*it;
+    const int64_t p2 = next_set(b.ustart);
+    if (p1 >= 0 && L.pos((uint64_t)p1).block == b.start) ++offsets[(long long)L.pos((uint64_t)p1).off];
+    else ++no_read;
+    if (p1 != p2) {
+      const uint64_t prev = i ? blocks[i - 1]->csize : 1;
+      wrong_pos += prev;
+      bad.push_back(std::to_string(b.start) + " (prev block size: " + std::to_string(prev) + "):\t" + show(p1) +
+                    "\t" + show(p2));
+    }
+  }
+  const uint64_t total = L.data.size();
+  auto offsets_info = [&]() {
+    if (no_read && offsets.size() == 1 && offsets.count(0))
+      printf("\n%llu blocks start with a read, %llu blocks didn't contain a read\n",
+             (unsigned long long)offsets[0], (unsigned long long)no_read);
+    else if (!no_read && offsets.size() == 1 && offsets.count(0))
+      printf("\nAll blocks start with reads\n");
+    else
+      printf("\nOffsets of blocks' first reads (%llu blocks didn't contain a read start):\n%s",
+             (unsigned long long)no_read, stats_hist(offsets).c_str());
+  };
+  if (bad.empty()) {
+    printf("First read-position matched in %zu BGZF blocks totaling %sB (compressed)\n", blocks.size(),
+           bytes_fmt(total).c_str());
+    offsets_info();
+  } else {
+    printf("First read-position mismatched in %zu of %zu BGZF blocks\n\n", bad.size(), blocks.size());
+    printf("%llu of %llu (%s) compressed positions would lead to bad splits\n", (unsigned long long)wrong_pos,
+           (unsigned long long)total, jdouble((double)wrong_pos / (double)total).c_str());
+    offsets_info();
+    printf("\n");
+    if ((long)bad.size() <= a.limit) printf("%zu mismatched blocks:\n", bad.size());
+    else printf("%ld of %zu mismatched blocks:\n", a.limit, bad.size());
+    for (size_t i = 0; i < bad.size() && (long)i < a.limit; ++i) printf("\t%s\n", bad[i].c_str());
+  }
+  return 0;
+}
+
 }  // namespace
 
 int main(int argc, char **argv) {
@@ -620,6 +758,7 @@ int main(int argc, char **argv) {
     else if (a.cmd == "full-check") rc = full_check(a);
     else if (a.cmd == "index-blocks") rc = index_blocks(a);
     else if (a.cmd == "index-records") rc = index_records(a);
+    else if (a.cmd == "check-blocks") rc = check_blocks(a);
     else throw Error(SBH_E_ARG, "unknown command " + a.cmd);
     sbh_ctx_destroy(g_ctx);
     return rc;

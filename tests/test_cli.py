@@ -72,3 +72,47 @@ def test_index_blocks_and_records(tmp_path):
         run("index-records", os.path.join(BAMS, name), str(orc))
         assert ob.read_text() == open(os.path.join(BAMS, name + ".blocks")).read()
         assert orc.read_text() == open(os.path.join(BAMS, name + ".records")).read()
+
+
+def _golden_check_blocks(name):
+    with open(os.path.join(GOLDEN, "output", "check-blocks", name), encoding="utf-8") as f:
+        return f.read()
+
+
+def test_check_blocks_spark_bam_1bam():
+    # CheckBlocksTest "1.bam spark-bam": indexed (.records) vs eager, byte-exact
+    assert run("check-blocks", "-s", os.path.join(BAMS, "1.bam")) == _golden_check_blocks("1.bam.s")
+
+
+@pytest.mark.parametrize("name", ["2.bam", "1.block-aligned.bam"])
+def test_check_blocks_matched_outputs(name, tmp_path):
+    # CheckBlocksTest "2.bam" / "1.block-aligned.bam" are default-mode (eager vs hadoop-bam)
+    # runs that matched everywhere, so eager's first-read offsets are the records'; the -s
+    # run (indexed vs eager) prints the same text.  1.block-aligned.bam has no .records in
+    # the reference: it is generated with index-records (IndexRecordsTest-pinned).
+    bam = os.path.join(BAMS, name)
+    recs = bam + ".records"
+    if not os.path.exists(recs):
+        recs = str(tmp_path / (name + ".records"))
+        run("index-records", bam, recs)
+    assert run("check-blocks", "-s", "-r", recs, bam) == _golden_check_blocks(name)
+
+
+def test_check_blocks_mismatch_report(tmp_path):
+    # The mismatch report (CheckBlocksTest "1.bam"): make the indexed side disagree at
+    # block 239479 by replacing its first record 239479:312 with 239479:311 in a copy
+    # of the records file; the counts, ratio and block line follow the golden's format.
+    recs = tmp_path / "1.bam.records"
+    lines = open(os.path.join(BAMS, "1.bam.records")).read().splitlines()
+    lines[lines.index("239479,312")] = "239479,311"
+    recs.write_text("\n".join(lines) + "\n")
+    out = run("check-blocks", "-s", "-r", str(recs), os.path.join(BAMS, "1.bam")).splitlines()
+    want = _golden_check_blocks("1.bam.default").splitlines()
+    assert out[:3] == want[:3]  # "... mismatched in 1 of 25 ...", "", "25871 of 597482 (0.0433...) ..."
+    assert out[-2:] == ["1 mismatched blocks:", "\t239479 (prev block size: 25871):\t239479:311\t239479:312"]
+
+
+def test_check_blocks_needs_spark_bam_mode():
+    r = subprocess.run([CLI, "check-blocks", os.path.join(BAMS, "1.bam")], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode != 0 and "hadoop-bam" in r.stderr
