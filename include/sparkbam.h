@@ -44,6 +44,7 @@ extern "C" {
 #define SBH_E_NEED_HALO 17           /* result depends on bytes past the resident range */
 #define SBH_E_STATE 18               /* call order violated (e.g. check before inflate) */
 #define SBH_E_NOT_FOUND 19           /* Pos not in the indexed block chain            */
+#define SBH_E_BAD_RECORD 20          /* record does not fit its block / the stream (htsjdk decode throws) */
 
 /* ---- full-checker result word (check/.../full/error/Flags.scala:21-45) ----
  *  bit 31     : Success(readsParsed)
@@ -206,6 +207,35 @@ int sbh_run_shard(sbh_shard *sh, uint64_t index_start, uint64_t own_end_file,
  * over the pipeline's launches, each timed on its own stream.  Returns the number of
  * stages written (<= cap, at most 6). */
 int sbh_stage_times(sbh_shard *sh, double *ms, int32_t cap);
+
+/* ---- record field extraction ----
+ * RecordStream from first_flat while the record start is < end_flat, decoded like
+ * htsjdk BAMRecordCodec.decode (check/.../iterator/RecordStream.scala:16-41,
+ * load/.../CanLoadBam.scala:244-264), into columns.  Record starts follow the chain
+ * (next = start + 4 + block_size; the verified eager bitmap when it covers the range).
+ * sbh_records_scan decodes on the device and reports the sizes; sbh_records_fetch copies
+ * the columns of the last scan into caller buffers (any pointer may be NULL). */
+typedef struct {
+  uint64_t n;           /* records                                              */
+  uint64_t name_bytes;  /* read names, each l_read_name bytes with its NUL      */
+  uint64_t cigar_ops;   /* CIGAR ops                                            */
+  uint64_t bases;       /* sequence letters (= quality bytes)                   */
+  uint64_t aux_bytes;   /* raw tag bytes                                        */
+} sbh_records_sizes;
+typedef struct {
+  uint64_t *flat;                                          /* [n] record start (flat) */
+  int32_t *ref_id, *pos, *next_ref_id, *next_pos, *tlen;   /* [n] as stored (pos 0-based, -1 unset) */
+  uint16_t *flag, *bin;                                    /* [n] */
+  uint8_t *mapq;                                           /* [n] */
+  uint64_t *name_off, *cigar_off, *seq_off, *aux_off;      /* [n + 1] exclusive prefix offsets */
+  char *names;                                             /* [name_bytes] */
+  uint32_t *cigar;                                         /* [cigar_ops] op_len << 4 | op */
+  char *seq;                                               /* [bases] "=ACMGRSVTWYHKDBN" letters */
+  uint8_t *qual;                                           /* [bases] phred (0xff: absent) */
+  uint8_t *aux;                                            /* [aux_bytes] tags as stored */
+} sbh_records_out;
+int sbh_records_scan(sbh_shard *sh, uint64_t first_flat, uint64_t end_flat, sbh_records_sizes *out);
+int sbh_records_fetch(sbh_shard *sh, const sbh_records_out *out);
 
 #ifdef __cplusplus
 }

@@ -12,11 +12,12 @@ from ._lib import (BLOCK_EMPTY, BLOCK_TRUNCATED, FULL_FLAGS_MASK, FULL_N_SHIFT, 
                    FULL_SUCCESS, FULL_UNKNOWN, SparkBamError, lib)
 from .device import Context, Shard  # noqa: F401
 from .api import (FLAG_NAMES, Header, Metadata, Pos, Split, bam_header, check_bam,  # noqa: F401
-                  file_splits, full_check, load_bam_count, load_splits_and_reads,
+                  file_splits, full_check, load_bam_count, load_reads, load_splits_and_reads,
                   parse_bam_header)
+from .records import Reads  # noqa: F401
 
 __all__ = [
     "Context", "Shard", "SparkBamError", "Pos", "Header", "Metadata", "Split", "FLAG_NAMES",
     "file_splits", "load_splits_and_reads", "load_bam_count", "check_bam", "full_check",
-    "bam_header", "parse_bam_header", "lib",
+    "bam_header", "parse_bam_header", "lib", "load_reads", "Reads",
 ]

@@ -15,11 +15,12 @@ STATUS_NAMES = {
     0: "SBH_OK", 1: "SBH_E_ARG", 2: "SBH_E_HIP", 3: "SBH_E_NOMEM", 10: "SBH_E_HEADER_PARSE",
     11: "SBH_E_HEADER_SEARCH_FAILED", 12: "SBH_E_TRUNCATED", 13: "SBH_E_INFLATE_SIZE",
     14: "SBH_E_INFLATE_DATA", 15: "SBH_E_BAD_ISIZE", 16: "SBH_E_NO_READ_FOUND",
-    17: "SBH_E_NEED_HALO", 18: "SBH_E_STATE", 19: "SBH_E_NOT_FOUND",
+    17: "SBH_E_NEED_HALO", 18: "SBH_E_STATE", 19: "SBH_E_NOT_FOUND", 20: "SBH_E_BAD_RECORD",
 }
 SBH_E_ARG, SBH_E_HIP, SBH_E_HEADER_PARSE, SBH_E_HEADER_SEARCH_FAILED = 1, 2, 10, 11
 SBH_E_TRUNCATED, SBH_E_INFLATE_SIZE, SBH_E_INFLATE_DATA, SBH_E_BAD_ISIZE = 12, 13, 14, 15
 SBH_E_NO_READ_FOUND, SBH_E_NEED_HALO, SBH_E_STATE, SBH_E_NOT_FOUND = 16, 17, 18, 19
+SBH_E_BAD_RECORD = 20
 
 FULL_SUCCESS = 0x80000000
 FULL_UNKNOWN = 0x40000000
@@ -35,7 +36,7 @@ EXPORTS = [
     "sbh_get_blocks", "sbh_inflate", "sbh_read_flat", "sbh_flat_device_ptr", "sbh_flat_of",
     "sbh_pos_of", "sbh_flat_bound", "sbh_set_contigs", "sbh_check_eager", "sbh_eager_bits", "sbh_check_full",
     "sbh_find_record_start", "sbh_count_records", "sbh_split", "sbh_run_shard",
-    "sbh_stage_times",
+    "sbh_stage_times", "sbh_records_scan", "sbh_records_fetch",
 ]
 
 
@@ -48,6 +49,17 @@ class SbhShardResult(C.Structure):
     _fields_ = [("n_blocks", C.c_uint64), ("comp_bytes", C.c_uint64), ("flat_bytes", C.c_uint64),
                 ("n_true", C.c_uint64), ("first_vpos", C.c_uint64), ("count", C.c_uint64),
                 ("exit_flat", C.c_uint64), ("status", C.c_int32), ("anomalies", C.c_int32)]
+
+
+class SbhRecordsSizes(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("name_bytes", C.c_uint64), ("cigar_ops", C.c_uint64),
+                ("bases", C.c_uint64), ("aux_bytes", C.c_uint64)]
+
+
+class SbhRecordsOut(C.Structure):  # host buffers (sbh_records_out); NULL = not copied
+    _fields_ = [(f, C.c_void_p) for f in (
+        "flat", "ref_id", "pos", "next_ref_id", "next_pos", "tlen", "flag", "bin", "mapq",
+        "name_off", "cigar_off", "seq_off", "aux_off", "names", "cigar", "seq", "qual", "aux")]
 
 
 class SparkBamError(RuntimeError):
@@ -95,6 +107,8 @@ def lib():
         "sbh_count_records": [P, U64, U64, PU64],
         "sbh_split": [P, U64, U64, I32, I32, I32, PU64, PU64],
         "sbh_run_shard": [P, U64, U64, I32, I32, C.POINTER(SbhShardResult)],
+        "sbh_records_scan": [P, U64, U64, C.POINTER(SbhRecordsSizes)],
+        "sbh_records_fetch": [P, C.POINTER(SbhRecordsOut)],
     }
     for name, args in sig.items():
         f = getattr(L, name)

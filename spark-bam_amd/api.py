@@ -12,6 +12,7 @@ import numpy as np
 
 from ._lib import FULL_FLAGS_MASK, FULL_N_SHIFT, SBH_OK, SparkBamError, lib
 from .device import Context
+from .records import Reads
 
 FLAG_NAMES = [  # check/.../full/error/Flags.scala:203-222 (serde order)
     "tooFewFixedBlockBytes", "negativeReadIdx", "tooLargeReadIdx", "negativeReadPos",
@@ -152,6 +153,27 @@ def load_splits_and_reads(path_or_bytes, split_size=DEFAULT_SPLIT_SIZE, ctx=None
                 firsts.append(Pos.from_htsjdk(v))
         ends = firsts[1:] + [Pos(L.data.size, 0)]
         return [Split(a, b) for a, b in zip(firsts, ends)], counts
+    finally:
+        L.close()
+
+
+def load_reads(path_or_bytes, ctx=None, reads_to_check=DEFAULT_READS_TO_CHECK):
+    """CanLoadBam.loadReads (load/.../CanLoadBam.scala:244-264) on one device: every
+    record of the file's BAM stream, in file order, decoded on the GPU into a columnar
+    `Reads` batch (RecordStream.scala:16-41 semantics: records from the first one after
+    the header while they start before the stream's end).  The eager bitmap of the
+    record range is computed first, so record starts come from it in parallel (verified
+    against the chain) rather than from a sequential chain walk."""
+    L = _Loaded(path_or_bytes, ctx, reads_to_check)
+    try:
+        sh = L.shard
+        end = sh.flat_size
+        for b in sh.blocks():
+            if b[5] & 1:  # BLOCK_EMPTY: the stream ends at its flat start
+                end = b[3]
+                break
+        sh.check_eager(L.header_end, end, reads_to_check, want_bits=False)
+        return Reads(sh.records(L.header_end, end), L.names)
     finally:
         L.close()
 

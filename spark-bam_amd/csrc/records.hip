@@ -1,0 +1,174 @@
+// records.hip -- BAM record field extraction on CDNA4.
+//
+// Replaces, for every record of a flat range at once, the decode behind RecordStream
+// (check/.../iterator/RecordStream.scala:16-41) and CanLoadBam.loadReads
+// (load/.../CanLoadBam.scala:244-264): htsjdk BAMRecordCodec.decode of the fixed fields,
+// read name, CIGAR, 4-bit sequence, qualities and the raw tag bytes.  Record starts come
+// from the chain (next = start + 4 + block_size): the verified eager bitmap when it
+// covers the range, otherwise a sequential walk.  Output is columnar: fixed fields as
+// arrays, variable-length fields packed into arenas addressed by exclusive prefix sums.
+#include <algorithm>
+
+#include "sbh_internal.h"
+
+namespace sbh {
+namespace {
+
+__device__ __forceinline__ uint32_t rd_u32(const uint8_t *U, uint64_t p) {
+  return (uint32_t)U[p] | (uint32_t)U[p + 1] << 8 | (uint32_t)U[p + 2] << 16 | (uint32_t)U[p + 3] << 24;
+}
+
+// Record starts = set bits of [first, E): a thread per bitmap word, positions written at
+// the word's exclusive popcount prefix (wpre).
+__global__ void k_bits_positions(const uint32_t *bits, uint64_t begin, uint64_t first, uint64_t E,
+                                 const uint64_t *wpre, uint64_t *pos) {
+  const uint64_t w0 = (first - begin) / 32;
+  const uint64_t w = w0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= (E - begin + 31) / 32) return;
+  uint32_t v = bits[w];
+  const uint64_t p0 = begin + 32 * w;
+  if (p0 < first) v &= ~0u << (uint32_t)(first - p0);
+  if (p0 + 32 > E) v &= (E - p0) >= 32 ? ~0u : ((1u << (uint32_t)(E - p0)) - 1u);
+  uint64_t o = wpre[w - w0];
+  while (v) {
+    pos[o++] = p0 + __builtin_ctz(v);
+    v &= v - 1;
+  }
+}
+
+__global__ void k_word_popcounts(const uint32_t *bits, uint64_t begin, uint64_t first, uint64_t E, uint64_t *cnt) {
+  const uint64_t w0 = (first - begin) / 32;
+  const uint64_t w = w0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= (E - begin + 31) / 32) return;
+  uint32_t v = bits[w];
+  const uint64_t p0 = begin + 32 * w;
+  if (p0 < first) v &= ~0u << (uint32_t)(first - p0);
+  if (p0 + 32 > E) v &= (E - p0) >= 32 ? ~0u : ((1u << (uint32_t)(E - p0)) - 1u);
+  cnt[w - w0] = __popc(v);
+}
+
+// Sequential chain from first while the start is < E (fallback when no verified bitmap).
+__global__ void k_chain_positions(const uint8_t *U, uint64_t first, uint64_t E, uint64_t total, uint64_t cap,
+                                  uint64_t *pos) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint64_t r = first, n = 0;
+  while (r < E && r + 4 <= total && n < cap) {
+    pos[n++] = r;
+    const int64_t nx = (int64_t)r + 4 + (int32_t)rd_u32(U, r);
+    if (nx <= (int64_t)r) break;
+    r = (uint64_t)nx;
+  }
+}
+
+// Per record: name bytes (l_read_name, with the NUL), CIGAR ops, bases, tag bytes
+// (block_size + 4 minus everything before the tags).  bad: a record whose parts do not
+// fit its block or the stream (htsjdk would throw).
+__global__ void k_rec_sizes(const uint8_t *U, const uint64_t *pos, uint64_t n, uint64_t total, uint64_t *nm,
+                            uint64_t *cg, uint64_t *sq, uint64_t *ax, unsigned long long *bad) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t p = pos[i];
+  uint64_t l_name = 0, n_cig = 0, l_seq = 0, l_aux = 0;
+  if (p + 36 > total) {
+    atomicMin(bad, (unsigned long long)i);
+  } else {
+    const int64_t bsz = (int32_t)rd_u32(U, p);
+    l_name = U[p + 12];
+    n_cig = rd_u32(U, p + 16) & 0xffff;
+    const int64_t ls = (int32_t)rd_u32(U, p + 20);
+    const int64_t fixed = 32 + (int64_t)l_name + 4 * (int64_t)n_cig + (ls + 1) / 2 + ls;
+    if (ls < 0 || bsz < fixed || p + 4 + (uint64_t)bsz > total) {
+      atomicMin(bad, (unsigned long long)i);
+      l_name = n_cig = 0;
+    } else {
+      l_seq = (uint64_t)ls;
+      l_aux = (uint64_t)(bsz - fixed);
+    }
+  }
+  nm[i] = l_name;
+  cg[i] = n_cig;
+  sq[i] = l_seq;
+  ax[i] = l_aux;
+}
+
+}  // namespace
+
+namespace {
+
+// One wave per record (grid-stride): lane 0 the fixed fields, all lanes the variable
+// parts -- name, CIGAR (unaligned u32 ops), bases (4-bit codes -> "=ACMGRSVTWYHKDBN"),
+// qualities and tag bytes, each at its prefix-sum offset.
+__global__ __launch_bounds__(256) void k_rec_fields(const uint8_t *__restrict__ U, const uint64_t *pos, uint64_t n,
+                                                    const uint64_t *nm_off, const uint64_t *cg_off,
+                                                    const uint64_t *sq_off, const uint64_t *ax_off, RecCols c) {
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / WAVE);
+  for (uint64_t i = (uint64_t)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE; i < n; i += nw) {
+    const uint64_t p = pos[i];
+    if (lane == 0) {
+      c.ref_id[i] = (int32_t)rd_u32(U, p + 4);
+      c.pos[i] = (int32_t)rd_u32(U, p + 8);
+      const uint32_t bmn = rd_u32(U, p + 12), fnc = rd_u32(U, p + 16);
+      c.mapq[i] = (uint8_t)(bmn >> 8);
+      c.bin[i] = (uint16_t)(bmn >> 16);
+      c.flag[i] = (uint16_t)(fnc >> 16);
+      c.next_ref_id[i] = (int32_t)rd_u32(U, p + 24);
+      c.next_pos[i] = (int32_t)rd_u32(U, p + 28);
+      c.tlen[i] = (int32_t)rd_u32(U, p + 32);
+    }
+    const uint64_t l_name = nm_off[i + 1] - nm_off[i], n_cig = cg_off[i + 1] - cg_off[i];
+    const uint64_t l_seq = sq_off[i + 1] - sq_off[i], l_aux = ax_off[i + 1] - ax_off[i];
+    const uint64_t q_name = p + 36, q_cig = q_name + l_name, q_seq = q_cig + 4 * n_cig;
+    const uint64_t q_qual = q_seq + (l_seq + 1) / 2, q_aux = q_qual + l_seq;
+    for (uint64_t k = lane; k < l_name; k += WAVE) c.names[nm_off[i] + k] = (char)U[q_name + k];
+    for (uint64_t k = lane; k < n_cig; k += WAVE) c.cigar[cg_off[i] + k] = rd_u32(U, q_cig + 4 * k);
+    for (uint64_t k = lane; k < l_seq; k += WAVE) {
+      const uint8_t b = U[q_seq + k / 2];
+      c.seq[sq_off[i] + k] = "=ACMGRSVTWYHKDBN"[(k & 1) ? (b & 15) : (b >> 4)];
+      c.qual[sq_off[i] + k] = U[q_qual + k];
+    }
+    for (uint64_t k = lane; k < l_aux; k += WAVE) c.aux[ax_off[i] + k] = U[q_aux + k];
+  }
+}
+
+}  // namespace
+
+hipError_t scan_exclusive_u64(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *tmp, hipStream_t st);
+
+// cnt, wpre: one u64 per bitmap word of [first, E); tmp: scan_tmp_words(words)
+hipError_t launch_rec_positions_bits(const uint32_t *bits, uint64_t begin, uint64_t first, uint64_t E, uint64_t *cnt,
+                                     uint64_t *wpre, uint64_t *tmp, uint64_t *pos, hipStream_t st) {
+  const uint64_t nw = (E - begin + 31) / 32 - (first - begin) / 32;
+  if (!nw) return hipSuccess;
+  const uint32_t g = (uint32_t)((nw + 255) / 256);
+  hipLaunchKernelGGL(k_word_popcounts, dim3(g), dim3(256), 0, st, bits, begin, first, E, cnt);
+  hipError_t e = scan_exclusive_u64(cnt, wpre, nw, tmp, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_bits_positions, dim3(g), dim3(256), 0, st, bits, begin, first, E, wpre, pos);
+  return hipGetLastError();
+}
+
+hipError_t launch_rec_positions_chain(const uint8_t *U, uint64_t first, uint64_t E, uint64_t total, uint64_t cap,
+                                      uint64_t *pos, hipStream_t st) {
+  hipLaunchKernelGGL(k_chain_positions, dim3(1), dim3(64), 0, st, U, first, E, total, cap, pos);
+  return hipGetLastError();
+}
+
+hipError_t launch_rec_sizes(const uint8_t *U, const uint64_t *pos, uint64_t n, uint64_t total, uint64_t *nm,
+                            uint64_t *cg, uint64_t *sq, uint64_t *ax, unsigned long long *bad, hipStream_t st) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_rec_sizes, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, U, pos, n, total, nm, cg, sq,
+                     ax, bad);
+  return hipGetLastError();
+}
+
+hipError_t launch_rec_fields(const uint8_t *U, const uint64_t *pos, uint64_t n, const uint64_t *nm_off,
+                             const uint64_t *cg_off, const uint64_t *sq_off, const uint64_t *ax_off, const RecCols &c,
+                             hipStream_t st) {
+  if (!n) return hipSuccess;
+  const uint32_t g = (uint32_t)std::min<uint64_t>((n + 3) / 4, 65536);  // 4 records (waves) per workgroup
+  hipLaunchKernelGGL(k_rec_fields, dim3(g), dim3(256), 0, st, U, pos, n, nm_off, cg_off, sq_off, ax_off, c);
+  return hipGetLastError();
+}
+
+}  // namespace sbh

@@ -120,6 +120,24 @@ struct sbh_shard {
   hipStream_t s_lz = nullptr, s_eg = nullptr;
   std::vector<hipEvent_t> pev;
   DBuf<uint64_t> defer;
+  // record field extraction (sbh_records_scan / fetch): positions, sizes -> offsets, columns
+  struct Recs {
+    DBuf<uint64_t> pos, wcnt, wpre, nm, cg, sq, ax, nmo, cgo, sqo, axo;
+    DBuf<int32_t> ref_id, p0, nref, npos, tlen;
+    DBuf<uint16_t> flag, bin;
+    DBuf<uint8_t> mapq, qual, aux;
+    DBuf<char> names, seq;
+    DBuf<uint32_t> cigar;
+    sbh_records_sizes sz{};
+    bool valid = false;
+    void release() {
+      for (auto *b : {&pos, &wcnt, &wpre, &nm, &cg, &sq, &ax, &nmo, &cgo, &sqo, &axo}) b->release();
+      for (auto *b : {&ref_id, &p0, &nref, &npos, &tlen}) b->release();
+      flag.release(); bin.release(); mapq.release(); qual.release(); aux.release();
+      names.release(); seq.release(); cigar.release();
+      valid = false;
+    }
+  } rec;
   hipEvent_t ev[9] = {};
   bool ev_ok = false, timing = false;
   double stage_ms[6] = {0, 0, 0, 0, 0, 0};
@@ -268,6 +286,7 @@ int sbh_shard_destroy(sbh_shard *sh) {
   if (sh->s_lz) (void)hipStreamDestroy(sh->s_lz);
   if (sh->s_eg) (void)hipStreamDestroy(sh->s_eg);
   sh->defer.release();
+  sh->rec.release();
   if (sh->h_ctr) (void)hipHostFree(sh->h_ctr);
   delete sh;
   return SBH_OK;
@@ -998,6 +1017,102 @@ int sbh_stage_times(sbh_shard *sh, double *ms, int32_t cap) {
   int n = cap < 6 ? cap : 6;
   for (int i = 0; i < n; ++i) ms[i] = sh->stage_ms[i];
   return n;
+}
+
+// RecordStream + BAMRecordCodec.decode over [first, end) (check/.../iterator/RecordStream.scala:16-41,
+// load/.../CanLoadBam.scala:244-264): record starts by the chain, sizes -> prefix offsets,
+// then one wave per record decodes into the columns.
+int sbh_records_scan(sbh_shard *sh, uint64_t first, uint64_t end_flat, sbh_records_sizes *out) {
+  if (!sh || !out) return SBH_E_ARG;
+  sbh_ctx *ctx = sh->ctx;
+  if (!sh->inflated) return fail(ctx, SBH_E_STATE, "records before inflate");
+  if (first > sh->utotal) return SBH_E_ARG;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  hipStream_t st = ctx->stream;
+  auto &R = sh->rec;
+  R.valid = false;
+  const uint64_t total = seg_end_of(sh, first);
+  const uint64_t E = std::min(std::min(end_flat, sh->utotal), total);
+  uint64_t n = 0;
+  int32_t anomalies = 0;
+  rc = count_records_impl(sh, first, E, &n, &anomalies);
+  if (rc) return rc;
+  HIPCHK(ctx, R.pos.ensure(n));
+  const bool covered = sh->bits_valid && sh->bits_begin <= first && E <= sh->bits_end && anomalies == 0;
+  if (n && covered) {
+    const uint64_t nw = (E - sh->bits_begin + 31) / 32 - (first - sh->bits_begin) / 32;
+    HIPCHK(ctx, R.wcnt.ensure(nw));
+    HIPCHK(ctx, R.wpre.ensure(nw));
+    HIPCHK(ctx, sh->tmp.ensure(scan_tmp_words(nw)));
+    HIPCHK(ctx, launch_rec_positions_bits(sh->bits.p, sh->bits_begin, first, E, R.wcnt.p, R.wpre.p, sh->tmp.p, R.pos.p,
+                                          st));
+  } else if (n) {
+    HIPCHK(ctx, launch_rec_positions_chain(sh->U.p, first, E, total, n, R.pos.p, st));
+  }
+  // per-record sizes (a trailing zero makes the exclusive scan's last entry the total)
+  DBuf<uint64_t> *sz[4] = {&R.nm, &R.cg, &R.sq, &R.ax}, *of[4] = {&R.nmo, &R.cgo, &R.sqo, &R.axo};
+  for (int k = 0; k < 4; ++k) {
+    HIPCHK(ctx, sz[k]->ensure(n + 1));
+    HIPCHK(ctx, of[k]->ensure(n + 1));
+    HIPCHK(ctx, hipMemsetAsync(sz[k]->p + n, 0, 8, st));
+  }
+  unsigned long long *bad = sh->ctr.p + 24;
+  HIPCHK(ctx, hipMemsetAsync(bad, 0xff, 8, st));
+  HIPCHK(ctx, launch_rec_sizes(sh->U.p, R.pos.p, n, total, R.nm.p, R.cg.p, R.sq.p, R.ax.p, bad, st));
+  HIPCHK(ctx, sh->tmp.ensure(scan_tmp_words(n + 1)));
+  for (int k = 0; k < 4; ++k) HIPCHK(ctx, scan_exclusive_u64(sz[k]->p, of[k]->p, n + 1, sh->tmp.p, st));
+  uint64_t tot[4] = {0, 0, 0, 0};
+  for (int k = 0; k < 4; ++k) HIPCHK(ctx, hipMemcpyAsync(&tot[k], of[k]->p + n, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 24, bad, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  if (sh->h_ctr[24] != ~0ull) return fail(ctx, SBH_E_BAD_RECORD, "record %llu of the range is malformed",
+                                          (unsigned long long)sh->h_ctr[24]);
+  HIPCHK(ctx, R.ref_id.ensure(n)); HIPCHK(ctx, R.p0.ensure(n)); HIPCHK(ctx, R.nref.ensure(n));
+  HIPCHK(ctx, R.npos.ensure(n)); HIPCHK(ctx, R.tlen.ensure(n)); HIPCHK(ctx, R.flag.ensure(n));
+  HIPCHK(ctx, R.bin.ensure(n)); HIPCHK(ctx, R.mapq.ensure(n));
+  HIPCHK(ctx, R.names.ensure(tot[0])); HIPCHK(ctx, R.cigar.ensure(tot[1]));
+  HIPCHK(ctx, R.seq.ensure(tot[2])); HIPCHK(ctx, R.qual.ensure(tot[2])); HIPCHK(ctx, R.aux.ensure(tot[3]));
+  const RecCols cols{R.ref_id.p, R.p0.p, R.nref.p, R.npos.p, R.tlen.p, R.flag.p, R.bin.p, R.mapq.p,
+                     R.names.p, R.cigar.p, R.seq.p, R.qual.p, R.aux.p};
+  HIPCHK(ctx, launch_rec_fields(sh->U.p, R.pos.p, n, R.nmo.p, R.cgo.p, R.sqo.p, R.axo.p, cols, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  R.sz = sbh_records_sizes{n, tot[0], tot[1], tot[2], tot[3]};
+  R.valid = true;
+  *out = R.sz;
+  return SBH_OK;
+}
+
+int sbh_records_fetch(sbh_shard *sh, const sbh_records_out *o) {
+  if (!sh || !o) return SBH_E_ARG;
+  sbh_ctx *ctx = sh->ctx;
+  auto &R = sh->rec;
+  if (!R.valid) return fail(ctx, SBH_E_STATE, "records_fetch without a records_scan");
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  const uint64_t n = R.sz.n;
+  auto cp = [&](void *dst, const void *src, uint64_t bytes) -> hipError_t {
+    return dst && bytes ? hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) : hipSuccess;
+  };
+  HIPCHK(ctx, cp(o->flat, R.pos.p, 8 * n));
+  HIPCHK(ctx, cp(o->ref_id, R.ref_id.p, 4 * n));
+  HIPCHK(ctx, cp(o->pos, R.p0.p, 4 * n));
+  HIPCHK(ctx, cp(o->next_ref_id, R.nref.p, 4 * n));
+  HIPCHK(ctx, cp(o->next_pos, R.npos.p, 4 * n));
+  HIPCHK(ctx, cp(o->tlen, R.tlen.p, 4 * n));
+  HIPCHK(ctx, cp(o->flag, R.flag.p, 2 * n));
+  HIPCHK(ctx, cp(o->bin, R.bin.p, 2 * n));
+  HIPCHK(ctx, cp(o->mapq, R.mapq.p, n));
+  HIPCHK(ctx, cp(o->name_off, R.nmo.p, 8 * (n + 1)));
+  HIPCHK(ctx, cp(o->cigar_off, R.cgo.p, 8 * (n + 1)));
+  HIPCHK(ctx, cp(o->seq_off, R.sqo.p, 8 * (n + 1)));
+  HIPCHK(ctx, cp(o->aux_off, R.axo.p, 8 * (n + 1)));
+  HIPCHK(ctx, cp(o->names, R.names.p, R.sz.name_bytes));
+  HIPCHK(ctx, cp(o->cigar, R.cigar.p, 4 * R.sz.cigar_ops));
+  HIPCHK(ctx, cp(o->seq, R.seq.p, R.sz.bases));
+  HIPCHK(ctx, cp(o->qual, R.qual.p, R.sz.bases));
+  HIPCHK(ctx, cp(o->aux, R.aux.p, R.sz.aux_bytes));
+  return SBH_OK;
 }
 
 }  // extern "C"

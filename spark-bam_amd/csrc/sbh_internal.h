@@ -65,4 +65,25 @@ hipError_t launch_huff(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, 
 hipError_t launch_lz(DevBlocks blocks, uint64_t nblocks, const uint32_t *tok, uint8_t *U,
                      hipStream_t stream);
 
+// Record field extraction (records.hip): device columns of a decoded batch (the host
+// view is sbh_records_out in sparkbam.h).
+struct RecCols {
+  int32_t *ref_id, *pos, *next_ref_id, *next_pos, *tlen;
+  uint16_t *flag, *bin;
+  uint8_t *mapq;
+  char *names;
+  uint32_t *cigar;
+  char *seq;
+  uint8_t *qual, *aux;
+};
+hipError_t launch_rec_positions_bits(const uint32_t *bits, uint64_t begin, uint64_t first, uint64_t E, uint64_t *cnt,
+                                     uint64_t *wpre, uint64_t *tmp, uint64_t *pos, hipStream_t st);
+hipError_t launch_rec_positions_chain(const uint8_t *U, uint64_t first, uint64_t E, uint64_t total, uint64_t cap,
+                                      uint64_t *pos, hipStream_t st);
+hipError_t launch_rec_sizes(const uint8_t *U, const uint64_t *pos, uint64_t n, uint64_t total, uint64_t *nm,
+                            uint64_t *cg, uint64_t *sq, uint64_t *ax, unsigned long long *bad, hipStream_t st);
+hipError_t launch_rec_fields(const uint8_t *U, const uint64_t *pos, uint64_t n, const uint64_t *nm_off,
+                             const uint64_t *cg_off, const uint64_t *sq_off, const uint64_t *ax_off, const RecCols &c,
+                             hipStream_t st);
+
 }  // namespace sbh

@@ -4,7 +4,8 @@ import weakref
 
 import numpy as np
 
-from ._lib import (SBH_OK, SbhBlock, SbhShardResult, SparkBamError, lib)
+from ._lib import (SBH_OK, SbhBlock, SbhRecordsOut, SbhRecordsSizes, SbhShardResult, SparkBamError,
+                   lib)
 
 
 def _check(ctx_handle, rc):
@@ -206,6 +207,28 @@ class Shard:
                                  max_read_size, C.byref(r))
         self._c(rc)
         return {f: getattr(r, f) for f, _ in SbhShardResult._fields_}
+
+    def records(self, first_flat, end_flat):
+        """RecordStream + BAMRecordCodec.decode of the records from first_flat while the
+        start is < end_flat (RecordStream.scala:16-41), decoded on the GPU: a dict of
+        numpy columns (fixed fields per record; names / cigar / seq / qual / aux packed,
+        with [n + 1] prefix offsets)."""
+        sz = SbhRecordsSizes()
+        self._c(lib().sbh_records_scan(self.h, first_flat, end_flat, C.byref(sz)))
+        n = sz.n
+        cols = {
+            "flat": np.empty(n, np.uint64), "ref_id": np.empty(n, np.int32), "pos": np.empty(n, np.int32),
+            "next_ref_id": np.empty(n, np.int32), "next_pos": np.empty(n, np.int32),
+            "tlen": np.empty(n, np.int32), "flag": np.empty(n, np.uint16), "bin": np.empty(n, np.uint16),
+            "mapq": np.empty(n, np.uint8), "name_off": np.empty(n + 1, np.uint64),
+            "cigar_off": np.empty(n + 1, np.uint64), "seq_off": np.empty(n + 1, np.uint64),
+            "aux_off": np.empty(n + 1, np.uint64), "names": np.empty(sz.name_bytes, np.uint8),
+            "cigar": np.empty(sz.cigar_ops, np.uint32), "seq": np.empty(sz.bases, np.uint8),
+            "qual": np.empty(sz.bases, np.uint8), "aux": np.empty(sz.aux_bytes, np.uint8),
+        }
+        out = SbhRecordsOut(**{k: v.ctypes.data if v.size else None for k, v in cols.items()})
+        self._c(lib().sbh_records_fetch(self.h, C.byref(out)))
+        return cols
 
     def stage_times(self):
         """[index, inflate+eager pipeline, eager (sum of launches), records, k_huff

@@ -69,8 +69,9 @@ def test_parse_bam_header_from_oracle_flat():
 
 
 def test_no_gpu_context_fails_loudly():
-    import torch
-    if torch.cuda.is_available():
+    # a GPU box exposes the KFD device node (torch's check is unreliable once another
+    # library in the process has initialised HIP)
+    if os.path.exists("/dev/kfd"):
         pytest.skip("GPU present")
     h = C.c_void_p()
     assert sb.lib().sbh_ctx_create(0, C.byref(h)) != 0
