@@ -56,21 +56,32 @@ def main():
     import torch
     import torch.distributed as dist
 
-    torch.cuda.set_device(local_rank)
+    # One rank per GPU over RCCL.  More ranks than devices (a rehearsal of the N>1 path on
+    # a one-GPU box) share the devices round-robin and exchange over gloo instead.
+    ndev = max(1, torch.cuda.device_count())
+    backend = "nccl" if world <= ndev else "gloo"
+    device = local_rank % ndev
+    xdev = "cuda" if backend == "nccl" else "cpu"
+    torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            log(f"note: {world} ranks on {ndev} device(s): gloo exchange (rehearsal, not a scaling run)")
+            dist.init_process_group("gloo")
 
     import synth
     from __graft_entry__ import load_package
 
     sb = load_package()
+    import spark_bam_amd.sharded as sharded
 
     # ---- input generation (not timed) ----
     t0 = time.time()
     p = synth.params(synth.SEEDS["B"], shape=synth.SHAPE_SHORT, level=6,
                      threads=min(16, os.cpu_count() or 1))
     seg = synth.Segment(p, args.records_per_gpu, world, rank, halo_blocks=16)
-    own = torch.tensor([seg.own_csize], dtype=torch.int64, device="cuda")
+    own = torch.tensor([seg.own_csize], dtype=torch.int64, device=xdev)
     if world > 1:
         gathered = [torch.zeros_like(own) for _ in range(world)]
         dist.all_gather(gathered, own)
@@ -82,25 +93,27 @@ def main():
         f"(owned {seg.own_csize / 2**30:.3f} GiB, file {seg.file_size / 2**30:.3f} GiB) "
         f"in {time.time() - t0:.1f}s")
 
-    ctx = sb.Context(local_rank)
+    ctx = sb.Context(device)
     shard = ctx.shard(seg.comp, file_offset=seg.file_offset, file_size=seg.file_size)
     header = synth.header_bytes()
     names, contig_len, _ = sb.parse_bam_header(header)
     shard.set_contigs(contig_len)
 
-    result_t = torch.zeros(4, dtype=torch.int64, device="cuda")
+    result_t = torch.zeros(5, dtype=torch.int64, device=xdev)
 
     def step():
         r = shard.run(seg.file_offset, seg.own_end)
         if r["status"] != 0:
             raise RuntimeError(f"run_shard status {r['status']}")
+        ex = shard.exit_vpos(r)  # the chain's exit from the owned range (None: the stream end)
+        ex = -1 if ex is None else ex
+        mine = [r["first_vpos"], r["count"], r["n_true"], r["flat_bytes"], ex]
         if world > 1:  # RCCL allgather of the per-shard split records (stitching)
-            result_t.copy_(torch.tensor([r["first_vpos"], r["count"], r["n_true"], r["flat_bytes"]],
-                                        dtype=torch.int64))
+            result_t.copy_(torch.tensor(mine, dtype=torch.int64))
             out = [torch.zeros_like(result_t) for _ in range(world)]
             dist.all_gather(out, result_t)
             return r, [o.cpu().tolist() for o in out]
-        return r, [[r["first_vpos"], r["count"], r["n_true"], r["flat_bytes"]]]
+        return r, [mine]
 
     for _ in range(args.warmup):
         step()
@@ -119,7 +132,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=xdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
@@ -128,7 +141,10 @@ def main():
     total_true = sum(x[2] for x in allr)
     total_flat = sum(x[3] for x in allr)
     expect = world * args.records_per_gpu
-    ok = total_records == expect and total_true == expect
+    parts = [sharded.RankPart(i, i, [x[0] if x[1] else None], [x[1]], x[0] if x[1] else None, x[1],
+                              None if x[4] < 0 else x[4]) for i, x in enumerate(allr)]
+    _, _, stitch = sharded.stitch(parts, seg.file_size)
+    ok = total_records == expect and total_true == expect and stitch["ok"]
     firsts = [x[0] for x in allr if x[1] > 0]
 
     stage_ms = stage_acc / args.steps
@@ -187,11 +203,13 @@ def main():
                 "records_per_gpu": args.records_per_gpu,
                 "compressed_bytes": int(sum(own_sizes)),
                 "decompressed_bytes": int(total_flat),
-                "parallelism": f"dp{world} byte-range shards + RCCL allgather stitch",
+                "parallelism": f"dp{world} byte-range shards + "
+                               f"{'RCCL' if backend == 'nccl' else 'gloo (rehearsal)'} allgather stitch",
             },
             "records_per_s": round(total_records * args.steps / elapsed, 1),
             "compressed_GBps": round(sum(own_sizes) * args.steps / elapsed / 1e9, 3),
             "correct": bool(ok),
+            "stitch_ok": bool(stitch["ok"]),
             "records": int(total_records),
             "stages_ms_rank0": {"index": round(stage_ms[0], 3),
                                 "inflate+eager pipeline": round(stage_ms[1], 3),
@@ -229,7 +247,8 @@ def main():
     if world > 1:
         dist.destroy_process_group()
     if not ok:
-        log(f"STITCH CHECK FAILED: records {total_records} true {total_true} expected {expect}")
+        log(f"STITCH CHECK FAILED: records {total_records} true {total_true} expected {expect}; "
+            f"stitch {stitch}")
         sys.exit(3)
 
 

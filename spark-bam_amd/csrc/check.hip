@@ -821,7 +821,8 @@ __global__ __launch_bounds__(256) void k_popcount(const uint32_t *bits, uint64_t
 // eager checker rejects); those ranges fall back to an exact sequential walk.
 __global__ __launch_bounds__(256) void k_verify_chain(const uint8_t *U, const uint32_t *bits, uint64_t begin,
                                                        uint64_t bits_end, uint64_t from, uint64_t E, uint64_t total,
-                                                       unsigned long long *n_anom, unsigned long long *first_anom) {
+                                                       unsigned long long *n_anom, unsigned long long *first_anom,
+                                                       unsigned long long *exit_pos) {
   const uint64_t w = ((from - begin) / 32 & ~3ull) + 4 * ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x);
   const uint64_t w_end = (E - begin + 31) / 32;
   if (w >= w_end) return;
@@ -875,6 +876,11 @@ __global__ __launch_bounds__(256) void k_verify_chain(const uint8_t *U, const ui
     if (!ok) {
       atomicAdd(n_anom, 1ull);
       atomicMin(first_anom, (unsigned long long)s);
+    } else if (nxt_set == ~0ull) {
+      // the last record of [from, E): its successor is the chain's exit (the first record
+      // at/after E, or the stream end); atomicMin since FP bits would add more candidates,
+      // and those runs are re-walked exactly anyway
+      atomicMin(exit_pos, (unsigned long long)(step > total ? total : step));
     }
     k = kn;
   }
@@ -883,12 +889,11 @@ __global__ __launch_bounds__(256) void k_verify_chain(const uint8_t *U, const ui
 // Exact sequential chain walk (fallback): counts records r in [first, E) following
 // next = r + 4 + block_size, stopping at the stream end.
 __global__ void k_chain_walk(const uint8_t *U, uint64_t first, uint64_t E, uint64_t total,
-                             unsigned long long *count, unsigned long long *last) {
+                             unsigned long long *count, unsigned long long *exit_pos) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  uint64_t r = first, n = 0, prev = first;
+  uint64_t r = first, n = 0;
   while (r < E && r + 4 <= total) {
     ++n;
-    prev = r;
     const int32_t rem = (int32_t)((uint32_t)U[r] | ((uint32_t)U[r + 1] << 8) | ((uint32_t)U[r + 2] << 16) |
                                   ((uint32_t)U[r + 3] << 24));
     const int64_t nx = (int64_t)r + 4 + rem;
@@ -896,7 +901,7 @@ __global__ void k_chain_walk(const uint8_t *U, uint64_t first, uint64_t E, uint6
     r = (uint64_t)nx;
   }
   *count = n;
-  *last = prev;
+  *exit_pos = r > total ? total : r;  // first record at/after E (or where the walk stopped)
 }
 
 // Positions the pipelined eager pass deferred (their exact check reached flat bytes that
@@ -996,17 +1001,17 @@ hipError_t launch_popcount(const uint32_t *bits, uint64_t begin, uint64_t from, 
 
 hipError_t launch_verify_chain(const uint8_t *U, const uint32_t *bits, uint64_t begin, uint64_t bits_end,
                                uint64_t from, uint64_t E, uint64_t total, unsigned long long *n_anom,
-                               unsigned long long *first_anom, hipStream_t st) {
+                               unsigned long long *first_anom, unsigned long long *exit_pos, hipStream_t st) {
   if (E <= from) return hipSuccess;
   const uint64_t nw = (E - begin + 31) / 32 - ((from - begin) / 32 & ~3ull);
   hipLaunchKernelGGL(k_verify_chain, dim3(ngrid(nw, 1024)), dim3(256), 0, st, U, bits, begin, bits_end, from,
-                     E, total, n_anom, first_anom);
+                     E, total, n_anom, first_anom, exit_pos);
   return hipGetLastError();
 }
 
 hipError_t launch_chain_walk(const uint8_t *U, uint64_t first, uint64_t E, uint64_t total,
-                             unsigned long long *count, unsigned long long *last, hipStream_t st) {
-  hipLaunchKernelGGL(k_chain_walk, dim3(1), dim3(64), 0, st, U, first, E, total, count, last);
+                             unsigned long long *count, unsigned long long *exit_pos, hipStream_t st) {
+  hipLaunchKernelGGL(k_chain_walk, dim3(1), dim3(64), 0, st, U, first, E, total, count, exit_pos);
   return hipGetLastError();
 }
 

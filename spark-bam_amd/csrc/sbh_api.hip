@@ -43,7 +43,7 @@ hipError_t launch_popcount(const uint32_t *bits, uint64_t begin, uint64_t from, 
                            unsigned long long *acc, hipStream_t st);
 hipError_t launch_verify_chain(const uint8_t *U, const uint32_t *bits, uint64_t begin, uint64_t bits_end,
                                uint64_t from, uint64_t E, uint64_t total, unsigned long long *n_anom,
-                               unsigned long long *first_anom, hipStream_t st);
+                               unsigned long long *first_anom, unsigned long long *exit_pos, hipStream_t st);
 hipError_t launch_chain_walk(const uint8_t *U, uint64_t first, uint64_t E, uint64_t total,
                              unsigned long long *count, unsigned long long *last, hipStream_t st);
 }  // namespace sbh
@@ -736,7 +736,11 @@ int sbh_find_record_start(sbh_shard *sh, uint64_t from, int32_t rtc, int32_t max
               (unsigned long long)from);
 }
 
-static int count_records_impl(sbh_shard *sh, uint64_t first, uint64_t E, uint64_t *count, int32_t *anomalies) {
+// Records of the chain from `first` whose start is < E; *exit_flat (optional) = the
+// first chain record at/after E (the successor of the last counted record, clamped to
+// the stream end) -- what the next shard's first record must equal when stitching.
+static int count_records_impl(sbh_shard *sh, uint64_t first, uint64_t E, uint64_t *count, int32_t *anomalies,
+                              uint64_t *exit_flat = nullptr) {
   sbh_ctx *ctx = sh->ctx;
   hipStream_t st = ctx->stream;
   const uint64_t total = seg_end_of(sh, first);
@@ -744,20 +748,24 @@ static int count_records_impl(sbh_shard *sh, uint64_t first, uint64_t E, uint64_
   if (anomalies) *anomalies = 0;
   if (first >= E) {
     *count = 0;
+    if (exit_flat) *exit_flat = first;
     return SBH_OK;
   }
   unsigned long long *c = sh->ctr.p + 16;
   const bool covered = sh->bits_valid && sh->bits_begin <= first && E <= sh->bits_end;
   if (covered) {
-    HIPCHK(ctx, hipMemsetAsync(c, 0, 16, st));
+    HIPCHK(ctx, hipMemsetAsync(c, 0, 8, st));
     HIPCHK(ctx, hipMemsetAsync(c + 1, 0xff, 8, st));
     HIPCHK(ctx, hipMemsetAsync(c + 2, 0, 8, st));
-    HIPCHK(ctx, launch_verify_chain(sh->U.p, sh->bits.p, sh->bits_begin, sh->bits_end, first, E, total, c, c + 1, st));
+    HIPCHK(ctx, hipMemsetAsync(c + 3, 0xff, 8, st));
+    HIPCHK(ctx, launch_verify_chain(sh->U.p, sh->bits.p, sh->bits_begin, sh->bits_end, first, E, total, c, c + 1,
+                                    c + 3, st));
     HIPCHK(ctx, launch_popcount(sh->bits.p, sh->bits_begin, first, E, c + 2, st));
-    HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 16, c, 24, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 16, c, 32, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipStreamSynchronize(st));
-    if (sh->h_ctr[16] == 0) {
+    if (sh->h_ctr[16] == 0 && sh->h_ctr[19] != ~0ull) {
       *count = sh->h_ctr[18];
+      if (exit_flat) *exit_flat = sh->h_ctr[19];
       return SBH_OK;
     }
     if (anomalies) *anomalies = (int32_t)std::min<uint64_t>(sh->h_ctr[16], INT32_MAX);
@@ -766,6 +774,7 @@ static int count_records_impl(sbh_shard *sh, uint64_t first, uint64_t E, uint64_
   HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 20, c + 4, 16, hipMemcpyDeviceToHost, st));
   HIPCHK(ctx, hipStreamSynchronize(st));
   *count = sh->h_ctr[20];
+  if (exit_flat) *exit_flat = sh->h_ctr[21];
   return SBH_OK;
 }
 
@@ -985,14 +994,14 @@ int sbh_run_shard(sbh_shard *sh, uint64_t index_start, uint64_t own_end_file, in
     res->count = 0;
     rc = SBH_OK;
   } else if (rc == SBH_OK) {
-    rc = count_records_impl(sh, first, E, &res->count, &res->anomalies);
+    rc = count_records_impl(sh, first, E, &res->count, &res->anomalies, &res->exit_flat);
     uint64_t bp = 0;
     uint32_t off = 0;
     if (!rc && sbh_pos_of(sh, first, &bp, &off) == SBH_OK) res->first_vpos = (bp << 16) | off;
   }
+  if (res->count == 0) res->exit_flat = E;
   mark(sh, 6);
   sh->timing = false;
-  res->exit_flat = E;
   if (sh->ev_ok) {
     (void)hipEventSynchronize(sh->ev[6]);
     // [index, inflate + eager pipeline, eager (sum of launches), split/count, k_huff, k_lz]

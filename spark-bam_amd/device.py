@@ -208,6 +208,16 @@ class Shard:
         self._c(rc)
         return {f: getattr(r, f) for f, _ in SbhShardResult._fields_}
 
+    def exit_vpos(self, result):
+        """The htsjdk vpos of a run() result's chain exit (the first record at/after the
+        owned end), or None when the chain ran into the end of the resident stream."""
+        if not result["count"]:
+            return None
+        bp, off = C.c_uint64(), C.c_uint32()
+        if lib().sbh_pos_of(self.h, result["exit_flat"], C.byref(bp), C.byref(off)) != SBH_OK:
+            return None
+        return (bp.value << 16) | off.value
+
     def records(self, first_flat, end_flat):
         """RecordStream + BAMRecordCodec.decode of the records from first_flat while the
         start is < end_flat (RecordStream.scala:16-41), decoded on the GPU: a dict of
