@@ -237,6 +237,18 @@ typedef struct {
 int sbh_records_scan(sbh_shard *sh, uint64_t first_flat, uint64_t end_flat, sbh_records_sizes *out);
 int sbh_records_fetch(sbh_shard *sh, const sbh_records_out *out);
 
+/* ---- loadBamIntervals ----
+ * CanLoadBam.loadBamIntervals (load/.../CanLoadBam.scala:78-154) after the host has turned
+ * the intervals into BAI chunks (getIntevalChunks, :410-444; Index.scala:11-93): for each
+ * chunk [chunk_begin[c], chunk_end[c]) (flat positions of the chunk's start/end Pos), the
+ * records from the chunk start while the start is < the chunk end, in chunk order, kept
+ * when region(record) (:446-454) overlaps one of the intervals: (iv_ref[k], [iv_begin[k],
+ * iv_end[k])) 0-based half-open, sorted by (ref, begin) and disjoint (a merged LociSet).
+ * Leaves the kept records' columns for sbh_records_fetch, like sbh_records_scan. */
+int sbh_records_scan_regions(sbh_shard *sh, const uint64_t *chunk_begin, const uint64_t *chunk_end,
+                             uint64_t n_chunks, const int32_t *iv_ref, const int64_t *iv_begin,
+                             const int64_t *iv_end, uint32_t n_iv, sbh_records_sizes *out);
+
 #ifdef __cplusplus
 }
 #endif

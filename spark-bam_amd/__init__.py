@@ -6,7 +6,8 @@ Import name: ``spark_bam_amd`` (the directory name contains a hyphen, so load it
 
   bgzf:   Pos, Header.make, Metadata, FindBlockStart, Stream (blocks / inflated bytes)
   check:  eager.Checker / full.Checker (batched over positions), FindRecordStart
-  load:   load_splits_and_reads / load_bam_count (CanLoadBam), FileSplits
+  load:   load_splits_and_reads / load_bam_count / load_reads / load_bam_intervals
+          (CanLoadBam), FileSplits, read_bai (bam.index.Index)
 """
 from ._lib import (BLOCK_EMPTY, BLOCK_TRUNCATED, FULL_FLAGS_MASK, FULL_N_SHIFT,  # noqa: F401
                    FULL_SUCCESS, FULL_UNKNOWN, SparkBamError, lib)
@@ -15,9 +16,12 @@ from .api import (FLAG_NAMES, Header, Metadata, Pos, Split, bam_header, check_ba
                   file_splits, full_check, load_bam_count, load_reads, load_splits_and_reads,
                   parse_bam_header)
 from .records import Reads  # noqa: F401
+from .intervals import (Chunk, Index, get_interval_chunks, load_bam_intervals,  # noqa: F401
+                        parse_loci, read_bai)
 
 __all__ = [
     "Context", "Shard", "SparkBamError", "Pos", "Header", "Metadata", "Split", "FLAG_NAMES",
     "file_splits", "load_splits_and_reads", "load_bam_count", "check_bam", "full_check",
-    "bam_header", "parse_bam_header", "lib", "load_reads", "Reads",
+    "bam_header", "parse_bam_header", "lib", "load_reads", "Reads", "Chunk", "Index",
+    "read_bai", "parse_loci", "get_interval_chunks", "load_bam_intervals",
 ]

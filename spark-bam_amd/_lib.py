@@ -36,7 +36,7 @@ EXPORTS = [
     "sbh_get_blocks", "sbh_inflate", "sbh_read_flat", "sbh_flat_device_ptr", "sbh_flat_of",
     "sbh_pos_of", "sbh_flat_bound", "sbh_set_contigs", "sbh_check_eager", "sbh_eager_bits", "sbh_check_full",
     "sbh_find_record_start", "sbh_count_records", "sbh_split", "sbh_run_shard",
-    "sbh_stage_times", "sbh_records_scan", "sbh_records_fetch",
+    "sbh_stage_times", "sbh_records_scan", "sbh_records_fetch", "sbh_records_scan_regions",
 ]
 
 
@@ -109,6 +109,7 @@ def lib():
         "sbh_run_shard": [P, U64, U64, I32, I32, C.POINTER(SbhShardResult)],
         "sbh_records_scan": [P, U64, U64, C.POINTER(SbhRecordsSizes)],
         "sbh_records_fetch": [P, C.POINTER(SbhRecordsOut)],
+        "sbh_records_scan_regions": [P, P, P, U64, P, P, P, C.c_uint32, C.POINTER(SbhRecordsSizes)],
     }
     for name, args in sig.items():
         f = getattr(L, name)

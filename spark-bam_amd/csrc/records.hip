@@ -91,6 +91,57 @@ __global__ void k_rec_sizes(const uint8_t *U, const uint64_t *pos, uint64_t n, u
   ax[i] = l_aux;
 }
 
+
+// loadBamIntervals' record filter (load/.../CanLoadBam.scala:137-152, region() at :446-454):
+// keep[i] = 1 when the record's reference span overlaps one of the query intervals.
+// Region(contig, getStart - 1, getEnd) is [pos, pos + reference length of the CIGAR)
+// (ops M D N = X consume the reference); no contig (refID < 0), an unmapped read
+// (htsjdk getAlignmentEnd = 0) or an empty span never intersects.  Intervals are the
+// LociSet's merged half-open ranges as (ref, begin, end), sorted by (ref, begin), so
+// ends are sorted too: binary search for the first interval of the record's ref whose
+// end exceeds pos.  A record whose fields run past `total` is kept, so the size pass
+// reports it as malformed (htsjdk would throw on it).
+__global__ void k_region_keep(const uint8_t *__restrict__ U, const uint64_t *pos, uint64_t n, uint64_t total,
+                              const int32_t *iv_ref, const int64_t *iv_begin, const int64_t *iv_end, uint32_t n_iv,
+                              uint64_t *keep) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t p = pos[i];
+  uint64_t k = 0;
+  if (p + 36 > total) {
+    k = 1;
+  } else {
+    const int32_t ref = (int32_t)rd_u32(U, p + 4), rp = (int32_t)rd_u32(U, p + 8);
+    const uint32_t fnc = rd_u32(U, p + 16), nc = fnc & 0xffff;
+    const uint64_t q = p + 36 + U[p + 12];
+    if (q + 4ull * nc > total) {
+      k = 1;
+    } else if (ref >= 0 && !((fnc >> 16) & 4) && rp >= 0) {
+      int64_t span = 0;
+      for (uint32_t c = 0; c < nc; ++c) {
+        const uint32_t op = rd_u32(U, q + 4ull * c);
+        const uint32_t t = op & 15;
+        if (t == 0 || t == 2 || t == 3 || t == 7 || t == 8) span += op >> 4;
+      }
+      if (span > 0) {
+        const int64_t b = rp, e = b + span;
+        uint32_t lo = 0, hi = n_iv;  // first interval with (ref, end) > (ref, b)
+        while (lo < hi) {
+          const uint32_t m = (lo + hi) >> 1;
+          if (iv_ref[m] < ref || (iv_ref[m] == ref && iv_end[m] <= b)) lo = m + 1; else hi = m;
+        }
+        k = lo < n_iv && iv_ref[lo] == ref && iv_begin[lo] < e;
+      }
+    }
+  }
+  keep[i] = k;
+}
+
+__global__ void k_compact_u64(const uint64_t *in, const uint64_t *keep, const uint64_t *kpre, uint64_t n,
+                              uint64_t *out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && keep[i]) out[kpre[i]] = in[i];
+}
 }  // namespace
 
 namespace {
@@ -168,6 +219,22 @@ hipError_t launch_rec_fields(const uint8_t *U, const uint64_t *pos, uint64_t n, 
   if (!n) return hipSuccess;
   const uint32_t g = (uint32_t)std::min<uint64_t>((n + 3) / 4, 65536);  // 4 records (waves) per workgroup
   hipLaunchKernelGGL(k_rec_fields, dim3(g), dim3(256), 0, st, U, pos, n, nm_off, cg_off, sq_off, ax_off, c);
+  return hipGetLastError();
+}
+
+hipError_t launch_region_keep(const uint8_t *U, const uint64_t *pos, uint64_t n, uint64_t total, const int32_t *iv_ref,
+                              const int64_t *iv_begin, const int64_t *iv_end, uint32_t n_iv, uint64_t *keep,
+                              hipStream_t st) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_region_keep, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, U, pos, n, total, iv_ref,
+                     iv_begin, iv_end, n_iv, keep);
+  return hipGetLastError();
+}
+
+hipError_t launch_compact_u64(const uint64_t *in, const uint64_t *keep, const uint64_t *kpre, uint64_t n,
+                              uint64_t *out, hipStream_t st) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_compact_u64, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, in, keep, kpre, n, out);
   return hipGetLastError();
 }
 

@@ -122,7 +122,9 @@ struct sbh_shard {
   DBuf<uint64_t> defer;
   // record field extraction (sbh_records_scan / fetch): positions, sizes -> offsets, columns
   struct Recs {
-    DBuf<uint64_t> pos, wcnt, wpre, nm, cg, sq, ax, nmo, cgo, sqo, axo;
+    DBuf<uint64_t> pos, wcnt, wpre, nm, cg, sq, ax, nmo, cgo, sqo, axo, keep, kpre, pos2;
+    DBuf<int64_t> iv_b, iv_e;
+    DBuf<int32_t> iv_ref;
     DBuf<int32_t> ref_id, p0, nref, npos, tlen;
     DBuf<uint16_t> flag, bin;
     DBuf<uint8_t> mapq, qual, aux;
@@ -131,7 +133,8 @@ struct sbh_shard {
     sbh_records_sizes sz{};
     bool valid = false;
     void release() {
-      for (auto *b : {&pos, &wcnt, &wpre, &nm, &cg, &sq, &ax, &nmo, &cgo, &sqo, &axo}) b->release();
+      for (auto *b : {&pos, &wcnt, &wpre, &nm, &cg, &sq, &ax, &nmo, &cgo, &sqo, &axo, &keep, &kpre, &pos2}) b->release();
+      iv_b.release(); iv_e.release(); iv_ref.release();
       for (auto *b : {&ref_id, &p0, &nref, &npos, &tlen}) b->release();
       flag.release(); bin.release(); mapq.release(); qual.release(); aux.release();
       names.release(); seq.release(); cigar.release();
@@ -182,6 +185,10 @@ static int set_device(sbh_ctx *ctx) {
 }
 
 extern "C" {
+
+static int records_positions(sbh_shard *sh, uint64_t first, uint64_t E, uint64_t total, uint64_t n, int32_t anomalies,
+                             uint64_t *pos);
+static int records_finish(sbh_shard *sh, uint64_t n, uint64_t total, sbh_records_sizes *out);
 
 const char *sbh_version(void) { return "sparkbam-hip 0.1 (gfx950)"; }
 
@@ -1038,7 +1045,6 @@ int sbh_records_scan(sbh_shard *sh, uint64_t first, uint64_t end_flat, sbh_recor
   if (first > sh->utotal) return SBH_E_ARG;
   int rc = set_device(ctx);
   if (rc) return rc;
-  hipStream_t st = ctx->stream;
   auto &R = sh->rec;
   R.valid = false;
   const uint64_t total = seg_end_of(sh, first);
@@ -1048,17 +1054,35 @@ int sbh_records_scan(sbh_shard *sh, uint64_t first, uint64_t end_flat, sbh_recor
   rc = count_records_impl(sh, first, E, &n, &anomalies);
   if (rc) return rc;
   HIPCHK(ctx, R.pos.ensure(n));
+  rc = records_positions(sh, first, E, total, n, anomalies, R.pos.p);
+  if (rc) return rc;
+  return records_finish(sh, n, total, out);
+}
+
+// Record starts of the chain from first while the start is < E, written at pos (cap n).
+static int records_positions(sbh_shard *sh, uint64_t first, uint64_t E, uint64_t total, uint64_t n, int32_t anomalies,
+                             uint64_t *pos) {
+  sbh_ctx *ctx = sh->ctx;
+  hipStream_t st = ctx->stream;
+  auto &R = sh->rec;
   const bool covered = sh->bits_valid && sh->bits_begin <= first && E <= sh->bits_end && anomalies == 0;
   if (n && covered) {
     const uint64_t nw = (E - sh->bits_begin + 31) / 32 - (first - sh->bits_begin) / 32;
     HIPCHK(ctx, R.wcnt.ensure(nw));
     HIPCHK(ctx, R.wpre.ensure(nw));
     HIPCHK(ctx, sh->tmp.ensure(scan_tmp_words(nw)));
-    HIPCHK(ctx, launch_rec_positions_bits(sh->bits.p, sh->bits_begin, first, E, R.wcnt.p, R.wpre.p, sh->tmp.p, R.pos.p,
-                                          st));
+    HIPCHK(ctx, launch_rec_positions_bits(sh->bits.p, sh->bits_begin, first, E, R.wcnt.p, R.wpre.p, sh->tmp.p, pos, st));
   } else if (n) {
-    HIPCHK(ctx, launch_rec_positions_chain(sh->U.p, first, E, total, n, R.pos.p, st));
+    HIPCHK(ctx, launch_rec_positions_chain(sh->U.p, first, E, total, n, pos, st));
   }
+  return SBH_OK;
+}
+
+// Sizes -> prefix offsets -> columns for the n record starts in R.pos.
+static int records_finish(sbh_shard *sh, uint64_t n, uint64_t total, sbh_records_sizes *out) {
+  sbh_ctx *ctx = sh->ctx;
+  hipStream_t st = ctx->stream;
+  auto &R = sh->rec;
   // per-record sizes (a trailing zero makes the exclusive scan's last entry the total)
   DBuf<uint64_t> *sz[4] = {&R.nm, &R.cg, &R.sq, &R.ax}, *of[4] = {&R.nmo, &R.cgo, &R.sqo, &R.axo};
   for (int k = 0; k < 4; ++k) {
@@ -1090,6 +1114,70 @@ int sbh_records_scan(sbh_shard *sh, uint64_t first, uint64_t end_flat, sbh_recor
   R.valid = true;
   *out = R.sz;
   return SBH_OK;
+}
+
+// loadBamIntervals (load/.../CanLoadBam.scala:78-154): for each BAI chunk, the records from
+// chunk.start while the start is < chunk.end (records.seek(chunk.start) + takeWhile), then the
+// region filter on the device, then the same column decode as sbh_records_scan.
+int sbh_records_scan_regions(sbh_shard *sh, const uint64_t *chunk_begin, const uint64_t *chunk_end, uint64_t n_chunks,
+                             const int32_t *iv_ref, const int64_t *iv_begin, const int64_t *iv_end, uint32_t n_iv,
+                             sbh_records_sizes *out) {
+  if (!sh || !out || (n_chunks && (!chunk_begin || !chunk_end)) || (n_iv && (!iv_ref || !iv_begin || !iv_end)))
+    return SBH_E_ARG;
+  sbh_ctx *ctx = sh->ctx;
+  if (!sh->inflated) return fail(ctx, SBH_E_STATE, "records before inflate");
+  for (uint32_t k = 0; k < n_iv; ++k) {
+    if (iv_begin[k] >= iv_end[k]) return fail(ctx, SBH_E_ARG, "interval %u is empty", k);
+    if (k && (iv_ref[k] < iv_ref[k - 1] || (iv_ref[k] == iv_ref[k - 1] && iv_begin[k] < iv_end[k - 1])))
+      return fail(ctx, SBH_E_ARG, "intervals must be sorted by (ref, begin) and disjoint");
+  }
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  hipStream_t st = ctx->stream;
+  auto &R = sh->rec;
+  R.valid = false;
+  std::vector<uint64_t> cn(n_chunks, 0), cfirst(n_chunks, 0), cE(n_chunks, 0), ctot(n_chunks, 0);
+  std::vector<int32_t> can(n_chunks, 0);
+  uint64_t n = 0;
+  for (uint64_t c = 0; c < n_chunks; ++c) {
+    const uint64_t first = chunk_begin[c];
+    if (first > sh->utotal) return fail(ctx, SBH_E_ARG, "chunk %llu starts past the stream", (unsigned long long)c);
+    ctot[c] = seg_end_of(sh, first);
+    cE[c] = std::min(std::min(chunk_end[c], sh->utotal), ctot[c]);
+    cfirst[c] = first;
+    if (first < cE[c]) {
+      rc = count_records_impl(sh, first, cE[c], &cn[c], &can[c]);
+      if (rc) return rc;
+    }
+    n += cn[c];
+  }
+  HIPCHK(ctx, R.pos2.ensure(n + 1));
+  uint64_t o = 0;
+  for (uint64_t c = 0; c < n_chunks; ++c) {
+    rc = records_positions(sh, cfirst[c], cE[c], ctot[c], cn[c], can[c], R.pos2.p + o);
+    if (rc) return rc;
+    o += cn[c];
+  }
+  HIPCHK(ctx, R.keep.ensure(n + 1));
+  HIPCHK(ctx, R.kpre.ensure(n + 1));
+  HIPCHK(ctx, R.iv_ref.ensure(n_iv + 1));
+  HIPCHK(ctx, R.iv_b.ensure(n_iv + 1));
+  HIPCHK(ctx, R.iv_e.ensure(n_iv + 1));
+  if (n_iv) {
+    HIPCHK(ctx, hipMemcpyAsync(R.iv_ref.p, iv_ref, 4ull * n_iv, hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(R.iv_b.p, iv_begin, 8ull * n_iv, hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(R.iv_e.p, iv_end, 8ull * n_iv, hipMemcpyHostToDevice, st));
+  }
+  HIPCHK(ctx, hipMemsetAsync(R.keep.p + n, 0, 8, st));
+  HIPCHK(ctx, launch_region_keep(sh->U.p, R.pos2.p, n, sh->utotal, R.iv_ref.p, R.iv_b.p, R.iv_e.p, n_iv, R.keep.p, st));
+  HIPCHK(ctx, sh->tmp.ensure(scan_tmp_words(n + 1)));
+  HIPCHK(ctx, scan_exclusive_u64(R.keep.p, R.kpre.p, n + 1, sh->tmp.p, st));
+  uint64_t kept = 0;
+  HIPCHK(ctx, hipMemcpyAsync(&kept, R.kpre.p + n, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  HIPCHK(ctx, R.pos.ensure(kept + 1));
+  HIPCHK(ctx, launch_compact_u64(R.pos2.p, R.keep.p, R.kpre.p, n, R.pos.p, st));
+  return records_finish(sh, kept, sh->utotal, out);
 }
 
 int sbh_records_fetch(sbh_shard *sh, const sbh_records_out *o) {

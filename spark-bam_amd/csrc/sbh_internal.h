@@ -85,5 +85,10 @@ hipError_t launch_rec_sizes(const uint8_t *U, const uint64_t *pos, uint64_t n, u
 hipError_t launch_rec_fields(const uint8_t *U, const uint64_t *pos, uint64_t n, const uint64_t *nm_off,
                              const uint64_t *cg_off, const uint64_t *sq_off, const uint64_t *ax_off, const RecCols &c,
                              hipStream_t st);
+hipError_t launch_region_keep(const uint8_t *U, const uint64_t *pos, uint64_t n, uint64_t total, const int32_t *iv_ref,
+                              const int64_t *iv_begin, const int64_t *iv_end, uint32_t n_iv, uint64_t *keep,
+                              hipStream_t st);
+hipError_t launch_compact_u64(const uint64_t *in, const uint64_t *keep, const uint64_t *kpre, uint64_t n,
+                              uint64_t *out, hipStream_t st);
 
 }  // namespace sbh

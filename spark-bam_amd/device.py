@@ -225,6 +225,24 @@ class Shard:
         with [n + 1] prefix offsets)."""
         sz = SbhRecordsSizes()
         self._c(lib().sbh_records_scan(self.h, first_flat, end_flat, C.byref(sz)))
+        return self._records_fetch(sz)
+
+    def records_regions(self, chunks_flat, intervals):
+        """loadBamIntervals' per-chunk record streams + region filter on the GPU
+        (CanLoadBam.scala:123-152): chunks_flat = [(begin_flat, end_flat)] in chunk order;
+        intervals = [(ref_idx, begin, end)] 0-based half-open, sorted and disjoint.
+        Returns the kept records' columns (same layout as records())."""
+        cb = np.ascontiguousarray([c[0] for c in chunks_flat], dtype=np.uint64)
+        ce = np.ascontiguousarray([c[1] for c in chunks_flat], dtype=np.uint64)
+        ir = np.ascontiguousarray([i[0] for i in intervals], dtype=np.int32)
+        ib = np.ascontiguousarray([i[1] for i in intervals], dtype=np.int64)
+        ie = np.ascontiguousarray([i[2] for i in intervals], dtype=np.int64)
+        sz = SbhRecordsSizes()
+        self._c(lib().sbh_records_scan_regions(self.h, _ptr(cb), _ptr(ce), cb.size, _ptr(ir), _ptr(ib),
+                                               _ptr(ie), ir.size, C.byref(sz)))
+        return self._records_fetch(sz)
+
+    def _records_fetch(self, sz):
         n = sz.n
         cols = {
             "flat": np.empty(n, np.uint64), "ref_id": np.empty(n, np.int32), "pos": np.empty(n, np.int32),

@@ -1,0 +1,301 @@
+"""loadBamIntervals: BAI chunks -> GPU record streams + region filter.
+
+Host side (small, per query):
+  * `read_bai` -- the BAI reader of check/.../bam/index/Index.scala:11-93 and Read.scala
+    (magic "BAI\\1", per reference: bins with chunks, the 37450 metadata pseudo-bin, the
+    linear index).
+  * `parse_loci` -- the LociSet the reference builds from interval strings
+    (CanLoadBam.scala:61-76: LociSet(ParsedLoci(intervals), ContigLengths(path))).
+  * `get_interval_chunks` -- CanLoadBam.getIntevalChunks (CanLoadBam.scala:410-444), which
+    calls htsjdk's BAMFileReader.getFileSpan(QueryInterval[], BAMIndex).  htsjdk is a
+    third-party dependency absent from /root/reference; its published algorithm is
+    restated here: per interval AbstractBAMFileIndex.getSpanOverlapping (UCSC reg2bins
+    over 5 bin levels, the chunks of the present bins, Chunk.optimizeChunkList with the
+    linear-index minimum offset), then BAMFileSpan.merge (optimizeChunkList(all, 0)).
+  * `capped_cost_groups` -- the partitioning of chunks by estimated size
+    (CanLoadBam.scala:105-112, Chunk.size = end - start with the compression ratio).
+
+Device side: the whole BAM is indexed and inflated on the GPU, and
+`Shard.records_regions` (sbh_records_scan_regions) produces the records of every chunk
+(records.seek(chunk.start) while pos < chunk.end, CanLoadBam.scala:132-152) and keeps
+those whose region overlaps the LociSet -- the region test runs in a HIP kernel
+(k_region_keep, records.hip).  Pinned by LoadBAMTest's "indexed *" cases.
+"""
+import re
+import struct
+from collections import namedtuple
+
+import numpy as np
+
+from ._lib import SparkBamError
+from .api import DEFAULT_READS_TO_CHECK, DEFAULT_SPLIT_SIZE, Pos, _Loaded
+from .records import Reads
+
+METADATA_BIN_ID = 37450  # Index.scala:91
+BIN_GENOMIC_SPAN = (1 << 29) - 1  # htsjdk GenomicIndexUtil.BIN_GENOMIC_SPAN
+LIDX_SHIFT = 14  # htsjdk LinearIndex.BAM_LIDX_SHIFT
+DEFAULT_COMPRESSION_RATIO = 3.0  # bgzf EstimatedCompressionRatio default
+
+Chunk = namedtuple("Chunk", "start end")  # Index.Chunk(start: Pos, end: Pos), Index.scala:55-60
+Bin = namedtuple("Bin", "id chunks")
+BaiMetadata = namedtuple("BaiMetadata", "unmapped_begin unmapped_end num_mapped num_unmapped")
+Reference = namedtuple("Reference", "bins offsets metadata")
+IntervalReads = namedtuple("IntervalReads", "reads partitions counts")
+
+
+def chunk_size(chunk, ratio=DEFAULT_COMPRESSION_RATIO):
+    """Chunk.size (Index.scala:57-59) = end - start (Pos.-, Pos.scala:17-22)."""
+    return chunk.end.minus(chunk.start, ratio)
+
+
+class Index:
+    """Index(references) (Index.scala:11-40)."""
+
+    def __init__(self, references):
+        self.references = references
+
+    @property
+    def chunks(self):
+        return [c for r in self.references for b in r.bins for c in b.chunks]
+
+    @property
+    def offsets(self):
+        return [o for r in self.references for o in r.offsets]
+
+
+def read_bai(path_or_bytes):
+    """Index.apply(path) for a .bai (Index.scala:71-89) with Read.scala's readers:
+    i32 counts, u64 virtual offsets, the metadata pseudo-bin (exactly 2 chunks, else
+    IllegalStateException), at most one metadata per reference."""
+    if isinstance(path_or_bytes, (bytes, bytearray, memoryview)):
+        b = bytes(path_or_bytes)
+    else:
+        with open(path_or_bytes, "rb") as f:
+            b = f.read()
+    if b[:4] != b"BAI\1":
+        raise IOError("Bad BAI magic")
+    p = [4]
+
+    def i32():
+        v = struct.unpack_from("<i", b, p[0])[0]
+        p[0] += 4
+        return v
+
+    def u64():
+        v = struct.unpack_from("<Q", b, p[0])[0]
+        p[0] += 8
+        return v
+
+    refs = []
+    for _ in range(i32()):
+        bins, meta = [], None
+        for _ in range(i32()):
+            bid = i32()
+            nch = i32()
+            if bid == METADATA_BIN_ID:
+                if nch != 2:
+                    raise ValueError(f"Metadata bin {bid} should have 2 chunks, found {nch}")
+                m = BaiMetadata(Pos.from_htsjdk(u64()), Pos.from_htsjdk(u64()), u64(), u64())
+                if meta is not None:
+                    raise ValueError(f"Found two metadata: {meta}, {m}")
+                meta = m
+            else:
+                bins.append(Bin(bid, [Chunk(Pos.from_htsjdk(u64()), Pos.from_htsjdk(u64()))
+                                      for _ in range(nch)]))
+        offsets = [Pos.from_htsjdk(u64()) for _ in range(i32())]
+        refs.append(Reference(bins, offsets, meta))
+    return Index(refs)
+
+
+_RANGE = re.compile(r"^([^:,\s]+):(\d+)-(\d*)$")
+_LOCUS = re.compile(r"^([^:,\s]+):(\d+)$")
+
+
+def parse_loci(intervals, contig_lengths):
+    """LociSet(ParsedLoci(intervals), ContigLengths) (CanLoadBam.scala:61-76), following
+    genomics-loci 2.0.4's ParsedLoci forms: "contig:start-end" (0-based half-open),
+    "contig:start-" (to the contig's end), "contig:locus" (one base), "contig" (whole
+    contig), "all", "none"; comma-separated.  Returns {contig: [(begin, end)]} with each
+    contig's ranges sorted and merged (a Guava RangeSet).  Only the "contig:start-end"
+    form is pinned by the reference's tests (LoadBAMTest)."""
+    if isinstance(intervals, str):
+        intervals = [intervals]
+    out = {}
+    for text in intervals:
+        for item in re.split(r"[,\s]+", text.strip()):
+            if not item or item == "none":
+                continue
+            if item == "all":
+                for c, n in contig_lengths.items():
+                    out.setdefault(c, []).append((0, n))
+                continue
+            m = _RANGE.match(item)
+            if m:
+                c, a = m.group(1), int(m.group(2))
+                e = int(m.group(3)) if m.group(3) else None
+            else:
+                m = _LOCUS.match(item)
+                if m:
+                    c, a = m.group(1), int(m.group(2))
+                    e = a + 1
+                else:
+                    c, a, e = item, 0, None
+            if c not in contig_lengths:
+                raise ValueError(f"Unknown contig {c!r} in intervals")
+            if e is None:
+                e = contig_lengths[c]
+            if e > a:
+                out.setdefault(c, []).append((a, e))
+    for c, rs in out.items():
+        rs.sort()
+        merged = []
+        for a, e in rs:
+            if merged and a <= merged[-1][1]:
+                merged[-1][1] = max(merged[-1][1], e)
+            else:
+                merged.append([a, e])
+        out[c] = [tuple(r) for r in merged]
+    return out
+
+
+def _reg2bins(start_pos, end_pos):
+    """htsjdk AbstractBAMFileIndex.getBinsOverlapping (1-based closed query)."""
+    start = 0 if start_pos <= 0 else (start_pos - 1) & BIN_GENOMIC_SPAN
+    end = BIN_GENOMIC_SPAN if end_pos <= 0 else (end_pos - 1) & BIN_GENOMIC_SPAN
+    if start > end:
+        return set()
+    bins = {0}
+    for off, sh in ((1, 26), (9, 23), (73, 20), (585, 17), (4681, 14)):
+        bins.update(range(off + (start >> sh), off + (end >> sh) + 1))
+    return bins
+
+
+def _cmp(a, b):
+    """htsjdk Chunk.compareTo: by start, then end (signum)."""
+    x = (a[0] > b[0]) - (a[0] < b[0])
+    return x if x else (a[1] > b[1]) - (a[1] < b[1])
+
+
+def _overlaps(a, b):
+    """htsjdk Chunk.overlaps."""
+    c = _cmp(a, b)
+    if c == 0:
+        return True
+    left, right = (a, b) if c == -1 else (b, a)
+    lb, rb = left[1] >> 16, right[0] >> 16
+    if lb > rb:
+        return True
+    if lb == rb:
+        return (left[1] & 0xFFFF) > (right[0] & 0xFFFF)
+    return False
+
+
+def _adjacent(a, b):
+    """htsjdk Chunk.isAdjacentTo (same BGZF block address at the touching ends)."""
+    return (a[1] >> 16) == (b[0] >> 16) or (a[0] >> 16) == (b[1] >> 16)
+
+
+def optimize_chunk_list(chunks, minimum_offset):
+    """htsjdk Chunk.optimizeChunkList over (start_vpos, end_vpos) pairs."""
+    out = []
+    for ch in sorted(chunks):
+        if ch[1] <= minimum_offset:
+            continue  # linear-index optimisation
+        if not out:
+            out.append(list(ch))
+            continue
+        last = out[-1]
+        if not _overlaps(last, ch) and not _adjacent(last, ch):
+            out.append(list(ch))
+        elif ch[1] > last[1]:
+            last[1] = ch[1]
+    return [tuple(c) for c in out]
+
+
+def _span_overlapping(index, ref_idx, start_pos, end_pos):
+    """htsjdk AbstractBAMFileIndex.getSpanOverlapping -> list of vpos chunks or None."""
+    if ref_idx < 0 or ref_idx >= len(index.references):
+        return None
+    ref = index.references[ref_idx]
+    wanted = _reg2bins(start_pos, end_pos)
+    chunks = [(c.start.to_htsjdk(), c.end.to_htsjdk()) for b in ref.bins if b.id in wanted for c in b.chunks]
+    if not chunks:
+        return None
+    lbin = (0 if start_pos <= 0 else start_pos - 1) >> LIDX_SHIFT
+    min_off = ref.offsets[lbin].to_htsjdk() if lbin < len(ref.offsets) else 0
+    return optimize_chunk_list(chunks, min_off)
+
+
+def get_interval_chunks(index, loci, contig_names):
+    """CanLoadBam.getIntevalChunks (CanLoadBam.scala:410-444): LociSet ->
+    htsjdk QueryIntervals (1-based closed: Interval(contig, begin + 1, end)) ->
+    BAMFileReader.getFileSpan -> [Chunk]."""
+    spans = []
+    for contig, ranges in loci.items():
+        idx = contig_names.index(contig)
+        for a, e in ranges:
+            spans.append(_span_overlapping(index, idx, a + 1, e))
+    merged = optimize_chunk_list([c for s in spans if s for c in s], 0)
+    return [Chunk(Pos.from_htsjdk(a), Pos.from_htsjdk(b)) for a, b in merged]
+
+
+def capped_cost_groups(items, cost, limit):
+    """cappedCostGroups (CanLoadBam.scala:105-112): consecutive items into groups,
+    a group closing before the item that would push its summed cost past `limit`
+    (every group takes at least one item)."""
+    groups, cur, tot = [], [], 0.0
+    for it in items:
+        c = cost(it)
+        if cur and tot + c > limit:
+            groups.append(cur)
+            cur, tot = [], 0.0
+        cur.append(it)
+        tot += c
+    if cur:
+        groups.append(cur)
+    return groups
+
+
+def _flat_of_pos(shard, pos):
+    try:
+        return shard.flat_of(pos.block_pos, pos.offset)
+    except SparkBamError:
+        if pos.block_pos >= shard.file_offset + shard.n:
+            return shard.flat_size
+        raise
+
+
+def load_bam_intervals(path, intervals, split_size=DEFAULT_SPLIT_SIZE,
+                       estimated_compression_ratio=DEFAULT_COMPRESSION_RATIO, ctx=None, bai=None,
+                       reads_to_check=DEFAULT_READS_TO_CHECK):
+    """CanLoadBam.loadBamIntervals(path, splitSize, ratio)(intervals*)
+    (CanLoadBam.scala:61-154) on one device.  Returns IntervalReads(reads, partitions,
+    counts): the kept records as a columnar Reads batch in partition/chunk order, the
+    chunk partitions (getNumPartitions = len(partitions)) and per-partition counts."""
+    index = read_bai(bai if bai is not None else str(path) + ".bai")
+    L = _Loaded(path, ctx, reads_to_check)
+    try:
+        sh = L.shard
+        names = list(L.names)
+        loci = parse_loci(intervals, dict(zip(names, (int(x) for x in L.contig_len))))
+        chunks = get_interval_chunks(index, loci, names)
+        parts = capped_cost_groups(chunks, lambda c: chunk_size(c, estimated_compression_ratio),
+                                   float(split_size))
+        flat = [(_flat_of_pos(sh, c.start), _flat_of_pos(sh, c.end)) for c in chunks]
+        ivs = sorted((names.index(c), a, e) for c, rs in loci.items() for a, e in rs)
+        if flat:
+            lo, hi = min(f[0] for f in flat), max(f[1] for f in flat)
+            sh.check_eager(lo, min(hi, sh.flat_size), reads_to_check, want_bits=False)
+        cols = sh.records_regions(flat, ivs)
+        # per-partition counts: chunks are disjoint in flat space; a record belongs to
+        # the chunk whose [begin, end) holds its start
+        begins = np.asarray([f[0] for f in flat], dtype=np.uint64)
+        which = np.searchsorted(begins, cols["flat"], side="right") - 1
+        per_chunk = np.bincount(which, minlength=len(chunks)) if len(chunks) else np.zeros(0, np.int64)
+        counts, k = [], 0
+        for g in parts:
+            counts.append(int(per_chunk[k:k + len(g)].sum()))
+            k += len(g)
+        return IntervalReads(Reads(cols, names), parts, counts)
+    finally:
+        L.close()

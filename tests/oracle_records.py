@@ -123,3 +123,46 @@ def sam_line(cols, i, refs):
         "*" if nref < 0 else "=" if nref == ref else refs[nref], str(s("next_pos") + 1), str(s("tlen")),
         sq or "*", "*" if len(ql) == 0 or ql[0] == 0xFF else "".join(chr(int(x) + 33) for x in ql),
     ] + _tag_strings(bytes(c["aux"][s("aux_off"):int(c["aux_off"][i + 1])])))
+
+
+REF_OPS = (0, 2, 3, 7, 8)  # M D N = X consume the reference
+
+
+def region(cols, i):
+    """CanLoadBam.region (load/.../CanLoadBam.scala:446-454) as (ref_idx, begin, end) or
+    None: no contig for refID -1; htsjdk getAlignmentEnd is 0 for an unmapped read and
+    alignmentStart + referenceLength - 1 otherwise; Region(contig, start - 1, end)."""
+    ref = int(cols["ref_id"][i])
+    if ref < 0:
+        return None
+    start = int(cols["pos"][i]) + 1
+    if cols["flag"][i] & 4:
+        end = 0
+    else:
+        ops = cols["cigar"][cols["cigar_off"][i]:cols["cigar_off"][i + 1]]
+        end = start + sum(int(o) >> 4 for o in ops if (int(o) & 15) in REF_OPS) - 1
+    return ref, start - 1, end
+
+
+def region_kept(cols, i, loci_by_ref):
+    """LociSet.intersects(region): some half-open range [a, b) of the contig with
+    max(a, begin) < min(b, end) (a non-empty Guava range intersection)."""
+    r = region(cols, i)
+    if r is None:
+        return False
+    ref, b, e = r
+    return any(max(a, b) < min(z, e) for a, z in loci_by_ref.get(ref, ()))
+
+
+def interval_records(flat, chunk_flats, loci_by_ref):
+    """loadBamIntervals' record loop (CanLoadBam.scala:132-152), one chunk after the
+    other: the chain from the chunk start while the start is < the chunk end, kept when
+    the region overlaps.  Returns (decoded columns of the kept records, per-chunk counts)."""
+    starts, per = [], []
+    for a, e in chunk_flats:
+        cs = record_starts(flat, a, min(e, len(flat)))
+        cols = decode(flat, cs)
+        kept = [cs[i] for i in range(len(cs)) if region_kept(cols, i, loci_by_ref)]
+        starts += kept
+        per.append(len(kept))
+    return decode(flat, starts), per
