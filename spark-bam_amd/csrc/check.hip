@@ -886,6 +886,81 @@ __global__ __launch_bounds__(256) void k_verify_chain(const uint8_t *U, const ui
   }
 }
 
+// ---- chain marking by pointer doubling (the parallel replacement of k_chain_walk when
+// the eager bitmap holds false positives or misses chain records) ----
+// Nodes are the n set bits of [from, E) in order (pos[], word prefix counts wpre from word
+// (from - begin) / 32).  J[i] = index of the node the chain steps to from node i
+// (next = s + 4 + block_size), or CM_TERM when the step leaves [from, E) / reaches the
+// stream end (a valid end of the counted range), or CM_BROKEN when it lands on a
+// position whose bit is clear or does not move forward (the exact walk must decide).
+// Since every step moves forward, the nodes reachable from node 0 are exactly the chain.
+__global__ void k_cm_succ(const uint8_t *U, const uint32_t *bits, uint64_t begin, uint64_t from, uint64_t E,
+                          uint64_t total, const uint64_t *pos, const uint64_t *wpre, uint64_t n, uint32_t *J,
+                          uint32_t *J0, uint64_t *mark) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t s = pos[i];
+  const uint32_t term = (uint32_t)n, broken = (uint32_t)n + 1;
+  uint32_t j;
+  if (s + 4 > total) {
+    j = term;
+  } else {
+    const int32_t rem = (int32_t)((uint32_t)U[s] | ((uint32_t)U[s + 1] << 8) | ((uint32_t)U[s + 2] << 16) |
+                                  ((uint32_t)U[s + 3] << 24));
+    const int64_t nx = (int64_t)s + 4 + rem;
+    if (nx <= (int64_t)s) {
+      j = broken;
+    } else if ((uint64_t)nx >= E || (uint64_t)nx + 4 > total) {
+      j = term;
+    } else {
+      const uint64_t q = (uint64_t)nx - begin, w = q >> 5;
+      const uint32_t v = bits[w], b = (uint32_t)(q & 31);
+      if (!((v >> b) & 1u)) {
+        j = broken;
+      } else {
+        const uint64_t w0 = (from - begin) >> 5;
+        uint32_t below = v & ((1u << b) - 1u);
+        if (w == w0) below &= ~0u << (uint32_t)((from - begin) & 31);  // bits before `from` are not nodes
+        j = (uint32_t)(wpre[w - w0] + __popc(below));
+      }
+    }
+  }
+  J[i] = j;
+  J0[i] = j;
+  mark[i] = i == 0;
+}
+
+// One doubling round: nodes at distance < 2^k are marked; mark their 2^k-successors
+// (Jin) and square the jump (Jout = Jin o Jin; terminal codes stay).  Marks written by
+// other threads during the round are reachable nodes too, so the race only marks early.
+__global__ void k_cm_round(const uint32_t *Jin, uint32_t *Jout, uint64_t *mark, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t j = Jin[i];
+  if (j < n) {
+    if (mark[i]) mark[j] = 1;
+    Jout[i] = Jin[j];
+  } else {
+    Jout[i] = j;
+  }
+}
+
+// The chain's last counted node (marked, J0 terminal): its successor is the exit.
+__global__ void k_cm_exit(const uint8_t *U, const uint64_t *pos, const uint32_t *J0, const uint64_t *mark,
+                          uint64_t n, uint64_t total, unsigned long long *exit_pos) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !mark[i] || J0[i] < n) return;
+  const uint64_t s = pos[i];
+  uint64_t x = total;
+  if (s + 4 <= total) {
+    const int32_t rem = (int32_t)((uint32_t)U[s] | ((uint32_t)U[s + 1] << 8) | ((uint32_t)U[s + 2] << 16) |
+                                  ((uint32_t)U[s + 3] << 24));
+    const int64_t nx = (int64_t)s + 4 + rem;
+    x = nx > (int64_t)total ? total : (uint64_t)nx;
+  }
+  atomicMin(exit_pos, (unsigned long long)x);
+}
+
 // Exact sequential chain walk (fallback): counts records r in [first, E) following
 // next = r + 4 + block_size, stopping at the stream end.
 __global__ void k_chain_walk(const uint8_t *U, uint64_t first, uint64_t E, uint64_t total,
@@ -1012,6 +1087,26 @@ hipError_t launch_verify_chain(const uint8_t *U, const uint32_t *bits, uint64_t 
 hipError_t launch_chain_walk(const uint8_t *U, uint64_t first, uint64_t E, uint64_t total,
                              unsigned long long *count, unsigned long long *exit_pos, hipStream_t st) {
   hipLaunchKernelGGL(k_chain_walk, dim3(1), dim3(64), 0, st, U, first, E, total, count, exit_pos);
+  return hipGetLastError();
+}
+
+// pos, wpre: from launch_rec_positions_bits over [from, E); J, J2, J0: n + 1 u32; mark: n + 1 u64.
+// *final_code = the chain's terminal code after doubling (n: ended validly, n + 1: broken).
+hipError_t launch_chain_mark(const uint8_t *U, const uint32_t *bits, uint64_t begin, uint64_t from, uint64_t E,
+                             uint64_t total, const uint64_t *pos, const uint64_t *wpre, uint64_t n, uint32_t *J,
+                             uint32_t *J2, uint32_t *J0, uint64_t *mark, unsigned long long *exit_pos,
+                             uint32_t *final_code, hipStream_t st) {
+  if (!n) return hipSuccess;
+  const uint32_t g = ngrid(n, 256);
+  hipLaunchKernelGGL(k_cm_succ, dim3(g), dim3(256), 0, st, U, bits, begin, from, E, total, pos, wpre, n, J, J0, mark);
+  uint32_t *a = J, *b = J2;
+  for (uint64_t span = 1; span < n; span <<= 1) {
+    hipLaunchKernelGGL(k_cm_round, dim3(g), dim3(256), 0, st, a, b, mark, n);
+    std::swap(a, b);
+  }
+  hipLaunchKernelGGL(k_cm_exit, dim3(g), dim3(256), 0, st, U, pos, J0, mark, n, total, exit_pos);
+  hipError_t e = hipMemcpyAsync(final_code, a, 4, hipMemcpyDeviceToHost, st);
+  if (e != hipSuccess) return e;
   return hipGetLastError();
 }
 

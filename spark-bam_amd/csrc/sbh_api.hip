@@ -14,6 +14,10 @@
 namespace sbh {
 uint64_t scan_tmp_words(uint64_t n);
 hipError_t scan_exclusive_u64(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *tmp, hipStream_t st);
+hipError_t launch_chain_mark(const uint8_t *U, const uint32_t *bits, uint64_t begin, uint64_t from, uint64_t E,
+                             uint64_t total, const uint64_t *pos, const uint64_t *wpre, uint64_t n, uint32_t *J,
+                             uint32_t *J2, uint32_t *J0, uint64_t *mark, unsigned long long *exit_pos,
+                             uint32_t *final_code, hipStream_t st);
 hipError_t launch_find_block_start(const uint8_t *comp, uint64_t n, uint64_t start, int32_t k, int at_eof,
                                    unsigned long long *best, hipStream_t st);
 uint64_t cand_chunks(uint64_t n);
@@ -107,6 +111,12 @@ struct sbh_shard {
   DBuf<int32_t> ctg;
   int32_t nctg = -1;
   DBuf<uint32_t> bits;
+  // chain marking (pointer doubling) over the set bits of [cm_first, cm_E) when the bitmap
+  // is not the chain: node positions, per-word prefix counts, jumps, marks and their prefix
+  DBuf<uint64_t> cm_pos, cm_wcnt, cm_wpre, cm_mark, cm_mpre;
+  DBuf<uint32_t> cm_j, cm_j2, cm_j0;
+  uint64_t cm_first = 0, cm_E = 0, cm_n = 0;
+  bool cm_valid = false;
   bool bits_valid = false;
   uint64_t bits_begin = 0, bits_end = 0;
   int32_t bits_rtc = 0;
@@ -753,6 +763,7 @@ static int count_records_impl(sbh_shard *sh, uint64_t first, uint64_t E, uint64_
   const uint64_t total = seg_end_of(sh, first);
   E = std::min(E, total);
   if (anomalies) *anomalies = 0;
+  sh->cm_valid = false;
   if (first >= E) {
     *count = 0;
     if (exit_flat) *exit_flat = first;
@@ -776,6 +787,44 @@ static int count_records_impl(sbh_shard *sh, uint64_t first, uint64_t E, uint64_
       return SBH_OK;
     }
     if (anomalies) *anomalies = (int32_t)std::min<uint64_t>(sh->h_ctr[16], INT32_MAX);
+    // the bitmap is not exactly the chain (false positives / rejected chain records):
+    // mark the chain through the set bits by pointer doubling; the exact walk only when
+    // the chain leaves the set bits
+    const uint64_t n = sh->h_ctr[18];
+    if (n > 0 && n < 0xfffffff0ull) {
+      const uint64_t nw = (E - sh->bits_begin + 31) / 32 - (first - sh->bits_begin) / 32;
+      HIPCHK(ctx, sh->cm_wcnt.ensure(nw));
+      HIPCHK(ctx, sh->cm_wpre.ensure(nw));
+      HIPCHK(ctx, sh->cm_pos.ensure(n));
+      HIPCHK(ctx, sh->cm_mark.ensure(n + 1));
+      HIPCHK(ctx, sh->cm_mpre.ensure(n + 1));
+      HIPCHK(ctx, sh->cm_j.ensure(n + 1));
+      HIPCHK(ctx, sh->cm_j2.ensure(n + 1));
+      HIPCHK(ctx, sh->cm_j0.ensure(n + 1));
+      HIPCHK(ctx, sh->tmp.ensure(std::max(scan_tmp_words(nw), scan_tmp_words(n + 1))));
+      HIPCHK(ctx, launch_rec_positions_bits(sh->bits.p, sh->bits_begin, first, E, sh->cm_wcnt.p, sh->cm_wpre.p,
+                                            sh->tmp.p, sh->cm_pos.p, st));
+      HIPCHK(ctx, hipMemsetAsync(c + 6, 0xff, 8, st));
+      uint32_t *code = reinterpret_cast<uint32_t *>(sh->h_ctr + 22);
+      HIPCHK(ctx, launch_chain_mark(sh->U.p, sh->bits.p, sh->bits_begin, first, E, total, sh->cm_pos.p,
+                                    sh->cm_wpre.p, n, sh->cm_j.p, sh->cm_j2.p, sh->cm_j0.p, sh->cm_mark.p, c + 6,
+                                    code, st));
+      HIPCHK(ctx, hipMemsetAsync(sh->cm_mark.p + n, 0, 8, st));
+      HIPCHK(ctx, scan_exclusive_u64(sh->cm_mark.p, sh->cm_mpre.p, n + 1, sh->tmp.p, st));
+      HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 23, sh->cm_mpre.p + n, 8, hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 24, sh->cm_pos.p, 8, hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 25, c + 6, 8, hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipStreamSynchronize(st));
+      if (*code == (uint32_t)n && sh->h_ctr[24] == first) {
+        sh->cm_valid = true;
+        sh->cm_first = first;
+        sh->cm_E = E;
+        sh->cm_n = n;
+        *count = sh->h_ctr[23];
+        if (exit_flat) *exit_flat = sh->h_ctr[25];
+        return SBH_OK;
+      }
+    }
   }
   HIPCHK(ctx, launch_chain_walk(sh->U.p, first, E, total, c + 4, c + 5, st));
   HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 20, c + 4, 16, hipMemcpyDeviceToHost, st));
@@ -1072,6 +1121,9 @@ static int records_positions(sbh_shard *sh, uint64_t first, uint64_t E, uint64_t
     HIPCHK(ctx, R.wpre.ensure(nw));
     HIPCHK(ctx, sh->tmp.ensure(scan_tmp_words(nw)));
     HIPCHK(ctx, launch_rec_positions_bits(sh->bits.p, sh->bits_begin, first, E, R.wcnt.p, R.wpre.p, sh->tmp.p, pos, st));
+  } else if (n && sh->cm_valid && sh->cm_first == first && sh->cm_E == E) {
+    // the chain marked by count_records_impl's pointer doubling: compact its nodes
+    HIPCHK(ctx, launch_compact_u64(sh->cm_pos.p, sh->cm_mark.p, sh->cm_mpre.p, sh->cm_n, pos, st));
   } else if (n) {
     HIPCHK(ctx, launch_rec_positions_chain(sh->U.p, first, E, total, n, pos, st));
   }

@@ -384,3 +384,33 @@ def test_pipelined_run_matches_separate_calls(ctx, synth_files, name, batch_bloc
     k = of.flat_size
     assert np.array_equal(np.unpackbits(bits_pipe, bitorder="little")[:k], np.unpackbits(bits_ref, bitorder="little")[:k])
     sh.close()
+
+
+@pytest.mark.parametrize("name", ["adversarial", "short_l6", "long"])
+def test_chain_count_with_false_positive_bits(ctx, synth_files, name):
+    """Record counts / exits / record starts over an eager bitmap that holds false
+    positives (config E's bait): the pointer-doubling chain marker must give exactly the
+    PosStream chain (oracle walk), for ranges starting at true records."""
+    data = synth_files[name]
+    of = OracleFile(data)
+    sh = load(ctx, data, of.contig_len)
+    try:
+        n_true, _ = sh.check_eager(0, of.flat_size)
+        _, _, first = sb.parse_bam_header(sh.read_flat(0, min(of.flat_size, 1 << 20)))
+        chain = of.record_chain(first)
+        if name == "adversarial":
+            assert n_true > len(chain)  # the bitmap really holds false positives
+        rng = np.random.default_rng(7)
+        cases = [(0, len(chain), of.flat_size)]
+        for _ in range(6):
+            i = int(rng.integers(0, len(chain) - 1))
+            e = int(rng.integers(int(chain[i]) + 1, of.flat_size + 1))
+            cases.append((i, None, e))
+        for i, _, e in cases:
+            f = int(chain[i])
+            want = [int(x) for x in chain[i:] if x < e]
+            assert sh.count_records(f, e) == len(want), (name, f, e)
+            got = sh.records(f, e)["flat"]
+            assert [int(x) for x in got] == want, (name, f, e)
+    finally:
+        sh.close()

@@ -123,7 +123,7 @@ class Segment:
     blocks of rank i+1 (or the EOF block) as its halo.  Only the per-rank compressed
     sizes must be exchanged to place the shard in the file (see set_offsets)."""
 
-    def __init__(self, p, records_per_rank, world, rank, halo_blocks=16):
+    def __init__(self, p, records_per_rank, world, rank, halo_blocks=16, log=None):
         if p.level < 0:
             raise ValueError("segments need a uniform payload size (level >= 0)")
         self.p, self.R, self.world, self.rank = p, records_per_rank, world, rank
@@ -158,6 +158,8 @@ class Segment:
             rec_end = nxt
         U = np.concatenate(parts) if len(parts) > 1 else parts[0]
         U = U[u0 - base:u1 - base]
+        if log:
+            log(f"[rank {rank}] records generated: {U.size / 2**30:.2f} GiB uncompressed; compressing")
         self.own_blocks = k1 - k0
         comp, nb = bgzf(p, U, k0, add_eof=(k_halo == self.k[world]))
         sizes = block_sizes(comp)
@@ -172,4 +174,21 @@ class Segment:
         self.file_offset = sum(own_csizes[:self.rank])
         self.own_end = self.file_offset + own_csizes[self.rank]
         self.file_size = sum(own_csizes) + 28
+        return self
+
+
+class WholeFile:
+    """A whole synthetic BAM (header + records + EOF) as rank 0's only shard, for
+    parameters without a uniform payload grid (mixed levels)."""
+
+    def __init__(self, p, n_records):
+        U = np.concatenate([header_bytes(), records(p, 0, n_records)])
+        comp, nb = bgzf(p, U, 0, add_eof=True)
+        self.comp = comp
+        self.own_csize = comp.size
+        self.rank = 0
+
+    def set_offsets(self, own_csizes):
+        self.file_offset = 0
+        self.own_end = self.file_size = int(self.comp.size)
         return self
