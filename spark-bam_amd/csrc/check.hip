@@ -278,7 +278,31 @@ struct EagerOut {
   uint64_t *defer_pos;            // positions whose exact check needs them (re-checked later)
   unsigned long long *defer_n;
   uint64_t defer_cap;
+  uint64_t *xq_pos;               // long-record candidates for the wave-cooperative exact pass
+  unsigned long long *xq_n;
+  uint64_t xq_cap;                // 0: every exact check runs inline
 };
+
+// A candidate whose first record is at least this long (block_size) leaves its exact check
+// to k_eager_xq: its name / CIGAR bytes are read by a whole wave instead of one lane.
+constexpr int32_t XQ_MIN_REC = 2048;
+constexpr int32_t XQ_MIN_OPS = 32;
+constexpr uint32_t EAGER_XQ = 4;
+
+// A plausible long first record at p (its fixed fields pass and it carries >= XQ_MIN_OPS
+// CIGAR ops): the candidates worth a whole wave.
+__device__ __forceinline__ bool long_candidate(const Src &s, uint64_t p, const Ctg &c) {
+  const int32_t rem = (int32_t)s.word_at(p);
+  if (rem < XQ_MIN_REC) return false;
+  const uint32_t fnc = s.word_at(p + 16);
+  const int32_t nc = (int32_t)(fnc & 0xffff), rnl = (int32_t)(s.word_at(p + 12) & 0xff);
+  if (nc < XQ_MIN_OPS || rnl < 2) return false;
+  if (rem < implied_min_remaining(rnl, nc, (int32_t)s.word_at(p + 20))) return false;
+  if (ref_pos_error((int32_t)s.word_at(p + 4), (int32_t)s.word_at(p + 8), c) ||
+      ref_pos_error((int32_t)s.word_at(p + 24), (int32_t)s.word_at(p + 28), c))
+    return false;
+  return true;
+}
 
 constexpr uint32_t ETILE = SBH_ETILE;     // eager tile: positions per workgroup
 constexpr uint32_t ELA = 4096;            // look-ahead: chains of short reads stay inside
@@ -404,6 +428,18 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
   uint32_t mytrue = 0;
   const uint64_t wbase = (uint64_t)blockIdx.x * (ETILE / 32);
   const uint64_t nwords = (end - begin + 31) / 32;
+  // exact check of a candidate: inline (one lane), or queued for k_eager_xq when its first
+  // record is long (CIGARs of hundreds of ops: a lane-serial walk would dominate the tile)
+  auto exact = [&](uint64_t p, uint64_t total, bool open) -> uint32_t {
+    if (o.xq_cap && rtc > 0 && p + 36 <= total && long_candidate(s, p, c)) {
+      const unsigned long long x = atomicAdd(o.xq_n, 1ull);
+      if (x < o.xq_cap) {
+        o.xq_pos[x] = p;
+        return EAGER_XQ;
+      }
+    }
+    return eager_at(s, p, total, open, c, rtc, o.front);
+  };
   auto call_at = [&](uint32_t i) -> uint32_t {
     const uint64_t p = t0 + i;
     const uint32_t k = p < e0 ? k0 : seg_index(sg, p, k0);
@@ -413,7 +449,7 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
 #ifdef SBH_EPROBE
     ++ncand;
 #endif
-    if (rtc <= 0 || und_p) return eager_at(s, p, total, open, c, rtc, o.front);  // exact path (HBM/L2 reads)
+    if (rtc <= 0 || und_p) return exact(p, total, open);  // exact path (HBM/L2 reads)
     // walk the chain through the window's ok bits (next record read at nominal)
     uint64_t q = p;
     int32_t n = 1;
@@ -432,7 +468,7 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
 #ifdef SBH_EPROBE
     ++nexact;
 #endif
-    return eager_at(s, p, total, open, c, rtc, o.front);
+    return exact(p, total, open);
   };
   auto defer = [&](uint32_t i) {
     const unsigned long long x = atomicAdd(o.defer_n, 1ull);
@@ -979,6 +1015,131 @@ __global__ void k_chain_walk(const uint8_t *U, uint64_t first, uint64_t E, uint6
   *exit_pos = r > total ? total : r;  // first record at/after E (or where the walk stopped)
 }
 
+// eager.Checker.apply at p by one wave (k_eager_xq): the control flow of eager_at is
+// wave-uniform; the read-name bytes and the CIGAR ops of each record are tested by all
+// 64 lanes at once (ballots), preserving eager_at's outcome order: the bound checks
+// (unknown / false at the stream end) against the first invalid byte or op before them.
+__device__ uint32_t eager_at_wave(const uint8_t *__restrict__ U, uint64_t p, uint64_t total, bool open, const Ctg &c,
+                                  int32_t rtc, uint32_t lane) {
+  auto word = [&](uint64_t q) -> uint32_t {
+    const uint32_t *g = reinterpret_cast<const uint32_t *>(U + (q & ~3ull));
+    return __builtin_amdgcn_alignbyte(g[1], g[0], (uint32_t)q & 3);
+  };
+  uint64_t cur = p, start = p;
+  for (int32_t n = 0;; ++n) {
+    if (n == rtc) return 1;
+    if (cur + 36 > total) {
+      if (open) return 2;
+      return (total == start && n > 0) ? 1 : 0;
+    }
+    const int32_t rem = (int32_t)word(cur);
+    const uint64_t nominal = start + 4 + (int64_t)rem;
+    if (ref_pos_error((int32_t)word(cur + 4), (int32_t)word(cur + 8), c)) return 0;
+    const int32_t rnl = (int32_t)(word(cur + 12) & 0xff);
+    if (rnl < 2) return 0;
+    const uint32_t fnc = word(cur + 16);
+    const uint32_t flags = fnc >> 16;
+    const int32_t nc = (int32_t)(fnc & 0xffff);
+    const int32_t seq_len = (int32_t)word(cur + 20);
+    if ((flags & 4) == 0 && (seq_len == 0 || nc == 0)) return 0;
+    if (rem < implied_min_remaining(rnl, nc, seq_len)) return 0;
+    if (ref_pos_error((int32_t)word(cur + 24), (int32_t)word(cur + 28), c)) return 0;
+    cur += 36;
+    if (cur + (uint64_t)rnl > total) return open ? 2 : 0;
+    // one round trip for the name bytes and the first 512 CIGAR op bytes: every load is
+    // issued before any test
+    const uint64_t avail = total > cur + rnl ? (total - cur - rnl) / 4 : 0;
+    const uint64_t lim = (uint64_t)nc < avail ? (uint64_t)nc : avail;
+    const uint64_t qc = cur + (uint64_t)rnl;
+    const uint8_t term = U[cur + rnl - 1];
+    uint8_t nb[4], ob[8];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+      const uint32_t k = lane + WAVE * j;
+      nb[j] = k < (uint32_t)rnl ? U[cur + k] : (uint8_t)'A';
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+      const uint64_t k = lane + WAVE * j;
+      ob[j] = k < lim ? U[qc + 4 * k] : (uint8_t)0;
+    }
+    if (term != 0) return 0;
+    bool bad = false;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) bad |= lane + WAVE * j + 1 < (uint32_t)rnl && !name_char_ok(nb[j]);
+    if (__ballot(bad)) return 0;
+    cur = qc;
+    bool badop = false;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) badop |= (ob[j] & 0xf) > 8;
+    if (__ballot(badop)) return 0;
+    for (uint64_t b = 8 * WAVE; b < lim; b += WAVE) {  // CIGARs longer than 512 ops
+      const uint64_t k = b + lane;
+      const bool bo = k < lim && (U[cur + 4 * k] & 0xf) > 8;
+      if (__ballot(bo)) return 0;
+    }
+    if ((uint64_t)nc > avail) return open ? 2 : 0;
+    cur += 4ull * (uint64_t)nc;
+    if ((int64_t)(nominal - cur) > 0) {
+      if (nominal > total) {
+        if (open) return 2;
+        cur = total;
+      } else {
+        cur = nominal;
+      }
+    }
+    start = nominal;
+  }
+}
+
+// The queued long-record candidates, pass 1 (a lane each): the read name and the first
+// XQ_MIN_OPS CIGAR ops must hold (random bytes fail there: an op byte passes with
+// probability 9/16); survivors go to the second queue.
+__global__ __launch_bounds__(256) void k_eager_xq_pre(const uint8_t *__restrict__ U, Segs sg, const uint64_t *pos,
+                                                      const unsigned long long *n, uint64_t cap, uint64_t *pos2,
+                                                      unsigned long long *n2) {
+  const uint64_t cnt = *n < cap ? *n : cap;
+  const uint64_t nt = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < cnt; x += nt) {
+    const uint64_t p = pos[x];
+    const uint64_t total = sg.end[seg_first(sg, p)];
+    const uint64_t q = p + 36;
+    const uint32_t rnl = U[p + 12];
+    bool alive = true;
+    if (q + rnl + 4ull * XQ_MIN_OPS <= total) {  // else: leave the EOF rules to the exact walk
+      const Src s{U, nullptr, 0, 0};
+      alive = U[q + rnl - 1] == 0 && name_bytes_ok(s, q, rnl - 1);
+      for (uint32_t k = 0; alive && k < (uint32_t)XQ_MIN_OPS; ++k) alive = (U[q + rnl + 4 * k] & 0xf) <= 8;
+    }
+    if (alive) pos2[atomicAdd(n2, 1ull)] = p;
+  }
+}
+
+// Pass 2: one wave per surviving candidate (grid-stride over the device count).
+__global__ __launch_bounds__(256) void k_eager_xq(const uint8_t *__restrict__ U, uint64_t begin, Segs sg, Ctg c,
+                                                  int32_t rtc, const uint64_t *pos, const unsigned long long *n,
+                                                  uint64_t cap, EagerOut o) {
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  const uint64_t cnt = *n < cap ? *n : cap;
+  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / WAVE);
+  for (uint64_t x = (uint64_t)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE; x < cnt; x += nw) {
+    const uint64_t p = pos[x];
+    const uint32_t k = seg_first(sg, p);
+    const uint64_t total = sg.end[k];
+    const bool open = sg.open_last && k == sg.n - 1;
+    const uint32_t r = eager_at_wave(U, p, total, open, c, rtc, lane);
+    if (lane == 0) {
+      if (r == 1) {
+        atomicOr(&o.bits[(p - begin) >> 5], 1u << ((p - begin) & 31));
+        atomicAdd(o.n_true, 1ull);
+      } else if (r == 2) {
+        atomicAdd(o.n_unknown, 1ull);
+        atomicMin(o.min_unknown, (unsigned long long)p);
+      }
+    }
+  }
+}
+
 // Positions the pipelined eager pass deferred (their exact check reached flat bytes that
 // were not inflated yet), re-checked once everything is: bit set atomically over the
 // tile's word, counters as in k_eager.
@@ -1008,11 +1169,12 @@ static inline uint32_t ngrid(uint64_t n, uint32_t t) { return (uint32_t)((n + t 
 hipError_t launch_eager(const uint8_t *U, uint64_t u_pad, uint64_t begin, uint64_t end, const uint64_t *seg_end,
                         uint32_t nseg, uint32_t open_last, const int32_t *ctg, int32_t nctg, int32_t rtc,
                         uint32_t *bits, unsigned long long *counters, hipStream_t st, uint64_t front,
-                        uint64_t *defer_pos, uint64_t defer_cap) {
+                        uint64_t *defer_pos, uint64_t defer_cap, uint64_t *xq_pos, uint64_t xq_cap) {
   if (end <= begin) return hipSuccess;
   Segs sg{seg_end, nseg, open_last};
   Ctg c{ctg, nctg};
-  EagerOut o{bits, counters, counters + 1, counters + 2, front, defer_pos, counters + 3, defer_cap};
+  EagerOut o{bits, counters, counters + 1, counters + 2, front, defer_pos, counters + 3, defer_cap,
+             xq_pos, counters + 4, xq_cap};
   hipLaunchKernelGGL(k_eager, dim3(ngrid(end - begin, ETILE)), dim3(T), 0, st, U, u_pad, begin, end, sg, c,
                      rtc, o);
   return hipGetLastError();
@@ -1027,7 +1189,7 @@ hipError_t launch_eager_defer(const uint8_t *U, uint64_t begin, const uint64_t *
   if (cap == 0) return hipSuccess;
   Segs sg{seg_end, nseg, open_last};
   Ctg c{ctg, nctg};
-  EagerOut o{bits, counters, counters + 1, counters + 2, ~0ull, nullptr, nullptr, 0};
+  EagerOut o{bits, counters, counters + 1, counters + 2, ~0ull, nullptr, nullptr, 0, nullptr, nullptr, 0};
   hipLaunchKernelGGL(k_eager_defer, dim3(ngrid(cap, 256)), dim3(256), 0, st, U, begin, sg, c, rtc, defer_pos,
                      counters + 3, o);
   return hipGetLastError();
@@ -1107,6 +1269,24 @@ hipError_t launch_chain_mark(const uint8_t *U, const uint32_t *bits, uint64_t be
   hipLaunchKernelGGL(k_cm_exit, dim3(g), dim3(256), 0, st, U, pos, J0, mark, n, total, exit_pos);
   hipError_t e = hipMemcpyAsync(final_code, a, 4, hipMemcpyDeviceToHost, st);
   if (e != hipSuccess) return e;
+  return hipGetLastError();
+}
+
+// The wave-cooperative exact pass over the long-record queue (counters[4] = its device
+// count, counters[5] = the survivors of the lane pre-test in xq_pos[cap, 2 cap)); fixed
+// grids stride over the device counts, so no host round trip is needed.  bits: the bitmap
+// from `begin`.  xq_pos holds 2 * cap entries.
+hipError_t launch_eager_xq(const uint8_t *U, uint64_t begin, const uint64_t *seg_end, uint32_t nseg,
+                           uint32_t open_last, const int32_t *ctg, int32_t nctg, int32_t rtc, uint32_t *bits,
+                           unsigned long long *counters, uint64_t *xq_pos, uint64_t cap, hipStream_t st) {
+  if (cap == 0) return hipSuccess;
+  Segs sg{seg_end, nseg, open_last};
+  Ctg c{ctg, nctg};
+  EagerOut o{bits, counters, counters + 1, counters + 2, ~0ull, nullptr, nullptr, 0, nullptr, nullptr, 0};
+  hipLaunchKernelGGL(k_eager_xq_pre, dim3(512), dim3(256), 0, st, U, sg, xq_pos, counters + 4, cap, xq_pos + cap,
+                     counters + 5);
+  hipLaunchKernelGGL(k_eager_xq, dim3(8192), dim3(256), 0, st, U, begin, sg, c, rtc, xq_pos + cap, counters + 5,
+                     cap, o);
   return hipGetLastError();
 }
 

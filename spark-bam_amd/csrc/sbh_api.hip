@@ -32,7 +32,10 @@ hipError_t build_chain(const uint8_t *comp, uint64_t n, const uint64_t *cand, ui
 hipError_t launch_eager(const uint8_t *U, uint64_t u_pad, uint64_t begin, uint64_t end, const uint64_t *seg_end,
                         uint32_t nseg, uint32_t open_last, const int32_t *ctg, int32_t nctg, int32_t rtc,
                         uint32_t *bits, unsigned long long *counters, hipStream_t st, uint64_t front,
-                        uint64_t *defer_pos, uint64_t defer_cap);
+                        uint64_t *defer_pos, uint64_t defer_cap, uint64_t *xq_pos, uint64_t xq_cap);
+hipError_t launch_eager_xq(const uint8_t *U, uint64_t begin, const uint64_t *seg_end, uint32_t nseg,
+                           uint32_t open_last, const int32_t *ctg, int32_t nctg, int32_t rtc, uint32_t *bits,
+                           unsigned long long *counters, uint64_t *xq_pos, uint64_t cap, hipStream_t st);
 hipError_t launch_eager_defer(const uint8_t *U, uint64_t begin, const uint64_t *seg_end, uint32_t nseg,
                               uint32_t open_last, const int32_t *ctg, int32_t nctg, int32_t rtc, uint32_t *bits,
                               unsigned long long *counters, const uint64_t *defer_pos, uint64_t cap,
@@ -130,6 +133,7 @@ struct sbh_shard {
   hipStream_t s_lz = nullptr, s_eg = nullptr;
   std::vector<hipEvent_t> pev;
   DBuf<uint64_t> defer;
+  DBuf<uint64_t> xq;  // long-record eager candidates for the wave-cooperative exact pass
   // record field extraction (sbh_records_scan / fetch): positions, sizes -> offsets, columns
   struct Recs {
     DBuf<uint64_t> pos, wcnt, wpre, nm, cg, sq, ax, nmo, cgo, sqo, axo, keep, kpre, pos2;
@@ -303,6 +307,7 @@ int sbh_shard_destroy(sbh_shard *sh) {
   if (sh->s_lz) (void)hipStreamDestroy(sh->s_lz);
   if (sh->s_eg) (void)hipStreamDestroy(sh->s_eg);
   sh->defer.release();
+  sh->xq.release();
   sh->rec.release();
   if (sh->h_ctr) (void)hipHostFree(sh->h_ctr);
   delete sh;
@@ -568,17 +573,28 @@ static int need_checkable(sbh_shard *sh, uint64_t begin, uint64_t end, int32_t r
   return SBH_OK;
 }
 
+static constexpr uint64_t XQ_CAP_MAX = 1 << 22;  // queued long-record eager candidates (2 x 32 MiB)
+// SBH_XQ=0 turns the long-record queue off (every exact check inline; for A/B timing)
+static uint64_t xq_cap() {
+  const char *e = std::getenv("SBH_XQ");
+  return e && e[0] == '0' ? 0 : XQ_CAP_MAX;
+}
+
 static int eager_range(sbh_shard *sh, uint64_t begin, uint64_t end, int32_t rtc, uint64_t *n_true) {
   sbh_ctx *ctx = sh->ctx;
   hipStream_t st = ctx->stream;
   const uint64_t nwords = (end - begin + 31) / 32;
   HIPCHK(ctx, sh->bits.ensure(nwords + 1));
+  HIPCHK(ctx, sh->xq.ensure(2 * XQ_CAP_MAX));
   unsigned long long *c = sh->ctr.p;
-  HIPCHK(ctx, hipMemsetAsync(c, 0, 32, st));
+  HIPCHK(ctx, hipMemsetAsync(c, 0, 48, st));
   HIPCHK(ctx, hipMemsetAsync(c + 2, 0xff, 8, st));
   mark(sh, 4);
   HIPCHK(ctx, launch_eager(sh->U.p, sh->utotal + sh->pad, begin, end, sh->d_seg.p, (uint32_t)sh->seg_end.size(),
-                           sh->open_last ? 1 : 0, sh->ctg.p, sh->nctg, rtc, sh->bits.p, c, st, ~0ull, nullptr, 0));
+                           sh->open_last ? 1 : 0, sh->ctg.p, sh->nctg, rtc, sh->bits.p, c, st, ~0ull, nullptr, 0,
+                           sh->xq.p, xq_cap()));
+  HIPCHK(ctx, launch_eager_xq(sh->U.p, begin, sh->d_seg.p, (uint32_t)sh->seg_end.size(), sh->open_last ? 1 : 0,
+                              sh->ctg.p, sh->nctg, rtc, sh->bits.p, c, sh->xq.p, xq_cap(), st));
   mark(sh, 5);
   HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr, c, 24, hipMemcpyDeviceToHost, st));
   HIPCHK(ctx, hipStreamSynchronize(st));
@@ -756,6 +772,8 @@ int sbh_find_record_start(sbh_shard *sh, uint64_t from, int32_t rtc, int32_t max
 // Records of the chain from `first` whose start is < E; *exit_flat (optional) = the
 // first chain record at/after E (the successor of the last counted record, clamped to
 // the stream end) -- what the next shard's first record must equal when stitching.
+static constexpr uint64_t CM_SPARSE = 1024;  // positions per set bit above which the chain is marked
+
 static int count_records_impl(sbh_shard *sh, uint64_t first, uint64_t E, uint64_t *count, int32_t *anomalies,
                               uint64_t *exit_flat = nullptr) {
   sbh_ctx *ctx = sh->ctx;
@@ -776,21 +794,29 @@ static int count_records_impl(sbh_shard *sh, uint64_t first, uint64_t E, uint64_
     HIPCHK(ctx, hipMemsetAsync(c + 1, 0xff, 8, st));
     HIPCHK(ctx, hipMemsetAsync(c + 2, 0, 8, st));
     HIPCHK(ctx, hipMemsetAsync(c + 3, 0xff, 8, st));
-    HIPCHK(ctx, launch_verify_chain(sh->U.p, sh->bits.p, sh->bits_begin, sh->bits_end, first, E, total, c, c + 1,
-                                    c + 3, st));
     HIPCHK(ctx, launch_popcount(sh->bits.p, sh->bits_begin, first, E, c + 2, st));
-    HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 16, c, 32, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 18, c + 2, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipStreamSynchronize(st));
-    if (sh->h_ctr[16] == 0 && sh->h_ctr[19] != ~0ull) {
-      *count = sh->h_ctr[18];
-      if (exit_flat) *exit_flat = sh->h_ctr[19];
-      return SBH_OK;
+    uint64_t n = sh->h_ctr[18];
+    // dense bits (short records): verify bitmap == chain in one pass; sparse bits (long
+    // records, > CM_SPARSE positions per set bit): the verify pass would scan long runs of
+    // empty words per record, so mark the chain by pointer doubling straight away
+    const bool dense = n == 0 || (E - first) / n <= CM_SPARSE;
+    if (dense) {
+      HIPCHK(ctx, launch_verify_chain(sh->U.p, sh->bits.p, sh->bits_begin, sh->bits_end, first, E, total, c, c + 1,
+                                      c + 3, st));
+      HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 16, c, 32, hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipStreamSynchronize(st));
+      if (sh->h_ctr[16] == 0 && sh->h_ctr[19] != ~0ull) {
+        *count = sh->h_ctr[18];
+        if (exit_flat) *exit_flat = sh->h_ctr[19];
+        return SBH_OK;
+      }
+      if (anomalies) *anomalies = (int32_t)std::min<uint64_t>(sh->h_ctr[16], INT32_MAX);
     }
-    if (anomalies) *anomalies = (int32_t)std::min<uint64_t>(sh->h_ctr[16], INT32_MAX);
-    // the bitmap is not exactly the chain (false positives / rejected chain records):
-    // mark the chain through the set bits by pointer doubling; the exact walk only when
-    // the chain leaves the set bits
-    const uint64_t n = sh->h_ctr[18];
+    // the bitmap is not exactly the chain (false positives / rejected chain records), or
+    // it is sparse: mark the chain through the set bits by pointer doubling; the exact
+    // walk only when the chain leaves the set bits
     if (n > 0 && n < 0xfffffff0ull) {
       const uint64_t nw = (E - sh->bits_begin + 31) / 32 - (first - sh->bits_begin) / 32;
       HIPCHK(ctx, sh->cm_wcnt.ensure(nw));
@@ -822,6 +848,8 @@ static int count_records_impl(sbh_shard *sh, uint64_t first, uint64_t E, uint64_
         sh->cm_n = n;
         *count = sh->h_ctr[23];
         if (exit_flat) *exit_flat = sh->h_ctr[25];
+        // set bits off the chain (false positives); 0 means the bitmap is the chain
+        if (anomalies) *anomalies = (int32_t)std::min<uint64_t>(n - *count, INT32_MAX);
         return SBH_OK;
       }
     }
@@ -924,15 +952,16 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
   HIPCHK(ctx, sh->tok.ensure(sh->utotal + 64));
   HIPCHK(ctx, sh->bits.ensure((E + 31) / 32 + 1));
   HIPCHK(ctx, sh->defer.ensure(DEFER_CAP));
+  HIPCHK(ctx, sh->xq.ensure(2 * XQ_CAP_MAX));
   HIPCHK(ctx, hipMemsetAsync(sh->U.p + sh->utotal, 0, sh->pad, sa));
   unsigned long long *c = sh->ctr.p;
-  HIPCHK(ctx, hipMemsetAsync(c, 0, 32, sa));
+  HIPCHK(ctx, hipMemsetAsync(c, 0, 48, sa));
   HIPCHK(ctx, hipMemsetAsync(c + 2, 0xff, 8, sa));
   sh->inflated = sh->bits_valid = false;
   const uint64_t nb = sh->nblocks;
   const uint64_t nbat = std::max<uint64_t>(1, std::min<uint64_t>(PIPE_MAX_BATCHES, nb / pipe_min_blocks()));
   // events: per batch [huff start, huff end, lz start, lz end, eager start, eager end]
-  for (size_t i = 0; i < 6 * nbat + 2; ++i)
+  for (size_t i = 0; i < 6 * nbat + 4; ++i)
     if (!pev(sh, i)) return fail(ctx, SBH_E_HIP, "hipEventCreate failed");
   hipEvent_t *ev = sh->pev.data();
   HIPCHK(ctx, hipEventRecord(ev[6 * nbat], sa));  // setup done: the other streams start after it
@@ -965,7 +994,7 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
       HIPCHK(ctx, hipEventRecord(e[4], se));
       HIPCHK(ctx, launch_eager(sh->U.p, sh->utotal + sh->pad, e_done, hi, sh->d_seg.p, (uint32_t)sh->seg_end.size(),
                                sh->open_last ? 1 : 0, sh->ctg.p, sh->nctg, rtc, sh->bits.p + e_done / 32, c, se,
-                               front, sh->defer.p, DEFER_CAP));
+                               front, sh->defer.p, DEFER_CAP, sh->xq.p, xq_cap()));
       HIPCHK(ctx, hipEventRecord(e[5], se));
       eager_launched[i] = 1;
       e_done = hi;
@@ -974,11 +1003,15 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
   HIPCHK(ctx, hipStreamWaitEvent(se, ev[6 * (nbat - 1) + 3], 0));
   HIPCHK(ctx, launch_eager_defer(sh->U.p, 0, sh->d_seg.p, (uint32_t)sh->seg_end.size(), sh->open_last ? 1 : 0,
                                  sh->ctg.p, sh->nctg, rtc, sh->bits.p, c, sh->defer.p, DEFER_CAP, se));
+  HIPCHK(ctx, hipEventRecord(ev[6 * nbat + 2], se));
+  HIPCHK(ctx, launch_eager_xq(sh->U.p, 0, sh->d_seg.p, (uint32_t)sh->seg_end.size(), sh->open_last ? 1 : 0,
+                              sh->ctg.p, sh->nctg, rtc, sh->bits.p, c, sh->xq.p, xq_cap(), se));
+  HIPCHK(ctx, hipEventRecord(ev[6 * nbat + 3], se));
   HIPCHK(ctx, hipEventRecord(ev[6 * nbat + 1], se));
   HIPCHK(ctx, hipStreamWaitEvent(sa, ev[6 * nbat + 1], 0));
   std::vector<uint32_t> status(nb);
   if (nb) HIPCHK(ctx, hipMemcpyAsync(status.data(), sh->b_status.p, nb * 4, hipMemcpyDeviceToHost, sa));
-  HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr, c, 32, hipMemcpyDeviceToHost, sa));
+  HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr, c, 48, hipMemcpyDeviceToHost, sa));
   HIPCHK(ctx, hipStreamSynchronize(sa));
   for (uint64_t i = 0; i < nb; ++i) {
     if (status[i] == INF_OK) continue;
@@ -1000,8 +1033,13 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
     }
     sh->pipe_ms[0] = hs;
     sh->pipe_ms[1] = ls;
+    float xs = 0;
+    if (hipEventElapsedTime(&xs, ev[6 * nbat + 2], ev[6 * nbat + 3]) == hipSuccess) es += xs;  // k_eager_xq
     sh->pipe_ms[2] = es;
   }
+  if (std::getenv("SBH_XQ_DEBUG"))
+    fprintf(stderr, "[sbh] eager: deferred %llu, long-record queue %llu (%llu past the pre-test)\n", sh->h_ctr[3],
+            sh->h_ctr[4], sh->h_ctr[5]);
   if (sh->h_ctr[3] > DEFER_CAP) return eager_range(sh, 0, E, rtc, n_true);  // deferral overflow: plain pass
   sh->bits_valid = true;
   sh->bits_begin = 0;
