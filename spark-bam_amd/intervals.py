@@ -15,8 +15,8 @@ Host side (small, per query):
   * `capped_cost_groups` -- the partitioning of chunks by estimated size
     (CanLoadBam.scala:105-112, Chunk.size = end - start with the compression ratio).
 
-Device side: the whole BAM is indexed and inflated on the GPU, and
-`Shard.records_regions` (sbh_records_scan_regions) produces the records of every chunk
+Device side: only the compressed block ranges the chunks cover (plus a growing halo) are
+moved to the device, indexed and inflated there, and `Shard.records_regions` (sbh_records_scan_regions) produces the records of every chunk
 (records.seek(chunk.start) while pos < chunk.end, CanLoadBam.scala:132-152) and keeps
 those whose region overlaps the LociSet -- the region test runs in a HIP kernel
 (k_region_keep, records.hip).  Pinned by LoadBAMTest's "indexed *" cases.
@@ -27,8 +27,9 @@ from collections import namedtuple
 
 import numpy as np
 
-from ._lib import SparkBamError
-from .api import DEFAULT_READS_TO_CHECK, DEFAULT_SPLIT_SIZE, Pos, _Loaded
+from ._lib import SBH_E_BAD_RECORD, SBH_E_NEED_HALO, SBH_E_NOT_FOUND, SparkBamError
+from .api import DEFAULT_READS_TO_CHECK, DEFAULT_SPLIT_SIZE, Pos
+from .device import Context
 from .records import Reads
 
 METADATA_BIN_ID = 37450  # Index.scala:91
@@ -256,41 +257,84 @@ def capped_cost_groups(items, cost, limit):
     return groups
 
 
-def _flat_of_pos(shard, pos):
-    try:
-        return shard.flat_of(pos.block_pos, pos.offset)
-    except SparkBamError:
-        if pos.block_pos >= shard.file_offset + shard.n:
-            return shard.flat_size
-        raise
+def _vpos_of_flat(blocks, flat):
+    """Shard flat positions -> htsjdk virtual offsets (canonical: a position at a block's
+    end is Pos(next block, 0)), vectorised over the shard's block table."""
+    starts = np.asarray([b[0] for b in blocks], dtype=np.uint64)
+    ustarts = np.asarray([b[3] for b in blocks], dtype=np.uint64)
+    usizes = np.asarray([b[2] for b in blocks], dtype=np.uint64)
+    live = usizes > 0  # empty blocks hold no positions
+    starts, ustarts = starts[live], ustarts[live]
+    k = np.searchsorted(ustarts, flat, side="right") - 1
+    return (starts[k] << np.uint64(16)) | (flat - ustarts[k])
 
 
 def load_bam_intervals(path, intervals, split_size=DEFAULT_SPLIT_SIZE,
                        estimated_compression_ratio=DEFAULT_COMPRESSION_RATIO, ctx=None, bai=None,
-                       reads_to_check=DEFAULT_READS_TO_CHECK):
+                       reads_to_check=DEFAULT_READS_TO_CHECK, halo=1 << 18, merge_gap=1 << 20):
     """CanLoadBam.loadBamIntervals(path, splitSize, ratio)(intervals*)
     (CanLoadBam.scala:61-154) on one device.  Returns IntervalReads(reads, partitions,
-    counts): the kept records as a columnar Reads batch in partition/chunk order, the
-    chunk partitions (getNumPartitions = len(partitions)) and per-partition counts."""
+    counts): the kept records as a columnar Reads batch in chunk order (its "vpos" column
+    holds each record's htsjdk virtual offset), the chunk partitions (getNumPartitions =
+    max(1, len(partitions))) and per-partition counts.
+
+    Only the compressed bytes the chunks need are moved and inflated: chunks whose block
+    ranges lie within `merge_gap` of each other share one device shard [first chunk's
+    block, last chunk's end block + halo); the halo grows x4 while a result depends on
+    bytes past it (SBH_E_NEED_HALO: an eager check reads on; SBH_E_BAD_RECORD: a kept
+    record runs past the shard)."""
+    from .sharded import bytes_reader, file_reader, read_header
     index = read_bai(bai if bai is not None else str(path) + ".bai")
-    L = _Loaded(path, ctx, reads_to_check)
+    read = bytes_reader(path) if isinstance(path, (bytes, bytearray, memoryview, np.ndarray)) \
+        else file_reader(path)
+    size = read.size
+    own_ctx = ctx is None
+    ctx = ctx or Context(0)
     try:
-        sh = L.shard
-        names = list(L.names)
-        loci = parse_loci(intervals, dict(zip(names, (int(x) for x in L.contig_len))))
+        names, lens, _ = read_header(ctx, read, size)
+        names = list(names)
+        loci = parse_loci(intervals, dict(zip(names, (int(x) for x in lens))))
         chunks = get_interval_chunks(index, loci, names)
         parts = capped_cost_groups(chunks, lambda c: chunk_size(c, estimated_compression_ratio),
                                    float(split_size))
-        flat = [(_flat_of_pos(sh, c.start), _flat_of_pos(sh, c.end)) for c in chunks]
         ivs = sorted((names.index(c), a, e) for c, rs in loci.items() for a, e in rs)
-        if flat:
-            lo, hi = min(f[0] for f in flat), max(f[1] for f in flat)
-            sh.check_eager(lo, min(hi, sh.flat_size), reads_to_check, want_bits=False)
-        cols = sh.records_regions(flat, ivs)
-        # per-partition counts: chunks are disjoint in flat space; a record belongs to
-        # the chunk whose [begin, end) holds its start
-        begins = np.asarray([f[0] for f in flat], dtype=np.uint64)
-        which = np.searchsorted(begins, cols["flat"], side="right") - 1
+        groups = []  # [lo, hi, [chunk indices]]: compressed block range per device shard
+        for k, c in enumerate(chunks):
+            lo, hi = c.start.block_pos, c.end.block_pos
+            if groups and lo <= groups[-1][1] + merge_gap:
+                groups[-1][1] = max(groups[-1][1], hi)
+                groups[-1][2].append(k)
+            else:
+                groups.append([lo, hi, [k]])
+        batches = []
+        for lo, hi, ks in groups:
+            h = halo
+            while True:
+                end = min(size, hi + h)
+                sh = ctx.shard(read(lo, end), file_offset=lo, file_size=size)
+                try:
+                    sh.index(lo)
+                    sh.inflate()
+                    sh.set_contigs(lens)
+                    fl = [(_flat_of_pos(sh, chunks[k].start), _flat_of_pos(sh, chunks[k].end)) for k in ks]
+                    a, b = min(f[0] for f in fl), min(max(f[1] for f in fl), sh.flat_size)
+                    if b > a:
+                        sh.check_eager(a, b, reads_to_check, want_bits=False)
+                    cols = sh.records_regions(fl, ivs)
+                    cols["vpos"] = _vpos_of_flat(sh.blocks(), cols["flat"]) if cols["flat"].size \
+                        else np.zeros(0, np.uint64)
+                    batches.append(cols)
+                    break
+                except SparkBamError as err:
+                    if err.code not in (SBH_E_NEED_HALO, SBH_E_BAD_RECORD, SBH_E_NOT_FOUND) or end >= size:
+                        raise
+                    h *= 4
+                finally:
+                    sh.close()
+        cols = _concat(batches)
+        # per-partition counts: a record belongs to the chunk whose [start, end) holds it
+        starts = np.asarray([c.start.to_htsjdk() for c in chunks], dtype=np.uint64)
+        which = np.searchsorted(starts, cols["vpos"], side="right") - 1
         per_chunk = np.bincount(which, minlength=len(chunks)) if len(chunks) else np.zeros(0, np.int64)
         counts, k = [], 0
         for g in parts:
@@ -298,4 +342,49 @@ def load_bam_intervals(path, intervals, split_size=DEFAULT_SPLIT_SIZE,
             k += len(g)
         return IntervalReads(Reads(cols, names), parts, counts)
     finally:
-        L.close()
+        if own_ctx:
+            ctx.close()
+
+
+def _flat_of_pos(shard, pos):
+    """A chunk boundary's flat position in the shard; a boundary at/after the file's last
+    block maps to the shard's flat end (SBH_E_NOT_FOUND when the shard does not reach it:
+    the caller grows the shard)."""
+    if pos.block_pos >= shard.file_size:
+        return shard.flat_size
+    try:
+        return shard.flat_of(pos.block_pos, pos.offset)
+    except SparkBamError as err:
+        if pos.block_pos >= shard.file_offset + shard.n and shard.file_offset + shard.n < shard.file_size:
+            raise SparkBamError(SBH_E_NOT_FOUND, "chunk end past the shard") from err
+        if pos.block_pos >= shard.file_offset + shard.n:
+            return shard.flat_size
+        raise
+
+
+_OFFS = ("name_off", "cigar_off", "seq_off", "aux_off")
+
+
+def _concat(batches):
+    """Concatenate record column batches (prefix-offset columns rebased)."""
+    if len(batches) == 1:
+        return batches[0]
+    if not batches:
+        return {"flat": np.zeros(0, np.uint64), "vpos": np.zeros(0, np.uint64), "ref_id": np.zeros(0, np.int32),
+                "pos": np.zeros(0, np.int32), "next_ref_id": np.zeros(0, np.int32),
+                "next_pos": np.zeros(0, np.int32), "tlen": np.zeros(0, np.int32),
+                "flag": np.zeros(0, np.uint16), "bin": np.zeros(0, np.uint16), "mapq": np.zeros(0, np.uint8),
+                **{k: np.zeros(1, np.uint64) for k in _OFFS}, "names": np.zeros(0, np.uint8),
+                "cigar": np.zeros(0, np.uint32), "seq": np.zeros(0, np.uint8), "qual": np.zeros(0, np.uint8),
+                "aux": np.zeros(0, np.uint8)}
+    out = {}
+    for k in batches[0]:
+        if k in _OFFS:
+            parts, base = [np.zeros(1, np.uint64)], 0
+            for b in batches:
+                parts.append(b[k][1:] + np.uint64(base))
+                base += int(b[k][-1])
+            out[k] = np.concatenate(parts)
+        else:
+            out[k] = np.concatenate([b[k] for b in batches])
+    return out

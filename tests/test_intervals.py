@@ -141,7 +141,7 @@ def test_optimize_chunk_list_rules():
 
 # ---------------------------------------------------------------- GPU (through the C-ABI)
 
-COLS = ("flat", "ref_id", "pos", "next_ref_id", "next_pos", "tlen", "flag", "bin", "mapq", "name_off",
+COLS = ("ref_id", "pos", "next_ref_id", "next_pos", "tlen", "flag", "bin", "mapq", "name_off",
         "cigar_off", "seq_off", "aux_off", "names", "cigar", "seq", "qual", "aux")
 
 
@@ -164,6 +164,13 @@ def test_gpu_load_bam_intervals_golden(ctx, text, split, parts, count):
     assert len(res.reads) == sum(res.counts) == count
     assert len(res.partitions) == parts
     _, want, per = _oracle("2.bam", text)
+    _check_cols("2.bam", res, want)
+
+
+def _check_cols(name, res, want):
+    of = _HDR[name][3]
+    vp = [(lambda bp, off: (bp << 16) | off)(*of.pos_of(int(f))) for f in want["flat"]]
+    assert [int(v) for v in res.reads.cols["vpos"]] == vp
     for k in COLS:
         assert np.array_equal(res.reads.cols[k], want[k]), k
 
@@ -181,5 +188,16 @@ def test_gpu_load_bam_intervals_random(ctx, name):
         res = sb.load_bam_intervals(golden_bam(name), text, ctx=ctx)
         _, want, per = _oracle(name, text)
         assert sum(res.counts) == sum(per)
-        for k in COLS:
-            assert np.array_equal(res.reads.cols[k], want[k]), (text, k)
+        _check_cols(name, res, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["2.bam", "5k.bam"])
+def test_gpu_load_bam_intervals_small_shards(ctx, name):
+    """One device shard per chunk (merge_gap 0) starting with a 4 KiB halo: the halo must
+    grow until every kept record and eager check is inside its shard."""
+    text = "1:100-900,1:13000-14000,1:30000-30100,1:60000-61000"
+    res = sb.load_bam_intervals(golden_bam(name), text, ctx=ctx, halo=4096, merge_gap=0)
+    _, want, per = _oracle(name, text)
+    assert res.counts and sum(res.counts) == sum(per)
+    _check_cols(name, res, want)
