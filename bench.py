@@ -227,7 +227,9 @@ def main():
             "dtype": "u8",
             "data": f"synthetic (tools/synth_bam.c, seed {cfg['seed']:#x}), generated per rank",
             "config": {
-                "workload": cfg["workload"],
+                "workload": cfg["workload"] + ("" if args.records_per_gpu == cfg["records"] else
+                                               f" [run at --records-per-gpu {args.records_per_gpu}: "
+                                               f"{sum(own_sizes) / world / 2**30:.2f} GiB compressed per GPU]"),
                 "records_per_gpu": args.records_per_gpu,
                 "compressed_bytes": int(sum(own_sizes)),
                 "decompressed_bytes": int(total_flat),
