@@ -1373,7 +1373,10 @@ __global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__rest
   if (tid == 0) bl.status[b] = INF_SERIAL;  // k_huff_serial<true> decodes it
 }
 
-constexpr uint32_t LZ_TPT = 2;                         // tokens per thread per chunk
+#ifndef SBH_LZ_TPT
+#define SBH_LZ_TPT 3
+#endif
+constexpr uint32_t LZ_TPT = SBH_LZ_TPT;                       // tokens per thread per chunk
 constexpr uint32_t LZ_CHUNK = LZ_THREADS * LZ_TPT;      // tokens per chunk
 constexpr uint32_t PTR_HALF = 8;                        // pointer slots per thread and pass
 constexpr uint32_t PTR_CAP = 7552;                      // chunk bytes resolved by pointer chasing
@@ -1458,7 +1461,7 @@ __device__ __forceinline__ uint4 pack8_u16(const uint32_t *c) {
                     __builtin_amdgcn_perm(c[5], c[4], 0x05040100u), __builtin_amdgcn_perm(c[7], c[6], 0x05040100u));
 }
 
-// LZ77 resolution of one block per workgroup, LZ_CHUNK tokens per chunk (two consecutive
+// LZ77 resolution of one block per workgroup, LZ_CHUNK tokens per chunk (LZ_TPT consecutive
 // tokens per thread); bytes before the chunk are final.  A chunk whose output fits PTR_CAP
 // bytes (the common case) is resolved by pointer chasing: every byte gets the position it
 // copies from (itself for a literal; match byte k: off - dist + k mod dist, always
@@ -1492,7 +1495,7 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
 #ifdef SBH_LZ_PROBE
     uint64_t ta = __builtin_readcyclecounter();
 #endif
-    // this thread's two tokens
+    // this thread's LZ_TPT tokens
     const uint32_t i0 = c0 + LZ_TPT * t;
     uint32_t x[LZ_TPT], len[LZ_TPT], dist[LZ_TPT], off[LZ_TPT];
     bool match[LZ_TPT];
