@@ -61,6 +61,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-full", action="store_true", help="skip the full-checker side measurement")
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes per launch of the dominant kernel (default: the committed "
                          "rocprofv3 --pmc summary, profiles/*_pmc_traffic.json)")
@@ -206,6 +207,27 @@ def main():
     def gbps(nbytes, ms):
         return round(nbytes / (ms * 1e-3) / 1e9, 2) if ms > 0 else None
 
+    # Full-checker mode, reported separately: full.Checker at every owned
+    # position with the FullCheck Counts aggregation (no per-position words), on the
+    # inflated shard the last step left; wall time of the synchronous call, best of 2.
+    full = None
+    if not args.no_full:
+        f0 = max(0, shard.flat_bound(seg.file_offset)) if seg.file_offset else 0
+        f1 = shard.flat_bound(seg.own_end)
+        best = None
+        for _ in range(2):
+            torch.cuda.synchronize()
+            t0f = time.perf_counter()
+            fr = shard.check_full(f0, f1, want_words=False, close_cap=1 << 16)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0f
+            best = dt if best is None else min(best, dt)
+        full = {"positions": int(f1 - f0), "ms": round(best * 1e3, 3),
+                "GBps_decompressed": round((f1 - f0) / best / 1e9, 2),
+                "n_success": int(fr["n_success"]), "close_calls": int(fr["n_close"]),
+                "note": "sbh_check_full over the owned flat range (Counts + rbe histograms + close calls), "
+                        "inflated shard already resident; not part of `value`"}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(shard, seg.comp, contig_len, args.cpu_seconds, args.cpu_threads)
@@ -270,6 +292,7 @@ def main():
                 },
                 "per_kernel_GBps": {k: gbps(v[0], v[1]) for k, v in kern.items()},
             },
+            "full_check": full,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -1771,7 +1771,7 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
     for (uint32_t l = 0; l < WAVE; ++l) tot += __builtin_amdgcn_readlane(njumps, l);
     njumps = tot;
   }
-  if (lane == 0 && b < 2)
+  if (lane == 0 && (b == 1 || b == 1000) && t < WAVE)
     printf("lz blk %llu wave %u ntok %u cyc %llu pre %llu marks %llu marks+slots %llu init+bar %llu chase %llu resolve+bar %llu fallback %u chase_rounds %u long %u\n",
            (unsigned long long)b, t / WAVE, n, (unsigned long long)(__builtin_readcyclecounter() - tp0),
            (unsigned long long)t_pre, (unsigned long long)t_mk, (unsigned long long)t_w, (unsigned long long)t_init,
