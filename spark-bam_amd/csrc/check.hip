@@ -23,7 +23,10 @@ namespace sbh {
 namespace {
 
 constexpr uint32_t TILE = 4096;
-constexpr uint32_t HALO = 1024;
+#ifndef SBH_FULL_HALO
+#define SBH_FULL_HALO 1024
+#endif
+constexpr uint32_t HALO = SBH_FULL_HALO;  // staged look-ahead: chains of short reads stay in LDS
 constexpr uint32_t STAGE = TILE + HALO + 8;  // bytes staged (+ slack for dword pairs)
 constexpr uint32_t T = 256;
 
@@ -103,6 +106,24 @@ __device__ __forceinline__ int32_t implied_min_remaining(int32_t rnl, int32_t nc
   return (int32_t)(32u + (uint32_t)rnl + 4u * (uint32_t)nc + (uint32_t)nsq);
 }
 
+// The first CIGAR op k < nc (ops at q + 4k) that does not fit below `bound`
+// (q + 4k + 4 > bound) or is invalid ((byte & 0xf) > 8); nc if none.  Eight op bytes are
+// loaded per step before any test, so a long run of valid ops costs one load latency per
+// eight ops rather than per op (op bytes past `bound` are loaded but never decide).
+__device__ __forceinline__ uint32_t first_bad_op(const Src &s, uint64_t q, uint32_t nc, uint64_t bound) {
+  const uint64_t fit = bound >= q ? (bound - q) / 4 : 0;
+  const uint32_t lim = fit < (uint64_t)nc ? (uint32_t)fit : nc;
+  for (uint32_t k = 0; k < lim; k += 8) {
+    uint8_t b[8];
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) b[j] = s.byte_at(q + 4ull * (k + j));
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j)
+      if (k + j < lim && (b[j] & 0xf) > 8) return k + j;
+  }
+  return lim;
+}
+
 // Eager check at p: 0 false, 1 true, 2 unknown (needs bytes past an open end), 3 deferred
 // (needs flat bytes at or past `front`, which are not inflated yet: the pipelined run
 // re-checks the position once they are).
@@ -135,11 +156,15 @@ __device__ uint32_t eager_at(const Src &s, uint64_t p, uint64_t total, bool open
     if (s.byte_at(cur + rnl - 1) != 0) return 0;
     if (!name_bytes_ok(s, cur, (uint32_t)rnl - 1)) return 0;
     cur += rnl;
-    for (int32_t k = 0; k < nc; ++k) {
-      if (cur + 4 > total) return open ? 2 : 0;
-      if (cur + 4 > front) return EAGER_DEFER;
-      if ((s.byte_at(cur) & 0xf) > 8) return 0;
-      cur += 4;
+    {  // the op loop's outcome order: past total, past front, invalid op
+      const uint32_t kb = first_bad_op(s, cur, (uint32_t)nc, total < front ? total : front);
+      if (kb < (uint32_t)nc) {
+        const uint64_t e = cur + 4ull * kb + 4;
+        if (e > total) return open ? 2 : 0;
+        if (e > front) return EAGER_DEFER;
+        return 0;
+      }
+      cur += 4ull * (uint32_t)nc;
     }
     if ((int64_t)(nominal - cur) > 0) {
       if (nominal > total) {
@@ -194,20 +219,17 @@ __device__ uint32_t full_at(const Src &s, uint64_t p, uint64_t total, bool open,
     }
     if (!name_eof) {
       bool cig_err = false;
-      for (int32_t k = 0; k < nc; ++k) {
-        if (cur + 4 > total) {
+      const uint32_t kb = first_bad_op(s, cur, (uint32_t)nc, total);
+      if (kb < (uint32_t)nc) {  // past the stream end first, else an invalid op
+        cig_err = true;
+        if (cur + 4ull * kb + 4 > total) {
           if (open) return FULL_UNKNOWN;
           f |= 1u << 14;
-          cig_err = true;
-          break;
-        }
-        if ((s.byte_at(cur) & 0xf) > 8) {
+        } else {
           f |= 1u << 15;
-          cig_err = true;
-          cur += 4;
-          break;
         }
-        cur += 4;
+      } else {
+        cur += 4ull * (uint32_t)nc;
       }
       if (!cig_err && (flags & 4) == 0 && (seq_len == 0 || nc == 0)) {
         if (seq_len == 0) f |= 1u << 16;  // EmptyMapped(emptySeq, emptyCigar) field swap
@@ -336,8 +358,8 @@ __device__ __forceinline__ uint32_t one_record(const Src &s, uint64_t q, uint64_
   if (s.byte_at(cur + rnl - 1) != 0) return 0;
   if (!name_bytes_ok(s, cur, (uint32_t)rnl - 1)) return 0;
   cur += rnl;
-  for (int32_t k = 0; k < nc; ++k, cur += 4)
-    if ((s.byte_at(cur) & 0xf) > 8) return 0;
+  if (first_bad_op(s, cur, (uint32_t)nc, cur + 4ull * (uint32_t)nc) < (uint32_t)nc) return 0;
+  cur += 4ull * (uint32_t)nc;
   const uint64_t nominal = q + 4 + (int64_t)rem;
   *succ = nominal;
   *normal = (int64_t)(nominal - cur) >= 0;

@@ -1,0 +1,42 @@
+#!/usr/bin/env python3
+"""Time sbh_check_full on a synthetic short-read shard for a few readsToCheck values
+(where does k_full's time go: the first record of every position, or the chains of
+the positions that pass it?).  usage: python tools/full_ab.py [--records N]"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--records", type=int, default=2_000_000)
+    a = ap.parse_args()
+    import synth
+    from __graft_entry__ import load_package
+    sb = load_package()
+    p = synth.params(synth.SEEDS["B"])
+    data, usize, nb = synth.make_bam(p, a.records)
+    with sb.Context(0) as ctx:
+        sh = ctx.shard(data)
+        _, cl, _ = sb.parse_bam_header(synth.header_bytes())
+        sh.set_contigs(cl)
+        sh.index(0)
+        sh.inflate()
+        for rtc in (10, 2, 1, 0):
+            best = None
+            for _ in range(3):
+                t0 = time.perf_counter()
+                r = sh.check_full(0, sh.flat_size, reads_to_check=rtc, close_cap=1 << 10)
+                dt = time.perf_counter() - t0
+                best = dt if best is None else min(best, dt)
+            print(f"rtc {rtc}: {best * 1e3:.2f} ms for {sh.flat_size} positions "
+                  f"({sh.flat_size / best / 1e9:.1f} GB/s), success {r['n_success']}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
