@@ -918,7 +918,7 @@ constexpr uint32_t HT = SBH_HT;              // k_huff lanes per BGZF block
 constexpr uint32_t STAGE_DW = SBH_STAGE_DW;  // deflate bytes staged in LDS (24 KiB)
 constexpr uint32_t PAR_MIN_USIZE = 4096;     // smaller blocks decode serially
 #ifndef SBH_MIN_SLICE
-#define SBH_MIN_SLICE 256
+#define SBH_MIN_SLICE 128
 #endif
 constexpr uint32_t MIN_SLICE = SBH_MIN_SLICE;  // bits per lane at least
 constexpr uint32_t NOPOS = 0xffffffffu;
