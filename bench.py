@@ -174,7 +174,10 @@ def main():
     _, _, stitch = sharded.stitch(parts, seg.file_size)
     # eager-true positions equal the records except where the input carries false-positive
     # bait (config E), whose exact bits are pinned by the parity tests, not here
-    ok = total_records == expect and (total_true == expect or not cfg["fp_free"]) and stitch["ok"]
+    # every inflated block of the last step against its BGZF footer CRC32 (full-size
+    # bit-exactness of the inflate), outside the timed region
+    crc_bad, _ = shard.verify_crc()
+    ok = total_records == expect and (total_true == expect or not cfg["fp_free"]) and stitch["ok"] and crc_bad == 0
     firsts = [x[0] for x in allr if x[1] > 0]
 
     stage_ms = stage_acc / args.steps
@@ -262,6 +265,7 @@ def main():
             "compressed_GBps": round(sum(own_sizes) * args.steps / elapsed / 1e9, 3),
             "correct": bool(ok),
             "stitch_ok": bool(stitch["ok"]),
+            "crc_bad_blocks_rank0": int(crc_bad),
             "records": int(total_records),
             "eager_true": int(total_true),
             "stages_ms_rank0": {"index": round(stage_ms[0], 3),

@@ -122,6 +122,11 @@ int sbh_get_blocks(sbh_shard *sh, uint64_t first, uint64_t count, sbh_block *out
  * indexed block: the shard's flat uncompressed buffer in HBM.  Fails with the first
  * block error in file order (SBH_E_INFLATE_SIZE / _DATA / _BAD_ISIZE, *bad_block). */
 int sbh_inflate(sbh_shard *sh, uint64_t *bad_block);
+
+/* CRC32 of every inflated block's bytes against its BGZF footer (the reference reads only
+ * ISIZE, Stream.scala:47-54; SURVEY 8d asks for CRC32 as the in-run correctness check).
+ * *n_bad = blocks whose CRC differs; *first_bad (optional) = the first one's file offset. */
+int sbh_verify_crc(sbh_shard *sh, uint64_t *n_bad, uint64_t *first_bad);
 /* Copy flat bytes [flat, flat + n) to host memory. */
 int sbh_read_flat(sbh_shard *sh, uint64_t flat, uint64_t n, uint8_t *out);
 const void *sbh_flat_device_ptr(sbh_shard *sh);

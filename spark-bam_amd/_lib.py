@@ -36,7 +36,7 @@ EXPORTS = [
     "sbh_get_blocks", "sbh_inflate", "sbh_read_flat", "sbh_flat_device_ptr", "sbh_flat_of",
     "sbh_pos_of", "sbh_flat_bound", "sbh_set_contigs", "sbh_check_eager", "sbh_eager_bits", "sbh_check_full",
     "sbh_find_record_start", "sbh_count_records", "sbh_split", "sbh_run_shard",
-    "sbh_stage_times", "sbh_records_scan", "sbh_records_fetch", "sbh_records_scan_regions",
+    "sbh_stage_times", "sbh_records_scan", "sbh_records_fetch", "sbh_records_scan_regions", "sbh_verify_crc",
 ]
 
 
@@ -110,6 +110,7 @@ def lib():
         "sbh_records_scan": [P, U64, U64, C.POINTER(SbhRecordsSizes)],
         "sbh_records_fetch": [P, C.POINTER(SbhRecordsOut)],
         "sbh_records_scan_regions": [P, P, P, U64, P, P, P, C.c_uint32, C.POINTER(SbhRecordsSizes)],
+        "sbh_verify_crc": [P, PU64, PU64],
     }
     for name, args in sig.items():
         f = getattr(L, name)

@@ -487,6 +487,26 @@ int sbh_inflate(sbh_shard *sh, uint64_t *bad_block) {
   return SBH_OK;
 }
 
+// BGZF footer CRC32 of every inflated block vs its bytes in U (crc.hip): the full-size
+// bit-exactness check of the inflate (the reference itself never checks CRC32).
+int sbh_verify_crc(sbh_shard *sh, uint64_t *n_bad, uint64_t *first_bad) {
+  if (!sh || !n_bad) return SBH_E_ARG;
+  sbh_ctx *ctx = sh->ctx;
+  if (!sh->inflated) return fail(ctx, SBH_E_STATE, "verify_crc before inflate");
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  hipStream_t st = ctx->stream;
+  unsigned long long *c = sh->ctr.p + 32;
+  HIPCHK(ctx, hipMemsetAsync(c, 0, 8, st));
+  HIPCHK(ctx, hipMemsetAsync(c + 1, 0xff, 8, st));
+  HIPCHK(ctx, launch_block_crc(sh->comp.p, sh->dev_blocks(), sh->nblocks, sh->U.p, c, c + 1, st));
+  HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 32, c, 16, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  *n_bad = sh->h_ctr[32];
+  if (first_bad) *first_bad = sh->h_ctr[32] ? sh->hb[sh->h_ctr[33]].start : 0;
+  return SBH_OK;
+}
+
 int sbh_read_flat(sbh_shard *sh, uint64_t flat, uint64_t n, uint8_t *out) {
   if (!sh || (!out && n)) return SBH_E_ARG;
   if (!sh->inflated) return fail(sh->ctx, SBH_E_STATE, "not inflated");

@@ -124,6 +124,13 @@ class Shard:
         bad = C.c_uint64()
         self._c(lib().sbh_inflate(self.h, C.byref(bad)))
 
+    def verify_crc(self):
+        """(blocks whose footer CRC32 differs from their inflated bytes, first such block's
+        file offset) -- sbh_verify_crc."""
+        n, f = C.c_uint64(), C.c_uint64()
+        self._c(lib().sbh_verify_crc(self.h, C.byref(n), C.byref(f)))
+        return n.value, f.value
+
     def read_flat(self, flat=0, n=None):
         n = self.flat_size - flat if n is None else n
         out = np.empty(n, dtype=np.uint8)
