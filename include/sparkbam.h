@@ -254,6 +254,20 @@ int sbh_records_scan_regions(sbh_shard *sh, const uint64_t *chunk_begin, const u
                              uint64_t n_chunks, const int32_t *iv_ref, const int64_t *iv_begin,
                              const int64_t *iv_end, uint32_t n_iv, sbh_records_sizes *out);
 
+/* ---- BGZF writer -------------------------------------------------
+ * The block compressor behind HTSJDKRewrite (cli/src/main/scala/org/hammerlab/bam/rewrite/
+ * HTSJDKRewrite.scala:62-67: SAMFileWriterFactory.makeBAMWriter -> htsjdk
+ * BlockCompressedOutputStream): the uncompressed stream src[0, n) is cut every 65498 bytes,
+ * each piece becomes one BGZF member (deflate; stored when it would not fit 64 KiB), CRC32 +
+ * ISIZE footer, then the 28-byte empty EOF member.  Member boundaries in uncompressed space
+ * match htsjdk's; the deflate bytes are this library's own (greedy LZ77, fixed Huffman), not
+ * zlib level 5.  src is a host or device pointer (src_on_device); out is host memory of at
+ * least sbh_bgzf_compress_bound(n) bytes.  *deflate_ms (optional): the compress kernel's
+ * device time (HIP events on the context's stream). */
+uint64_t sbh_bgzf_compress_bound(uint64_t n);
+int sbh_bgzf_compress(sbh_ctx *ctx, const void *src, uint64_t n, int src_on_device, uint8_t *out,
+                      uint64_t out_cap, uint64_t *out_size, uint64_t *n_blocks, float *deflate_ms);
+
 #ifdef __cplusplus
 }
 #endif

@@ -37,6 +37,7 @@ EXPORTS = [
     "sbh_pos_of", "sbh_flat_bound", "sbh_set_contigs", "sbh_check_eager", "sbh_eager_bits", "sbh_check_full",
     "sbh_find_record_start", "sbh_count_records", "sbh_split", "sbh_run_shard",
     "sbh_stage_times", "sbh_records_scan", "sbh_records_fetch", "sbh_records_scan_regions", "sbh_verify_crc",
+    "sbh_bgzf_compress_bound", "sbh_bgzf_compress",
 ]
 
 
@@ -111,11 +112,14 @@ def lib():
         "sbh_records_fetch": [P, C.POINTER(SbhRecordsOut)],
         "sbh_records_scan_regions": [P, P, P, U64, P, P, P, C.c_uint32, C.POINTER(SbhRecordsSizes)],
         "sbh_verify_crc": [P, PU64, PU64],
+        "sbh_bgzf_compress": [P, P, U64, I32, P, U64, PU64, PU64, C.POINTER(C.c_float)],
     }
     for name, args in sig.items():
         f = getattr(L, name)
         f.argtypes = args
         f.restype = C.c_int
+    L.sbh_bgzf_compress_bound.argtypes = [U64]
+    L.sbh_bgzf_compress_bound.restype = U64
     L.sbh_stage_times.argtypes = [P, C.POINTER(C.c_double), I32]
     L.sbh_stage_times.restype = C.c_int
     L.sbh_last_error.argtypes = [P]

@@ -278,3 +278,32 @@ def word_flags_mask(word):
 
 def here():
     return os.path.dirname(os.path.abspath(__file__))
+
+
+def htsjdk_rewrite(path_or_bytes, out_path=None, read_ranges=None, ctx=None):
+    """HTSJDKRewrite (cli/src/main/scala/org/hammerlab/bam/rewrite/HTSJDKRewrite.scala:40-67):
+    the BAM's uncompressed stream -- header, then every record (or only those whose index is
+    in `read_ranges`, a collection supporting `in`, like the reference's `-r` IntRanges,
+    :48-58) -- re-cut into 65498-byte BGZF members on the GPU (sbh_bgzf_compress) plus the
+    EOF member.  Records pass through byte-for-byte (htsjdk's decode/re-encode is the
+    identity on the records of a BAM it wrote).  Returns the file bytes (numpy uint8); writes
+    them to out_path when given.  The `-b`/`-i` index side-outputs are the CLI's
+    `index-blocks` / `index-records` run on the result."""
+    L = _Loaded(path_or_bytes, ctx)
+    try:
+        sh = L.shard
+        if read_ranges is None:
+            out, _, _ = L.ctx.bgzf_compress(sh.flat_ptr(), sh.flat_size)
+        else:
+            flat = sh.read_flat()
+            starts = sh.records(L.header_end, sh.flat_size)["flat"].astype(np.int64)
+            ends = np.append(starts[1:], np.int64(sh.flat_size))
+            parts = [flat[:L.header_end]]
+            parts += [flat[s:e] for i, (s, e) in enumerate(zip(starts, ends)) if i in read_ranges]
+            out, _, _ = L.ctx.bgzf_compress(np.concatenate(parts))
+    finally:
+        L.close()
+    if out_path is not None:
+        with open(out_path, "wb") as f:
+            f.write(out.tobytes())
+    return out

@@ -1322,4 +1322,71 @@ int sbh_records_fetch(sbh_shard *sh, const sbh_records_out *o) {
   return SBH_OK;
 }
 
+// ---- BGZF writer (deflate.hip; HTSJDKRewrite.scala:62-67) ----------------------------
+uint64_t sbh_bgzf_compress_bound(uint64_t n) { return deflate_nblocks(n) * 65536ull + 28; }
+
+int sbh_bgzf_compress(sbh_ctx *ctx, const void *src, uint64_t n, int src_on_device, uint8_t *out,
+                      uint64_t out_cap, uint64_t *out_size, uint64_t *n_blocks, float *deflate_ms) {
+  if (!ctx || !out_size || (!src && n) || !out) return SBH_E_ARG;
+  const uint64_t nb = deflate_nblocks(n);
+  if (out_cap < sbh_bgzf_compress_bound(n)) return fail(ctx, SBH_E_ARG, "bgzf_compress: out_cap < bound");
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  hipStream_t st = ctx->stream;
+  struct Bufs {  // per-call scratch, freed on every return path
+    DBuf<uint8_t> in, slots, packed;
+    DBuf<uint16_t> heads;
+    DBuf<uint32_t> sizes;
+    DBuf<uint64_t> offs;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    ~Bufs() {
+      in.release(), slots.release(), packed.release(), heads.release(), sizes.release(), offs.release();
+      if (e0) (void)hipEventDestroy(e0);
+      if (e1) (void)hipEventDestroy(e1);
+    }
+  } B;
+  const uint8_t *d_src = static_cast<const uint8_t *>(src);
+  if (!src_on_device && n) {
+    HIPCHK(ctx, B.in.ensure(n));
+    HIPCHK(ctx, hipMemcpyAsync(B.in.p, src, n, hipMemcpyHostToDevice, st));
+    d_src = B.in.p;
+  }
+  uint64_t total = 0;
+  if (nb) {
+    HIPCHK(ctx, B.slots.ensure(nb * 65536ull));
+    HIPCHK(ctx, B.heads.ensure(nb * 8192ull));
+    HIPCHK(ctx, B.sizes.ensure(nb));
+    HIPCHK(ctx, B.offs.ensure(nb));
+    HIPCHK(ctx, hipEventCreate(&B.e0));
+    HIPCHK(ctx, hipEventCreate(&B.e1));
+    HIPCHK(ctx, hipEventRecord(B.e0, st));
+    HIPCHK(ctx, launch_deflate(d_src, n, B.slots.p, B.heads.p, B.sizes.p, st));
+    HIPCHK(ctx, hipEventRecord(B.e1, st));
+    std::vector<uint32_t> hs(nb);
+    std::vector<uint64_t> ho(nb);
+    HIPCHK(ctx, hipMemcpyAsync(hs.data(), B.sizes.p, 4 * nb, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    for (uint64_t b = 0; b < nb; ++b) {
+      if (hs[b] < 26 || hs[b] > 65536) return fail(ctx, SBH_E_HIP, "bgzf_compress: block %llu size %u", (unsigned long long)b, hs[b]);
+      ho[b] = total;
+      total += hs[b];
+    }
+    HIPCHK(ctx, B.packed.ensure(total));
+    HIPCHK(ctx, hipMemcpyAsync(B.offs.p, ho.data(), 8 * nb, hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, launch_deflate_gather(B.slots.p, B.sizes.p, B.offs.p, nb, B.packed.p, st));
+    HIPCHK(ctx, hipMemcpyAsync(out, B.packed.p, total, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    if (deflate_ms) HIPCHK(ctx, hipEventElapsedTime(deflate_ms, B.e0, B.e1));
+  } else if (deflate_ms) {
+    *deflate_ms = 0.f;
+  }
+  static const uint8_t eof[28] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0,
+                                  27, 0,   3, 0, 0, 0, 0, 0, 0, 0,   0, 0};
+  memcpy(out + total, eof, 28);
+  *out_size = total + 28;
+  if (n_blocks) *n_blocks = nb;
+  return SBH_OK;
+}
+
 }  // extern "C"
+

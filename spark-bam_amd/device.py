@@ -55,6 +55,20 @@ class Context:
     def __exit__(self, *a):
         self.close()
 
+    def bgzf_compress(self, data, nbytes=None):
+        """BGZF-compress a flat byte stream (sbh_bgzf_compress; htsjdk BlockCompressedOutputStream as
+        driven by HTSJDKRewrite.scala:62-67).  data: numpy uint8 (host) or a device pointer (int)
+        with nbytes.  Returns (file bytes as numpy uint8, number of data members, kernel ms)."""
+        on_dev = isinstance(data, int)
+        n = int(nbytes) if on_dev else int(data.size)
+        cap = lib().sbh_bgzf_compress_bound(n)
+        out = np.empty(cap, dtype=np.uint8)
+        size, nb, ms = C.c_uint64(), C.c_uint64(), C.c_float()
+        src = C.c_void_p(data) if on_dev else _ptr(np.ascontiguousarray(data, dtype=np.uint8))
+        _check(self.h, lib().sbh_bgzf_compress(self.h, src, n, 1 if on_dev else 0, _ptr(out), cap,
+                                               C.byref(size), C.byref(nb), C.byref(ms)))
+        return out[:size.value], nb.value, ms.value
+
     def shard(self, comp, file_offset=0, file_size=None, on_device=False, nbytes=None):
         return Shard(self, comp, file_offset, file_size, on_device, nbytes)
 
@@ -130,6 +144,10 @@ class Shard:
         n, f = C.c_uint64(), C.c_uint64()
         self._c(lib().sbh_verify_crc(self.h, C.byref(n), C.byref(f)))
         return n.value, f.value
+
+    def flat_ptr(self):
+        """Device pointer of the inflated flat bytes (sbh_flat_device_ptr)."""
+        return lib().sbh_flat_device_ptr(self.h)
 
     def read_flat(self, flat=0, n=None):
         n = self.flat_size - flat if n is None else n

@@ -1,0 +1,93 @@
+"""BGZF writer's block coder (spark-bam_amd/csrc/deflate_core.h), host build, round-tripped
+through zlib: the same code k_deflate runs one lane per block.  Checks the member framing
+htsjdk-rewrite produces (HTSJDKRewrite.scala:62-67): 65498-byte payload cut (the usize column
+of the reference's 2.bam.blocks), header/BSIZE, CRC32 + ISIZE footer, the EOF member."""
+import ctypes as C
+import os
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+from conftest import read_blocks
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PAYLOAD = 65498
+EOF_MEMBER = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+
+
+def host_lib():
+    p = os.path.join(ROOT, "tools", "libdeflate_host.so")
+    if not os.path.exists(p):
+        pytest.skip("tools/libdeflate_host.so not built (run __graft_entry__.build())")
+    L = C.CDLL(p)
+    L.sbh_host_bgzf_compress.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p]
+    L.sbh_host_bgzf_compress.restype = C.c_uint64
+    return L
+
+
+def compress(data):
+    a = np.frombuffer(bytes(data), dtype=np.uint8)
+    out = np.empty(((len(a) + PAYLOAD - 1) // PAYLOAD) * 65536 + 28, dtype=np.uint8)
+    n = host_lib().sbh_host_bgzf_compress(a.ctypes.data, len(a), out.ctypes.data)
+    return out[:n].tobytes()
+
+
+def parse_members(f):
+    """[(offset, csize, usize, payload)] of every member, checking framing and CRC32."""
+    out, o = [], 0
+    while o < len(f):
+        assert f[o:o + 4] == b"\x1f\x8b\x08\x04" and f[o + 12:o + 16] == b"BC\x02\x00"
+        bsize = struct.unpack_from("<H", f, o + 16)[0] + 1
+        crc, isize = struct.unpack_from("<II", f, o + bsize - 8)
+        data = zlib.decompressobj(-15).decompress(f[o + 18:o + bsize - 8])
+        assert len(data) == isize and zlib.crc32(data) == crc
+        out.append((o, bsize, isize, data))
+        o += bsize
+    assert o == len(f)
+    return out
+
+
+def check_roundtrip(data):
+    f = compress(data)
+    m = parse_members(f)
+    assert f.endswith(EOF_MEMBER) and m[-1][2] == 0
+    assert b"".join(x[3] for x in m) == bytes(data)
+    us = [x[2] for x in m[:-1]]
+    assert all(u == PAYLOAD for u in us[:-1]) and (not us or 0 < us[-1] <= PAYLOAD)
+    return f, m
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 257, PAYLOAD - 1, PAYLOAD, PAYLOAD + 1, 3 * PAYLOAD + 17])
+def test_sizes_random_and_runs(n):
+    rng = np.random.default_rng(n)
+    check_roundtrip(rng.integers(0, 256, n, dtype=np.uint8).tobytes())  # incompressible: stored
+    check_roundtrip(bytes(n))                                            # one long run
+    check_roundtrip(rng.integers(0, 4, n, dtype=np.uint8).tobytes())     # small alphabet
+
+
+def test_every_length_and_distance_code():
+    # matches of every length 3..258 at distances across every distance code (1..32768)
+    rng = np.random.default_rng(7)
+    parts = []
+    for d in [1, 2, 3, 4, 5, 7, 8, 9, 13, 17, 33, 65, 129, 257, 513, 1025, 2049, 4097, 8193, 16385, 24577, 32768]:
+        base = rng.integers(0, 256, d, dtype=np.uint8).tobytes()
+        parts.append(base + (base * (300 // d + 2))[:int(rng.integers(3, 259))])
+    data = b"".join(parts)
+    for L in range(3, 259):
+        data += bytes([L & 0xff, 0xAB, L >> 8]) * (L // 3 + 2)
+    f, _ = check_roundtrip(data)
+    assert len(f) < len(data)
+
+
+def test_rewrite_2bam_member_layout(bams):
+    """2.bam's flat stream re-cut: the same usize sequence as the reference's 2.bam.blocks
+    (24 x 65498 + 34570), every member CRC-correct, and compressed (not stored)."""
+    with open(os.path.join(bams, "2.bam"), "rb") as fh:
+        comp = fh.read()
+    flat = b"".join(zlib.decompressobj(-15).decompress(comp[o + 18:o + c - 8])
+                    for o, c, _ in read_blocks("2.bam"))
+    f, m = check_roundtrip(flat)
+    assert [x[2] for x in m[:-1]] == [u for _, _, u in read_blocks("2.bam")]
+    assert len(f) < 0.6 * len(flat)
