@@ -1334,13 +1334,13 @@ int sbh_bgzf_compress(sbh_ctx *ctx, const void *src, uint64_t n, int src_on_devi
   if (rc) return rc;
   hipStream_t st = ctx->stream;
   struct Bufs {  // per-call scratch, freed on every return path
-    DBuf<uint8_t> in, slots, packed;
+    DBuf<uint8_t> in, slots, packed, segbuf;
     DBuf<uint16_t> heads;
     DBuf<uint32_t> sizes;
     DBuf<uint64_t> offs;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     ~Bufs() {
-      in.release(), slots.release(), packed.release(), heads.release(), sizes.release(), offs.release();
+      in.release(), slots.release(), packed.release(), segbuf.release(), heads.release(), sizes.release(), offs.release();
       if (e0) (void)hipEventDestroy(e0);
       if (e1) (void)hipEventDestroy(e1);
     }
@@ -1354,13 +1354,14 @@ int sbh_bgzf_compress(sbh_ctx *ctx, const void *src, uint64_t n, int src_on_devi
   uint64_t total = 0;
   if (nb) {
     HIPCHK(ctx, B.slots.ensure(nb * 65536ull));
-    HIPCHK(ctx, B.heads.ensure(nb * 8192ull));
+    HIPCHK(ctx, B.heads.ensure(nb * 16ull * 4096ull));
+    HIPCHK(ctx, B.segbuf.ensure(nb * 16ull * 4624ull));
     HIPCHK(ctx, B.sizes.ensure(nb));
     HIPCHK(ctx, B.offs.ensure(nb));
     HIPCHK(ctx, hipEventCreate(&B.e0));
     HIPCHK(ctx, hipEventCreate(&B.e1));
     HIPCHK(ctx, hipEventRecord(B.e0, st));
-    HIPCHK(ctx, launch_deflate(d_src, n, B.slots.p, B.heads.p, B.sizes.p, st));
+    HIPCHK(ctx, launch_deflate(d_src, n, B.slots.p, B.segbuf.p, B.heads.p, B.sizes.p, st));
     HIPCHK(ctx, hipEventRecord(B.e1, st));
     std::vector<uint32_t> hs(nb);
     std::vector<uint64_t> ho(nb);

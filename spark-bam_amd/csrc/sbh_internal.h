@@ -97,8 +97,8 @@ hipError_t launch_block_crc(const uint8_t *comp, DevBlocks bl, uint64_t nblocks,
 // BGZF writer (deflate.hip): k_deflate fills one 64 KiB slot per 65498-byte piece and its
 // member size; k_gather packs the slots at the host-computed file offsets.
 uint64_t deflate_nblocks(uint64_t n);
-hipError_t launch_deflate(const uint8_t *src, uint64_t n, uint8_t *slots, uint16_t *heads, uint32_t *sizes,
-                          hipStream_t st);
+hipError_t launch_deflate(const uint8_t *src, uint64_t n, uint8_t *slots, uint8_t *segbuf, uint16_t *heads,
+                          uint32_t *sizes, hipStream_t st);
 hipError_t launch_deflate_gather(const uint8_t *slots, const uint32_t *sizes, const uint64_t *offs, uint64_t nblocks,
                                  uint8_t *out, hipStream_t st);
 

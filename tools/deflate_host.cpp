@@ -16,13 +16,13 @@ extern "C" uint64_t sbh_host_bgzf_compress(const uint8_t *src, uint64_t n, uint8
     for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
     tab[t] = c;
   }
-  std::vector<uint16_t> head(HSIZE);
-  std::vector<uint8_t> slot(SLOT);
+  std::vector<uint16_t> head(SHSIZE);
+  std::vector<uint8_t> slot(SLOT), segbuf(NSEG * SEGCAP);
   uint64_t o = 0;
   for (uint64_t s = 0; s < n; s += PAYLOAD) {
     const uint32_t len = (uint32_t)(n - s < PAYLOAD ? n - s : PAYLOAD);
-    std::fill(head.begin(), head.end(), 0);
-    const uint32_t m = bgzf_block(src + s, len, slot.data(), head.data(), tab);
+    std::fill(slot.begin(), slot.end(), 0);
+    const uint32_t m = bgzf_block(src + s, len, slot.data(), segbuf.data(), head.data(), tab);
     memcpy(out + o, slot.data(), m);
     o += m;
   }
