@@ -59,7 +59,8 @@ def main():
     ap.add_argument("--records-per-gpu", type=int, default=None,
                     help="~1.0 GiB compressed per GPU at level 6 (config B)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="CPU baseline threads (default: every host core this process may use)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-full", action="store_true", help="skip the full-checker side measurement")
     ap.add_argument("--traffic", type=float, default=None,
@@ -310,6 +311,19 @@ def main():
         sys.exit(3)
 
 
+def host_cores():
+    """(cores this process may run on, what limits it): the scheduler affinity mask capped by
+    the cgroup CPU quota (a GPU box's share of the host), so no thread waits for a core."""
+    n, why = len(os.sched_getaffinity(0)), "sched_getaffinity"
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max" and int(quota) // int(period) < n:
+            n, why = max(1, int(quota) // int(period)), f"cgroup cpu.max {quota}/{period}"
+    except (OSError, ValueError):
+        pass
+    return n, why
+
+
 def cpu_baseline(shard, comp, contig_len, budget_s, threads):
     """The oracle (C restatement of the reference path: zlib inflate + eager check at
     every offset) on the host cores, over a bounded sample of the same shard's
@@ -320,6 +334,9 @@ def cpu_baseline(shard, comp, contig_len, budget_s, threads):
     from oracle_lib import Block, lib as olib  # the CPU oracle, timed as the baseline
 
     lib = olib()
+    limit = None
+    if threads is None:
+        threads, limit = host_cores()
     shard.index(shard.file_offset)  # host copy of the block table
     blocks = shard.blocks()
     base = shard.file_offset
@@ -345,6 +362,9 @@ def cpu_baseline(shard, comp, contig_len, budget_s, threads):
         "value": round(pos.value / ts / 1e9, 4),
         "unit": "GB/s decompressed",
         "cores": threads,
+        "cores_limit": limit or "--cpu-threads",
+        "host_cpus_visible": os.cpu_count(),
+        "zlib_version": lib.or_zlib_version().decode(),
         "kind": "port",
         "sample": f"first {n} of {nb} BGZF blocks of the rank-0 shard ({pos.value / 1e6:.0f} MB "
                   f"uncompressed): zlib inflate + eager check at every offset, {threads} pthreads, "

@@ -278,15 +278,21 @@ struct SplitsResult {
 
 // CanLoadBam.loadSplitsAndReads (load/.../CanLoadBam.scala:268-302)
 SplitsResult spark_bam_splits(Loaded &L, const Args &a, uint64_t split_size) {
-  uint64_t n_true = 0;
-  chk(sbh_check_eager(L.sh, 0, L.flat, a.reads_to_check, nullptr, &n_true), "eager");
+  // every split in one batch: FindBlockStart + FindRecordStart + counts on the device
+  const auto sp = file_splits(L.data.size(), split_size);
+  const uint64_t n = sp.size();
+  std::vector<uint64_t> st(n), en(n), v(n), cnt(n);
+  std::vector<int32_t> status(n);
+  for (uint64_t i = 0; i < n; ++i) st[i] = sp[i].first, en[i] = sp[i].second;
+  chk(sbh_split_starts(L.sh, st.data(), en.data(), n, a.blocks_to_check, a.reads_to_check, a.max_read_size,
+                       v.data(), cnt.data(), status.data(), nullptr),
+      "splits");
   SplitsResult r;
   std::vector<Pos> firsts;
-  for (auto &sp : file_splits(L.data.size(), split_size)) {
-    uint64_t v = 0, n = 0;
-    chk(sbh_split(L.sh, sp.first, sp.second, a.blocks_to_check, a.reads_to_check, a.max_read_size, &v, &n), "split");
-    r.counts.push_back(n);
-    if (n) firsts.push_back(Pos{v >> 16, (uint32_t)(v & 0xffff)});
+  for (uint64_t i = 0; i < n; ++i) {
+    if (status[i]) throw Error(status[i], "split " + std::to_string(sp[i].first) + "-" + std::to_string(sp[i].second));
+    r.counts.push_back(cnt[i]);
+    if (cnt[i]) firsts.push_back(Pos{v[i] >> 16, (uint32_t)(v[i] & 0xffff)});
   }
   for (size_t i = 0; i < firsts.size(); ++i)
     r.splits.push_back({firsts[i], i + 1 < firsts.size() ? firsts[i + 1] : Pos{L.data.size(), 0}});
@@ -359,10 +365,15 @@ std::vector<Pos> read_records_file(const std::string &p) {
   return out;
 }
 
+// Set bits of an LSB-first bitmap as positions base + i (64 positions per step).
 std::vector<uint64_t> bits_to_positions(const std::vector<uint8_t> &bits, uint64_t base, uint64_t n) {
   std::vector<uint64_t> out;
-  for (uint64_t i = 0; i < n; ++i)
-    if (bits[i >> 3] & (1u << (i & 7))) out.push_back(base + i);
+  for (uint64_t i = 0; i < n; i += 64) {
+    uint64_t w = 0;
+    std::memcpy(&w, bits.data() + i / 8, std::min<uint64_t>(8, bits.size() - i / 8));
+    if (n - i < 64) w &= (1ull << (n - i)) - 1;
+    for (; w; w &= w - 1) out.push_back(base + i + (uint64_t)__builtin_ctzll(w));
+  }
   return out;
 }
 
@@ -370,33 +381,22 @@ int check_bam(const Args &a) {
   if (!a.s) no_hadoop_bam();
   Loaded L(a.path);
   std::vector<Pos> recs = read_records_file(a.records.empty() ? a.path + ".records" : a.records);
-  std::vector<uint64_t> truth;
-  for (auto &r : recs) {
-    uint64_t f = 0;
-    chk(sbh_flat_of(L.sh, r.block, r.off, &f), "records file position");
-    truth.push_back(f);
-  }
-  std::sort(truth.begin(), truth.end());
+  std::vector<uint64_t> truth(recs.size());
+  for (size_t i = 0; i < recs.size(); ++i) truth[i] = recs[i].block << 16 | recs[i].off;
   uint64_t comp = 0;
   auto fr = selected(L, a, &comp);
-  uint64_t tp = 0, fp = 0, fn = 0, positions = 0;
-  std::vector<uint64_t> fps, fns;
-  for (auto &r : fr) {
-    std::vector<uint8_t> bits((r.second - r.first + 7) / 8);
-    uint64_t n = 0;
-    chk(sbh_check_eager(L.sh, r.first, r.second, a.reads_to_check, bits.data(), &n), "eager");
-    auto called = bits_to_positions(bits, r.first, r.second - r.first);
-    auto lo = std::lower_bound(truth.begin(), truth.end(), r.first);
-    auto hi = std::lower_bound(truth.begin(), truth.end(), r.second);
-    std::vector<uint64_t> t(lo, hi), both;
-    std::set_intersection(called.begin(), called.end(), t.begin(), t.end(), std::back_inserter(both));
-    std::set_difference(called.begin(), called.end(), t.begin(), t.end(), std::back_inserter(fps));
-    std::set_difference(t.begin(), t.end(), called.begin(), called.end(), std::back_inserter(fns));
-    tp += both.size();
-    positions += r.second - r.first;
-  }
-  fp = fps.size();
-  fn = fns.size();
+  std::vector<uint64_t> rb(fr.size()), re(fr.size());
+  uint64_t positions = 0;
+  for (size_t i = 0; i < fr.size(); ++i) rb[i] = fr[i].first, re[i] = fr[i].second, positions += re[i] - rb[i];
+  // TP / FP / FN on the device: eager bitmap vs the truth bitmap, mismatches compacted
+  const uint64_t cap = (uint64_t)std::max(a.limit, 0L);
+  std::vector<uint64_t> fps(cap + 1), fns(cap + 1);
+  uint64_t out[4] = {0, 0, 0, 0};
+  chk(sbh_check_records(L.sh, rb.data(), re.data(), fr.size(), a.reads_to_check, truth.data(), truth.size(), out,
+                        fps.data(), cap, fns.data(), cap),
+      "check-bam");
+  if (out[3]) throw Error(SBH_E_NOT_FOUND, std::to_string(out[3]) + " records-file positions are not block starts");
+  const uint64_t tp = out[0], fp = out[1], fn = out[2];
   printf("%llu uncompressed positions\n%s compressed\nCompression ratio: %.2f\n%llu reads\n",
          (unsigned long long)positions, bytes_fmt(comp).c_str(), (double)positions / (double)comp,
          (unsigned long long)(tp + fn));
@@ -407,11 +407,11 @@ int check_bam(const Args &a) {
   printf("%llu false positives, %llu false negatives\n\n", (unsigned long long)fp, (unsigned long long)fn);
   if (fp) {
     printf("False positives:\n");
-    for (size_t i = 0; i < fps.size() && (long)i < a.limit; ++i) printf("\t%s\n", L.pos(fps[i]).str().c_str());
+    for (uint64_t i = 0; i < std::min(fp, cap); ++i) printf("\t%s\n", L.pos(fps[i]).str().c_str());
   }
   if (fn) {
     printf("%llu false negatives:\n", (unsigned long long)fn);
-    for (size_t i = 0; i < fns.size() && (long)i < a.limit; ++i) printf("\t%s\n", L.pos(fns[i]).str().c_str());
+    for (uint64_t i = 0; i < std::min(fn, cap); ++i) printf("\t%s\n", L.pos(fns[i]).str().c_str());
   }
   return 0;
 }

@@ -185,6 +185,36 @@ int sbh_split(sbh_shard *sh, uint64_t start, uint64_t end, int32_t bgzf_blocks_t
               int32_t reads_to_check, int32_t max_read_size, uint64_t *first_vpos,
               uint64_t *count);
 
+/* The record chain from first_flat (PosStream.scala:14-22) as sbh_count_records, plus its
+ * exit: the first chain record at/after end_flat (or the stream end).  The multi-GPU stitch
+ * re-walks a shard from its upstream neighbour's exit with this. */
+int sbh_chain_from(sbh_shard *sh, uint64_t first_flat, uint64_t end_flat, uint64_t *count,
+                   uint64_t *exit_flat);
+
+/* Every split of loadSplitsAndReads at once (CanLoadBam.scala:283-297, 316-356): for split
+ * i = [starts[i], ends[i]) (file offsets) the same (status[i], first_vpos[i], counts[i]) as
+ * sbh_split.  FindBlockStart + FindRecordStart of all splits run in one launch over the
+ * eager bitmap, the record chain is proven once over their union, and every count is one
+ * more launch; a split off that path (a failed or halo-crossing search, an empty block, a
+ * record start outside the bitmap, a start that is a false positive) is decided by
+ * sbh_split.  *n_host (optional) = how many were.  Returns SBH_OK unless the batch itself
+ * failed; per-split errors are in status[]. */
+int sbh_split_starts(sbh_shard *sh, const uint64_t *starts, const uint64_t *ends, uint64_t n,
+                     int32_t bgzf_blocks_to_check, int32_t reads_to_check, int32_t max_read_size,
+                     uint64_t *first_vpos, uint64_t *counts, int32_t *status, uint64_t *n_host);
+
+/* check-bam -s's comparison of the eager checker with the `.records` truth
+ * (cli/.../CheckerApp.scala:65-227, CheckBam.scala) on the device, over the flat ranges
+ * [range_begin[r], range_end[r]) (sorted, disjoint): rec_vpos[] are the truth records as
+ * htsjdk virtual positions (the `.records` lines, any order).  out[0..3] = true positives,
+ * false positives, false negatives, truth records whose block is not in the shard.  fp_flat /
+ * fn_flat (optional) receive up to fp_cap / fn_cap mismatching flat positions, sorted (all of
+ * them when out[1] <= fp_cap, resp. out[2] <= fn_cap). */
+int sbh_check_records(sbh_shard *sh, const uint64_t *range_begin, const uint64_t *range_end,
+                      uint64_t n_ranges, int32_t reads_to_check, const uint64_t *rec_vpos,
+                      uint64_t n_rec, uint64_t *out, uint64_t *fp_flat, uint64_t fp_cap,
+                      uint64_t *fn_flat, uint64_t fn_cap);
+
 /* The whole per-shard hot path as one call (the benchmark step): index from
  * index_start, inflate, eager check at every position of the owned flat range
  * [flat(own_begin_file), flat_bound(own_end_file)), then the owned split:

@@ -24,6 +24,8 @@ static inline int32_t rd_i32(const uint8_t *p) {
 }
 static inline uint32_t rd_u16(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
 
+const char *or_zlib_version(void) { return zlibVersion(); }
+
 uint32_t or_crc32(const uint8_t *b, int64_t n) {
   uLong c = crc32(0L, Z_NULL, 0);
   while (n > 0) {

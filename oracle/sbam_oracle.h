@@ -158,6 +158,9 @@ double or_bench_inflate_check(const uint8_t *file, int64_t fsize, const or_block
 /* CRC32 of a buffer (zlib), for block footers. */
 uint32_t or_crc32(const uint8_t *b, int64_t n);
 
+/* zlib version string of the library the oracle links (stated beside the CPU baseline). */
+const char *or_zlib_version(void);
+
 #ifdef __cplusplus
 }
 #endif

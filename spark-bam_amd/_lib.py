@@ -35,7 +35,8 @@ EXPORTS = [
     "sbh_shard_destroy", "sbh_shard_comp_device_ptr", "sbh_find_block_start", "sbh_index",
     "sbh_get_blocks", "sbh_inflate", "sbh_read_flat", "sbh_flat_device_ptr", "sbh_flat_of",
     "sbh_pos_of", "sbh_flat_bound", "sbh_set_contigs", "sbh_check_eager", "sbh_eager_bits", "sbh_check_full",
-    "sbh_find_record_start", "sbh_count_records", "sbh_split", "sbh_run_shard",
+    "sbh_find_record_start", "sbh_count_records", "sbh_chain_from", "sbh_split", "sbh_split_starts",
+    "sbh_check_records", "sbh_run_shard",
     "sbh_stage_times", "sbh_records_scan", "sbh_records_fetch", "sbh_records_scan_regions", "sbh_verify_crc",
     "sbh_bgzf_compress_bound", "sbh_bgzf_compress",
 ]
@@ -107,6 +108,9 @@ def lib():
         "sbh_find_record_start": [P, U64, I32, I32, PU64, PI32],
         "sbh_count_records": [P, U64, U64, PU64],
         "sbh_split": [P, U64, U64, I32, I32, I32, PU64, PU64],
+        "sbh_chain_from": [P, U64, U64, PU64, PU64],
+        "sbh_split_starts": [P, P, P, U64, I32, I32, I32, P, P, P, PU64],
+        "sbh_check_records": [P, P, P, U64, I32, P, U64, P, P, U64, P, U64],
         "sbh_run_shard": [P, U64, U64, I32, I32, C.POINTER(SbhShardResult)],
         "sbh_records_scan": [P, U64, U64, C.POINTER(SbhRecordsSizes)],
         "sbh_records_fetch": [P, C.POINTER(SbhRecordsOut)],

@@ -141,16 +141,14 @@ def load_splits_and_reads(path_or_bytes, split_size=DEFAULT_SPLIT_SIZE, ctx=None
     L = _Loaded(path_or_bytes, ctx, reads_to_check)
     try:
         sh = L.shard
-        sh.check_eager(0, sh.flat_size, reads_to_check, want_bits=False)  # one pass, reused
-        firsts, counts = [], []
-        for s, e in file_splits(L.data.size, split_size):
-            try:
-                v, n = sh.split(s, e, bgzf_blocks_to_check, reads_to_check, max_read_size)
-            except SparkBamError:
-                raise
-            counts.append(n)
-            if n > 0:
-                firsts.append(Pos.from_htsjdk(v))
+        # every split in one batch (FindBlockStart + FindRecordStart + counts on the device)
+        status, v, n, _ = sh.split_starts(file_splits(L.data.size, split_size), bgzf_blocks_to_check,
+                                          reads_to_check, max_read_size)
+        bad = np.flatnonzero(status)
+        if bad.size:
+            raise SparkBamError(int(status[bad[0]]), f"split {int(bad[0])}")
+        counts = [int(x) for x in n]
+        firsts = [Pos.from_htsjdk(int(x)) for x, c in zip(v, n) if c > 0]
         ends = firsts[1:] + [Pos(L.data.size, 0)]
         return [Split(a, b) for a, b in zip(firsts, ends)], counts
     finally:
@@ -211,29 +209,19 @@ def check_bam(path_or_bytes, records=None, ranges=None, ctx=None,
     try:
         sh = L.shard
         fr, comp = _selected_flat_ranges(sh, ranges)
-        truth = None
-        if records is not None:
-            truth = np.asarray(sorted(sh.flat_of(b, o) for b, o in records), dtype=np.int64)
-        tp = fp = fn = positions = 0
-        fps, fns = [], []
-        for a, b in fr:
-            n, bits = sh.check_eager(a, b, reads_to_check)
-            called = np.flatnonzero(np.unpackbits(bits, bitorder="little")[: b - a]) + a
-            positions += b - a
-            if truth is not None:
-                t = truth[(truth >= a) & (truth < b)]
-                tp += np.intersect1d(called, t).size
-                fpl = np.setdiff1d(called, t)
-                fnl = np.setdiff1d(t, called)
-                fp += fpl.size
-                fn += fnl.size
-                fps += [Pos(*sh.pos_of(int(x))) for x in fpl]
-                fns += [Pos(*sh.pos_of(int(x))) for x in fnl]
-            else:
-                tp += n
+        positions = sum(b - a for a, b in fr)
+        if records is None:
+            tp = sum(sh.check_eager(a, b, reads_to_check, want_bits=False)[0] for a, b in fr)
+            return {"positions": positions, "compressed": comp, "reads": tp, "true_positives": tp,
+                    "false_positives": 0, "false_negatives": 0, "fp_positions": [], "fn_positions": []}
+        vpos = np.asarray([(b << 16) | o for b, o in records], dtype=np.uint64)
+        tp, fp, fn, unknown, fpl, fnl = sh.check_records(fr, vpos, reads_to_check)
+        if unknown:
+            raise SparkBamError(19, f"{unknown} .records positions are not block starts of this file")
         return {"positions": positions, "compressed": comp, "reads": tp + fn,
                 "true_positives": tp, "false_positives": fp, "false_negatives": fn,
-                "fp_positions": fps, "fn_positions": fns}
+                "fp_positions": [Pos(*sh.pos_of(int(x))) for x in fpl],
+                "fn_positions": [Pos(*sh.pos_of(int(x))) for x in fnl]}
     finally:
         L.close()
 

@@ -100,6 +100,7 @@ struct sbh_shard {
   DBuf<uint32_t> b_csize, b_hsize, b_usize, b_flags, b_status, b_ntok;
   DBuf<uint64_t> counts, offs, cand, v, rank, tmp;
   DBuf<uint32_t> cfirst;  // per scan chunk: offset of its first candidate
+  uint64_t ncand = 0, cand_from = 0;  // header candidates in cand[] (shard-relative, >= cand_from)
   DBuf<int64_t> J0, J1;
   DBuf<uint8_t> on;
   std::vector<sbh_block> hb;
@@ -120,6 +121,9 @@ struct sbh_shard {
   DBuf<uint32_t> cm_j, cm_j2, cm_j0;
   uint64_t cm_first = 0, cm_E = 0, cm_n = 0;
   bool cm_valid = false;
+  // the bitmap verified equal to the record chain over [chain_first, chain_E) (k_verify_chain)
+  bool chain_ok = false;
+  uint64_t chain_first = 0, chain_E = 0;
   bool bits_valid = false;
   uint64_t bits_begin = 0, bits_end = 0;
   int32_t bits_rtc = 0;
@@ -155,6 +159,12 @@ struct sbh_shard {
       valid = false;
     }
   } rec;
+  // batched splits (sbh_split_starts) and check-bam truth (sbh_check_records)
+  DBuf<uint64_t> sp_start, sp_end, sp_first, sp_E, sp_vpos;
+  DBuf<uint32_t> sp_code;
+  DBuf<unsigned long long> sp_count;
+  DBuf<uint32_t> tbits;
+  DBuf<uint64_t> t_rb, t_re, t_fp, t_fn;
   hipEvent_t ev[9] = {};
   bool ev_ok = false, timing = false;
   double stage_ms[6] = {0, 0, 0, 0, 0, 0};
@@ -309,6 +319,14 @@ int sbh_shard_destroy(sbh_shard *sh) {
   sh->defer.release();
   sh->xq.release();
   sh->rec.release();
+  for (auto *b : {&sh->sp_start, &sh->sp_end, &sh->sp_first, &sh->sp_E, &sh->sp_vpos, &sh->t_rb, &sh->t_re,
+                  &sh->t_fp, &sh->t_fn})
+    b->release();
+  sh->sp_code.release();
+  sh->sp_count.release();
+  sh->tbits.release();
+  sh->cm_pos.release(); sh->cm_wcnt.release(); sh->cm_wpre.release(); sh->cm_mark.release(); sh->cm_mpre.release();
+  sh->cm_j.release(); sh->cm_j2.release(); sh->cm_j0.release();
   if (sh->h_ctr) (void)hipHostFree(sh->h_ctr);
   delete sh;
   return SBH_OK;
@@ -346,7 +364,8 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
   hipStream_t st = ctx->stream;
   int rc = set_device(ctx);
   if (rc) return rc;
-  sh->indexed = sh->inflated = sh->bits_valid = false;
+  sh->indexed = sh->inflated = sh->bits_valid = sh->chain_ok = sh->cm_valid = false;
+  sh->ncand = 0;
   const uint64_t rel = start - sh->file_off;
   const uint64_t n = sh->n;
   // the start must itself be a header
@@ -394,6 +413,8 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
                             sh->tmp.p, sh->dev_blocks(), sh->usz.p, &nchain, st));
     HIPCHK(ctx, scan_exclusive_u64(sh->usz.p, sh->b_ustart.p, nchain, sh->tmp.p, st));
   }
+  sh->ncand = nc;
+  sh->cand_from = rel;
   // host copy of the block table (Pos mapping, segments)
   sh->hb.assign(nchain, sbh_block{});
   if (nchain) {
@@ -483,7 +504,7 @@ int sbh_inflate(sbh_shard *sh, uint64_t *bad_block) {
     return fail(ctx, SBH_E_INFLATE_DATA, "block %llu: invalid deflate data", (unsigned long long)b.start);
   }
   sh->inflated = true;
-  sh->bits_valid = false;
+  sh->bits_valid = sh->chain_ok = sh->cm_valid = false;
   return SBH_OK;
 }
 
@@ -579,7 +600,7 @@ int sbh_set_contigs(sbh_shard *sh, const int32_t *lens, int32_t n) {
   if (n) HIPCHK(sh->ctx, hipMemcpyAsync(sh->ctg.p, lens, (uint64_t)n * 4, hipMemcpyHostToDevice, sh->ctx->stream));
   HIPCHK(sh->ctx, hipStreamSynchronize(sh->ctx->stream));
   sh->nctg = n;
-  sh->bits_valid = false;
+  sh->bits_valid = sh->chain_ok = sh->cm_valid = false;
   return SBH_OK;
 }
 
@@ -604,6 +625,7 @@ static int eager_range(sbh_shard *sh, uint64_t begin, uint64_t end, int32_t rtc,
   sbh_ctx *ctx = sh->ctx;
   hipStream_t st = ctx->stream;
   const uint64_t nwords = (end - begin + 31) / 32;
+  sh->chain_ok = sh->cm_valid = false;
   HIPCHK(ctx, sh->bits.ensure(nwords + 1));
   HIPCHK(ctx, sh->xq.ensure(2 * XQ_CAP_MAX));
   unsigned long long *c = sh->ctr.p;
@@ -802,6 +824,7 @@ static int count_records_impl(sbh_shard *sh, uint64_t first, uint64_t E, uint64_
   E = std::min(E, total);
   if (anomalies) *anomalies = 0;
   sh->cm_valid = false;
+  sh->chain_ok = false;
   if (first >= E) {
     *count = 0;
     if (exit_flat) *exit_flat = first;
@@ -828,6 +851,9 @@ static int count_records_impl(sbh_shard *sh, uint64_t first, uint64_t E, uint64_
       HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 16, c, 32, hipMemcpyDeviceToHost, st));
       HIPCHK(ctx, hipStreamSynchronize(st));
       if (sh->h_ctr[16] == 0 && sh->h_ctr[19] != ~0ull) {
+        sh->chain_ok = true;
+        sh->chain_first = first;
+        sh->chain_E = E;
         *count = sh->h_ctr[18];
         if (exit_flat) *exit_flat = sh->h_ctr[19];
         return SBH_OK;
@@ -926,6 +952,199 @@ int sbh_split(sbh_shard *sh, uint64_t start, uint64_t end, int32_t k, int32_t rt
   return SBH_OK;
 }
 
+// The record chain from first_flat (PosStream.scala:14-22): records whose start is < end_flat,
+// and the chain's exit (its first record at/after end_flat, or where the stream ends).
+int sbh_chain_from(sbh_shard *sh, uint64_t first_flat, uint64_t end_flat, uint64_t *count, uint64_t *exit_flat) {
+  if (!sh || !count) return SBH_E_ARG;
+  if (!sh->inflated) return fail(sh->ctx, SBH_E_STATE, "chain before inflate");
+  if (first_flat > sh->utotal) return SBH_E_ARG;
+  int rc = set_device(sh->ctx);
+  if (rc) return rc;
+  uint64_t ex = first_flat;
+  rc = count_records_impl(sh, first_flat, std::min(end_flat, sh->utotal), count, nullptr, &ex);
+  if (!rc && exit_flat) *exit_flat = ex;
+  return rc;
+}
+
+// Every split of loadReadsAndPositions / loadSplitsAndReads at once (CanLoadBam.scala:283-297,
+// 316-356; SURVEY 8b sbh_split_starts): one launch runs FindBlockStart + FindRecordStart for
+// all splits (splits.hip), one proves the record chain over their union, one counts every
+// split.  Splits off the common path take the exact per-split path (sbh_split), so each
+// split's (status, first_vpos, count) equals sbh_split's.
+int sbh_split_starts(sbh_shard *sh, const uint64_t *starts, const uint64_t *ends, uint64_t n, int32_t k, int32_t rtc,
+                     int32_t mrs, uint64_t *first_vpos, uint64_t *counts, int32_t *status, uint64_t *n_host) {
+  if (!sh || (n && (!starts || !ends || !first_vpos || !counts || !status)) || k < 0) return SBH_E_ARG;
+  sbh_ctx *ctx = sh->ctx;
+  if (!sh->inflated) return fail(ctx, SBH_E_STATE, "splits before inflate");
+  int rc = need_checkable(sh, 0, 0, rtc);
+  if (rc) return rc;
+  rc = set_device(ctx);
+  if (rc) return rc;
+  if (n_host) *n_host = 0;
+  if (!n) return SBH_OK;
+  hipStream_t st = ctx->stream;
+  const uint64_t end_res = sh->file_off + sh->n;
+  // the eager bitmap from the stream start (reused when one is resident, e.g. sbh_run_shard's
+  // over the owned range; a record start past its end takes the host path)
+  if (!(sh->bits_valid && sh->bits_rtc == rtc && sh->bits_begin == 0)) {
+    rc = eager_range(sh, 0, sh->utotal, rtc, nullptr);
+    if (rc && rc != SBH_E_NEED_HALO) return rc;
+    sh->bits_valid = true;  // positions needing the halo are clear; record starts past them go to the host path
+    sh->bits_begin = 0;
+    sh->bits_end = sh->utotal;
+    sh->bits_rtc = rtc;
+    if (rc == SBH_E_NEED_HALO) sh->bits_end = std::min<uint64_t>(sh->utotal, sh->h_ctr[2]);
+  }
+  std::vector<uint64_t> rs(n), re(n);
+  for (uint64_t i = 0; i < n; ++i) {
+    rs[i] = starts[i] >= sh->file_off ? starts[i] - sh->file_off : ~0ull;
+    re[i] = ends[i] >= sh->file_off ? ends[i] - sh->file_off : 0;
+    if (starts[i] < sh->file_off || starts[i] >= end_res) rs[i] = 0;  // host path (flagged below)
+  }
+  HIPCHK(ctx, sh->sp_start.ensure(n));
+  HIPCHK(ctx, sh->sp_end.ensure(n));
+  HIPCHK(ctx, sh->sp_first.ensure(n));
+  HIPCHK(ctx, sh->sp_E.ensure(n));
+  HIPCHK(ctx, sh->sp_code.ensure(n));
+  HIPCHK(ctx, sh->sp_count.ensure(n));
+  HIPCHK(ctx, hipMemcpyAsync(sh->sp_start.p, rs.data(), 8 * n, hipMemcpyHostToDevice, st));
+  HIPCHK(ctx, hipMemcpyAsync(sh->sp_end.p, re.data(), 8 * n, hipMemcpyHostToDevice, st));
+  const SplitArgs a{sh->comp.p, sh->n, sh->at_eof ? 1 : 0, sh->cand.p, sh->ncand, sh->cand_from, k,
+                    sh->b_cstart.p, sh->b_ustart.p, sh->b_flags.p, sh->nblocks, sh->utotal,
+                    sh->hb.empty() ? 0 : sh->hb.back().start - sh->file_off, sh->d_seg.p,
+                    (uint32_t)sh->seg_end.size(), sh->bits.p, sh->bits_begin, sh->bits_end,
+                    (int64_t)std::max(mrs, 0)};
+  HIPCHK(ctx, launch_split_prologue(a, sh->sp_start.p, sh->sp_end.p, n, sh->sp_first.p, sh->sp_E.p, sh->sp_code.p, st));
+  std::vector<uint64_t> first(n), E(n);
+  std::vector<uint32_t> code(n);
+  HIPCHK(ctx, hipMemcpyAsync(first.data(), sh->sp_first.p, 8 * n, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipMemcpyAsync(E.data(), sh->sp_E.p, 8 * n, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipMemcpyAsync(code.data(), sh->sp_code.p, 4 * n, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  uint64_t fmin = ~0ull, Emax = 0, span = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (starts[i] < sh->file_off || starts[i] >= end_res) code[i] = SPLIT_HOST;
+    if (code[i] != SPLIT_OK || first[i] >= E[i]) continue;
+    fmin = std::min(fmin, first[i]);
+    Emax = std::max(Emax, E[i]);
+    span = std::max(span, E[i] - first[i]);
+  }
+  bool dense = false, marked = false;
+  if (fmin < Emax) {
+    // the chain proof over the union of the splits: the bitmap verified equal to the chain
+    // (then a split's count is a popcount), or the chain marked through the set bits
+    dense = sh->chain_ok && sh->chain_first <= fmin && Emax <= sh->chain_E;
+    marked = sh->cm_valid && sh->cm_first <= fmin && Emax <= sh->cm_E;
+    if (!dense && !marked) {
+      uint64_t cnt = 0;
+      rc = count_records_impl(sh, fmin, Emax, &cnt, nullptr);
+      if (rc) return rc;
+      dense = sh->chain_ok && sh->chain_first <= fmin && Emax <= sh->chain_E;
+      marked = sh->cm_valid && sh->cm_first <= fmin && Emax <= sh->cm_E;
+    }
+  }
+  HIPCHK(ctx, hipMemsetAsync(sh->sp_count.p, 0, 8 * n, st));
+  if (dense) {
+    HIPCHK(ctx, hipMemcpyAsync(sh->sp_code.p, code.data(), 4 * n, hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, launch_split_popcount(sh->bits.p, sh->bits_begin, sh->sp_first.p, sh->sp_E.p, sh->sp_code.p, n, span,
+                                      sh->sp_count.p, st));
+  } else if (marked) {
+    HIPCHK(ctx, hipMemcpyAsync(sh->sp_code.p, code.data(), 4 * n, hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, launch_split_cm_count(sh->cm_pos.p, sh->cm_mark.p, sh->cm_mpre.p, sh->cm_n, sh->sp_first.p,
+                                      sh->sp_E.p, sh->sp_code.p, n, sh->sp_count.p, st));
+    HIPCHK(ctx, hipMemcpyAsync(code.data(), sh->sp_code.p, 4 * n, hipMemcpyDeviceToHost, st));
+  } else {
+    for (uint64_t i = 0; i < n; ++i)
+      if (code[i] == SPLIT_OK && first[i] < E[i]) code[i] = SPLIT_HOST;
+  }
+  std::vector<unsigned long long> cnt(n);
+  HIPCHK(ctx, hipMemcpyAsync(cnt.data(), sh->sp_count.p, 8 * n, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  uint64_t nh = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (code[i] == SPLIT_OK) {
+      uint64_t bp = 0;
+      uint32_t off = 0;
+      rc = sbh_pos_of(sh, first[i], &bp, &off);
+      if (rc) return rc;
+      first_vpos[i] = (bp << 16) | off;
+      counts[i] = first[i] < E[i] ? cnt[i] : 0;
+      status[i] = SBH_OK;
+      continue;
+    }
+    ++nh;
+    first_vpos[i] = counts[i] = 0;
+    status[i] = sbh_split(sh, starts[i], ends[i], k, rtc, mrs, &first_vpos[i], &counts[i]);
+  }
+  if (n_host) *n_host = nh;
+  return SBH_OK;
+}
+
+// check-bam's comparison with the `.records` truth (CheckerApp.scala:65-227) on the device:
+// the eager bitmap over the hull of the selected flat ranges, the truth (htsjdk vpos of every
+// record) scattered into a second bitmap, and one word-parallel compare.  fp_flat / fn_flat
+// (optional) receive the first fp_cap / fn_cap mismatching flat positions in order.
+int sbh_check_records(sbh_shard *sh, const uint64_t *range_begin, const uint64_t *range_end, uint64_t n_ranges,
+                      int32_t rtc, const uint64_t *rec_vpos, uint64_t n_rec, uint64_t *out /*tp, fp, fn, unknown*/,
+                      uint64_t *fp_flat, uint64_t fp_cap, uint64_t *fn_flat, uint64_t fn_cap) {
+  if (!sh || !out || (n_ranges && (!range_begin || !range_end)) || (n_rec && !rec_vpos)) return SBH_E_ARG;
+  sbh_ctx *ctx = sh->ctx;
+  for (uint64_t r = 0; r < n_ranges; ++r)
+    if (range_begin[r] > range_end[r] || (r && range_begin[r] < range_end[r - 1]))
+      return fail(ctx, SBH_E_ARG, "ranges must be sorted and disjoint");
+  out[0] = out[1] = out[2] = out[3] = 0;
+  if (!n_ranges) return SBH_OK;
+  const uint64_t begin = range_begin[0], end = range_end[n_ranges - 1];
+  int rc = need_checkable(sh, begin, end, rtc);
+  if (rc) return rc;
+  rc = set_device(ctx);
+  if (rc) return rc;
+  hipStream_t st = ctx->stream;
+  // the eager bitmap over the hull, aligned so its words line up with the truth words
+  const uint64_t hb0 = begin & ~31ull;
+  if (!(sh->bits_valid && sh->bits_rtc == rtc && sh->bits_begin <= hb0 && end <= sh->bits_end &&
+        sh->bits_begin % 32 == 0)) {
+    rc = eager_range(sh, hb0, end, rtc, nullptr);
+    if (rc) return rc;
+  }
+  const uint64_t nw = (end - hb0 + 31) / 32;
+  HIPCHK(ctx, sh->tbits.ensure(nw + 1));
+  HIPCHK(ctx, hipMemsetAsync(sh->tbits.p, 0, 4 * (nw + 1), st));
+  HIPCHK(ctx, sh->sp_vpos.ensure(n_rec + 1));
+  if (n_rec) HIPCHK(ctx, hipMemcpyAsync(sh->sp_vpos.p, rec_vpos, 8 * n_rec, hipMemcpyHostToDevice, st));
+  HIPCHK(ctx, sh->t_rb.ensure(n_ranges));
+  HIPCHK(ctx, sh->t_re.ensure(n_ranges));
+  HIPCHK(ctx, hipMemcpyAsync(sh->t_rb.p, range_begin, 8 * n_ranges, hipMemcpyHostToDevice, st));
+  HIPCHK(ctx, hipMemcpyAsync(sh->t_re.p, range_end, 8 * n_ranges, hipMemcpyHostToDevice, st));
+  const uint64_t cap_fp = fp_flat ? fp_cap : 0, cap_fn = fn_flat ? fn_cap : 0;
+  HIPCHK(ctx, sh->t_fp.ensure(cap_fp + 1));
+  HIPCHK(ctx, sh->t_fn.ensure(cap_fn + 1));
+  unsigned long long *acc = sh->ctr.p + 40;  // tp, fp, fn, fp slots, fn slots, unknown
+  HIPCHK(ctx, hipMemsetAsync(acc, 0, 6 * 8, st));
+  HIPCHK(ctx, launch_truth_scatter(sh->sp_vpos.p, n_rec, sh->b_cstart.p, sh->b_ustart.p, sh->nblocks, sh->file_off,
+                                   hb0, end, sh->tbits.p, acc + 5, st));
+  HIPCHK(ctx, launch_truth_compare(sh->bits.p, sh->bits_begin, sh->tbits.p, hb0, end, sh->t_rb.p, sh->t_re.p,
+                                   n_ranges, acc, sh->t_fp.p, cap_fp, sh->t_fn.p, cap_fn, st));
+  HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 40, acc, 6 * 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  out[0] = sh->h_ctr[40];
+  out[1] = sh->h_ctr[41];
+  out[2] = sh->h_ctr[42];
+  out[3] = sh->h_ctr[45];
+  // the mismatch lists arrive in atomic order and are sorted here; when there are more
+  // mismatches than the cap, the listed ones are a (sorted) subset
+  auto fetch = [&](uint64_t *dst, const uint64_t *src, uint64_t cap, uint64_t total) -> int {
+    const uint64_t k = std::min(cap, total);
+    if (!dst || !k) return SBH_OK;
+    HIPCHK(ctx, hipMemcpy(dst, src, 8 * k, hipMemcpyDeviceToHost));
+    std::sort(dst, dst + k);
+    return SBH_OK;
+  };
+  rc = fetch(fp_flat, sh->t_fp.p, cap_fp, out[1]);
+  if (!rc) rc = fetch(fn_flat, sh->t_fn.p, cap_fn, out[2]);
+  return rc;
+}
+
 // Inflate + eager check of flat [0, E) as one pipeline over batches of blocks, on three
 // streams: k_huff of batch i+1 runs beside k_lz of batch i and beside the eager tiles
 // whose staged windows batch i completed (k_huff is latency-bound on LDS and VALU, k_lz on
@@ -977,7 +1196,7 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
   unsigned long long *c = sh->ctr.p;
   HIPCHK(ctx, hipMemsetAsync(c, 0, 48, sa));
   HIPCHK(ctx, hipMemsetAsync(c + 2, 0xff, 8, sa));
-  sh->inflated = sh->bits_valid = false;
+  sh->inflated = sh->bits_valid = sh->chain_ok = sh->cm_valid = false;
   const uint64_t nb = sh->nblocks;
   const uint64_t nbat = std::max<uint64_t>(1, std::min<uint64_t>(PIPE_MAX_BATCHES, nb / pipe_min_blocks()));
   // events: per batch [huff start, huff end, lz start, lz end, eager start, eager end]

@@ -102,4 +102,39 @@ hipError_t launch_deflate(const uint8_t *src, uint64_t n, uint8_t *slots, uint8_
 hipError_t launch_deflate_gather(const uint8_t *slots, const uint32_t *sizes, const uint64_t *offs, uint64_t nblocks,
                                  uint8_t *out, hipStream_t st);
 
+// Batched splits and check-bam truth comparison (splits.hip).
+constexpr uint32_t SPLIT_OK = 0;    // first record and flat end decided on the device
+constexpr uint32_t SPLIT_HOST = 1;  // off the common path: the exact per-split host path decides
+struct SplitArgs {
+  const uint8_t *comp;
+  uint64_t n;
+  int at_eof;
+  const uint64_t *cand;
+  uint64_t ncand, cand_from;
+  int32_t k_check;
+  const uint64_t *cstart, *ustart;
+  const uint32_t *flags;
+  uint64_t nblocks, utotal, last_start;
+  const uint64_t *seg_end;
+  uint32_t nseg;
+  const uint32_t *bits;
+  uint64_t bits_begin, bits_end;
+  int64_t mrs;
+};
+hipError_t launch_split_prologue(const SplitArgs &a, const uint64_t *starts, const uint64_t *ends, uint64_t nsplit,
+                                 uint64_t *first, uint64_t *E, uint32_t *code, hipStream_t st);
+hipError_t launch_split_popcount(const uint32_t *bits, uint64_t begin, const uint64_t *first, const uint64_t *E,
+                                 const uint32_t *code, uint64_t nsplit, uint64_t max_span,
+                                 unsigned long long *counts, hipStream_t st);
+hipError_t launch_split_cm_count(const uint64_t *pos, const uint64_t *mark, const uint64_t *mpre, uint64_t n,
+                                 const uint64_t *first, const uint64_t *E, uint32_t *code, uint64_t nsplit,
+                                 unsigned long long *counts, hipStream_t st);
+hipError_t launch_truth_scatter(const uint64_t *vpos, uint64_t n, const uint64_t *cstart, const uint64_t *ustart,
+                                uint64_t nblocks, uint64_t file_off, uint64_t begin, uint64_t end, uint32_t *tbits,
+                                unsigned long long *bad, hipStream_t st);
+hipError_t launch_truth_compare(const uint32_t *ebits, uint64_t ebegin, const uint32_t *tbits, uint64_t begin,
+                                uint64_t end, const uint64_t *rb, const uint64_t *re, uint64_t nr,
+                                unsigned long long *acc, uint64_t *fp_pos, uint64_t fp_cap, uint64_t *fn_pos,
+                                uint64_t fn_cap, hipStream_t st);
+
 }  // namespace sbh

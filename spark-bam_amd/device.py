@@ -219,6 +219,42 @@ class Shard:
         self._c(lib().sbh_count_records(self.h, first_flat, end_flat, C.byref(out)))
         return out.value
 
+    def chain_from(self, first_flat, end_flat):
+        """(records of the chain from first_flat starting before end_flat, the chain's exit
+        flat position) -- sbh_chain_from."""
+        n, x = C.c_uint64(), C.c_uint64()
+        self._c(lib().sbh_chain_from(self.h, first_flat, end_flat, C.byref(n), C.byref(x)))
+        return n.value, x.value
+
+    def split_starts(self, splits, bgzf_blocks_to_check=5, reads_to_check=10, max_read_size=100000000):
+        """Every split [(start, end), ...] at once (sbh_split_starts): numpy arrays
+        (status, first_vpos, count) per split, and how many took the per-split path."""
+        st = np.ascontiguousarray([a for a, _ in splits], dtype=np.uint64)
+        en = np.ascontiguousarray([b for _, b in splits], dtype=np.uint64)
+        n = st.size
+        v = np.zeros(max(n, 1), np.uint64)
+        c = np.zeros(max(n, 1), np.uint64)
+        status = np.zeros(max(n, 1), np.int32)
+        nh = C.c_uint64()
+        self._c(lib().sbh_split_starts(self.h, _ptr(st), _ptr(en), n, bgzf_blocks_to_check, reads_to_check,
+                                       max_read_size, _ptr(v), _ptr(c), _ptr(status), C.byref(nh)))
+        return status[:n], v[:n], c[:n], nh.value
+
+    def check_records(self, ranges, rec_vpos, reads_to_check=10, cap=1 << 20):
+        """check-bam's TP/FP/FN against the `.records` truth on the device (sbh_check_records):
+        ranges = sorted disjoint [(begin_flat, end_flat)], rec_vpos = htsjdk vpos of the truth
+        records.  Returns (tp, fp, fn, unknown, fp_flat, fn_flat)."""
+        rb = np.ascontiguousarray([a for a, _ in ranges], dtype=np.uint64)
+        re_ = np.ascontiguousarray([b for _, b in ranges], dtype=np.uint64)
+        rv = np.ascontiguousarray(rec_vpos, dtype=np.uint64)
+        out = np.zeros(4, np.uint64)
+        fp = np.zeros(max(cap, 1), np.uint64)
+        fn = np.zeros(max(cap, 1), np.uint64)
+        self._c(lib().sbh_check_records(self.h, _ptr(rb), _ptr(re_), rb.size, reads_to_check, _ptr(rv), rv.size,
+                                        _ptr(out), _ptr(fp), cap, _ptr(fn), cap))
+        tp, nfp, nfn, unk = (int(x) for x in out)
+        return tp, nfp, nfn, unk, fp[:min(nfp, cap)], fn[:min(nfn, cap)]
+
     def split(self, start, end, bgzf_blocks_to_check=5, reads_to_check=10,
               max_read_size=100000000):
         v, n = C.c_uint64(), C.c_uint64()

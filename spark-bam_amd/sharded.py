@@ -91,44 +91,79 @@ def read_header(ctx, read, file_size, first=DEFAULT_HALO):
         n = min(file_size, n * 4)
 
 
-def run_rank(ctx, read, file_size, split_index, splits, contig_len, rank=0, halo=DEFAULT_HALO,
-             bgzf_blocks_to_check=DEFAULT_BGZF_BLOCKS_TO_CHECK,
-             reads_to_check=DEFAULT_READS_TO_CHECK, max_read_size=DEFAULT_MAX_READ_SIZE):
-    """One rank's share of the hot path over its splits [lo, hi): the shard is loaded with
-    a halo that grows until no result depends on bytes past it (SBH_E_NEED_HALO)."""
-    if not splits:
-        return RankPart(rank, split_index, [], [], None, 0, None)
-    lo, hi = splits[0][0], splits[-1][1]
-    while True:
-        end = min(file_size, hi + halo)
-        sh = ctx.shard(read(lo, end), file_offset=lo, file_size=file_size)
-        try:
-            sh.set_contigs(contig_len)
-            start = sh.find_block_start(lo, bgzf_blocks_to_check)
-            r = sh.run(start, hi, reads_to_check, max_read_size)
-            firsts, counts = [], []
-            for s, e in splits:
-                try:
-                    v, n = sh.split(s, e, bgzf_blocks_to_check, reads_to_check, max_read_size)
-                except SparkBamError as err:
-                    if err.code != SBH_E_NO_READ_FOUND:  # an empty split
-                        raise
-                    v, n = 0, 0
-                firsts.append(v if n else None)
-                counts.append(n)
-            exit_vpos = sh.exit_vpos(r)
-            return RankPart(rank, split_index, firsts, counts,
-                            r["first_vpos"] if r["count"] else None, r["count"], exit_vpos)
-        except SparkBamError as err:
-            if err.code != SBH_E_NEED_HALO or end >= file_size:
+class RankRun:
+    """One rank's share of the hot path over its splits [lo, hi): the shard +
+    halo stays resident after the run, so the stitch can re-walk its chain later."""
+
+    def __init__(self, ctx, read, file_size, split_index, splits, contig_len, rank=0, halo=DEFAULT_HALO,
+                 bgzf_blocks_to_check=DEFAULT_BGZF_BLOCKS_TO_CHECK,
+                 reads_to_check=DEFAULT_READS_TO_CHECK, max_read_size=DEFAULT_MAX_READ_SIZE):
+        self.sh = None
+        self.rank = rank
+        if not splits:
+            self.part = RankPart(rank, split_index, [], [], None, 0, None)
+            return
+        lo, hi = splits[0][0], splits[-1][1]
+        while True:
+            end = min(file_size, hi + halo)
+            sh = ctx.shard(read(lo, end), file_offset=lo, file_size=file_size)
+            try:
+                sh.set_contigs(contig_len)
+                start = sh.find_block_start(lo, bgzf_blocks_to_check)
+                r = sh.run(start, hi, reads_to_check, max_read_size)
+                # every split of the rank in one batch (FindBlockStart + FindRecordStart +
+                # counts on the device; CanLoadBam.scala:283-297, 316-356)
+                status, v, n, _ = sh.split_starts(splits, bgzf_blocks_to_check, reads_to_check, max_read_size)
+                for k in np.flatnonzero((status != 0) & (status != SBH_E_NO_READ_FOUND)):
+                    raise SparkBamError(int(status[k]), f"split {splits[k][0]}-{splits[k][1]}")
+                counts = [int(c) if st == 0 else 0 for st, c in zip(status, n)]
+                firsts = [int(x) if c else None for x, c in zip(v, counts)]
+                self.part = RankPart(rank, split_index, firsts, counts,
+                                     r["first_vpos"] if r["count"] else None, r["count"], sh.exit_vpos(r))
+                self.sh, self.hi = sh, hi
+                return
+            except SparkBamError as err:
+                sh.close()
+                if err.code != SBH_E_NEED_HALO or end >= file_size:
+                    raise
+                halo *= 4
+            except BaseException:
+                sh.close()
                 raise
-            halo *= 4
-        finally:
-            sh.close()
+
+    def rewalk(self, from_vpos):
+        """The chain from the upstream rank's exit (SURVEY 8e stitch fix-up): (records from
+        from_vpos that start before the owned end, the chain's exit vpos or None)."""
+        sh = self.sh
+        f = sh.flat_of(from_vpos >> 16, from_vpos & 0xFFFF)
+        n, x = sh.chain_from(f, sh.flat_bound(self.hi))
+        ex = None
+        if n and x < sh.flat_size:
+            bp, off = sh.pos_of(x)
+            ex = (bp << 16) | off
+        return n, ex
+
+    def close(self):
+        if self.sh is not None:
+            self.sh.close()
+            self.sh = None
 
 
-def stitch(parts, file_size):
-    """Every rank's RankPart (any order) -> (splits, counts, stitch report)."""
+def run_rank(ctx, read, file_size, split_index, splits, contig_len, rank=0, halo=DEFAULT_HALO, **kw):
+    """One rank's RankPart (RankRun without keeping the shard)."""
+    run = RankRun(ctx, read, file_size, split_index, splits, contig_len, rank, halo, **kw)
+    run.close()
+    return run.part
+
+
+def stitch(parts, file_size, rewalks=None):
+    """Every rank's RankPart (any order) -> (splits, counts, stitch report).
+
+    The splits and counts are the reference's per-split answer.  The report checks the
+    record chain across ranks: `exit_r == first_{r+1}` for non-empty neighbours (`ok`,
+    `mismatches`).  `rewalks` ({rank: (from_vpos, count, exit_vpos)}) replaces a rank's
+    chain by its re-walk from the upstream exit; `chain_ok` / `chain_mismatches` /
+    `chain_count` describe the chain after those re-walks (SURVEY 8e fix-up)."""
     parts = sorted(parts, key=lambda p: p.split_index)
     firsts, counts = [], []
     for p in parts:
@@ -137,14 +172,37 @@ def stitch(parts, file_size):
     starts = [Pos.from_htsjdk(v) for v, n in zip(firsts, counts) if n > 0 and v is not None]
     ends = starts[1:] + [Pos(file_size, 0)]
     splits = [Split(a, b) for a, b in zip(starts, ends)]
-    nonempty = [p for p in parts if p.count > 0]
-    mismatches = []
-    for a, b in zip(nonempty, nonempty[1:]):
-        if a.exit_vpos != b.first_vpos:
-            mismatches.append({"rank": a.rank, "exit": a.exit_vpos, "next_rank": b.rank,
-                               "next_first": b.first_vpos})
+
+    def mism(chain):
+        nonempty = [c for c in chain if c[2] > 0]
+        return [{"rank": a[0], "exit": a[3], "next_rank": b[0], "next_first": b[1]}
+                for a, b in zip(nonempty, nonempty[1:]) if a[3] != b[1]]
+
+    orig = [(p.rank, p.first_vpos, p.count, p.exit_vpos) for p in parts]
+    rewalks = rewalks or {}
+    eff = [(r, *rewalks[r]) if r in rewalks else (r, f, n, x) for r, f, n, x in orig]
+    mismatches, chain_mismatches = mism(orig), mism(eff)
     return splits, counts, {"ok": not mismatches, "mismatches": mismatches,
-                            "rank_counts": [p.count for p in parts]}
+                            "rank_counts": [p.count for p in parts],
+                            "rewalk": {r: {"from": f, "count": n, "exit": x} for r, (f, n, x) in rewalks.items()},
+                            "chain_ok": not chain_mismatches, "chain_mismatches": chain_mismatches,
+                            "chain_count": sum(c[2] for c in eff)}
+
+
+def _allgather(obj, group=None):
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()):
+        return [obj]
+    out = [None] * dist.get_world_size(group)
+    dist.all_gather_object(out, obj, group=group)
+    return out
+
+
+def _wire(x):
+    """An exception as what the other ranks receive."""
+    return ("error", x.code if isinstance(x, SparkBamError) else -1, repr(x) if not isinstance(x, SparkBamError)
+            else str(x))
 
 
 def exchange(part, group=None):
@@ -157,10 +215,7 @@ def exchange(part, group=None):
         if isinstance(part, BaseException):
             raise part
         return [part]
-    mine = ("error", part.code if isinstance(part, SparkBamError) else -1, str(part)) \
-        if isinstance(part, BaseException) else tuple(part)
-    out = [None] * dist.get_world_size(group)
-    dist.all_gather_object(out, mine, group=group)
+    out = _allgather(_wire(part) if isinstance(part, BaseException) else tuple(part), group)
     for i, p in enumerate(out):
         if p[0] == "error":
             if isinstance(part, BaseException):
@@ -169,31 +224,72 @@ def exchange(part, group=None):
     return [RankPart(*p) for p in out]
 
 
+def reconcile(parts, file_size, rank, rewalk, group=None, max_rounds=None):
+    """The stitch with the SURVEY 8e fix-up: while the chain leaving a rank does not enter
+    its next non-empty rank at that rank's first record (a false-positive record start on
+    one side), the next rank re-walks its chain from the upstream exit (`rewalk(vpos) ->
+    (count, exit_vpos)`, run on the rank that holds those bytes), and every rank learns the
+    re-walk through one more allgather.  A re-walk can move a rank's exit, so this repeats
+    until the chain holds (at most world rounds).  The per-split answer is unchanged."""
+    world = len(parts)
+    rewalks = {}
+    for _ in range(max_rounds or world):
+        splits, counts, st = stitch(parts, file_size, rewalks)
+        if st["chain_ok"]:
+            break
+        mine = None
+        todo = [m for m in st["chain_mismatches"] if m["next_rank"] == rank]
+        if todo:
+            try:
+                n, ex = rewalk(todo[0]["exit"])
+                mine = (rank, todo[0]["exit"], n, ex)
+            except Exception as err:  # every rank must reach the allgather
+                mine = err
+        got = _allgather(_wire(mine) if isinstance(mine, BaseException) else mine, group)
+        for i, g in enumerate(got):
+            if g and g[0] == "error":
+                if isinstance(mine, BaseException):
+                    raise mine
+                raise SparkBamError(g[1], f"rank {i}: {g[2]}")
+        new = {g[0]: (g[1], g[2], g[3]) for g in got if g}
+        if not new:
+            break
+        rewalks.update(new)
+    return stitch(parts, file_size, rewalks)
+
+
 def load_splits_and_reads(path_or_bytes, split_size=None, ctx=None, rank=None, world=None,
                           group=None, halo=DEFAULT_HALO, **kw):
     """CanLoadBam.loadSplitsAndReads (load/.../CanLoadBam.scala:268-302) over the ranks of
     the default (or given) process group, each on its own device.  `split_size` defaults to
     ceil(fileSize / world): one byte-range shard per rank.  Returns (splits, counts, stitch),
-    identical on every rank."""
+    identical on every rank.  Any failure on a rank (not only a SparkBamError) is exchanged,
+    so every rank raises it instead of waiting in a collective."""
     import torch.distributed as dist
 
     on = dist.is_available() and dist.is_initialized()
     rank = rank if rank is not None else (dist.get_rank(group) if on else 0)
     world = world if world is not None else (dist.get_world_size(group) if on else 1)
-    read = file_reader(path_or_bytes) if isinstance(path_or_bytes, (str, os.PathLike)) \
-        else bytes_reader(path_or_bytes)
-    file_size = read.size
-    if split_size is None:
-        split_size = max(1, -(-file_size // world))
     own_ctx = ctx is None
-    ctx = ctx or Context(int(os.environ.get("LOCAL_RANK", "0")))
+    run = None
     try:
-        _, contig_len, _ = read_header(ctx, read, file_size)
-        a, mine = rank_splits(file_size, split_size, world, rank)
-        part = run_rank(ctx, read, file_size, a, mine, contig_len, rank, halo, **kw)
-    except SparkBamError as err:
-        part = err
+        try:
+            read = file_reader(path_or_bytes) if isinstance(path_or_bytes, (str, os.PathLike)) \
+                else bytes_reader(path_or_bytes)
+            file_size = read.size
+            if split_size is None:
+                split_size = max(1, -(-file_size // world))
+            ctx = ctx or Context(int(os.environ.get("LOCAL_RANK", "0")))
+            _, contig_len, _ = read_header(ctx, read, file_size)
+            a, mine = rank_splits(file_size, split_size, world, rank)
+            run = RankRun(ctx, read, file_size, a, mine, contig_len, rank, halo, **kw)
+            part = run.part
+        except Exception as err:  # exchanged: the peers must not block in the allgather
+            part = err
+        parts = exchange(part, group)
+        return reconcile(parts, file_size, rank, run.rewalk, group)
     finally:
-        if own_ctx:
+        if run is not None:
+            run.close()
+        if own_ctx and ctx is not None:
             ctx.close()
-    return stitch(exchange(part, group), file_size)

@@ -77,6 +77,7 @@ def lib():
         "or_bench_inflate_check": (C.c_double, [P, I64, P, I64, I64, P, I32, I32, I32,
                                                 C.POINTER(I64), C.POINTER(I64)]),
         "or_crc32": (U32, [P, I64]),
+        "or_zlib_version": (C.c_char_p, []),
         "or_stream_next": (C.c_int, [P, I64, I64, P, P]),
     }
     for name, (res, args) in sig.items():
