@@ -276,7 +276,12 @@ def htsjdk_rewrite(path_or_bytes, out_path=None, read_ranges=None, ctx=None):
     EOF member.  Records pass through byte-for-byte (htsjdk's decode/re-encode is the
     identity on the records of a BAM it wrote).  Returns the file bytes (numpy uint8); writes
     them to out_path when given.  The `-b`/`-i` index side-outputs are the CLI's
-    `index-blocks` / `index-records` run on the result."""
+    `index-blocks` / `index-records` run on the result.
+
+    Size trade-off: members are cut exactly where htsjdk cuts them (65498 uncompressed
+    bytes), but each is coded by this library's GPU coder (greedy LZ77 + fixed Huffman codes,
+    see deflate_core.h), not zlib level 5, so the compressed bytes -- and therefore the
+    block positions in `.blocks` / `.records` -- differ from htsjdk's output."""
     L = _Loaded(path_or_bytes, ctx)
     try:
         sh = L.shard
@@ -286,8 +291,11 @@ def htsjdk_rewrite(path_or_bytes, out_path=None, read_ranges=None, ctx=None):
             flat = sh.read_flat()
             starts = sh.records(L.header_end, sh.flat_size)["flat"].astype(np.int64)
             ends = np.append(starts[1:], np.int64(sh.flat_size))
-            parts = [flat[:L.header_end]]
-            parts += [flat[s:e] for i, (s, e) in enumerate(zip(starts, ends)) if i in read_ranges]
+            idx = np.arange(starts.size)
+            sel = np.asarray(read_ranges, dtype=np.int64) if isinstance(read_ranges, range) else \
+                np.fromiter((int(i) for i in read_ranges), dtype=np.int64)  # any collection (IntRanges)
+            keep = idx[np.isin(idx, sel)]
+            parts = [flat[:L.header_end]] + [flat[starts[i]:ends[i]] for i in keep]
             out, _, _ = L.ctx.bgzf_compress(np.concatenate(parts))
     finally:
         L.close()

@@ -137,11 +137,7 @@ class RankRun:
         sh = self.sh
         f = sh.flat_of(from_vpos >> 16, from_vpos & 0xFFFF)
         n, x = sh.chain_from(f, sh.flat_bound(self.hi))
-        ex = None
-        if n and x < sh.flat_size:
-            bp, off = sh.pos_of(x)
-            ex = (bp << 16) | off
-        return n, ex
+        return n, sh.exit_vpos({"count": n, "exit_flat": x})
 
     def close(self):
         if self.sh is not None:
@@ -238,7 +234,8 @@ def reconcile(parts, file_size, rank, rewalk, group=None, max_rounds=None):
         if st["chain_ok"]:
             break
         mine = None
-        todo = [m for m in st["chain_mismatches"] if m["next_rank"] == rank]
+        # (an upstream chain that ran into its stream end has no exit to re-walk from)
+        todo = [m for m in st["chain_mismatches"] if m["next_rank"] == rank and m["exit"] is not None]
         if todo:
             try:
                 n, ex = rewalk(todo[0]["exit"])

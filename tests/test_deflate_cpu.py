@@ -41,7 +41,10 @@ def parse_members(f):
         assert f[o:o + 4] == b"\x1f\x8b\x08\x04" and f[o + 12:o + 16] == b"BC\x02\x00"
         bsize = struct.unpack_from("<H", f, o + 16)[0] + 1
         crc, isize = struct.unpack_from("<II", f, o + bsize - 8)
-        data = zlib.decompressobj(-15).decompress(f[o + 18:o + bsize - 8])
+        d = zlib.decompressobj(-15)
+        data = d.decompress(f[o + 18:o + bsize - 8])
+        # the member's deflate stream ends exactly at the footer (final block seen, no slack)
+        assert d.eof and not d.unused_data and not d.unconsumed_tail
         assert len(data) == isize and zlib.crc32(data) == crc
         out.append((o, bsize, isize, data))
         o += bsize

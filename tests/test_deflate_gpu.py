@@ -83,3 +83,43 @@ def test_rewrite_read_ranges(ctx):
     got = b"".join(x[3] for x in parse_members(out))
     assert got == want
     assert len(sb.load_reads(out, ctx=ctx)) == len(keep)
+
+
+def _vpos_list(records_rows):
+    return [(b << 16) | o for b, o in records_rows]
+
+
+def test_htsjdk_rewrite_test_slice(ctx):
+    """HTSJDKRewriteTest (cli/src/test/scala/org/hammerlab/bam/rewrite/HTSJDKRewriteTest.scala:14-24):
+    `htsjdk-rewrite -r 100-1000 2.bam` -> slice/2.100-1000.bam{,.blocks,.records}.  The
+    compressed bytes differ (htsjdk's level-5 Deflater vs this coder), so the test pins
+    everything else: the uncompressed stream (header + records [100, 1000)), the member usize
+    column of `.blocks`, and `.records` mapped through (member index, offset)."""
+    out = sb.htsjdk_rewrite(golden_bam("2.bam"), read_ranges=range(100, 1000), ctx=ctx).tobytes()
+    ref = np.fromfile(golden_bam("2.100-1000.bam"), dtype=np.uint8).tobytes()
+    m, mr = parse_members(out), parse_members(ref)
+    flat, flat_ref = b"".join(x[3] for x in m), b"".join(x[3] for x in mr)
+    assert len(flat_ref) == 578330 and flat == flat_ref
+    ref_blocks = read_blocks("2.100-1000.bam")
+    assert [x[2] for x in m[:-1]] == [u for _, _, u in ref_blocks]  # 8 x 65498, 54346
+    assert [x[0] for x in mr[:-1]] == [s for s, _, _ in ref_blocks]
+    # .records of the fixture, re-expressed on this file's members
+    member_of_ref = {s: i for i, (s, _, _) in enumerate(ref_blocks)}
+    want = [(m[member_of_ref[b]][0] << 16) | o for b, o in read_records("2.100-1000.bam")]
+    sh = ctx.shard(np.frombuffer(out, dtype=np.uint8))
+    try:
+        sh.index(0)
+        sh.inflate()
+        of = OracleFile(np.frombuffer(out, dtype=np.uint8))
+        sh.set_contigs(of.contig_len)
+        fs = sh.flat_size
+        first = sh.find_record_start(of.header_end)[0]
+        assert first == of.header_end
+        starts = sh.records(first, fs)["flat"]
+        got = []
+        for f in starts.tolist():
+            bp, off = sh.pos_of(int(f))
+            got.append((bp << 16) | off)
+        assert len(got) == 900 and got == want
+    finally:
+        sh.close()
