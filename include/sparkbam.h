@@ -93,6 +93,12 @@ int sbh_ctx_set_stream(sbh_ctx *ctx, void *hip_stream);
 int sbh_ctx_synchronize(sbh_ctx *ctx);
 const char *sbh_version(void);
 
+/* Page-locked host memory (hipHostMalloc): compressed bytes handed over in it are copied to
+ * HBM asynchronously, overlapping the kernels (sbh_run_stream).  A JNI binding wraps it in a
+ * direct ByteBuffer. */
+int sbh_host_alloc(uint64_t n, void **out);
+int sbh_host_free(void *p);
+
 /* Header.make (bgzf/.../block/Header.scala:48-83): host-side parse of 18 bytes. */
 int sbh_header_make(const uint8_t *bytes, uint64_t avail, int32_t *hsize, int32_t *csize);
 
@@ -242,6 +248,37 @@ int sbh_run_shard(sbh_shard *sh, uint64_t index_start, uint64_t own_end_file,
  * over the pipeline's launches, each timed on its own stream.  Returns the number of
  * stages written (<= cap, at most 6). */
 int sbh_stage_times(sbh_shard *sh, double *ms, int32_t cap);
+
+/* ---- a shard streamed through bounded HBM ----
+ * sbh_run_shard over host-resident compressed bytes [file_offset, file_offset + n) (pinned
+ * memory lets the copies overlap the kernels), in windows of about `window` compressed bytes:
+ * window w owns the blocks starting in [lo_w, hi_w), loads [lo_w, hi_w + halo), and its
+ * successor's bytes are copied host -> HBM on a second stream while it runs, so HBM holds two
+ * windows' compressed bytes and one window's working set however large the shard
+ * (Stream.scala:80-122 / SplitRDD.scala:33-52 bound the reference per split).  index_start is
+ * the owned range's first block (UINT64_MAX: FindBlockStart(file_offset, 5)).  Windows stitch
+ * like ranks (a mismatch re-walks the later window from the earlier exit); a window
+ * that needs bytes past its halo grows the halo x4 and runs again.  out_bits (optional, host,
+ * zeroed by the caller, out_bits_cap bytes): the eager bit of every owned flat position. */
+typedef struct {
+  uint64_t n_windows, n_blocks;
+  uint64_t comp_bytes;  /* compressed bytes of the owned blocks                      */
+  uint64_t flat_bytes;  /* their uncompressed bytes (checked positions)              */
+  uint64_t n_true;      /* eager-true owned positions                                */
+  uint64_t count;       /* records of the owned range (the stitched chain)           */
+  uint64_t first_vpos;  /* first record (UINT64_MAX if none)                         */
+  uint64_t exit_vpos;   /* first chain record at/after the owned end (UINT64_MAX: none) */
+  int32_t status, rewalks, host_pinned, pad;
+  double ms_wall;       /* wall time of the call (host clock), copies included       */
+  double ms_h2d;        /* summed host -> HBM copy time (HIP events on the copy stream) */
+  double stage_ms[6];   /* sbh_stage_times summed over the windows                   */
+  uint64_t halo_final;
+} sbh_stream_result;
+int sbh_run_stream(sbh_ctx *ctx, const void *host_comp, uint64_t n, uint64_t file_offset,
+                   uint64_t file_size, uint64_t index_start, uint64_t own_end_file, uint64_t window,
+                   uint64_t halo, const int32_t *contig_len, int32_t n_contigs, int32_t reads_to_check,
+                   int32_t max_read_size, uint8_t *out_bits, uint64_t out_bits_cap,
+                   sbh_stream_result *res);
 
 /* ---- record field extraction ----
  * RecordStream from first_flat while the record start is < end_flat, decoded like

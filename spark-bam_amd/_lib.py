@@ -31,13 +31,13 @@ BLOCK_EMPTY, BLOCK_TRUNCATED = 1, 2
 # Every symbol include/sparkbam.h declares (checked by tests/test_abi.py).
 EXPORTS = [
     "sbh_ctx_create", "sbh_ctx_destroy", "sbh_last_error", "sbh_ctx_set_stream",
-    "sbh_ctx_synchronize", "sbh_version", "sbh_header_make", "sbh_shard_create",
+    "sbh_ctx_synchronize", "sbh_version", "sbh_host_alloc", "sbh_host_free", "sbh_header_make", "sbh_shard_create",
     "sbh_shard_destroy", "sbh_shard_comp_device_ptr", "sbh_find_block_start", "sbh_index",
     "sbh_get_blocks", "sbh_inflate", "sbh_read_flat", "sbh_flat_device_ptr", "sbh_flat_of",
     "sbh_pos_of", "sbh_flat_bound", "sbh_set_contigs", "sbh_check_eager", "sbh_eager_bits", "sbh_check_full",
     "sbh_find_record_start", "sbh_count_records", "sbh_chain_from", "sbh_split", "sbh_split_starts",
     "sbh_check_records", "sbh_run_shard",
-    "sbh_stage_times", "sbh_records_scan", "sbh_records_fetch", "sbh_records_scan_regions", "sbh_verify_crc",
+    "sbh_stage_times", "sbh_run_stream", "sbh_records_scan", "sbh_records_fetch", "sbh_records_scan_regions", "sbh_verify_crc",
     "sbh_bgzf_compress_bound", "sbh_bgzf_compress",
 ]
 
@@ -51,6 +51,15 @@ class SbhShardResult(C.Structure):
     _fields_ = [("n_blocks", C.c_uint64), ("comp_bytes", C.c_uint64), ("flat_bytes", C.c_uint64),
                 ("n_true", C.c_uint64), ("first_vpos", C.c_uint64), ("count", C.c_uint64),
                 ("exit_flat", C.c_uint64), ("status", C.c_int32), ("anomalies", C.c_int32)]
+
+
+class SbhStreamResult(C.Structure):
+    _fields_ = [("n_windows", C.c_uint64), ("n_blocks", C.c_uint64), ("comp_bytes", C.c_uint64),
+                ("flat_bytes", C.c_uint64), ("n_true", C.c_uint64), ("count", C.c_uint64),
+                ("first_vpos", C.c_uint64), ("exit_vpos", C.c_uint64), ("status", C.c_int32),
+                ("rewalks", C.c_int32), ("host_pinned", C.c_int32), ("pad", C.c_int32),
+                ("ms_wall", C.c_double), ("ms_h2d", C.c_double), ("stage_ms", C.c_double * 6),
+                ("halo_final", C.c_uint64)]
 
 
 class SbhRecordsSizes(C.Structure):
@@ -90,6 +99,8 @@ def lib():
         "sbh_ctx_destroy": [P],
         "sbh_ctx_set_stream": [P, P],
         "sbh_ctx_synchronize": [P],
+        "sbh_host_alloc": [U64, C.POINTER(P)],
+        "sbh_host_free": [P],
         "sbh_header_make": [P, U64, PI32, PI32],
         "sbh_shard_create": [P, P, U64, U64, U64, C.c_int, C.POINTER(P)],
         "sbh_shard_destroy": [P],
@@ -112,6 +123,8 @@ def lib():
         "sbh_split_starts": [P, P, P, U64, I32, I32, I32, P, P, P, PU64],
         "sbh_check_records": [P, P, P, U64, I32, P, U64, P, P, U64, P, U64],
         "sbh_run_shard": [P, U64, U64, I32, I32, C.POINTER(SbhShardResult)],
+        "sbh_run_stream": [P, P, U64, U64, U64, U64, U64, U64, U64, P, I32, I32, I32, P, U64,
+                           C.POINTER(SbhStreamResult)],
         "sbh_records_scan": [P, U64, U64, C.POINTER(SbhRecordsSizes)],
         "sbh_records_fetch": [P, C.POINTER(SbhRecordsOut)],
         "sbh_records_scan_regions": [P, P, P, U64, P, P, P, C.c_uint32, C.POINTER(SbhRecordsSizes)],

@@ -2,6 +2,7 @@
 // buffers, and the orchestration of the HIP kernels (bgzf_index.hip, inflate.hip,
 // check.hip) that replace spark-bam's per-split Scala/JDK-zlib work.
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -243,6 +244,14 @@ int sbh_ctx_destroy(sbh_ctx *ctx) {
 }
 
 const char *sbh_last_error(const sbh_ctx *ctx) { return ctx ? ctx->err.c_str() : "no context"; }
+
+int sbh_host_alloc(uint64_t n, void **out) {
+  if (!out) return SBH_E_ARG;
+  *out = nullptr;
+  return hipHostMalloc(out, std::max<uint64_t>(n, 1), hipHostMallocDefault) == hipSuccess ? SBH_OK : SBH_E_NOMEM;
+}
+
+int sbh_host_free(void *p) { return p && hipHostFree(p) != hipSuccess ? SBH_E_HIP : SBH_OK; }
 
 int sbh_ctx_set_stream(sbh_ctx *ctx, void *hip_stream) {
   if (!ctx) return SBH_E_ARG;
@@ -1359,6 +1368,205 @@ int sbh_stage_times(sbh_shard *sh, double *ms, int32_t cap) {
   int n = cap < 6 ? cap : 6;
   for (int i = 0; i < n; ++i) ms[i] = sh->stage_ms[i];
   return n;
+}
+
+// A shard larger than the HBM budget, streamed through it (Stream.scala:80-122 and
+// SplitRDD.scala:33-52 bound the reference's memory the same way: per split, a bounded
+// block cache).  The owned range [index_start, own_end_file) is cut into windows of about
+// `window` compressed bytes; window w owns the blocks starting in [lo_w, hi_w) and loads
+// [lo_w, hi_w + halo).  While window w runs the whole per-shard path (sbh_run_shard), the
+// bytes of window w+1 move host -> HBM on a copy stream into the other of two buffers, so
+// HBM holds two windows of compressed bytes and one window's flat bytes, tokens and bitmap,
+// whatever the shard size.  Window w+1 indexes from the first block at/after hi_w (known
+// from window w's block table).  Consecutive non-empty windows stitch like ranks (SURVEY
+// 8e): the chain leaving window w must enter window w+1 at its first record, else window
+// w+1 is re-walked from that exit.  A result that needs bytes past a window's halo grows
+// the halo x4 and redoes the window.
+int sbh_run_stream(sbh_ctx *ctx, const void *host, uint64_t n, uint64_t file_offset, uint64_t file_size,
+                   uint64_t index_start, uint64_t own_end_file, uint64_t window, uint64_t halo, const int32_t *contigs,
+                   int32_t n_contigs, int32_t rtc, int32_t mrs, uint8_t *out_bits, uint64_t out_bits_cap,
+                   sbh_stream_result *res) {
+  if (!ctx || !res || (!host && n) || !window || file_offset + n > file_size || own_end_file > file_offset + n ||
+      own_end_file <= file_offset || n_contigs < 0 || (n_contigs && !contigs))
+    return SBH_E_ARG;
+  std::memset(res, 0, sizeof *res);
+  res->first_vpos = res->exit_vpos = ~0ull;
+  const auto t_start = std::chrono::steady_clock::now();
+  int rc = set_device(ctx);
+  if (rc) return res->status = rc;
+  const uint8_t *src = static_cast<const uint8_t *>(host);
+  hipPointerAttribute_t pa{};
+  res->host_pinned = hipPointerGetAttributes(&pa, host) == hipSuccess && pa.type == hipMemoryTypeHost ? 1 : 0;
+  (void)hipGetLastError();
+  struct Run {  // everything the call owns, released on every return path
+    sbh_shard *sh = nullptr;
+    DBuf<uint8_t> buf[2];
+    hipStream_t cs = nullptr;
+    hipEvent_t done[2] = {nullptr, nullptr}, c0[2] = {nullptr, nullptr};
+    ~Run() {
+      if (cs) (void)hipStreamSynchronize(cs);
+      if (sh) {
+        sh->comp.p = nullptr;  // the window buffers are not the shard's
+        sh->comp.cap = 0;
+        sbh_shard_destroy(sh);
+      }
+      buf[0].release();
+      buf[1].release();
+      for (int i = 0; i < 2; ++i) {
+        if (done[i]) (void)hipEventDestroy(done[i]);
+        if (c0[i]) (void)hipEventDestroy(c0[i]);
+      }
+      if (cs) (void)hipStreamDestroy(cs);
+    }
+  } R;
+  rc = sbh_shard_create(ctx, nullptr, 0, file_offset, file_size, 0, &R.sh);
+  if (rc) return res->status = rc;
+  sbh_shard *sh = R.sh;
+  sh->comp.release();
+  rc = sbh_set_contigs(sh, contigs, n_contigs);
+  if (rc) return res->status = rc;
+  HIPCHK(ctx, hipStreamCreateWithFlags(&R.cs, hipStreamNonBlocking));
+  for (int i = 0; i < 2; ++i) {
+    HIPCHK(ctx, hipEventCreate(&R.done[i]));
+    HIPCHK(ctx, hipEventCreate(&R.c0[i]));
+  }
+  const uint64_t data_end = file_offset + n, pad = sh->pad;
+  auto win_end = [&](uint64_t lo) {
+    uint64_t hi = std::min(lo + window, own_end_file);
+    if (own_end_file - hi < window / 4) hi = own_end_file;  // no sliver of a last window
+    return hi;
+  };
+  auto load_end = [&](uint64_t hi) { return std::min(hi + halo, data_end); };
+  auto size_bufs = [&]() -> hipError_t {
+    const uint64_t cap = window + window / 4 + halo + pad;
+    for (auto &b : R.buf) {
+      hipError_t e = b.ensure(cap);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  };
+  double h2d_ms = 0;
+  bool timed[2] = {false, false};
+  auto account = [&](int b) {  // copy time of the last copy into buffer b
+    if (!timed[b]) return;
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, R.c0[b], R.done[b]) == hipSuccess) h2d_ms += ms;
+    timed[b] = false;
+  };
+  auto enqueue = [&](int b, uint64_t lo, uint64_t ld) -> hipError_t {
+    hipError_t e = hipEventRecord(R.c0[b], R.cs);
+    if (e == hipSuccess) e = hipMemcpyAsync(R.buf[b].p, src + (lo - file_offset), ld - lo, hipMemcpyHostToDevice, R.cs);
+    if (e == hipSuccess) e = hipMemsetAsync(R.buf[b].p + (ld - lo), 0, pad, R.cs);
+    if (e == hipSuccess) e = hipEventRecord(R.done[b], R.cs);
+    timed[b] = e == hipSuccess;
+    return e;
+  };
+  HIPCHK(ctx, size_bufs());
+  uint64_t lo = file_offset, hi = win_end(lo), start = index_start;
+  int cur = 0;
+  HIPCHK(ctx, enqueue(cur, lo, load_end(hi)));
+  bool prefetch = true, have_prev = false;
+  uint64_t prev_exit = ~0ull, flat_base = 0;
+  std::vector<uint32_t> wbits;
+  for (;;) {
+    const bool more = hi < own_end_file;
+    const uint64_t lo2 = hi, hi2 = more ? win_end(lo2) : 0;
+    if (prefetch && more) HIPCHK(ctx, enqueue(1 - cur, lo2, load_end(hi2)));
+    const uint64_t ld = load_end(hi);
+    HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, R.done[cur], 0));
+    sh->comp.p = R.buf[cur].p;
+    sh->comp.cap = R.buf[cur].cap;
+    sh->file_off = lo;
+    sh->n = ld - lo;
+    sh->at_eof = ld == file_size;
+    if (start == ~0ull) {
+      rc = sbh_find_block_start(sh, lo, 5, &start);  // BGZFBlocksToCheck (bgzf/.../block/package.scala:20)
+      if (rc) return res->status = rc;
+    }
+    sbh_shard_result r{};
+    rc = sbh_run_shard(sh, start, hi, rtc, mrs, &r);
+    if (rc == SBH_E_NEED_HALO && ld < data_end) {  // grow the halo and redo this window
+      HIPCHK(ctx, hipStreamSynchronize(R.cs));
+      HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+      account(0);
+      account(1);
+      halo *= 4;
+      for (auto &b : R.buf) b.release();
+      sh->comp.p = nullptr;
+      sh->comp.cap = 0;
+      HIPCHK(ctx, size_bufs());
+      HIPCHK(ctx, enqueue(cur, lo, load_end(hi)));
+      prefetch = true;
+      continue;
+    }
+    if (rc) return res->status = rc;
+    account(cur);
+    // this window's chain exit, and the stitch with the previous non-empty window
+    uint64_t count = r.count, exit_vpos = ~0ull;
+    auto vpos_of = [&](uint64_t flat, uint64_t *v) {
+      uint64_t bp = 0;
+      uint32_t off = 0;
+      if (sbh_pos_of(sh, flat, &bp, &off) != SBH_OK) return false;
+      *v = (bp << 16) | off;
+      return true;
+    };
+    if (count) {
+      uint64_t first_v = r.first_vpos;
+      if (have_prev && prev_exit != ~0ull && first_v != prev_exit) {
+        uint64_t f = 0, x = 0, E = 0;
+        rc = sbh_flat_of(sh, prev_exit >> 16, (uint32_t)(prev_exit & 0xffff), &f);
+        if (!rc) rc = sbh_flat_bound(sh, hi, &E);
+        if (!rc) rc = sbh_chain_from(sh, f, E, &count, &x);
+        if (rc) return res->status = rc;
+        r.exit_flat = x;
+        first_v = prev_exit;
+        ++res->rewalks;
+      }
+      if (!vpos_of(r.exit_flat, &exit_vpos)) exit_vpos = ~0ull;
+      if (res->first_vpos == ~0ull) res->first_vpos = first_v;
+      if (count) {
+        prev_exit = exit_vpos;
+        have_prev = true;
+      }
+    }
+    if (out_bits && r.flat_bytes) {  // this window's owned bits at global flat offset flat_base
+      const uint64_t nb = (flat_base + r.flat_bytes + 7) / 8;
+      if (nb > out_bits_cap) return res->status = fail(ctx, SBH_E_ARG, "out_bits_cap too small");
+      wbits.assign((r.flat_bytes + 31) / 32 + 1, 0);
+      HIPCHK(ctx, hipMemcpy(wbits.data(), sh->bits.p, (r.flat_bytes + 7) / 8, hipMemcpyDeviceToHost));
+      for (uint64_t i = 0; i < r.flat_bytes; ++i)
+        if ((wbits[i >> 5] >> (i & 31)) & 1u) out_bits[(flat_base + i) >> 3] |= (uint8_t)(1u << ((flat_base + i) & 7));
+    }
+    ++res->n_windows;
+    res->n_blocks += r.n_blocks;
+    res->comp_bytes += r.comp_bytes;
+    res->flat_bytes += r.flat_bytes;
+    res->n_true += r.n_true;
+    res->count += count;
+    if (count) res->exit_vpos = exit_vpos;
+    for (int i = 0; i < 6; ++i) res->stage_ms[i] += sh->stage_ms[i];
+    flat_base += r.flat_bytes;
+    if (!more) break;
+    // the next window indexes from its first block: the first block at/after hi
+    auto it = std::lower_bound(sh->hb.begin(), sh->hb.end(), hi,
+                               [](const sbh_block &b, uint64_t v) { return b.start < v; });
+    if (it == sh->hb.end()) return res->status = fail(ctx, SBH_E_NEED_HALO, "halo %llu holds no block past %llu",
+                                                     (unsigned long long)halo, (unsigned long long)hi);
+    start = it->start;
+    sh->comp.p = nullptr;
+    sh->comp.cap = 0;
+    lo = lo2;
+    hi = hi2;
+    cur = 1 - cur;
+    prefetch = true;
+  }
+  HIPCHK(ctx, hipStreamSynchronize(R.cs));
+  account(0);
+  account(1);
+  res->ms_h2d = h2d_ms;
+  res->halo_final = halo;
+  res->ms_wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+  return res->status = SBH_OK;
 }
 
 // RecordStream + BAMRecordCodec.decode over [first, end) (check/.../iterator/RecordStream.scala:16-41,

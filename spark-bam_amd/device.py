@@ -4,8 +4,8 @@ import weakref
 
 import numpy as np
 
-from ._lib import (SBH_OK, SbhBlock, SbhRecordsOut, SbhRecordsSizes, SbhShardResult, SparkBamError,
-                   lib)
+from ._lib import (SBH_OK, SbhBlock, SbhRecordsOut, SbhRecordsSizes, SbhShardResult, SbhStreamResult,
+                   SparkBamError, lib)
 
 
 def _check(ctx_handle, rc):
@@ -16,6 +16,31 @@ def _check(ctx_handle, rc):
 
 def _ptr(a):
     return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+class PinnedBuffer:
+    """Page-locked host bytes (sbh_host_alloc) as a numpy uint8 array (`.array`): compressed
+    bytes in it stream to HBM with copies that overlap the kernels."""
+
+    def __init__(self, n):
+        p = C.c_void_p()
+        rc = lib().sbh_host_alloc(int(n), C.byref(p))
+        if rc != SBH_OK:
+            raise SparkBamError(rc, f"cannot pin {n} host bytes")
+        self.p = p
+        self.array = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(int(n),))
+
+    def close(self):
+        if self.p:
+            self.array = None
+            lib().sbh_host_free(self.p)
+            self.p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Context:
@@ -68,6 +93,34 @@ class Context:
         _check(self.h, lib().sbh_bgzf_compress(self.h, src, n, 1 if on_dev else 0, _ptr(out), cap,
                                                C.byref(size), C.byref(nb), C.byref(ms)))
         return out[:size.value], nb.value, ms.value
+
+    def run_stream(self, comp, contig_len, file_offset=0, file_size=None, own_end=None, index_start=None,
+                   window=1 << 30, halo=4 << 20, reads_to_check=10, max_read_size=100000000, want_bits=False):
+        """sbh_run_stream: the per-shard hot path over host-resident compressed bytes `comp`
+        (numpy uint8, ideally pinned) = file bytes [file_offset, file_offset + comp.size),
+        streamed through HBM in windows.  Returns (result dict, eager bits or None)."""
+        arr = np.ascontiguousarray(comp, dtype=np.uint8) if isinstance(comp, np.ndarray) else comp
+        n = int(arr.size)
+        file_size = file_offset + n if file_size is None else int(file_size)
+        own_end = file_offset + n if own_end is None else int(own_end)
+        cl = np.ascontiguousarray(np.asarray(contig_len, dtype=np.int32))
+        bits = None
+        if want_bits:
+            bits = np.zeros(max(1, 4 * n + 64), dtype=np.uint8)  # > (flat + 7) / 8 at any ratio <= 32
+        r = SbhStreamResult()
+        _check(self.h, lib().sbh_run_stream(self.h, _ptr(arr), n, int(file_offset), file_size,
+                                            0xFFFFFFFFFFFFFFFF if index_start is None else int(index_start),
+                                            own_end, int(window), int(halo), _ptr(cl), int(cl.size),
+                                            reads_to_check, max_read_size, _ptr(bits),
+                                            0 if bits is None else bits.size, C.byref(r)))
+        out = {f: getattr(r, f) for f, _ in SbhStreamResult._fields_ if f != "stage_ms"}
+        out["stage_ms"] = list(r.stage_ms)
+        for k in ("first_vpos", "exit_vpos"):
+            if out[k] == 0xFFFFFFFFFFFFFFFF:
+                out[k] = None
+        if bits is not None:
+            bits = bits[:(out["flat_bytes"] + 7) // 8]
+        return out, bits
 
     def shard(self, comp, file_offset=0, file_size=None, on_device=False, nbytes=None):
         return Shard(self, comp, file_offset, file_size, on_device, nbytes)

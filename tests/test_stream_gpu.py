@@ -1,0 +1,106 @@
+"""A shard streamed through bounded HBM (sbh_run_stream) must give exactly what the resident
+run (sbh_run_shard over the whole shard) gives: the eager bit of every owned position, the
+eager-true count, the first record and the stitched record count -- with windows small enough
+that records, halos and false-positive bait cross many window edges."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from oracle_lib import OracleFile
+from pkg import sb
+
+pytestmark = pytest.mark.gpu
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tools"))
+
+CORPORA = {
+    "short_l6": (dict(seed=0x5B4D0001, shape=0, level=6), 30000),
+    "wgs_c": (dict(seed=0x5B4D0030, shape=0, level=6), 20000),
+    "long": (dict(seed=0x5B4D004C, shape=1, level=6), 200),
+    "adversarial": (dict(seed=0x5B4D00AD, shape=2, level=-1), 30000),
+}
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = sb.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def files():
+    import synth
+    out = {}
+    for name, (kw, nrec) in CORPORA.items():
+        p = synth.params(kw["seed"], shape=kw["shape"], level=kw["level"])
+        out[name] = (synth.make_bam(p, nrec)[0], nrec)
+    return out
+
+
+def resident(ctx, data, contig_len):
+    sh = ctx.shard(data)
+    try:
+        sh.set_contigs(contig_len)
+        r = sh.run(0, data.size)
+        bits = sh.eager_bits(0, r["flat_bytes"])
+        ex = sh.exit_vpos(r)
+    finally:
+        sh.close()
+    return r, bits, ex
+
+
+@pytest.mark.parametrize("name", list(CORPORA))
+@pytest.mark.parametrize("window,halo", [(150_000, 1 << 16), (400_000, 1 << 20)])
+def test_stream_equals_resident(ctx, files, name, window, halo):
+    data, nrec = files[name]
+    of = OracleFile(data)
+    r, bits, _ = resident(ctx, data, of.contig_len)
+    s, sbits = ctx.run_stream(data, of.contig_len, index_start=0, window=window, halo=halo, want_bits=True)
+    assert s["status"] == 0 and s["n_windows"] >= 3
+    assert s["flat_bytes"] == r["flat_bytes"] and s["comp_bytes"] == r["comp_bytes"]
+    nb = (r["flat_bytes"] + 7) // 8
+    d = np.flatnonzero(sbits[:nb] != bits[:nb])
+    assert d.size == 0, f"eager bits differ at byte {d[0]}"
+    assert s["n_true"] == r["n_true"]
+    assert s["count"] == r["count"] == nrec
+    assert s["first_vpos"] == r["first_vpos"]
+
+
+def test_stream_pinned_host_and_halo_growth(ctx, files):
+    """Pinned host memory (the overlapped-copy path) and a halo too small for long records
+    (grown x4 until every window's records fit)."""
+    data, nrec = files["long"]
+    of = OracleFile(data)
+    buf = sb.PinnedBuffer(data.size)
+    buf.array[:] = data
+    s, _ = ctx.run_stream(buf.array, of.contig_len, window=300_000, halo=4096)
+    buf.close()
+    assert s["host_pinned"] == 1 and s["halo_final"] > 4096
+    assert s["count"] == nrec and s["ms_h2d"] > 0
+
+
+def test_stream_subrange_of_a_file(ctx, files):
+    """Host bytes = a byte range of a file (file_offset > 0, not at EOF): the owned blocks'
+    bits equal the whole-file resident bits at the same flat positions."""
+    data, _ = files["wgs_c"]
+    of = OracleFile(data)
+    sh = ctx.shard(data)
+    sh.index(0)
+    blocks = sh.blocks()
+    k0, k1 = 10, 45  # of 74 data blocks
+    lo, own_end, hi = blocks[k0][0], blocks[k1][0], blocks[k1 + 20][0]
+    base, E = blocks[k0][3], blocks[k1][3]
+    sh.inflate()
+    sh.set_contigs(of.contig_len)
+    _, want = sh.check_eager(base, E)
+    n_ref = sh.count_records(sh.find_record_start(base)[0], E)
+    sh.close()
+    s, got = ctx.run_stream(data[lo:hi], of.contig_len, file_offset=lo, file_size=data.size, own_end=own_end,
+                            window=200_000, halo=1 << 16, want_bits=True)
+    assert s["flat_bytes"] == E - base
+    assert np.array_equal(np.unpackbits(got, bitorder="little")[:E - base],
+                          np.unpackbits(want, bitorder="little")[:E - base])
+    assert s["count"] == n_ref
