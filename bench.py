@@ -36,9 +36,9 @@ CONFIGS = {  # BASELINE.json configs; SURVEY 8d
     "B": dict(seed=0x5B4D0001, shape=0, level=6, records=12_400_000, fp_free=True,
               workload="configs[1]: synthetic ~1 GiB-compressed BAM per GPU, 100 bp short reads, BGZF level 6 "
                        "(htsjdk 65498 B payloads)"),
-    "C": dict(seed=0x5B4D0030, shape=0, level=6, records=155_000_000, fp_free=True,
+    "C": dict(seed=0x5B4D0030, shape=0, level=6, records=155_000_000, fp_free=True, stream=True,
               workload="configs[2] per-GPU shard: 12.5 GiB compressed (the 100 GB WGS file / 8 GPUs), 100 bp "
-                       "short reads, level 6"),
+                       "short reads, level 6, streamed from pinned host memory through HBM in 1 GiB windows"),
     "D": dict(seed=0x5B4D004C, shape=1, level=6, records=71_000, fp_free=True,
               workload="configs[3]: ~1 GiB-compressed long-read BAM per GPU (10-50 kb records spanning BGZF "
                        "blocks and shard edges), level 6"),
@@ -63,6 +63,12 @@ def main():
                     help="CPU baseline threads (default: every host core this process may use)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-full", action="store_true", help="skip the full-checker side measurement")
+    ap.add_argument("--stream", action="store_true",
+                    help="stream the shard from pinned host memory through HBM (sbh_run_stream; default for C)")
+    ap.add_argument("--window", type=int, default=1 << 30, help="stream window, compressed bytes")
+    ap.add_argument("--e2e-window", type=int, default=256 << 20,
+                    help="window of the H2D-inclusive side measurement of the resident configs")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the H2D-inclusive side measurement")
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes per launch of the dominant kernel (default: the committed "
                          "rocprofv3 --pmc summary, profiles/*_pmc_traffic.json)")
@@ -104,12 +110,20 @@ def main():
         args.records_per_gpu = cfg["records"]
     p = synth.params(cfg["seed"], shape=cfg["shape"], level=cfg["level"],
                      threads=min(16, os.cpu_count() or 1))
+    streaming = args.stream or cfg.get("stream", False)
+    pins = []
+
+    def pinned(n):  # page-locked host memory for the streamed shard (overlapped H2D copies)
+        pins.append(sb.PinnedBuffer(n))
+        return pins[-1].array
+
     if cfg["level"] < 0:  # mixed levels: no uniform payload grid, so one whole file (N=1)
         if world != 1:
             raise SystemExit(f"config {args.config} runs at N=1 only")
         seg = synth.WholeFile(p, args.records_per_gpu)
     else:
-        seg = synth.Segment(p, args.records_per_gpu, world, rank, halo_blocks=16, log=log)
+        seg = synth.Segment(p, args.records_per_gpu, world, rank, halo_blocks=64 if streaming else 16, log=log,
+                            alloc=pinned if streaming else None)
     own = torch.tensor([seg.own_csize], dtype=torch.int64, device=xdev)
     if world > 1:
         gathered = [torch.zeros_like(own) for _ in range(world)]
@@ -123,19 +137,34 @@ def main():
         f"in {time.time() - t0:.1f}s")
 
     ctx = sb.Context(device)
-    shard = ctx.shard(seg.comp, file_offset=seg.file_offset, file_size=seg.file_size)
     header = synth.header_bytes()
     names, contig_len, _ = sb.parse_bam_header(header)
-    shard.set_contigs(contig_len)
+    shard = None
+    if not streaming:
+        shard = ctx.shard(seg.comp, file_offset=seg.file_offset, file_size=seg.file_size)
+        shard.set_contigs(contig_len)
 
     result_t = torch.zeros(5, dtype=torch.int64, device=xdev)
+    stream_last = {}
+
+    def run_once():
+        if streaming:  # windows through HBM; copies of window w+1 overlap window w's kernels
+            r, _ = ctx.run_stream(seg.comp, contig_len, file_offset=seg.file_offset, file_size=seg.file_size,
+                                  own_end=seg.own_end, index_start=seg.file_offset, window=args.window,
+                                  halo=4 << 20)
+            stream_last.update(r)
+            first = r["first_vpos"] or 0
+            ex = r["exit_vpos"]
+            return dict(r, first_vpos=first), r["stage_ms"], ex
+        r = shard.run(seg.file_offset, seg.own_end)
+        return r, shard.stage_times(), shard.exit_vpos(r)  # exit: None when the chain hit the stream end
 
     def step():
-        r = shard.run(seg.file_offset, seg.own_end)
+        r, stages, ex = run_once()
         if r["status"] != 0:
-            raise RuntimeError(f"run_shard status {r['status']}")
-        ex = shard.exit_vpos(r)  # the chain's exit from the owned range (None: the stream end)
+            raise RuntimeError(f"run status {r['status']}")
         ex = -1 if ex is None else ex
+        r["stages"] = stages
         mine = [r["first_vpos"], r["count"], r["n_true"], r["flat_bytes"], ex]
         if world > 1:  # RCCL allgather of the per-shard split records (stitching)
             result_t.copy_(torch.tensor(mine, dtype=torch.int64))
@@ -154,7 +183,7 @@ def main():
     t_start = time.perf_counter()
     for _ in range(args.steps):
         r, allr = step()
-        stage_acc += np.asarray(shard.stage_times())
+        stage_acc += np.asarray(r["stages"])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -177,7 +206,7 @@ def main():
     # bait (config E), whose exact bits are pinned by the parity tests, not here
     # every inflated block of the last step against its BGZF footer CRC32 (full-size
     # bit-exactness of the inflate), outside the timed region
-    crc_bad, _ = shard.verify_crc()
+    crc_bad = shard.verify_crc()[0] if shard is not None else 0  # (stream mode: windows are gone)
     ok = total_records == expect and (total_true == expect or not cfg["fp_free"]) and stitch["ok"] and crc_bad == 0
     firsts = [x[0] for x in allr if x[1] > 0]
 
@@ -215,7 +244,7 @@ def main():
     # position with the FullCheck Counts aggregation (no per-position words), on the
     # inflated shard the last step left; wall time of the synchronous call, best of 2.
     full = None
-    if not args.no_full:
+    if not args.no_full and shard is not None:
         f0 = max(0, shard.flat_bound(seg.file_offset)) if seg.file_offset else 0
         f1 = shard.flat_bound(seg.own_end)
         best = None
@@ -232,9 +261,43 @@ def main():
                 "note": "sbh_check_full over the owned flat range (Counts + rbe histograms + close calls), "
                         "inflated shard already resident; not part of `value`"}
 
+    # End-to-end rate with the compressed shard starting in (pinned) host memory: the same
+    # per-shard path streamed through HBM in windows, H2D copies overlapped with the kernels
+    # (sbh_run_stream).  Reported beside `value` (which has the inputs resident in HBM).
+    e2e = None
+    if streaming:
+        e2e = {"GBps_decompressed": round(total_flat * args.steps / elapsed / 1e9, 2),
+               "windows": stream_last.get("n_windows"), "window_bytes": args.window,
+               "h2d_ms_per_step": round(stream_last.get("ms_h2d", 0), 3),
+               "h2d_GBps": round(stream_last["comp_bytes"] / (stream_last["ms_h2d"] * 1e-3) / 1e9, 2)
+               if stream_last.get("ms_h2d") else None,
+               "device_ms_per_step": round(float(stage_acc[1] + stage_acc[0] + stage_acc[3]) / args.steps, 3),
+               "host_pinned": bool(stream_last.get("host_pinned")),
+               "note": "value IS the streamed rate here: shard in pinned host memory, windows through HBM"}
+    elif not args.no_e2e and seg.file_offset is not None:
+        buf = sb.PinnedBuffer(seg.comp.size)
+        buf.array[:] = seg.comp
+        best, sr = None, None
+        for _ in range(2):
+            t0e = time.perf_counter()
+            sr, _ = ctx.run_stream(buf.array, contig_len, file_offset=seg.file_offset, file_size=seg.file_size,
+                                   own_end=seg.own_end, index_start=seg.file_offset, window=args.e2e_window,
+                                   halo=4 << 20)
+            dt = time.perf_counter() - t0e
+            best = dt if best is None else min(best, dt)
+        buf.close()
+        e2e = {"GBps_decompressed": round(sr["flat_bytes"] / best / 1e9, 2),
+               "compressed_GBps": round(sr["comp_bytes"] / best / 1e9, 2),
+               "ms": round(best * 1e3, 3), "windows": sr["n_windows"], "window_bytes": args.e2e_window,
+               "h2d_ms": round(sr["ms_h2d"], 3),
+               "h2d_GBps": round(sr["comp_bytes"] / (sr["ms_h2d"] * 1e-3) / 1e9, 2) if sr["ms_h2d"] else None,
+               "records_match": sr["count"] == r["count"] and sr["n_true"] == r["n_true"],
+               "note": "rank-local shard from pinned host memory, streamed through HBM in windows (sbh_run_stream); "
+                       "not `value`"}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(shard, seg.comp, contig_len, args.cpu_seconds, args.cpu_threads)
+        cpu = cpu_baseline(seg.comp, seg.file_offset or 0, contig_len, args.cpu_seconds, args.cpu_threads)
 
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
@@ -298,11 +361,15 @@ def main():
                 "per_kernel_GBps": {k: gbps(v[0], v[1]) for k, v in kern.items()},
             },
             "full_check": full,
+            "e2e_h2d": e2e,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    shard.close()
+    if shard is not None:
+        shard.close()
     ctx.close()
+    for b in pins:
+        b.close()
     if world > 1:
         dist.destroy_process_group()
     if not ok:
@@ -324,7 +391,23 @@ def host_cores():
     return n, why
 
 
-def cpu_baseline(shard, comp, contig_len, budget_s, threads):
+def host_block_table(comp, limit=None):
+    """(start, csize, hsize, usize) of the consecutive BGZF blocks of `comp` (host-side header
+    walk for the CPU baseline's sample; empty blocks skipped)."""
+    out, pos, n = [], 0, comp.size
+    while pos + 18 <= n and (limit is None or len(out) < limit):
+        xlen = int(comp[pos + 10]) | int(comp[pos + 11]) << 8
+        cs = (int(comp[pos + 16]) | int(comp[pos + 17]) << 8) + 1
+        if pos + cs > n:
+            break
+        us = int.from_bytes(comp[pos + cs - 4:pos + cs].tobytes(), "little")
+        if us:
+            out.append((pos, cs, 18 + xlen - 6, us))
+        pos += cs
+    return out
+
+
+def cpu_baseline(comp, base, contig_len, budget_s, threads):
     """The oracle (C restatement of the reference path: zlib inflate + eager check at
     every offset) on the host cores, over a bounded sample of the same shard's
     blocks.  Reported beside the GPU number; it is a baseline, not the target."""
@@ -337,15 +420,11 @@ def cpu_baseline(shard, comp, contig_len, budget_s, threads):
     limit = None
     if threads is None:
         threads, limit = host_cores()
-    shard.index(shard.file_offset)  # host copy of the block table
-    blocks = shard.blocks()
-    base = shard.file_offset
+    blocks = host_block_table(comp)
     arr = (Block * len(blocks))()
     nb = 0
-    for start, csize, usize, _us, hsize, flags in blocks:
-        if flags or usize == 0:
-            continue
-        arr[nb].start, arr[nb].csize, arr[nb].hsize, arr[nb].usize = start - base, csize, hsize, usize
+    for start, csize, hsize, usize in blocks:
+        arr[nb].start, arr[nb].csize, arr[nb].hsize, arr[nb].usize = start, csize, hsize, usize
         nb += 1
     cl = np.ascontiguousarray(contig_len, dtype=np.int32)
     pos, tr = ctypes.c_int64(), ctypes.c_int64()

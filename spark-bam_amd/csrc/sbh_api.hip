@@ -58,11 +58,15 @@ hipError_t launch_chain_walk(const uint8_t *U, uint64_t first, uint64_t E, uint6
 
 using namespace sbh;
 
+struct StreamCache;  // sbh_run_stream's window shard, buffers and copy stream (kept between calls)
+static void stream_cache_free(StreamCache *sc);
+
 struct sbh_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   bool own_stream = false;
   std::string err;
+  StreamCache *sc = nullptr;
 };
 
 namespace {
@@ -176,6 +180,30 @@ struct sbh_shard {
   }
 };
 
+struct StreamCache {
+  sbh_shard *sh = nullptr;
+  DBuf<uint8_t> buf[2];
+  hipStream_t cs = nullptr;
+  hipEvent_t done[2] = {nullptr, nullptr}, c0[2] = {nullptr, nullptr};
+};
+
+static void stream_cache_free(StreamCache *sc) {
+  if (sc->cs) (void)hipStreamSynchronize(sc->cs);
+  if (sc->sh) {
+    sc->sh->comp.p = nullptr;
+    sc->sh->comp.cap = 0;
+    sbh_shard_destroy(sc->sh);
+  }
+  sc->buf[0].release();
+  sc->buf[1].release();
+  for (int i = 0; i < 2; ++i) {
+    if (sc->done[i]) (void)hipEventDestroy(sc->done[i]);
+    if (sc->c0[i]) (void)hipEventDestroy(sc->c0[i]);
+  }
+  if (sc->cs) (void)hipStreamDestroy(sc->cs);
+  delete sc;
+}
+
 static int fail(sbh_ctx *ctx, int code, const char *fmt, ...) {
   if (ctx) {
     char buf[512];
@@ -235,6 +263,11 @@ int sbh_ctx_create(int device, sbh_ctx **out) {
 
 int sbh_ctx_destroy(sbh_ctx *ctx) {
   if (!ctx) return SBH_OK;
+  if (ctx->sc) {
+    (void)hipSetDevice(ctx->device);
+    stream_cache_free(ctx->sc);
+    ctx->sc = nullptr;
+  }
   if (ctx->own_stream && ctx->stream) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamDestroy(ctx->stream);
@@ -1398,41 +1431,41 @@ int sbh_run_stream(sbh_ctx *ctx, const void *host, uint64_t n, uint64_t file_off
   hipPointerAttribute_t pa{};
   res->host_pinned = hipPointerGetAttributes(&pa, host) == hipSuccess && pa.type == hipMemoryTypeHost ? 1 : 0;
   (void)hipGetLastError();
-  struct Run {  // everything the call owns, released on every return path
-    sbh_shard *sh = nullptr;
-    DBuf<uint8_t> buf[2];
-    hipStream_t cs = nullptr;
-    hipEvent_t done[2] = {nullptr, nullptr}, c0[2] = {nullptr, nullptr};
-    ~Run() {
-      if (cs) (void)hipStreamSynchronize(cs);
-      if (sh) {
-        sh->comp.p = nullptr;  // the window buffers are not the shard's
-        sh->comp.cap = 0;
-        sbh_shard_destroy(sh);
-      }
-      buf[0].release();
-      buf[1].release();
-      for (int i = 0; i < 2; ++i) {
-        if (done[i]) (void)hipEventDestroy(done[i]);
-        if (c0[i]) (void)hipEventDestroy(c0[i]);
-      }
-      if (cs) (void)hipStreamDestroy(cs);
+  // the window shard, the two window buffers and the copy stream persist in the context
+  // (grow-only), so repeated calls allocate nothing
+  if (!ctx->sc) {
+    ctx->sc = new StreamCache();
+    rc = sbh_shard_create(ctx, nullptr, 0, file_offset, file_size, 0, &ctx->sc->sh);
+    if (rc) {
+      delete ctx->sc;
+      ctx->sc = nullptr;
+      return res->status = rc;
     }
-  } R;
-  rc = sbh_shard_create(ctx, nullptr, 0, file_offset, file_size, 0, &R.sh);
-  if (rc) return res->status = rc;
+    ctx->sc->sh->comp.release();
+    HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->sc->cs, hipStreamNonBlocking));
+    for (int i = 0; i < 2; ++i) {
+      HIPCHK(ctx, hipEventCreate(&ctx->sc->done[i]));
+      HIPCHK(ctx, hipEventCreate(&ctx->sc->c0[i]));
+    }
+  }
+  StreamCache &R = *ctx->sc;
+  struct Detach {  // the window buffers are never the shard's own: detach on every return path
+    StreamCache &R;
+    ~Detach() {
+      if (R.cs) (void)hipStreamSynchronize(R.cs);
+      R.sh->comp.p = nullptr;
+      R.sh->comp.cap = 0;
+    }
+  } detach{R};
   sbh_shard *sh = R.sh;
-  sh->comp.release();
+  sh->file_size = file_size;
   rc = sbh_set_contigs(sh, contigs, n_contigs);
   if (rc) return res->status = rc;
-  HIPCHK(ctx, hipStreamCreateWithFlags(&R.cs, hipStreamNonBlocking));
-  for (int i = 0; i < 2; ++i) {
-    HIPCHK(ctx, hipEventCreate(&R.done[i]));
-    HIPCHK(ctx, hipEventCreate(&R.c0[i]));
-  }
   const uint64_t data_end = file_offset + n, pad = sh->pad;
+  // the first window is short: its copy is the only one no kernel overlaps
+  const uint64_t first_window = std::max<uint64_t>(std::min<uint64_t>(window, 64ull << 20), window / 8);
   auto win_end = [&](uint64_t lo) {
-    uint64_t hi = std::min(lo + window, own_end_file);
+    uint64_t hi = std::min(lo + (lo == file_offset ? first_window : window), own_end_file);
     if (own_end_file - hi < window / 4) hi = own_end_file;  // no sliver of a last window
     return hi;
   };

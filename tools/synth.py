@@ -123,7 +123,11 @@ class Segment:
     blocks of rank i+1 (or the EOF block) as its halo.  Only the per-rank compressed
     sizes must be exchanged to place the shard in the file (see set_offsets)."""
 
-    def __init__(self, p, records_per_rank, world, rank, halo_blocks=16, log=None):
+    def __init__(self, p, records_per_rank, world, rank, halo_blocks=16, log=None, alloc=None,
+                 chunk_blocks=4096):
+        """alloc(n) -> a writable uint8 array of n bytes for the shard's compressed bytes (e.g.
+        pinned host memory); records are generated and compressed chunk_blocks blocks at a
+        time, so host memory holds the compressed shard plus one chunk."""
         if p.level < 0:
             raise ValueError("segments need a uniform payload size (level >= 0)")
         self.p, self.R, self.world, self.rank = p, records_per_rank, world, rank
@@ -143,26 +147,45 @@ class Segment:
         k0, k1 = self.k[rank], self.k[rank + 1]
         k_halo = min(k1 + halo_blocks, self.k[world])
         u0, u1 = k0 * P, min(k_halo * P, self.u_total)
-        # generate records covering [u0, u1)
+        # records covering [u0, u1), cut into P-aligned chunks of whole blocks as they come:
+        # block k is U[kP, (k+1)P) whatever chunk it is compressed in
         first_rec = rank * records_per_rank
-        base = self.u_start[rank] if rank else 0
-        parts = [hdr] if rank == 0 else []
-        rec_end = first_rec
-        have = base + sum(x.size for x in parts)
         total_recs = world * records_per_rank
-        step = max(1024, records_per_rank // 8)
-        while have < u1 and rec_end < total_recs:
-            nxt = min(total_recs, rec_end + (records_per_rank if rec_end == first_rec else step))
-            parts.append(records(p, rec_end, nxt))
-            have += parts[-1].size
-            rec_end = nxt
-        U = np.concatenate(parts) if len(parts) > 1 else parts[0]
-        U = U[u0 - base:u1 - base]
-        if log:
-            log(f"[rank {rank}] records generated: {U.size / 2**30:.2f} GiB uncompressed; compressing")
+        pending = [hdr] if rank == 0 else []
+        pend_at = 0 if rank == 0 else self.u_start[rank]  # U offset of pending's first byte
+        pend_n = sum(x.size for x in pending)
+        rec_end, k, chunks, sizes = first_rec, k0, [], []
+        step = max(1024, min(records_per_rank, 200_000))
+        done_u = 0
+        while k < k_halo:
+            need_end = min(u1, (k + chunk_blocks) * P)
+            while pend_at + pend_n < need_end and rec_end < total_recs:
+                nxt = min(total_recs, rec_end + step)
+                pending.append(records(p, rec_end, nxt))
+                pend_n += pending[-1].size
+                rec_end = nxt
+            buf = np.concatenate(pending) if len(pending) > 1 else pending[0]
+            lo = k * P - pend_at  # the chunk's first byte within buf
+            hi = min(need_end, pend_at + buf.size) - pend_at
+            kb = (hi - lo + P - 1) // P
+            last = k + kb >= k_halo
+            comp, _ = bgzf(p, buf[lo:hi], k, add_eof=last and k_halo == self.k[world])
+            chunks.append(comp)
+            sizes += block_sizes(comp)
+            done_u += hi - lo
+            k += kb
+            pending, pend_at, pend_n = [buf[hi:]], pend_at + hi, buf.size - hi
+            if log and (len(chunks) % 8 == 0 or last):
+                log(f"[rank {rank}] generated {done_u / 2**30:.2f} GiB uncompressed, "
+                    f"{sum(c.size for c in chunks) / 2**30:.2f} GiB compressed")
+        total = sum(c.size for c in chunks)
+        comp = alloc(total) if alloc else np.empty(total, dtype=np.uint8)
+        o = 0
+        while chunks:  # free each chunk once it is placed
+            c = chunks.pop(0)
+            comp[o:o + c.size] = c
+            o += c.size
         self.own_blocks = k1 - k0
-        comp, nb = bgzf(p, U, k0, add_eof=(k_halo == self.k[world]))
-        sizes = block_sizes(comp)
         self.own_csize = sum(sizes[:self.own_blocks])
         self.comp = comp
         self.n_records_owned = None  # known only by the chain walk (GPU result)
