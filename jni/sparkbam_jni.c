@@ -1,0 +1,352 @@
+/*
+ * sparkbam_jni.c -- the JNI shim a maintainer adds to spark-bam so its Scala host side
+ * (modules bgzf / check / load / cli) calls libsparkbam_hip.so (include/sparkbam.h).
+ *
+ * Java class: org.hammerlab.bam.gpu.Native (jni/Native.scala).  Handles are jlongs; byte
+ * buffers are direct ByteBuffers (no copies through the JVM heap); status codes map onto
+ * the reference's exception classes:
+ *   SBH_E_HEADER_PARSE         -> org.hammerlab.bgzf.block.HeaderParseException
+ *                                 (bgzf/.../block/Header.scala:50-57)
+ *   SBH_E_HEADER_SEARCH_FAILED -> org.hammerlab.bgzf.block.HeaderSearchFailedException
+ *                                 (bgzf/.../block/FindBlockStart.scala:31-35)
+ *   SBH_E_INFLATE_SIZE         -> java.io.IOException (Stream.scala:52-54)
+ *   SBH_E_INFLATE_DATA         -> java.util.zip.DataFormatException
+ *   SBH_E_NO_READ_FOUND        -> org.hammerlab.bam.check.NoReadFoundException
+ *                                 (check/.../spark/FindRecordStart.scala:66-71)
+ *   SBH_E_NEED_HALO            -> org.hammerlab.bam.gpu.NeedHaloException (the façade re-reads
+ *                                 a larger halo; never user-visible)
+ *   anything else              -> java.lang.IllegalStateException(sbh_last_error)
+ *
+ * Built by jni/Makefile only when $JAVA_HOME/include/jni.h exists (no JDK in this image).
+ */
+#include <jni.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include "sparkbam.h"
+
+#define CTX(x) ((sbh_ctx *)(intptr_t)(x))
+#define SH(x) ((sbh_shard *)(intptr_t)(x))
+
+static void throw_status(JNIEnv *env, sbh_ctx *ctx, int rc) {
+  const char *cls = rc == SBH_E_HEADER_PARSE           ? "org/hammerlab/bgzf/block/HeaderParseException"
+                    : rc == SBH_E_HEADER_SEARCH_FAILED ? "org/hammerlab/bgzf/block/HeaderSearchFailedException"
+                    : rc == SBH_E_INFLATE_SIZE         ? "java/io/IOException"
+                    : rc == SBH_E_INFLATE_DATA         ? "java/util/zip/DataFormatException"
+                    : rc == SBH_E_NO_READ_FOUND        ? "org/hammerlab/bam/check/NoReadFoundException"
+                    : rc == SBH_E_NEED_HALO            ? "org/hammerlab/bam/gpu/NeedHaloException"
+                                                       : "java/lang/IllegalStateException";
+  jclass c = (*env)->FindClass(env, cls);
+  if (!c) return; /* NoClassDefFoundError is pending */
+  (*env)->ThrowNew(env, c, ctx ? sbh_last_error(ctx) : "libsparkbam_hip");
+}
+
+/* status check: throws and returns 1 on failure */
+static int failed(JNIEnv *env, jlong ctx, int rc) {
+  if (rc == SBH_OK) return 0;
+  throw_status(env, CTX(ctx), rc);
+  return 1;
+}
+
+static void *direct(JNIEnv *env, jobject buf) { return buf ? (*env)->GetDirectBufferAddress(env, buf) : NULL; }
+
+static int put_longs(JNIEnv *env, jlongArray out, const jlong *v, jsize n) {
+  if ((*env)->GetArrayLength(env, out) < n) {
+    throw_status(env, NULL, SBH_E_ARG);
+    return 1;
+  }
+  (*env)->SetLongArrayRegion(env, out, 0, n, v);
+  return 0;
+}
+
+/* ---- context / pinned memory ---- */
+JNIEXPORT jlong JNICALL Java_org_hammerlab_bam_gpu_Native_00024_ctxCreate(JNIEnv *env, jobject self, jint dev) {
+  sbh_ctx *ctx = NULL;
+  int rc = sbh_ctx_create(dev, &ctx);
+  if (rc) {
+    throw_status(env, NULL, rc);
+    return 0;
+  }
+  return (jlong)(intptr_t)ctx;
+}
+
+JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_ctxDestroy(JNIEnv *env, jobject self, jlong ctx) {
+  sbh_ctx_destroy(CTX(ctx));
+}
+
+/* Page-locked host bytes as a direct ByteBuffer (compressed input for shardCreate/runStream). */
+JNIEXPORT jobject JNICALL Java_org_hammerlab_bam_gpu_Native_00024_hostAlloc(JNIEnv *env, jobject self, jlong n) {
+  void *p = NULL;
+  int rc = sbh_host_alloc((uint64_t)n, &p);
+  if (rc) {
+    throw_status(env, NULL, rc);
+    return NULL;
+  }
+  return (*env)->NewDirectByteBuffer(env, p, n);
+}
+
+JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_hostFree(JNIEnv *env, jobject self, jobject buf) {
+  sbh_host_free(direct(env, buf));
+}
+
+/* ---- shards: compressed bytes [fileOffset, fileOffset + n) of a BGZF file ---- */
+JNIEXPORT jlong JNICALL Java_org_hammerlab_bam_gpu_Native_00024_shardCreate(JNIEnv *env, jobject self, jlong ctx,
+                                                                            jobject buf, jlong n, jlong fileOffset,
+                                                                            jlong fileSize) {
+  sbh_shard *sh = NULL;
+  if (failed(env, ctx, sbh_shard_create(CTX(ctx), direct(env, buf), (uint64_t)n, (uint64_t)fileOffset,
+                                        (uint64_t)fileSize, 0, &sh)))
+    return 0;
+  return (jlong)(intptr_t)sh;
+}
+
+JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_shardDestroy(JNIEnv *env, jobject self, jlong sh) {
+  sbh_shard_destroy(SH(sh));
+}
+
+/* FindBlockStart.apply (bgzf/.../block/FindBlockStart.scala:8-36) */
+JNIEXPORT jlong JNICALL Java_org_hammerlab_bam_gpu_Native_00024_findBlockStart(JNIEnv *env, jobject self, jlong ctx,
+                                                                               jlong sh, jlong start,
+                                                                               jint blocksToCheck) {
+  uint64_t out = 0;
+  if (failed(env, ctx, sbh_find_block_start(SH(sh), (uint64_t)start, blocksToCheck, &out))) return -1;
+  return (jlong)out;
+}
+
+/* MetadataStream + Stream inflate: out = {nBlocks, flatSize} */
+JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_indexAndInflate(JNIEnv *env, jobject self, jlong ctx,
+                                                                               jlong sh, jlong start,
+                                                                               jlongArray out) {
+  uint64_t nb = 0, fs = 0, bad = 0;
+  if (failed(env, ctx, sbh_index(SH(sh), (uint64_t)start, &nb, &fs))) return;
+  if (failed(env, ctx, sbh_inflate(SH(sh), &bad))) return;
+  jlong v[2] = {(jlong)nb, (jlong)fs};
+  put_longs(env, out, v, 2);
+}
+
+/* Block table as 6 longs per block: start, ustart, csize, hsize, usize, flags (Metadata.scala:6-8) */
+JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_blocks(JNIEnv *env, jobject self, jlong ctx, jlong sh,
+                                                                      jlong first, jlong count, jlongArray out) {
+  sbh_block *b = (sbh_block *)malloc(sizeof(sbh_block) * (size_t)(count > 0 ? count : 1));
+  if (!b) {
+    throw_status(env, NULL, SBH_E_NOMEM);
+    return;
+  }
+  if (!failed(env, ctx, sbh_get_blocks(SH(sh), (uint64_t)first, (uint64_t)count, b))) {
+    jlong *v = (jlong *)malloc(sizeof(jlong) * 6 * (size_t)(count > 0 ? count : 1));
+    if (v) {
+      for (jlong i = 0; i < count; ++i) {
+        v[6 * i] = (jlong)b[i].start, v[6 * i + 1] = (jlong)b[i].ustart, v[6 * i + 2] = b[i].csize;
+        v[6 * i + 3] = b[i].hsize, v[6 * i + 4] = b[i].usize, v[6 * i + 5] = b[i].flags;
+      }
+      put_longs(env, out, v, (jsize)(6 * count));
+      free(v);
+    }
+  }
+  free(b);
+}
+
+/* Block.bytes on demand: flat [flat, flat + n) into a direct ByteBuffer */
+JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_readFlat(JNIEnv *env, jobject self, jlong ctx,
+                                                                        jlong sh, jlong flat, jlong n, jobject buf) {
+  failed(env, ctx, sbh_read_flat(SH(sh), (uint64_t)flat, (uint64_t)n, (uint8_t *)direct(env, buf)));
+}
+
+JNIEXPORT jlong JNICALL Java_org_hammerlab_bam_gpu_Native_00024_flatOf(JNIEnv *env, jobject self, jlong ctx,
+                                                                       jlong sh, jlong vpos) {
+  uint64_t f = 0;
+  if (failed(env, ctx, sbh_flat_of(SH(sh), (uint64_t)vpos >> 16, (uint32_t)(vpos & 0xffff), &f))) return -1;
+  return (jlong)f;
+}
+
+JNIEXPORT jlong JNICALL Java_org_hammerlab_bam_gpu_Native_00024_posOf(JNIEnv *env, jobject self, jlong ctx, jlong sh,
+                                                                      jlong flat) {
+  uint64_t bp = 0;
+  uint32_t off = 0;
+  if (failed(env, ctx, sbh_pos_of(SH(sh), (uint64_t)flat, &bp, &off))) return -1;
+  return (jlong)((bp << 16) | off);
+}
+
+/* ContigLengths (check/.../header/ContigLengths.scala) */
+JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_setContigs(JNIEnv *env, jobject self, jlong ctx,
+                                                                          jlong sh, jintArray lens) {
+  const jsize n = (*env)->GetArrayLength(env, lens);
+  jint *v = (*env)->GetIntArrayElements(env, lens, NULL);
+  if (!v) return;
+  const int rc = sbh_set_contigs(SH(sh), (const int32_t *)v, (int32_t)n);
+  (*env)->ReleaseIntArrayElements(env, lens, v, JNI_ABORT);
+  failed(env, ctx, rc);
+}
+
+/* eager.Checker over flat [begin, end): bit per position into `bits` (may be null) */
+JNIEXPORT jlong JNICALL Java_org_hammerlab_bam_gpu_Native_00024_checkEager(JNIEnv *env, jobject self, jlong ctx,
+                                                                           jlong sh, jlong begin, jlong end,
+                                                                           jint readsToCheck, jobject bits) {
+  uint64_t n_true = 0;
+  if (failed(env, ctx, sbh_check_eager(SH(sh), (uint64_t)begin, (uint64_t)end, readsToCheck,
+                                       (uint8_t *)direct(env, bits), &n_true)))
+    return -1;
+  return (jlong)n_true;
+}
+
+/* full.Checker over flat [begin, end): words (may be null), counts 21*19, rbe 21*64, close
+ * calls; out = {nSuccess, nClose} */
+JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_checkFull(JNIEnv *env, jobject self, jlong ctx,
+                                                                         jlong sh, jlong begin, jlong end,
+                                                                         jint readsToCheck, jobject words,
+                                                                         jobject counts, jobject rbe,
+                                                                         jobject closeFlat, jobject closeWord,
+                                                                         jlong closeCap, jlongArray out) {
+  uint64_t ns = 0, nclose = 0;
+  if (failed(env, ctx, sbh_check_full(SH(sh), (uint64_t)begin, (uint64_t)end, readsToCheck,
+                                      (uint32_t *)direct(env, words), (uint64_t *)direct(env, counts),
+                                      (uint64_t *)direct(env, rbe), &ns, (uint64_t *)direct(env, closeFlat),
+                                      (uint32_t *)direct(env, closeWord), (uint64_t)closeCap, &nclose)))
+    return;
+  jlong v[2] = {(jlong)ns, (jlong)nclose};
+  put_longs(env, out, v, 2);
+}
+
+/* FindRecordStart.withDelta: out = {flat, delta} */
+JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_findRecordStart(JNIEnv *env, jobject self, jlong ctx,
+                                                                               jlong sh, jlong from,
+                                                                               jint readsToCheck, jint maxReadSize,
+                                                                               jlongArray out) {
+  uint64_t f = 0;
+  int32_t d = 0;
+  if (failed(env, ctx, sbh_find_record_start(SH(sh), (uint64_t)from, readsToCheck, maxReadSize, &f, &d))) return;
+  jlong v[2] = {(jlong)f, (jlong)d};
+  put_longs(env, out, v, 2);
+}
+
+/* PosStream from a flat position: out = {records before endFlat, exit flat} */
+JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_chainFrom(JNIEnv *env, jobject self, jlong ctx,
+                                                                         jlong sh, jlong first, jlong endFlat,
+                                                                         jlongArray out) {
+  uint64_t n = 0, x = 0;
+  if (failed(env, ctx, sbh_chain_from(SH(sh), (uint64_t)first, (uint64_t)endFlat, &n, &x))) return;
+  jlong v[2] = {(jlong)n, (jlong)x};
+  put_longs(env, out, v, 2);
+}
+
+/* loadSplitsAndReads for every split of a shard at once (CanLoadBam.scala:283-297,316-356):
+ * starts/ends file offsets; out = 3 longs per split {status, firstVpos, count} */
+JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_splitStarts(JNIEnv *env, jobject self, jlong ctx,
+                                                                           jlong sh, jlongArray starts,
+                                                                           jlongArray ends, jint blocksToCheck,
+                                                                           jint readsToCheck, jint maxReadSize,
+                                                                           jlongArray out) {
+  const jsize n = (*env)->GetArrayLength(env, starts);
+  if ((*env)->GetArrayLength(env, ends) != n) {
+    throw_status(env, NULL, SBH_E_ARG);
+    return;
+  }
+  uint64_t *buf = (uint64_t *)malloc(sizeof(uint64_t) * 4 * (size_t)(n > 0 ? n : 1));
+  int32_t *status = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+  jlong *v = (jlong *)malloc(sizeof(jlong) * 3 * (size_t)(n > 0 ? n : 1));
+  if (buf && status && v) {
+    uint64_t *s = buf, *e = buf + n, *first = buf + 2 * n, *cnt = buf + 3 * n;
+    (*env)->GetLongArrayRegion(env, starts, 0, n, (jlong *)s);
+    (*env)->GetLongArrayRegion(env, ends, 0, n, (jlong *)e);
+    if (!failed(env, ctx, sbh_split_starts(SH(sh), s, e, (uint64_t)n, blocksToCheck, readsToCheck, maxReadSize,
+                                           first, cnt, status, NULL))) {
+      for (jsize i = 0; i < n; ++i) v[3 * i] = status[i], v[3 * i + 1] = (jlong)first[i], v[3 * i + 2] = (jlong)cnt[i];
+      put_longs(env, out, v, 3 * n);
+    }
+  } else {
+    throw_status(env, NULL, SBH_E_NOMEM);
+  }
+  free(buf);
+  free(status);
+  free(v);
+}
+
+/* check-bam -s on the device: ranges as 2 longs each, truth records as vpos;
+ * out = {tp, fp, fn, unknown}; fp/fn flat positions into direct buffers (may be null) */
+JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_checkRecords(JNIEnv *env, jobject self, jlong ctx,
+                                                                            jlong sh, jlongArray ranges,
+                                                                            jint readsToCheck, jobject recVpos,
+                                                                            jlong nRec, jobject fpFlat, jobject fnFlat,
+                                                                            jlong cap, jlongArray out) {
+  const jsize nr = (*env)->GetArrayLength(env, ranges) / 2;
+  uint64_t *r = (uint64_t *)malloc(sizeof(uint64_t) * 2 * (size_t)(nr > 0 ? nr : 1));
+  if (!r) {
+    throw_status(env, NULL, SBH_E_NOMEM);
+    return;
+  }
+  uint64_t *rb = r, *re = r + nr;
+  for (jsize i = 0; i < nr; ++i) {
+    jlong ab[2];
+    (*env)->GetLongArrayRegion(env, ranges, 2 * i, 2, ab);
+    rb[i] = (uint64_t)ab[0];
+    re[i] = (uint64_t)ab[1];
+  }
+  uint64_t o[4] = {0, 0, 0, 0};
+  if (!failed(env, ctx, sbh_check_records(SH(sh), rb, re, (uint64_t)nr, readsToCheck,
+                                          (const uint64_t *)direct(env, recVpos), (uint64_t)nRec, o,
+                                          (uint64_t *)direct(env, fpFlat), (uint64_t)cap,
+                                          (uint64_t *)direct(env, fnFlat), (uint64_t)cap))) {
+    jlong v[4] = {(jlong)o[0], (jlong)o[1], (jlong)o[2], (jlong)o[3]};
+    put_longs(env, out, v, 4);
+  }
+  free(r);
+}
+
+/* The whole per-shard path (sbh_run_shard): out = {nBlocks, compBytes, flatBytes, nTrue,
+ * firstVpos, count, exitFlat} */
+JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_runShard(JNIEnv *env, jobject self, jlong ctx,
+                                                                        jlong sh, jlong indexStart, jlong ownEnd,
+                                                                        jint readsToCheck, jint maxReadSize,
+                                                                        jlongArray out) {
+  sbh_shard_result r;
+  if (failed(env, ctx, sbh_run_shard(SH(sh), (uint64_t)indexStart, (uint64_t)ownEnd, readsToCheck, maxReadSize, &r)))
+    return;
+  jlong v[7] = {(jlong)r.n_blocks, (jlong)r.comp_bytes, (jlong)r.flat_bytes, (jlong)r.n_true,
+                (jlong)r.first_vpos, (jlong)r.count, (jlong)r.exit_flat};
+  put_longs(env, out, v, 7);
+}
+
+/* A split larger than HBM streamed through it (sbh_run_stream) from a (pinned) direct buffer:
+ * out = {nWindows, compBytes, flatBytes, nTrue, count, firstVpos, exitVpos} */
+JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_runStream(JNIEnv *env, jobject self, jlong ctx,
+                                                                         jobject comp, jlong n, jlong fileOffset,
+                                                                         jlong fileSize, jlong indexStart,
+                                                                         jlong ownEnd, jlong window, jlong halo,
+                                                                         jintArray contigs, jint readsToCheck,
+                                                                         jint maxReadSize, jlongArray out) {
+  const jsize nc = (*env)->GetArrayLength(env, contigs);
+  jint *cl = (*env)->GetIntArrayElements(env, contigs, NULL);
+  if (!cl) return;
+  sbh_stream_result r;
+  const int rc = sbh_run_stream(CTX(ctx), direct(env, comp), (uint64_t)n, (uint64_t)fileOffset, (uint64_t)fileSize,
+                                (uint64_t)indexStart, (uint64_t)ownEnd, (uint64_t)window, (uint64_t)halo,
+                                (const int32_t *)cl, (int32_t)nc, readsToCheck, maxReadSize, NULL, 0, &r);
+  (*env)->ReleaseIntArrayElements(env, contigs, cl, JNI_ABORT);
+  if (failed(env, ctx, rc)) return;
+  jlong v[7] = {(jlong)r.n_windows, (jlong)r.comp_bytes, (jlong)r.flat_bytes, (jlong)r.n_true,
+                (jlong)r.count, (jlong)r.first_vpos, (jlong)r.exit_vpos};
+  put_longs(env, out, v, 7);
+}
+
+/* RecordStream + BAMRecordCodec.decode into columns: out = {n, nameBytes, cigarOps, bases,
+ * auxBytes}; then recordsFetch fills one direct buffer per column (null = skip) */
+JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_recordsScan(JNIEnv *env, jobject self, jlong ctx,
+                                                                           jlong sh, jlong first, jlong endFlat,
+                                                                           jlongArray out) {
+  sbh_records_sizes z;
+  if (failed(env, ctx, sbh_records_scan(SH(sh), (uint64_t)first, (uint64_t)endFlat, &z))) return;
+  jlong v[5] = {(jlong)z.n, (jlong)z.name_bytes, (jlong)z.cigar_ops, (jlong)z.bases, (jlong)z.aux_bytes};
+  put_longs(env, out, v, 5);
+}
+
+JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_recordsFetch(JNIEnv *env, jobject self, jlong ctx,
+                                                                            jlong sh, jobjectArray cols) {
+  /* 18 direct buffers in sbh_records_out field order */
+  void *p[18];
+  for (jsize i = 0; i < 18; ++i) p[i] = direct(env, (*env)->GetObjectArrayElement(env, cols, i));
+  sbh_records_out o = {(uint64_t *)p[0], (int32_t *)p[1],  (int32_t *)p[2],  (int32_t *)p[3],  (int32_t *)p[4],
+                       (int32_t *)p[5],  (uint16_t *)p[6], (uint16_t *)p[7], (uint8_t *)p[8],  (uint64_t *)p[9],
+                       (uint64_t *)p[10], (uint64_t *)p[11], (uint64_t *)p[12], (char *)p[13], (uint32_t *)p[14],
+                       (char *)p[15], (uint8_t *)p[16], (uint8_t *)p[17]};
+  failed(env, ctx, sbh_records_fetch(SH(sh), &o));
+}

@@ -8,13 +8,14 @@
 // and the record-chain bookkeeping behind split/count computation
 // (check/.../iterator/PosStream.scala:14-22, load/.../CanLoadBam.scala:346-355).
 //
-// Layout: a workgroup owns a 4096-position tile.  Eager: it stages the tile plus a
-// 4.5 KiB look-ahead into LDS with coalesced dword loads, evaluates the single-record
-// predicate at every position of the window (99% reject on refID/pos), then walks each
-// surviving position's record chain through those LDS bits; only chains that leave
-// the window (long reads) or touch an EOF edge re-read HBM/L2.  Full: per-position
-// words + an LDS histogram folded into global counters once per tile.  Results are a
-// bit per position (512 B per tile) or a word per position.
+// Layout: a workgroup owns a tile of positions (eager: 16 Ki, full: 8 Ki).  Eager: it stages
+// the tile plus a 4.5 KiB look-ahead into LDS with coalesced 16-byte loads, evaluates the
+// single-record predicate at every position of the window (97% reject on refID), then walks
+// each surviving position's record chain through those LDS bits; only chains that leave the
+// window (long reads) or touch an EOF edge re-read HBM/L2.  Full: byte-class bitmaps of the
+// staged window make each position's first record O(1) LDS work, histograms are counted by
+// wave ballots.  Results are a bit per position (2 KiB per tile, 16-byte stores) or a word
+// per position.
 #include <algorithm>
 
 #include "sbh_internal.h"
@@ -22,12 +23,6 @@
 namespace sbh {
 namespace {
 
-constexpr uint32_t TILE = 4096;
-#ifndef SBH_FULL_HALO
-#define SBH_FULL_HALO 1024
-#endif
-constexpr uint32_t HALO = SBH_FULL_HALO;  // staged look-ahead: chains of short reads stay in LDS
-constexpr uint32_t STAGE = TILE + HALO + 8;  // bytes staged (+ slack for dword pairs)
 constexpr uint32_t T = 256;
 
 constexpr uint32_t FULL_SUCCESS = 0x80000000u;
@@ -378,7 +373,8 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
   constexpr uint32_t NV = (ESTAGE + 32) / 16;
   constexpr uint32_t NWV = T / WAVE, SEGCAP = EQ_CHUNK / NWV;
   __shared__ uint4 ldsv[NV];
-  __shared__ uint32_t ok[EW / 32], nrm[EW / 32], und[EW / 32], res[ETILE / 32];
+  __shared__ uint32_t ok[EW / 32], nrm[EW / 32], und[EW / 32];
+  __shared__ __attribute__((aligned(16))) uint32_t res[ETILE / 32];
   __shared__ uint32_t lnk[EQ_CHUNK / 32], lfail[EQ_CHUNK / 32];  // per sorted candidate: LINK / FAIL step
   __shared__ uint32_t seg0, ntrue, nq, wcnt[NWV];
   __shared__ uint64_t seg_end0;
@@ -506,11 +502,19 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
       atomicMin(o.min_unknown, (unsigned long long)(t0 + i));
     }
   };
-  auto write_res = [&]() {
-    for (uint32_t w = threadIdx.x; w < ETILE / 32; w += T) {
-      if (wbase + w >= nwords) break;
-      o.bits[wbase + w] = res[w];
-      mytrue += __popc(res[w]);
+  auto write_res = [&]() {  // 16 B per lane: the tile's 2 KiB of bits in one wave-store per 1 KiB
+    static_assert(ETILE % 128 == 0, "whole uint4 groups of result words");
+    for (uint32_t w4 = threadIdx.x; w4 < ETILE / 128; w4 += T) {
+      const uint64_t w = wbase + 4ull * w4;
+      if (w >= nwords) break;
+      const uint4 v = reinterpret_cast<const uint4 *>(res)[w4];
+      if (w + 4 <= nwords) {
+        *reinterpret_cast<uint4 *>(o.bits + w) = v;
+      } else {
+        const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+        for (uint32_t k = 0; w + k < nwords; ++k) o.bits[w + k] = x[k];
+      }
+      mytrue += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
     }
   };
 
@@ -765,54 +769,239 @@ struct FullOut {
   uint64_t close_cap;
 };
 
+// ---- full check, one tile per workgroup, O(1) LDS work per position for the first record ----
+// Tiles are 16-byte aligned (tile b covers flat [B + b * FTILE, B + (b + 1) * FTILE), B =
+// begin rounded down to 16; positions before `begin` are skipped), so the staged window
+// starts at the tile's first position and lane t owns 16 consecutive positions: three
+// 16-byte LDS reads give the fixed fields of all 16 (v_alignbyte on neighbouring dwords).
+// Per staged window two byte-class bitmaps are built once: `bad name byte` (outside
+// [0x21..0x3F] u [0x41..0x7E]) and `bad CIGAR op byte` ((b & 0xf) > 8); a position's read
+// name is valid iff no bad name byte lies in [name, name + l_read_name - 1), and its first
+// invalid op is the first bad op byte at a stride of 4 from the CIGAR start -- one or two
+// word reads each.  Positions whose first record passes (record starts: the chain must be
+// followed) or whose CIGAR runs past the window take the exact full_at().  Histograms are
+// counted per wave by ballots (one LDS add per distinct numNonZeroFields and flag); close
+// calls are collected in LDS and appended with one global atomic per workgroup.
+constexpr uint32_t FTILE = 8192;              // positions per workgroup
+constexpr uint32_t FPL = 16;                  // positions per lane and step
+constexpr uint32_t FNV = FTILE / 16 + 64;     // staged 16-byte vectors: tile + 1 KiB look-ahead
+constexpr uint32_t FSN = FNV * 16;            // staged bytes
+constexpr uint32_t FBW = FSN / 32;            // bitmap words
+constexpr uint32_t FCCAP = 512;               // close calls buffered per workgroup
+constexpr uint32_t FULL_SLOW = 0xFFFFFFFFu;   // "take the exact path" (no valid word has all bits)
+static_assert(FTILE % (FPL * T) == 0 && FSN % 32 == 0 && FSN >= FTILE + 36 + 255 + 16, "full tile layout");
+
+// exact per-byte classes of the 4 bytes of x, as 4 bits (bit k = byte k)
+__device__ __forceinline__ uint32_t pack4(uint32_t hi_bits) {  // bit 7 of each byte -> 4 bits
+  return (((hi_bits >> 7) & 0x01010101u) * 0x01020408u) >> 24;
+}
+__device__ __forceinline__ uint32_t bad_name4(uint32_t x) {
+  const uint32_t lo7 = x & 0x7f7f7f7fu;
+  const uint32_t lt21 = ~((lo7 + 0x5f5f5f5fu) | x) & 0x80808080u;  // b < 0x21
+  const uint32_t gt7e = (x | (lo7 + 0x01010101u)) & 0x80808080u;   // b > 0x7e
+  const uint32_t y = x ^ 0x40404040u;
+  const uint32_t eq40 = ~(((y & 0x7f7f7f7fu) + 0x7f7f7f7fu) | y) & 0x80808080u;  // b == 0x40
+  return pack4(lt21 | gt7e | eq40);
+}
+__device__ __forceinline__ uint32_t bad_op4(uint32_t x) {  // (b & 0xf) > 8
+  return pack4((((x & 0x0f0f0f0fu) + 0x07070707u) & 0x10101010u) << 3);
+}
+
+// first set bit y in [x, lim) of an LDS bitmap (bit positions = staged byte offsets), masked
+// per word by `pat` (all ones, or every 4th bit from x's residue); lim if none
+__device__ __forceinline__ uint32_t next_set(const uint32_t *bm, uint32_t x, uint32_t lim, uint32_t pat) {
+  if (x >= lim) return lim;
+  uint32_t w = x >> 5;
+  const uint32_t wl = (lim + 31) >> 5;
+  uint32_t m = bm[w] & pat & (~0u << (x & 31));
+  while (!m) {
+    if (++w >= wl) return lim;
+    m = bm[w] & pat;
+  }
+  const uint32_t y = 32 * w + __builtin_ctz(m);
+  return y < lim ? y : lim;
+}
+
+struct Fixed {  // the 36-byte fixed part of a record (tlen unused by the checkers)
+  int32_t rem, idx, pos, seq_len, nidx, npos;
+  uint32_t bmn, fnc;
+};
+
+// The full check's first record at p (window offset q) from its fixed fields, the staged
+// window and its bitmaps: the result word when the first record fails (or at EOF / open-end
+// rules), FULL_SLOW when the exact path must decide.
+__device__ __forceinline__ uint32_t full_first(const Src &s, const uint32_t *bname, const uint32_t *bop, uint64_t p,
+                                               uint32_t q, const Fixed &x, uint64_t total, bool open, const Ctg &c,
+                                               int32_t rtc) {
+  if (rtc == 0) return FULL_SUCCESS;
+  if (p + 36 > total) return open ? FULL_UNKNOWN : 1u;
+  const int32_t rnl = (int32_t)(x.bmn & 0xff), nc = (int32_t)(x.fnc & 0xffff);
+  uint32_t f = ref_pos_error(x.idx, x.pos, c) << 1;
+  if (x.rem < implied_min_remaining(rnl, nc, x.seq_len)) f |= 1u << 18;
+  f |= ref_pos_error(x.nidx, x.npos, c) << 5;
+  uint64_t cur = p + 36;
+  uint32_t a = q + 36;  // window offset of cur
+  if (rnl == 0) {
+    f |= 1u << 12;
+  } else if (rnl == 1) {
+    f |= 1u << 13;
+  } else if (cur + (uint64_t)rnl > total) {
+    if (open) return FULL_UNKNOWN;
+    return f | (1u << 9);  // tooFewBytesForReadName: the CIGAR is not read
+  } else {
+    const uint32_t z = a + (uint32_t)rnl - 1;  // name bytes [a, z), its NUL at z
+    if ((uint8_t)(s.lds32[z >> 2] >> (8 * (z & 3))) != 0) f |= 1u << 10;
+    else if (next_set(bname, a, z, ~0u) < z) f |= 1u << 11;
+    cur += rnl;
+    a = z + 1;
+  }
+  // CIGAR: the first op k < lim = min(nc, ops that fit below total) with a bad op byte
+  const uint64_t fit = total >= cur ? (total - cur) / 4 : 0;
+  const uint32_t lim = fit < (uint64_t)nc ? (uint32_t)fit : (uint32_t)nc;
+  const uint64_t stop = (uint64_t)a + 4ull * lim;  // window offset past the ops to test
+  const uint32_t hi = stop < FSN ? (uint32_t)stop : FSN;
+  const uint32_t y = next_set(bop, a, hi, 0x11111111u << (a & 3));
+  bool cig_err = false;
+  if (y < hi) {
+    cig_err = true;
+    f |= 1u << 15;
+  } else if (stop > hi) {
+    return FULL_SLOW;  // ops past the window: exact path
+  } else if (lim < (uint32_t)nc) {
+    if (open) return FULL_UNKNOWN;
+    cig_err = true;
+    f |= 1u << 14;
+  }
+  if (!cig_err && (x.fnc & (4u << 16)) == 0 && (x.seq_len == 0 || nc == 0)) {
+    if (x.seq_len == 0) f |= 1u << 16;  // EmptyMapped(emptySeq, emptyCigar) field swap
+    if (nc == 0) f |= 1u << 17;
+  }
+  return f ? f : FULL_SLOW;  // a passing first record: follow the chain exactly
+}
+
+__device__ __noinline__ uint32_t full_at_slow(const Src &s, uint64_t p, uint64_t total, bool open, const Ctg &c,
+                                              int32_t rtc) {
+  return full_at(s, p, total, open, c, rtc);
+}
+
 __global__ __launch_bounds__(T) void k_full(const uint8_t *__restrict__ U, uint64_t u_pad, uint64_t begin,
                                             uint64_t end, Segs sg, Ctg c, int32_t rtc, FullOut o) {
-  constexpr uint32_t NV = (STAGE + 16 + 15) / 16;
-  __shared__ uint4 ldsv[NV];
+  __shared__ uint4 ldsv[FNV];
+  __shared__ uint32_t bname[FBW], bop[FBW];
   __shared__ uint32_t hist[21 * 19 + 21 * 64];
-  __shared__ uint32_t seg0, nsucc;
+  __shared__ uint64_t cpos[FCCAP];
+  __shared__ uint32_t cword[FCCAP];
+  __shared__ uint32_t seg0, nsucc, ncl;
+  __shared__ uint64_t e0;
+  __shared__ unsigned long long cbase;
   const uint32_t *lds32 = reinterpret_cast<const uint32_t *>(ldsv);
-  const uint64_t t0 = begin + (uint64_t)blockIdx.x * TILE;
-  const uint64_t s0 = t0 & ~15ull;
-  stage_vec<NV>(ldsv, U, s0, u_pad);
+  const uint64_t s0 = (begin & ~15ull) + (uint64_t)blockIdx.x * FTILE;  // 16-aligned tile start
+  stage_vec<FNV>(ldsv, U, s0, u_pad);
   for (uint32_t i = threadIdx.x; i < 21 * 19 + 21 * 64; i += T) hist[i] = 0;
-  if (threadIdx.x == 0) { seg0 = seg_first(sg, t0); nsucc = 0; }
+  if (threadIdx.x == 0) {
+    seg0 = seg_first(sg, s0 > begin ? s0 : begin);
+    e0 = sg.end[seg0];
+    nsucc = 0;
+    ncl = 0;
+  }
   __syncthreads();
-  Src s{U, lds32, s0, STAGE & ~3u};
-  uint32_t mysucc = 0;
-  for (uint32_t i = threadIdx.x; i < TILE; i += T) {
-    const uint64_t p = t0 + i;
-    if (p >= end) break;
-    const uint32_t k = seg_index(sg, p, seg0);
-    const uint64_t total = sg.end[k];
-    const bool open = sg.open_last && k == sg.n - 1;
-    const uint32_t r = full_at(s, p, total, open, c, rtc);
-    if (o.words) o.words[p - begin] = r;
-    if (r & FULL_SUCCESS) { ++mysucc; continue; }
-    if (r & FULL_UNKNOWN) {
-      atomicAdd(o.n_unknown, 1ull);
-      atomicMin(o.min_unknown, (unsigned long long)p);
-      continue;
+  for (uint32_t w = threadIdx.x; w < FBW; w += T) {  // byte classes of staged bytes 32w..32w+31
+    uint32_t bn = 0, bo = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+      const uint32_t x = lds32[8 * w + j];
+      bn |= bad_name4(x) << (4 * j);
+      bo |= bad_op4(x) << (4 * j);
     }
-    const uint32_t f = r & 0x7FFFFu;
-    const uint32_t rbe = (r >> N_SHIFT) & 0x3FFu;
-    if (f == 1u && rbe == 0) continue;  // Flags.TooFewFixedBlockBytes is excluded
-    const uint32_t nnz = __popc(f) + (rbe > 0);
-    for (uint32_t b = 0; b < 19; ++b)
-      if (f & (1u << b)) atomicAdd(&hist[nnz * 19 + b], 1u);
-    if (rbe > 0 && rbe < 64) atomicAdd(&hist[21 * 19 + nnz * 64 + rbe], 1u);
-    if (nnz <= 2) {
-      const unsigned long long slot = atomicAdd(o.close_n, 1ull);
-      if (slot < o.close_cap) { o.close_pos[slot] = p; o.close_word[slot] = r; }
+    bname[w] = bn;
+    bop[w] = bo;
+  }
+  __syncthreads();
+  Src s{U, lds32, s0, FSN};
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  uint32_t mysucc = 0;
+  for (uint32_t step = 0; step < FTILE / (FPL * T); ++step) {
+    const uint32_t j = threadIdx.x + step * T;  // this lane's 16 positions: window bytes 16j..16j+15
+    const uint4 v0 = ldsv[j], v1 = ldsv[j + 1], v2 = ldsv[j + 2];
+    const uint32_t D[12] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w};
+    uint32_t res[FPL];
+#pragma unroll
+    for (uint32_t k = 0; k < FPL; ++k) {
+      const uint32_t q = 16 * j + k;
+      const uint64_t p = s0 + q;
+      res[k] = FULL_SUCCESS;
+      if (p < begin || p >= end) continue;
+      const uint32_t b = k >> 2, sh = k & 3;
+      Fixed x;
+      x.rem = (int32_t)__builtin_amdgcn_alignbyte(D[b + 1], D[b], sh);
+      x.idx = (int32_t)__builtin_amdgcn_alignbyte(D[b + 2], D[b + 1], sh);
+      x.pos = (int32_t)__builtin_amdgcn_alignbyte(D[b + 3], D[b + 2], sh);
+      x.bmn = __builtin_amdgcn_alignbyte(D[b + 4], D[b + 3], sh);
+      x.fnc = __builtin_amdgcn_alignbyte(D[b + 5], D[b + 4], sh);
+      x.seq_len = (int32_t)__builtin_amdgcn_alignbyte(D[b + 6], D[b + 5], sh);
+      x.nidx = (int32_t)__builtin_amdgcn_alignbyte(D[b + 7], D[b + 6], sh);
+      x.npos = (int32_t)__builtin_amdgcn_alignbyte(D[b + 8], D[b + 7], sh);
+      const uint32_t kseg = p < e0 ? seg0 : seg_index(sg, p, seg0);
+      const uint64_t total = p < e0 ? e0 : sg.end[kseg];
+      const bool open = sg.open_last && kseg == sg.n - 1;
+      uint32_t r = full_first(s, bname, bop, p, q, x, total, open, c, rtc);
+      if (r == FULL_SLOW) r = full_at_slow(s, p, total, open, c, rtc);
+      res[k] = r;
+      if (o.words) o.words[p - begin] = r;
+      if (r & FULL_UNKNOWN) {
+        atomicAdd(o.n_unknown, 1ull);
+        atomicMin(o.min_unknown, (unsigned long long)p);
+      }
+      if (r & FULL_SUCCESS) ++mysucc;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < FPL; ++k) {
+      const uint32_t r = res[k];
+      const uint32_t f = r & 0x7FFFFu, rbe = (r >> N_SHIFT) & 0x3FFu;
+      // counted: a failure other than Flags.TooFewFixedBlockBytes alone (FullCheck.scala:143-150)
+      const bool cnt = !(r & (FULL_SUCCESS | FULL_UNKNOWN)) && !(f == 1u && rbe == 0);
+      const uint32_t nnz = __popc(f) + (rbe > 0);
+      uint64_t live = __ballot(cnt);
+      while (live) {  // per distinct numNonZeroFields: 19 flag counts by ballot, one LDS add each
+        const uint32_t v = __builtin_amdgcn_readlane(nnz, (uint32_t)__builtin_ctzll(live));
+        const bool g = cnt && nnz == v;
+        live &= ~__ballot(g);
+        uint32_t mine = 0;
+#pragma unroll
+        for (uint32_t b = 0; b < 19; ++b) {
+          const uint32_t cb = (uint32_t)__popcll(__ballot(g && ((f >> b) & 1u)));
+          mine = lane == b ? cb : mine;
+        }
+        if (lane < 19 && mine) atomicAdd(&hist[v * 19 + lane], mine);
+      }
+      if (cnt && rbe > 0 && rbe < 64) atomicAdd(&hist[21 * 19 + nnz * 64 + rbe], 1u);
+      if (cnt && nnz <= 2) {
+        const uint64_t p = s0 + 16 * j + k;
+        const uint32_t slot = atomicAdd(&ncl, 1u);
+        if (slot < FCCAP) {
+          cpos[slot] = p;
+          cword[slot] = r;
+        } else {
+          const unsigned long long gs = atomicAdd(o.close_n, 1ull);
+          if (gs < o.close_cap) { o.close_pos[gs] = p; o.close_word[gs] = r; }
+        }
+      }
     }
   }
   if (mysucc) atomicAdd(&nsucc, mysucc);
   __syncthreads();
+  const uint32_t nc = ncl < FCCAP ? ncl : FCCAP;
+  if (threadIdx.x == 0) cbase = nc ? atomicAdd(o.close_n, (unsigned long long)nc) : 0;
   for (uint32_t i = threadIdx.x; i < 21 * 19; i += T)
     if (hist[i]) atomicAdd(&o.counts[i], (unsigned long long)hist[i]);
   for (uint32_t i = threadIdx.x; i < 21 * 64; i += T)
     if (hist[21 * 19 + i]) atomicAdd(&o.rbe[i], (unsigned long long)hist[21 * 19 + i]);
   if (threadIdx.x == 0 && nsucc) atomicAdd(o.n_success, (unsigned long long)nsucc);
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nc; i += T) {
+    const unsigned long long g = cbase + i;
+    if (g < o.close_cap) { o.close_pos[g] = cpos[i]; o.close_word[g] = cword[i]; }
+  }
 }
 
 // ---------------------------------------------------------------- bitmap utilities
@@ -1235,7 +1424,7 @@ hipError_t launch_full(const uint8_t *U, uint64_t u_pad, uint64_t begin, uint64_
   o.close_pos = close_pos;
   o.close_word = close_word;
   o.close_cap = close_cap;
-  hipLaunchKernelGGL(k_full, dim3(ngrid(end - begin, TILE)), dim3(T), 0, st, U, u_pad, begin, end, sg, c, rtc,
+  hipLaunchKernelGGL(k_full, dim3(ngrid(end - (begin & ~15ull), FTILE)), dim3(T), 0, st, U, u_pad, begin, end, sg, c, rtc,
                      o);
   return hipGetLastError();
 }
