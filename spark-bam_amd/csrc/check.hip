@@ -123,7 +123,9 @@ __device__ __forceinline__ uint32_t first_bad_op(const Src &s, uint64_t q, uint3
 // (needs flat bytes at or past `front`, which are not inflated yet: the pipelined run
 // re-checks the position once they are).
 constexpr uint32_t EAGER_DEFER = 3;
-__device__ uint32_t eager_at(const Src &s, uint64_t p, uint64_t total, bool open, const Ctg &c,
+// Src / Ctg by value: passed in registers (a reference would materialize them in scratch
+// memory at every launch of the calling kernel)
+__device__ uint32_t eager_at(const Src s, uint64_t p, uint64_t total, bool open, const Ctg c,
                              int32_t rtc, uint64_t front = ~0ull) {
   uint64_t cur = p, start = p;
   for (int32_t n = 0;; ++n) {
@@ -174,7 +176,7 @@ __device__ uint32_t eager_at(const Src &s, uint64_t p, uint64_t total, bool open
 }
 
 // Full check at p: result word (see include/sparkbam.h), or FULL_UNKNOWN.
-__device__ uint32_t full_at(const Src &s, uint64_t p, uint64_t total, bool open, const Ctg &c,
+__device__ uint32_t full_at(const Src s, uint64_t p, uint64_t total, bool open, const Ctg c,
                             int32_t rtc) {
   uint64_t cur = p, start = p;
   for (int32_t n = 0;; ++n) {
@@ -779,9 +781,11 @@ struct FullOut {
 // name is valid iff no bad name byte lies in [name, name + l_read_name - 1), and its first
 // invalid op is the first bad op byte at a stride of 4 from the CIGAR start -- one or two
 // word reads each.  Positions whose first record passes (record starts: the chain must be
-// followed) or whose CIGAR runs past the window take the exact full_at().  Histograms are
-// counted per wave by ballots (one LDS add per distinct numNonZeroFields and flag); close
-// calls are collected in LDS and appended with one global atomic per workgroup.
+// followed) or whose CIGAR runs past the window are queued and decided by the exact full_at()
+// after the tile's sweep, one per lane (no wave waits on another lane's chain).  Histograms
+// are LDS adds into 16 replicas (lane mod 16, stride coprime to the 32 banks), so lanes
+// counting the same (numNonZeroFields, flag) rarely meet on one address; close calls are
+// collected in LDS and appended with one global atomic per workgroup.
 constexpr uint32_t FTILE = 8192;              // positions per workgroup
 constexpr uint32_t FPL = 16;                  // positions per lane and step
 constexpr uint32_t FNV = FTILE / 16 + 64;     // staged 16-byte vectors: tile + 1 KiB look-ahead
@@ -879,30 +883,29 @@ __device__ __forceinline__ uint32_t full_first(const Src &s, const uint32_t *bna
   return f ? f : FULL_SLOW;  // a passing first record: follow the chain exactly
 }
 
-__device__ __noinline__ uint32_t full_at_slow(const Src &s, uint64_t p, uint64_t total, bool open, const Ctg &c,
-                                              int32_t rtc) {
-  return full_at(s, p, total, open, c, rtc);
-}
-
 __global__ __launch_bounds__(T) void k_full(const uint8_t *__restrict__ U, uint64_t u_pad, uint64_t begin,
                                             uint64_t end, Segs sg, Ctg c, int32_t rtc, FullOut o) {
+  constexpr uint32_t NREP = 16, REP = 21 * 19 + 2;  // histogram replicas (stride coprime to 32 banks)
+  constexpr uint32_t SLOWCAP = 1024;
   __shared__ uint4 ldsv[FNV];
   __shared__ uint32_t bname[FBW], bop[FBW];
-  __shared__ uint32_t hist[21 * 19 + 21 * 64];
+  __shared__ uint32_t hist[NREP * REP];   // [lane % NREP][nnz * 19 + flag]
+  __shared__ uint32_t rbeh[21 * 64];
   __shared__ uint64_t cpos[FCCAP];
   __shared__ uint32_t cword[FCCAP];
-  __shared__ uint32_t seg0, nsucc, ncl;
+  __shared__ uint32_t slowq[SLOWCAP];     // tile offsets of positions for the exact path
+  __shared__ uint32_t seg0, nsucc, ncl, nslow;
   __shared__ uint64_t e0;
   __shared__ unsigned long long cbase;
   const uint32_t *lds32 = reinterpret_cast<const uint32_t *>(ldsv);
   const uint64_t s0 = (begin & ~15ull) + (uint64_t)blockIdx.x * FTILE;  // 16-aligned tile start
   stage_vec<FNV>(ldsv, U, s0, u_pad);
-  for (uint32_t i = threadIdx.x; i < 21 * 19 + 21 * 64; i += T) hist[i] = 0;
+  for (uint32_t i = threadIdx.x; i < NREP * REP; i += T) hist[i] = 0;
+  for (uint32_t i = threadIdx.x; i < 21 * 64; i += T) rbeh[i] = 0;
   if (threadIdx.x == 0) {
     seg0 = seg_first(sg, s0 > begin ? s0 : begin);
     e0 = sg.end[seg0];
-    nsucc = 0;
-    ncl = 0;
+    nsucc = ncl = nslow = 0;
   }
   __syncthreads();
   for (uint32_t w = threadIdx.x; w < FBW; w += T) {  // byte classes of staged bytes 32w..32w+31
@@ -917,19 +920,56 @@ __global__ __launch_bounds__(T) void k_full(const uint8_t *__restrict__ U, uint6
     bop[w] = bo;
   }
   __syncthreads();
-  Src s{U, lds32, s0, FSN};
-  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  const Src s{U, lds32, s0, FSN};
+  uint32_t *myhist = hist + (threadIdx.x % NREP) * REP;
   uint32_t mysucc = 0;
+  // one position's result into the counters (FullCheck.scala:142-192): Success, unknown, or a
+  // failure counted per (numNonZeroFields, flag) unless it is TooFewFixedBlockBytes alone
+  auto account = [&](uint64_t p, uint32_t r) {
+    if (o.words) o.words[p - begin] = r;
+    if (r & FULL_SUCCESS) {
+      ++mysucc;
+      return;
+    }
+    if (r & FULL_UNKNOWN) {
+      atomicAdd(o.n_unknown, 1ull);
+      atomicMin(o.min_unknown, (unsigned long long)p);
+      return;
+    }
+    uint32_t f = r & 0x7FFFFu;
+    const uint32_t rbe = (r >> N_SHIFT) & 0x3FFu;
+    if (f == 1u && rbe == 0) return;
+    const uint32_t nnz = __popc(f) + (rbe > 0);
+    uint32_t *row = myhist + nnz * 19;
+    while (f) {
+      atomicAdd(&row[__builtin_ctz(f)], 1u);
+      f &= f - 1;
+    }
+    if (rbe > 0 && rbe < 64) atomicAdd(&rbeh[nnz * 64 + rbe], 1u);
+    if (nnz <= 2) {
+      const uint32_t slot = atomicAdd(&ncl, 1u);
+      if (slot < FCCAP) {
+        cpos[slot] = p;
+        cword[slot] = r;
+      } else {
+        const unsigned long long gs = atomicAdd(o.close_n, 1ull);
+        if (gs < o.close_cap) { o.close_pos[gs] = p; o.close_word[gs] = r; }
+      }
+    }
+  };
+  auto where = [&](uint64_t p, uint64_t *total, bool *open) {
+    const uint32_t kseg = p < e0 ? seg0 : seg_index(sg, p, seg0);
+    *total = p < e0 ? e0 : sg.end[kseg];
+    *open = sg.open_last && kseg == sg.n - 1;
+  };
   for (uint32_t step = 0; step < FTILE / (FPL * T); ++step) {
     const uint32_t j = threadIdx.x + step * T;  // this lane's 16 positions: window bytes 16j..16j+15
     const uint4 v0 = ldsv[j], v1 = ldsv[j + 1], v2 = ldsv[j + 2];
     const uint32_t D[12] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w};
-    uint32_t res[FPL];
 #pragma unroll
     for (uint32_t k = 0; k < FPL; ++k) {
       const uint32_t q = 16 * j + k;
       const uint64_t p = s0 + q;
-      res[k] = FULL_SUCCESS;
       if (p < begin || p >= end) continue;
       const uint32_t b = k >> 2, sh = k & 3;
       Fixed x;
@@ -941,61 +981,43 @@ __global__ __launch_bounds__(T) void k_full(const uint8_t *__restrict__ U, uint6
       x.seq_len = (int32_t)__builtin_amdgcn_alignbyte(D[b + 6], D[b + 5], sh);
       x.nidx = (int32_t)__builtin_amdgcn_alignbyte(D[b + 7], D[b + 6], sh);
       x.npos = (int32_t)__builtin_amdgcn_alignbyte(D[b + 8], D[b + 7], sh);
-      const uint32_t kseg = p < e0 ? seg0 : seg_index(sg, p, seg0);
-      const uint64_t total = p < e0 ? e0 : sg.end[kseg];
-      const bool open = sg.open_last && kseg == sg.n - 1;
-      uint32_t r = full_first(s, bname, bop, p, q, x, total, open, c, rtc);
-      if (r == FULL_SLOW) r = full_at_slow(s, p, total, open, c, rtc);
-      res[k] = r;
-      if (o.words) o.words[p - begin] = r;
-      if (r & FULL_UNKNOWN) {
-        atomicAdd(o.n_unknown, 1ull);
-        atomicMin(o.min_unknown, (unsigned long long)p);
-      }
-      if (r & FULL_SUCCESS) ++mysucc;
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < FPL; ++k) {
-      const uint32_t r = res[k];
-      const uint32_t f = r & 0x7FFFFu, rbe = (r >> N_SHIFT) & 0x3FFu;
-      // counted: a failure other than Flags.TooFewFixedBlockBytes alone (FullCheck.scala:143-150)
-      const bool cnt = !(r & (FULL_SUCCESS | FULL_UNKNOWN)) && !(f == 1u && rbe == 0);
-      const uint32_t nnz = __popc(f) + (rbe > 0);
-      uint64_t live = __ballot(cnt);
-      while (live) {  // per distinct numNonZeroFields: 19 flag counts by ballot, one LDS add each
-        const uint32_t v = __builtin_amdgcn_readlane(nnz, (uint32_t)__builtin_ctzll(live));
-        const bool g = cnt && nnz == v;
-        live &= ~__ballot(g);
-        uint32_t mine = 0;
-#pragma unroll
-        for (uint32_t b = 0; b < 19; ++b) {
-          const uint32_t cb = (uint32_t)__popcll(__ballot(g && ((f >> b) & 1u)));
-          mine = lane == b ? cb : mine;
+      uint64_t total;
+      bool open;
+      where(p, &total, &open);
+      const uint32_t r = full_first(s, bname, bop, p, q, x, total, open, c, rtc);
+      if (r == FULL_SLOW) {  // record starts and CIGARs past the window: the balanced pass below
+        const uint32_t qi = atomicAdd(&nslow, 1u);
+        if (qi < SLOWCAP) {
+          slowq[qi] = q;
+          continue;
         }
-        if (lane < 19 && mine) atomicAdd(&hist[v * 19 + lane], mine);
+        account(p, full_at(s, p, total, open, c, rtc));
+        continue;
       }
-      if (cnt && rbe > 0 && rbe < 64) atomicAdd(&hist[21 * 19 + nnz * 64 + rbe], 1u);
-      if (cnt && nnz <= 2) {
-        const uint64_t p = s0 + 16 * j + k;
-        const uint32_t slot = atomicAdd(&ncl, 1u);
-        if (slot < FCCAP) {
-          cpos[slot] = p;
-          cword[slot] = r;
-        } else {
-          const unsigned long long gs = atomicAdd(o.close_n, 1ull);
-          if (gs < o.close_cap) { o.close_pos[gs] = p; o.close_word[gs] = r; }
-        }
-      }
+      account(p, r);
     }
+  }
+  __syncthreads();
+  const uint32_t ns = nslow < SLOWCAP ? nslow : SLOWCAP;
+  for (uint32_t i = threadIdx.x; i < ns; i += T) {
+    const uint64_t p = s0 + slowq[i];
+    uint64_t total;
+    bool open;
+    where(p, &total, &open);
+    account(p, full_at(s, p, total, open, c, rtc));
   }
   if (mysucc) atomicAdd(&nsucc, mysucc);
   __syncthreads();
   const uint32_t nc = ncl < FCCAP ? ncl : FCCAP;
   if (threadIdx.x == 0) cbase = nc ? atomicAdd(o.close_n, (unsigned long long)nc) : 0;
-  for (uint32_t i = threadIdx.x; i < 21 * 19; i += T)
-    if (hist[i]) atomicAdd(&o.counts[i], (unsigned long long)hist[i]);
+  for (uint32_t i = threadIdx.x; i < 21 * 19; i += T) {
+    uint32_t t = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < NREP; ++r) t += hist[r * REP + i];
+    if (t) atomicAdd(&o.counts[i], (unsigned long long)t);
+  }
   for (uint32_t i = threadIdx.x; i < 21 * 64; i += T)
-    if (hist[21 * 19 + i]) atomicAdd(&o.rbe[i], (unsigned long long)hist[21 * 19 + i]);
+    if (rbeh[i]) atomicAdd(&o.rbe[i], (unsigned long long)rbeh[i]);
   if (threadIdx.x == 0 && nsucc) atomicAdd(o.n_success, (unsigned long long)nsucc);
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < nc; i += T) {
@@ -1230,7 +1252,7 @@ __global__ void k_chain_walk(const uint8_t *U, uint64_t first, uint64_t E, uint6
 // wave-uniform; the read-name bytes and the CIGAR ops of each record are tested by all
 // 64 lanes at once (ballots), preserving eager_at's outcome order: the bound checks
 // (unknown / false at the stream end) against the first invalid byte or op before them.
-__device__ uint32_t eager_at_wave(const uint8_t *__restrict__ U, uint64_t p, uint64_t total, bool open, const Ctg &c,
+__device__ uint32_t eager_at_wave(const uint8_t *__restrict__ U, uint64_t p, uint64_t total, bool open, const Ctg c,
                                   int32_t rtc, uint32_t lane) {
   auto word = [&](uint64_t q) -> uint32_t {
     const uint32_t *g = reinterpret_cast<const uint32_t *>(U + (q & ~3ull));
