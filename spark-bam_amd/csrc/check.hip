@@ -783,16 +783,18 @@ struct FullOut {
 // word reads each.  Positions whose first record passes (record starts: the chain must be
 // followed) or whose CIGAR runs past the window are queued and decided by the exact full_at()
 // after the tile's sweep, one per lane (no wave waits on another lane's chain).  Histograms
-// are LDS adds into 16 replicas (lane mod 16, stride coprime to the 32 banks), so lanes
+// are LDS adds into 4 replicas (lane mod 4, stride coprime to the 32 banks), so lanes
 // counting the same (numNonZeroFields, flag) rarely meet on one address; close calls are
 // collected in LDS and appended with one global atomic per workgroup.
 constexpr uint32_t FTILE = 8192;              // positions per workgroup
 constexpr uint32_t FPL = 16;                  // positions per lane and step
-constexpr uint32_t FNV = FTILE / 16 + 64;     // staged 16-byte vectors: tile + 1 KiB look-ahead
+constexpr uint32_t FNV = FTILE / 16 + 256;    // staged 16-byte vectors: tile + 4 KiB look-ahead (chains of
+                                              // 10 short records stay in LDS)
 constexpr uint32_t FSN = FNV * 16;            // staged bytes
 constexpr uint32_t FBW = FSN / 32;            // bitmap words
-constexpr uint32_t FCCAP = 512;               // close calls buffered per workgroup
+constexpr uint32_t FCCAP = 256;               // close calls buffered per workgroup
 constexpr uint32_t FULL_SLOW = 0xFFFFFFFFu;   // "take the exact path" (no valid word has all bits)
+constexpr uint32_t FULL_PASS = 0xFFFFFFFEu;   // the first record passes: the chain decides
 static_assert(FTILE % (FPL * T) == 0 && FSN % 32 == 0 && FSN >= FTILE + 36 + 255 + 16, "full tile layout");
 
 // exact per-byte classes of the 4 bytes of x, as 4 bits (bit k = byte k)
@@ -833,7 +835,7 @@ struct Fixed {  // the 36-byte fixed part of a record (tlen unused by the checke
 
 // The full check's first record at p (window offset q) from its fixed fields, the staged
 // window and its bitmaps: the result word when the first record fails (or at EOF / open-end
-// rules), FULL_SLOW when the exact path must decide.
+// rules), FULL_PASS when it passes, FULL_SLOW when the window cannot decide it.
 __device__ __forceinline__ uint32_t full_first(const Src &s, const uint32_t *bname, const uint32_t *bop, uint64_t p,
                                                uint32_t q, const Fixed &x, uint64_t total, bool open, const Ctg &c,
                                                int32_t rtc) {
@@ -880,17 +882,60 @@ __device__ __forceinline__ uint32_t full_first(const Src &s, const uint32_t *bna
     if (x.seq_len == 0) f |= 1u << 16;  // EmptyMapped(emptySeq, emptyCigar) field swap
     if (nc == 0) f |= 1u << 17;
   }
-  return f ? f : FULL_SLOW;  // a passing first record: follow the chain exactly
+  return f ? f : FULL_PASS;  // a passing first record: the chain decides
 }
 
-__global__ __launch_bounds__(T) void k_full(const uint8_t *__restrict__ U, uint64_t u_pad, uint64_t begin,
+__device__ __forceinline__ Fixed fixed_at(const uint32_t *lds32, uint32_t q) {
+  const uint32_t *d = lds32 + (q >> 2);
+  const uint32_t k = q & 3;
+  Fixed x;
+  x.rem = (int32_t)__builtin_amdgcn_alignbyte(d[1], d[0], k);
+  x.idx = (int32_t)__builtin_amdgcn_alignbyte(d[2], d[1], k);
+  x.pos = (int32_t)__builtin_amdgcn_alignbyte(d[3], d[2], k);
+  x.bmn = __builtin_amdgcn_alignbyte(d[4], d[3], k);
+  x.fnc = __builtin_amdgcn_alignbyte(d[5], d[4], k);
+  x.seq_len = (int32_t)__builtin_amdgcn_alignbyte(d[6], d[5], k);
+  x.nidx = (int32_t)__builtin_amdgcn_alignbyte(d[7], d[6], k);
+  x.npos = (int32_t)__builtin_amdgcn_alignbyte(d[8], d[7], k);
+  return x;
+}
+
+// full.Checker.apply at p through the window (full/Checker.scala:22-184): record n of the
+// chain sits at the previous record's nominal end, so while records stay normal (their name
+// and CIGAR end at or before the nominal end) and inside the window, each one is the
+// first-record check at its own start (full_first), with readsBeforeError = n and the clean
+// end rule (the stream ends exactly at a record boundary after n > 0 records) in between.
+// Anything else -- an abnormal record, a nominal end past the stream, a record the window
+// does not hold -- returns FULL_SLOW for the exact full_at().
+__device__ uint32_t chain_full(const Src &s, const uint32_t *bname, const uint32_t *bop, uint64_t p, uint64_t total,
+                               bool open, const Ctg &c, int32_t rtc) {
+  uint64_t q = p;
+  for (uint32_t n = 0;; ++n) {
+    if ((int32_t)n == rtc) return FULL_SUCCESS | (n << N_SHIFT);
+    if (q + 36 > total) {
+      if (open) return FULL_UNKNOWN;
+      return n > 0 && q == total ? FULL_SUCCESS | (n << N_SHIFT) : 1u | (n << N_SHIFT);
+    }
+    if (q - s.s0 + 36 + 255 + 8 > FSN) return FULL_SLOW;  // fixed fields + the longest name staged
+    const uint32_t qw = (uint32_t)(q - s.s0);
+    const Fixed x = fixed_at(s.lds32, qw);
+    const uint32_t r = full_first(s, bname, bop, q, qw, x, total, open, c, 1);
+    if (r == FULL_SLOW || r == FULL_UNKNOWN) return r;
+    if (r != FULL_PASS) return r | (n << N_SHIFT);
+    const uint64_t nominal = q + 4 + (int64_t)x.rem;
+    const uint64_t cur = q + 36 + (x.bmn & 0xff) + 4ull * (x.fnc & 0xffff);
+    if ((int64_t)(nominal - cur) < 0 || nominal > total) return FULL_SLOW;
+    q = nominal;
+  }
+}
+
+__global__ __launch_bounds__(T, 5) void k_full(const uint8_t *__restrict__ U, uint64_t u_pad, uint64_t begin,
                                             uint64_t end, Segs sg, Ctg c, int32_t rtc, FullOut o) {
-  constexpr uint32_t NREP = 16, REP = 21 * 19 + 2;  // histogram replicas (stride coprime to 32 banks)
-  constexpr uint32_t SLOWCAP = 1024;
+  constexpr uint32_t NREP = 4, REP = 21 * 19 + 2;  // histogram replicas (stride coprime to 32 banks)
+  constexpr uint32_t SLOWCAP = 512;
   __shared__ uint4 ldsv[FNV];
   __shared__ uint32_t bname[FBW], bop[FBW];
   __shared__ uint32_t hist[NREP * REP];   // [lane % NREP][nnz * 19 + flag]
-  __shared__ uint32_t rbeh[21 * 64];
   __shared__ uint64_t cpos[FCCAP];
   __shared__ uint32_t cword[FCCAP];
   __shared__ uint32_t slowq[SLOWCAP];     // tile offsets of positions for the exact path
@@ -901,7 +946,6 @@ __global__ __launch_bounds__(T) void k_full(const uint8_t *__restrict__ U, uint6
   const uint64_t s0 = (begin & ~15ull) + (uint64_t)blockIdx.x * FTILE;  // 16-aligned tile start
   stage_vec<FNV>(ldsv, U, s0, u_pad);
   for (uint32_t i = threadIdx.x; i < NREP * REP; i += T) hist[i] = 0;
-  for (uint32_t i = threadIdx.x; i < 21 * 64; i += T) rbeh[i] = 0;
   if (threadIdx.x == 0) {
     seg0 = seg_first(sg, s0 > begin ? s0 : begin);
     e0 = sg.end[seg0];
@@ -940,12 +984,15 @@ __global__ __launch_bounds__(T) void k_full(const uint8_t *__restrict__ U, uint6
     const uint32_t rbe = (r >> N_SHIFT) & 0x3FFu;
     if (f == 1u && rbe == 0) return;
     const uint32_t nnz = __popc(f) + (rbe > 0);
+#ifdef SBH_FULL_NOHIST  // A/B: the check without its aggregation (tools/full_ab.py)
+    if (nnz != 77) return;
+#endif
     uint32_t *row = myhist + nnz * 19;
     while (f) {
       atomicAdd(&row[__builtin_ctz(f)], 1u);
       f &= f - 1;
     }
-    if (rbe > 0 && rbe < 64) atomicAdd(&rbeh[nnz * 64 + rbe], 1u);
+    if (rbe > 0 && rbe < 64) atomicAdd(&o.rbe[nnz * 64 + rbe], 1ull);  // rare: positions past a record
     if (nnz <= 2) {
       const uint32_t slot = atomicAdd(&ncl, 1u);
       if (slot < FCCAP) {
@@ -985,13 +1032,14 @@ __global__ __launch_bounds__(T) void k_full(const uint8_t *__restrict__ U, uint6
       bool open;
       where(p, &total, &open);
       const uint32_t r = full_first(s, bname, bop, p, q, x, total, open, c, rtc);
-      if (r == FULL_SLOW) {  // record starts and CIGARs past the window: the balanced pass below
+      if (r == FULL_SLOW || r == FULL_PASS) {  // record starts, long CIGARs: the balanced pass below
         const uint32_t qi = atomicAdd(&nslow, 1u);
         if (qi < SLOWCAP) {
           slowq[qi] = q;
           continue;
         }
-        account(p, full_at(s, p, total, open, c, rtc));
+        const uint32_t rc = chain_full(s, bname, bop, p, total, open, c, rtc);
+        account(p, rc == FULL_SLOW ? full_at(s, p, total, open, c, rtc) : rc);
         continue;
       }
       account(p, r);
@@ -1004,7 +1052,8 @@ __global__ __launch_bounds__(T) void k_full(const uint8_t *__restrict__ U, uint6
     uint64_t total;
     bool open;
     where(p, &total, &open);
-    account(p, full_at(s, p, total, open, c, rtc));
+    const uint32_t rc = chain_full(s, bname, bop, p, total, open, c, rtc);
+    account(p, rc == FULL_SLOW ? full_at(s, p, total, open, c, rtc) : rc);
   }
   if (mysucc) atomicAdd(&nsucc, mysucc);
   __syncthreads();
@@ -1016,8 +1065,6 @@ __global__ __launch_bounds__(T) void k_full(const uint8_t *__restrict__ U, uint6
     for (uint32_t r = 0; r < NREP; ++r) t += hist[r * REP + i];
     if (t) atomicAdd(&o.counts[i], (unsigned long long)t);
   }
-  for (uint32_t i = threadIdx.x; i < 21 * 64; i += T)
-    if (rbeh[i]) atomicAdd(&o.rbe[i], (unsigned long long)rbeh[i]);
   if (threadIdx.x == 0 && nsucc) atomicAdd(o.n_success, (unsigned long long)nsucc);
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < nc; i += T) {

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""Time sbh_check_full on a synthetic short-read shard for a few readsToCheck values
-(where does k_full's time go: the first record of every position, or the chains of
-the positions that pass it?).  usage: python tools/full_ab.py [--records N]"""
+"""A/B timing of sbh_check_full (k_full) on a synthetic short-read shard: the library given by
+SBH_LIB_PATH (default: the in-tree build), a few readsToCheck values.
+usage: SBH_LIB_PATH=build/variants/lib_fnh.so python tools/full_ab.py [--records N]"""
 import argparse
 import os
 import sys
@@ -15,6 +15,7 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--records", type=int, default=2_000_000)
+    ap.add_argument("--rtc", default="10,1")
     a = ap.parse_args()
     import synth
     from __graft_entry__ import load_package
@@ -27,15 +28,16 @@ def main():
         sh.set_contigs(cl)
         sh.index(0)
         sh.inflate()
-        for rtc in (10, 2, 1, 0):
+        for rtc in (int(x) for x in a.rtc.split(",")):
             best = None
             for _ in range(3):
                 t0 = time.perf_counter()
                 r = sh.check_full(0, sh.flat_size, reads_to_check=rtc, close_cap=1 << 10)
                 dt = time.perf_counter() - t0
                 best = dt if best is None else min(best, dt)
-            print(f"rtc {rtc}: {best * 1e3:.2f} ms for {sh.flat_size} positions "
-                  f"({sh.flat_size / best / 1e9:.1f} GB/s), success {r['n_success']}", flush=True)
+            print(f"{os.path.basename(os.environ.get('SBH_LIB_PATH', 'main'))} rtc {rtc}: {best * 1e3:.2f} ms for "
+                  f"{sh.flat_size} positions ({sh.flat_size / best / 1e9:.1f} GB/s), success {r['n_success']}",
+                  flush=True)
 
 
 if __name__ == "__main__":
