@@ -349,9 +349,7 @@ def main():
                 "traffic_source": traffic_src,
                 "alg_bytes_per_step": int(alg_bytes),
                 "alg_units": dom_units,
-                "limiter": "not HBM: k_huff ~57% VALU-issue busy, the rest LDS latency of the per-lane decode "
-                           "chains and the repair round (max sync distance over 256 lanes); k_lz ~80% VALU-issue "
-                           "bound (pointer slot pass + chase); PMC in profiles/",
+                "limiter": limiter_text(dom),
                 "path": {  # B_alg = C + U (inflate write) + U (checker read) + U/8 (bitmap) per step
                     "alg_bytes_per_step": int(sum(own_sizes) / world + 2.125 * flat_bytes),
                     "achieved": round((sum(own_sizes) / world + 2.125 * flat_bytes) * args.steps / elapsed / 1e9, 2),
@@ -376,6 +374,24 @@ def main():
         log(f"STITCH CHECK FAILED: records {total_records} true {total_true} expected {expect}; "
             f"stitch {stitch}")
         sys.exit(3)
+
+
+def limiter_text(kernel):
+    """What bounds `kernel`, from the committed counter ratios (tools/pmc_derived.py over the
+    rocprofv3 passes of tools/pmc_collect.sh)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc", "derived.json")))
+    if not files:
+        return "no counter data committed"
+    with open(files[-1]) as fh:
+        k = json.load(fh)["kernels"].get(kernel)
+    if not k:
+        return f"no counter data for {kernel}"
+    return (f"not HBM: {kernel} issues on {100 * k['issuing_frac']:.0f}% of wave cycles and is parked on "
+            f"s_waitcnt/barrier {100 * k['parked_waitcnt_barrier_frac']:.0f}% (LDS round trips of the per-lane "
+            f"decode chains, repair-round barriers), VALU active {100 * k['valu_active_frac']:.0f}%, LDS bank "
+            f"conflicts {100 * k['lds_bank_conflict_frac']:.0f}% of LDS-array cycles (random table lookups) -- "
+            f"{os.path.relpath(files[-1], ROOT)} from sq_lds.csv / sq_wait.csv")
 
 
 def host_cores():
