@@ -53,11 +53,15 @@ def main():
     a = ap.parse_args()
     if a.child is not None:
         return child(a.child, a.records, a.reps)
-    libs = [""] + (a.variants or sorted(glob.glob(os.path.join(ROOT, "spark-bam_amd/build/variants/lib_*.so"))))
+    vdir = os.path.join(ROOT, "spark-bam_amd/build/variants")
+    named = [v if v.endswith(".so") else os.path.join(vdir, f"lib_{v}.so") for v in a.variants]
+    libs = [""] + (named or sorted(glob.glob(os.path.join(vdir, "lib_*.so"))))
     for lib in libs:
         r = subprocess.run([sys.executable, __file__, "--child", lib, "--records", str(a.records),
                             "--reps", str(a.reps)], capture_output=True, text=True, timeout=900)
         print(r.stdout.strip() or r.stderr[-2000:], flush=True)
+        if r.stderr and r.stdout:  # probe variants print their counters on stderr/stdout
+            print(r.stderr[-4000:], flush=True)
 
 
 if __name__ == "__main__":
