@@ -1,12 +1,20 @@
 // deflate.hip -- BGZF writer on CDNA4 (htsjdk-rewrite's block compressor).
 //
 // The flat uncompressed stream is already resident in HBM (an inflated shard, or bytes the
-// caller uploaded).  k_deflate: four 65498-byte pieces per wave, each runs the
-// greedy-LZ77 / fixed-Huffman coder of deflate_core.h, one 4 KiB segment per lane, into
-// the member's 64 KiB slot (hash heads and segment streams in HBM scratch) and records the
-// member size; k_footer adds CRC32 + ISIZE.  The host turns
-// the sizes into file offsets; k_gather then packs the slots into the contiguous BGZF file,
-// one workgroup per member with 16-byte stores where the destination allows.
+// caller uploaded).  Members are coded in batches of up to DEFLATE_BATCH 65498-byte pieces,
+// one workgroup (4 waves) per member, giving exactly the bytes of deflate_core.h's serial
+// definition (tools/deflate_host.cpp):
+//  k_prev     the hash chains prev[] of the member: each wave links a quarter of it, 64
+//             positions a step (the step's (hash, lane) keys bitonic-sorted across the wave:
+//             same-hash neighbours link, the first takes the wave's LDS head table entry),
+//             then each quarter's first occurrence of a hash links to the quarters before;
+//  k_deflate  the member in LDS; each lane parses one 256-byte segment once into tokens
+//             (batch scratch) and the member's histogram (LDS atomics); the dynamic Huffman
+//             codes (symbol ranks over all threads, the two trees on two waves, the header on
+//             one lane); the lanes' bit counts and a workgroup scan give bit offsets; the
+//             bits are written as whole dwords into the member's 64 KiB slot (a lane's first
+//             and last dword, shared with its neighbours, through atomicOr);
+//  k_footer   CRC32 + ISIZE;  k_gather  packs the slots at the host-computed file offsets.
 #define SBH_HD __host__ __device__
 #include "deflate_core.h"
 #include "sbh_internal.h"
@@ -16,61 +24,285 @@ namespace {
 
 using namespace sbh_deflate;
 
-// Four members per wave, one 4 KiB segment per lane (deflate_core.h seg_encode), the
-// segment streams bit-concatenated in the zeroed slot: bytes a lane shares a dword with a
-// neighbour (its first and last four) go through atomicOr, the rest are plain stores.
-__global__ __launch_bounds__(64) void k_deflate(const uint8_t *__restrict__ src, uint64_t n, uint64_t nblocks,
-                                                uint8_t *__restrict__ slots, uint8_t *__restrict__ segbuf,
-                                                uint16_t *__restrict__ heads, uint32_t *__restrict__ sizes) {
-  const uint32_t lane = threadIdx.x, g = lane / NSEG, i = lane % NSEG;
-  const uint64_t b = (uint64_t)blockIdx.x * (64 / NSEG) + g;
-  const bool live_blk = b < nblocks;
+constexpr uint32_t QLEN = 16384;  // positions per wave in k_prev (a quarter of a member)
+static_assert(4 * QLEN >= PAYLOAD, "four quarters cover a member");
+constexpr uint32_t PREV_STRIDE = 65536;  // u16 prev[] entries per member in the batch scratch
+constexpr uint32_t TOK_STRIDE = LSEG * NLANE;  // u32 tokens per member in the batch scratch
+
+// v from lane ^ M: quad DPP for 1 and 2, ds_swizzle (bit mode, within 32 lanes) for 4..16,
+// ds_bpermute for 32.
+template <uint32_t M>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v) {
+  if constexpr (M == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false);
+  else if constexpr (M == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false);
+  else if constexpr (M < 32) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (int)((M << 10) | 0x1f));
+  else return (uint32_t)__shfl_xor((int)v, (int)M);
+}
+template <uint32_t SIZE, uint32_t STRIDE>
+__device__ __forceinline__ uint32_t bitonic_step(uint32_t k, uint32_t lane) {
+  const uint32_t o = xor_lane<STRIDE>(k);
+  const bool up = (lane & SIZE) == 0, lower = (lane & STRIDE) == 0;
+  return (lower == up) ? (k < o ? k : o) : (k > o ? k : o);
+}
+// ascending sort of one key per lane across the wave
+__device__ __forceinline__ uint32_t bitonic64(uint32_t k, uint32_t lane) {
+  k = bitonic_step<2, 1>(k, lane);
+  k = bitonic_step<4, 2>(k, lane), k = bitonic_step<4, 1>(k, lane);
+  k = bitonic_step<8, 4>(k, lane), k = bitonic_step<8, 2>(k, lane), k = bitonic_step<8, 1>(k, lane);
+  k = bitonic_step<16, 8>(k, lane), k = bitonic_step<16, 4>(k, lane), k = bitonic_step<16, 2>(k, lane);
+  k = bitonic_step<16, 1>(k, lane);
+  k = bitonic_step<32, 16>(k, lane), k = bitonic_step<32, 8>(k, lane), k = bitonic_step<32, 4>(k, lane);
+  k = bitonic_step<32, 2>(k, lane), k = bitonic_step<32, 1>(k, lane);
+  k = bitonic_step<64, 32>(k, lane), k = bitonic_step<64, 16>(k, lane), k = bitonic_step<64, 8>(k, lane);
+  k = bitonic_step<64, 4>(k, lane), k = bitonic_step<64, 2>(k, lane), k = bitonic_step<64, 1>(k, lane);
+  return k;
+}
+
+// prev[] of one member per workgroup.  Each wave links its quarter 64 positions a step: the
+// step's (hash, lane) keys are sorted across the wave, so a position's predecessor inside
+// the step is its sorted neighbour; the first of a hash in the step takes the wave's head
+// table entry, the last one replaces it.  Then the first occurrence of each hash in a
+// quarter is linked to the latest one in the quarters before it.
+__global__ __launch_bounds__(256) void k_prev(const uint8_t *__restrict__ src, uint64_t n, uint64_t b0,
+                                              uint64_t nblocks, uint16_t *__restrict__ prevg) {
+  __shared__ uint16_t head[4][HN];   // latest position of each hash in the wave's quarter so far
+  __shared__ uint16_t first[4][HN];  // first position of each hash in the quarter
+  const uint32_t t = threadIdx.x, w = t / WAVE, lane = t % WAVE;
+  const uint64_t b = b0 + blockIdx.x;
+  if (b >= nblocks) return;
   const uint64_t s0 = b * PAYLOAD;
-  const uint32_t len = live_blk ? (uint32_t)((n - s0) < PAYLOAD ? (n - s0) : PAYLOAD) : 0;
-  const uint32_t nseg = (len + SEG - 1) / SEG;
-  const uint32_t lo = i * SEG, slen = i < nseg ? ((len - lo) < SEG ? len - lo : SEG) : 0;
-  uint8_t *buf = segbuf + (b * NSEG + i) * SEGCAP;
-  uint32_t nbits = 0;
-  if (slen) nbits = seg_encode(src + s0 + lo, slen, i + 1 == nseg, buf, heads + (b * NSEG + i) * SHSIZE);
-  uint32_t off = 0, tot = 0;
-  for (uint32_t k = 0; k < NSEG; ++k) {
-    const uint32_t v = (uint32_t)__shfl((int)nbits, (int)(g * NSEG + k));
-    off += k < i ? v : 0u;
-    tot += v;
+  const uint32_t len = (uint32_t)((n - s0) < PAYLOAD ? (n - s0) : PAYLOAD);
+  const uint8_t *m = src + s0;
+  uint16_t *pv = prevg + (uint64_t)blockIdx.x * PREV_STRIDE;
+  for (uint32_t i = t; i < 4 * HN; i += 256) {
+    (&head[0][0])[i] = NONE16;
+    (&first[0][0])[i] = NONE16;
   }
-  if (!live_blk) return;
-  uint8_t *slot = slots + b * SLOT;
-  uint8_t *d0 = slot + 18;
-  uint32_t dsize = (tot + 7) / 8;
-  if (dsize <= BUDGET) {
-    if (slen) {
-      const uint32_t first = off / 8, last = (off + nbits - 1) / 8;
-      for (uint32_t j = first; j <= last; ++j) {
-        const uint8_t v = seg_byte(buf, nbits, off, j);
-        if (j < first + 4 || j + 4 > last) {
-          const uintptr_t a = (uintptr_t)(d0 + j);
-          if (v) atomicOr(reinterpret_cast<uint32_t *>(a & ~(uintptr_t)3), (uint32_t)v << (8 * (a & 3)));
-        } else {
-          d0[j] = v;
-        }
+  __syncthreads();
+  const uint32_t hp = len >= 3 ? len - 2 : 0;  // positions with a hash (p + 3 <= len)
+  const uint32_t qlo = w * QLEN, qhi = qlo + QLEN < len ? qlo + QLEN : len;
+  // the step's three bytes are loaded one step ahead
+  uint32_t c0 = 0, c1 = 0, c2 = 0;
+  if (qlo + lane < hp) c0 = m[qlo + lane], c1 = m[qlo + lane + 1], c2 = m[qlo + lane + 2];
+  for (uint32_t base = qlo; base < qhi; base += WAVE) {
+    const uint32_t p = base + lane;
+    const bool live = p < hp && p < qhi;
+    const uint32_t v = c0 | c1 << 8 | c2 << 16;
+    const uint32_t np = p + WAVE;
+    if (np < hp && np < qhi) c0 = m[np], c1 = m[np + 1], c2 = m[np + 2];
+    // dead lanes get keys past every hash, so they sort last
+    const uint32_t h = live ? (v * 2654435761u) >> (32 - HB) : HN + lane;
+    const uint32_t k = bitonic64(h << 6 | lane, lane);
+    const uint32_t kp = (uint32_t)__shfl_up((int)k, 1), kn = (uint32_t)__shfl_down((int)k, 1);
+    const uint32_t hs = k >> 6, ps = base + (k & 63);
+    if (hs < HN) {
+      uint16_t pr;
+      if (lane > 0 && (kp >> 6) == hs) {
+        pr = (uint16_t)(base + (kp & 63));
+      } else {
+        pr = head[w][hs];
+        if (pr == NONE16) first[w][hs] = (uint16_t)ps;
       }
+      pv[ps] = pr;
+      if (lane == WAVE - 1 || (kn >> 6) != hs) head[w][hs] = (uint16_t)ps;
+    } else if (ps < qhi) {
+      pv[ps] = NONE16;
+    }
+  }
+  __syncthreads();
+  // a quarter's first occurrence of h links to the latest h of the quarters before it
+  for (uint32_t i = t + HN; i < 4 * HN; i += 256) {
+    const uint32_t q = i / HN, h = i % HN;
+    const uint16_t f = first[q][h];
+    if (f == NONE16) continue;
+    for (int32_t r = (int32_t)q - 1; r >= 0; --r) {
+      const uint16_t l = head[r][h];
+      if (l != NONE16) {
+        pv[f] = l;
+        break;
+      }
+    }
+  }
+}
+
+struct DeflateLds {
+  uint32_t src[(SLOT + 8) / 4];  // the member's bytes, zero padded
+  uint32_t fl[286], fd[30];      // token histogram (fl[256]: the end-of-block code)
+  Codes cd;
+  uint8_t hdr[HDR_CAP];
+  HuffWork wl, wd;
+  HdrWork H;
+  uint32_t wsum[4];
+  uint32_t hbits;
+};
+static_assert(sizeof(DeflateLds) <= 80 * 1024, "two workgroups per CU");
+
+// Writes a lane's bit range into the slot as dwords: the first and last dword (shared with
+// the neighbouring lanes' ranges) through atomicOr into the zeroed slot, the rest as stores.
+struct DwordBits {
+  uint32_t *base;
+  uint32_t wi, nb;
+  uint64_t acc;
+  bool first;
+  __device__ void put(uint32_t v, uint32_t k) {  // k <= 24
+    acc |= (uint64_t)v << nb;
+    nb += k;
+    if (nb >= 32) {
+      if (first) {
+        atomicOr(base + wi, (uint32_t)acc);
+        first = false;
+      } else {
+        base[wi] = (uint32_t)acc;
+      }
+      ++wi;
+      acc >>= 32;
+      nb -= 32;
+    }
+  }
+  __device__ void put48(uint64_t v, uint32_t k) {
+    put((uint32_t)v & 0xffffffu, k < 24 ? k : 24);
+    if (k > 24) put((uint32_t)(v >> 24), k - 24);
+  }
+  __device__ void finish() {
+    if (nb) atomicOr(base + wi, (uint32_t)acc);
+  }
+};
+
+__global__ __launch_bounds__(256) void k_deflate(const uint8_t *__restrict__ src, uint64_t n, uint64_t b0,
+                                                 uint64_t nblocks, const uint16_t *__restrict__ prevg,
+                                                 uint32_t *__restrict__ toks, uint8_t *__restrict__ slots,
+                                                 uint32_t *__restrict__ sizes) {
+  __shared__ DeflateLds S;
+  const uint32_t t = threadIdx.x, w = t / WAVE, lane = t % WAVE;
+  const uint64_t b = b0 + blockIdx.x;
+  if (b >= nblocks) return;
+  const uint64_t s0 = b * PAYLOAD;
+  const uint32_t len = (uint32_t)((n - s0) < PAYLOAD ? (n - s0) : PAYLOAD);
+  const uint16_t *pv = prevg + (uint64_t)blockIdx.x * PREV_STRIDE;
+  uint32_t *tk = toks + (uint64_t)blockIdx.x * TOK_STRIDE + t;  // token j of this lane: tk[j * NLANE]
+  uint8_t *slot = slots + (uint64_t)blockIdx.x * SLOT;
+
+  // the member into LDS: aligned source dwords (never past the buffer's last dword that
+  // holds data), realigned with alignbyte, bytes past the member zeroed
+  {
+    const uint8_t *m = src + s0;
+    const uintptr_t a0 = (uintptr_t)m & ~(uintptr_t)3;
+    const uint32_t sh = (uint32_t)((uintptr_t)m & 3);
+    const uintptr_t end = (uintptr_t)m + len;  // first address past the member
+    const uintptr_t lim = (uintptr_t)(src + n);  // first address past the buffer
+    for (uint32_t j = t; j < (SLOT + 8) / 4; j += 256) {
+      uint32_t v = 0;
+      if (4 * j < len) {
+        const uintptr_t a = a0 + 4 * (uintptr_t)j;
+        const uint32_t lo = *reinterpret_cast<const uint32_t *>(a);
+        const uint32_t hi = a + 4 < lim ? *reinterpret_cast<const uint32_t *>(a + 4) : 0u;
+        v = __builtin_amdgcn_alignbyte(hi, lo, sh);
+        const uintptr_t p = (uintptr_t)m + 4 * (uintptr_t)j;  // first byte of this dword
+        if (p + 4 > end) v &= (uint32_t)((1ull << (8 * (end - p))) - 1);
+      }
+      S.src[j] = v;
+    }
+    for (uint32_t i = t; i < 286 + 30; i += 256) {
+      if (i < 286) S.fl[i] = i == 256 ? 1u : 0u;
+      else S.fd[i - 286] = 0;
+    }
+  }
+  __syncthreads();
+  const auto ld = [&](uint32_t i) -> uint64_t {  // 8 bytes from byte i
+    const uint32_t a = i >> 2, r = i & 3;
+    const uint32_t x0 = S.src[a], x1 = S.src[a + 1], x2 = S.src[a + 2];
+    return (uint64_t)__builtin_amdgcn_alignbyte(x2, x1, r) << 32 | __builtin_amdgcn_alignbyte(x1, x0, r);
+  };
+  const auto prv = [&](uint32_t i) -> uint32_t { return pv[i]; };
+  const uint32_t lo = t * LSEG, hi = lo + LSEG < len ? lo + LSEG : len;
+  const uint32_t last_seg = (len - 1) / LSEG;
+
+  // (1) the segment's tokens (kept in the batch scratch) and the member's histogram
+  uint32_t ntok = 0;
+  if (lo < len)
+    parse_seg(ld, prv, lo, hi, [&](uint32_t tok) {
+      tk[(ntok++) * NLANE] = tok;
+      uint32_t ls;
+      int32_t ds;
+      tok_syms(tok, &ls, &ds);
+      atomicAdd(&S.fl[ls], 1u);
+      if (ds >= 0) atomicAdd(&S.fd[ds], 1u);
+    });
+  __syncthreads();
+  for (uint32_t i = t; i < 286 + 30; i += 256) {
+    if (i < 286) {
+      if (S.fl[i]) S.wl.sym[huff_rank(S.fl, 286, i)] = (uint16_t)i;
+    } else if (S.fd[i - 286]) {
+      S.wd.sym[huff_rank(S.fd, 30, i - 286)] = (uint16_t)(i - 286);
+    }
+  }
+  __syncthreads();
+  if (t == 0) huff_tree(S.fl, 286, 15, S.H.ll, S.wl);
+  if (t == WAVE) huff_tree(S.fd, 30, 15, S.H.dl, S.wd);
+  __syncthreads();
+  if (t == 0) S.hbits = build_header(S.H, S.wl, S.cd, S.hdr);
+  __syncthreads();
+
+  // (2) bit counts and offsets
+  uint32_t nbits = 0;
+  for (uint32_t j = 0; j < ntok; ++j) {
+    uint64_t v;
+    nbits += tok_bits(tk[j * NLANE], S.cd, &v);
+  }
+  const uint32_t hbits = S.hbits;
+  if (t == 0) nbits += hbits;
+  if (t == last_seg) nbits += S.cd.lit[256] >> 16;
+  uint32_t x = nbits;
+  for (uint32_t d = 1; d < (uint32_t)WAVE; d <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, d);
+    if (lane >= d) x += y;
+  }
+  if (lane == WAVE - 1) S.wsum[w] = x;
+  __syncthreads();
+  uint32_t off = x - nbits, total = 0;
+  for (uint32_t k = 0; k < 4; ++k) {
+    off += k < w ? S.wsum[k] : 0u;
+    total += S.wsum[k];
+  }
+  uint32_t dsize = (total + 7) / 8;
+  uint32_t *words = reinterpret_cast<uint32_t *>(slot);
+  if (dsize <= BUDGET) {
+    // (3) the bits: zero the data dwords first (atomicOr targets), then write
+    const uint32_t wend = (18 + dsize + 3) / 4;
+    for (uint32_t i = 4 + t; i < wend; i += 256) words[i] = 0;
+    __syncthreads();
+    if (nbits) {
+      const uint32_t bit0 = 8 * 18 + off;
+      DwordBits o{words, bit0 / 32, bit0 % 32, 0, true};
+      if (t == 0)
+        for (uint32_t i = 0; i < hbits; i += 8) o.put(S.hdr[i / 8], hbits - i < 8 ? hbits - i : 8);
+      for (uint32_t j = 0; j < ntok; ++j) {
+        uint64_t v;
+        const uint32_t k = tok_bits(tk[j * NLANE], S.cd, &v);
+        o.put48(v, k);
+      }
+      if (t == last_seg) o.put(S.cd.lit[256] & 0xffff, S.cd.lit[256] >> 16);
+      o.finish();
     }
   } else {
     dsize = stored_dsize(len);
-    if (i == 0) put_stored_head(d0, len);
-    for (uint32_t k = 0; k < slen; ++k) d0[5 + lo + k] = src[s0 + lo + k];
+    uint8_t *d0 = slot + 18;
+    if (t == 0) put_stored_head(d0, len);
+    for (uint32_t i = t; i < len; i += 256) d0[5 + i] = (uint8_t)(S.src[i >> 2] >> (8 * (i & 3)));
   }
-  if (i == 0) {
+  __syncthreads();
+  if (t == 0) {
     put_header(slot, 18 + dsize + 8);
-    sizes[b] = 18 + dsize + 8;
+    sizes[blockIdx.x] = 18 + dsize + 8;
   }
 }
 
 // Footer: CRC32 (one wave per member, 1 KiB per lane chained with the GF(2) matrix of 1024
 // zero bytes, as in crc.hip) and ISIZE, at the member's end.
 constexpr uint32_t CSEG = 1024;
-__global__ __launch_bounds__(256) void k_footer(const uint8_t *__restrict__ src, uint64_t n, uint64_t nblocks,
-                                                uint8_t *__restrict__ slots, const uint32_t *__restrict__ sizes) {
+__global__ __launch_bounds__(256) void k_footer(const uint8_t *__restrict__ src, uint64_t n, uint64_t b0,
+                                                uint64_t nblocks, uint32_t nbatch, uint8_t *__restrict__ slots,
+                                                const uint32_t *__restrict__ sizes) {
   __shared__ uint32_t tab[256];
   __shared__ uint32_t T[32];
   const uint32_t t = threadIdx.x, lane = t & (WAVE - 1);
@@ -86,8 +318,9 @@ __global__ __launch_bounds__(256) void k_footer(const uint8_t *__restrict__ src,
     T[t] = s;
   }
   __syncthreads();
-  const uint64_t b = (uint64_t)blockIdx.x * (blockDim.x / WAVE) + t / WAVE;
-  if (b >= nblocks) return;
+  const uint32_t j = blockIdx.x * (blockDim.x / WAVE) + t / WAVE;  // member within the batch
+  const uint64_t b = b0 + j;
+  if (j >= nbatch || b >= nblocks) return;
   const uint64_t s0 = b * PAYLOAD;
   const uint32_t len = (uint32_t)((n - s0) < PAYLOAD ? (n - s0) : PAYLOAD);
   const uint8_t *p = src + s0;
@@ -99,13 +332,13 @@ __global__ __launch_bounds__(256) void k_footer(const uint8_t *__restrict__ src,
   for (uint32_t q = 0; q < nseg; ++q) {
     const uint32_t cq = (uint32_t)__shfl((int)c, (int)q);
     uint32_t r = 0;
-    for (uint32_t j = 0; j < 32; ++j)
-      if ((s >> j) & 1u) r ^= T[j];
+    for (uint32_t i = 0; i < 32; ++i)
+      if ((s >> i) & 1u) r ^= T[i];
     s = r ^ cq;
   }
   if (lane == 0) {
     for (uint32_t k = nseg * CSEG; k < len; ++k) s = tab[(s ^ p[k]) & 0xff] ^ (s >> 8);
-    uint8_t *f = slots + b * SLOT + sizes[b] - 8;
+    uint8_t *f = slots + (uint64_t)j * SLOT + sizes[j] - 8;
     put_le32(f, s ^ 0xffffffffu);
     put_le32(f + 4, len);
   }
@@ -139,16 +372,14 @@ __global__ __launch_bounds__(256) void k_gather(const uint8_t *__restrict__ slot
 
 uint64_t deflate_nblocks(uint64_t n) { return (n + PAYLOAD - 1) / PAYLOAD; }
 
-hipError_t launch_deflate(const uint8_t *src, uint64_t n, uint8_t *slots, uint8_t *segbuf, uint16_t *heads,
-                          uint32_t *sizes, hipStream_t st) {
+hipError_t launch_deflate(const uint8_t *src, uint64_t n, uint64_t b0, uint32_t nbatch, uint16_t *prev,
+                          uint32_t *toks, uint8_t *slots, uint32_t *sizes, hipStream_t st) {
   const uint64_t nb = deflate_nblocks(n);
-  if (!nb) return hipSuccess;
-  hipError_t e = hipMemsetAsync(heads, 0, nb * NSEG * SHSIZE * sizeof(uint16_t), st);
-  if (e == hipSuccess) e = hipMemsetAsync(slots, 0, nb * SLOT, st);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_deflate, dim3((uint32_t)((nb + 3) / 4)), dim3(64), 0, st, src, n, nb, slots, segbuf, heads,
-                     sizes);
-  hipLaunchKernelGGL(k_footer, dim3((uint32_t)((nb + 3) / 4)), dim3(256), 0, st, src, n, nb, slots, sizes);
+  if (!nbatch || b0 >= nb) return hipSuccess;
+  if (nbatch > DEFLATE_BATCH || b0 + nbatch > nb) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_prev, dim3(nbatch), dim3(256), 0, st, src, n, b0, nb, prev);
+  hipLaunchKernelGGL(k_deflate, dim3(nbatch), dim3(256), 0, st, src, n, b0, nb, prev, toks, slots, sizes);
+  hipLaunchKernelGGL(k_footer, dim3((nbatch + 3) / 4), dim3(256), 0, st, src, n, b0, nb, nbatch, slots, sizes);
   return hipGetLastError();
 }
 

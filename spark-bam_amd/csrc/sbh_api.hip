@@ -1794,13 +1794,13 @@ int sbh_bgzf_compress(sbh_ctx *ctx, const void *src, uint64_t n, int src_on_devi
   if (rc) return rc;
   hipStream_t st = ctx->stream;
   struct Bufs {  // per-call scratch, freed on every return path
-    DBuf<uint8_t> in, slots, packed, segbuf;
-    DBuf<uint16_t> heads;
-    DBuf<uint32_t> sizes;
+    DBuf<uint8_t> in, slots, packed;
+    DBuf<uint16_t> prev;
+    DBuf<uint32_t> toks, sizes;
     DBuf<uint64_t> offs;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     ~Bufs() {
-      in.release(), slots.release(), packed.release(), segbuf.release(), heads.release(), sizes.release(), offs.release();
+      in.release(), slots.release(), packed.release(), prev.release(), toks.release(), sizes.release(), offs.release();
       if (e0) (void)hipEventDestroy(e0);
       if (e1) (void)hipEventDestroy(e1);
     }
@@ -1812,35 +1812,46 @@ int sbh_bgzf_compress(sbh_ctx *ctx, const void *src, uint64_t n, int src_on_devi
     d_src = B.in.p;
   }
   uint64_t total = 0;
+  float kms = 0.f;
   if (nb) {
-    HIPCHK(ctx, B.slots.ensure(nb * 65536ull));
-    HIPCHK(ctx, B.heads.ensure(nb * 16ull * 4096ull));
-    HIPCHK(ctx, B.segbuf.ensure(nb * 16ull * 4624ull));
-    HIPCHK(ctx, B.sizes.ensure(nb));
-    HIPCHK(ctx, B.offs.ensure(nb));
+    // members in batches: scratch (prev, slots, packed) bounded by the batch, not the input
+    const uint64_t cap = nb < DEFLATE_BATCH ? nb : DEFLATE_BATCH;
+    HIPCHK(ctx, B.slots.ensure(cap * 65536ull));
+    HIPCHK(ctx, B.packed.ensure(cap * 65536ull));
+    HIPCHK(ctx, B.prev.ensure(cap * (DEFLATE_PREV_BYTES / 2)));
+    HIPCHK(ctx, B.toks.ensure(cap * (DEFLATE_TOK_BYTES / 4)));
+    HIPCHK(ctx, B.sizes.ensure(cap));
+    HIPCHK(ctx, B.offs.ensure(cap));
     HIPCHK(ctx, hipEventCreate(&B.e0));
     HIPCHK(ctx, hipEventCreate(&B.e1));
-    HIPCHK(ctx, hipEventRecord(B.e0, st));
-    HIPCHK(ctx, launch_deflate(d_src, n, B.slots.p, B.segbuf.p, B.heads.p, B.sizes.p, st));
-    HIPCHK(ctx, hipEventRecord(B.e1, st));
-    std::vector<uint32_t> hs(nb);
-    std::vector<uint64_t> ho(nb);
-    HIPCHK(ctx, hipMemcpyAsync(hs.data(), B.sizes.p, 4 * nb, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipStreamSynchronize(st));
-    for (uint64_t b = 0; b < nb; ++b) {
-      if (hs[b] < 26 || hs[b] > 65536) return fail(ctx, SBH_E_HIP, "bgzf_compress: block %llu size %u", (unsigned long long)b, hs[b]);
-      ho[b] = total;
-      total += hs[b];
+    std::vector<uint32_t> hs(cap);
+    std::vector<uint64_t> ho(cap);
+    for (uint64_t b0 = 0; b0 < nb; b0 += cap) {
+      const uint32_t k = (uint32_t)(nb - b0 < cap ? nb - b0 : cap);
+      HIPCHK(ctx, hipEventRecord(B.e0, st));
+      HIPCHK(ctx, launch_deflate(d_src, n, b0, k, B.prev.p, B.toks.p, B.slots.p, B.sizes.p, st));
+      HIPCHK(ctx, hipEventRecord(B.e1, st));
+      HIPCHK(ctx, hipMemcpyAsync(hs.data(), B.sizes.p, 4ull * k, hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipStreamSynchronize(st));
+      float ms = 0.f;
+      HIPCHK(ctx, hipEventElapsedTime(&ms, B.e0, B.e1));
+      kms += ms;
+      uint64_t bt = 0;
+      for (uint32_t j = 0; j < k; ++j) {
+        if (hs[j] < 26 || hs[j] > 65536)
+          return fail(ctx, SBH_E_HIP, "bgzf_compress: block %llu size %u", (unsigned long long)(b0 + j), hs[j]);
+        ho[j] = bt;
+        bt += hs[j];
+      }
+      if (total + bt + 28 > out_cap) return fail(ctx, SBH_E_ARG, "bgzf_compress: out_cap exceeded");
+      HIPCHK(ctx, hipMemcpyAsync(B.offs.p, ho.data(), 8ull * k, hipMemcpyHostToDevice, st));
+      HIPCHK(ctx, launch_deflate_gather(B.slots.p, B.sizes.p, B.offs.p, k, B.packed.p, st));
+      HIPCHK(ctx, hipMemcpyAsync(out + total, B.packed.p, bt, hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipStreamSynchronize(st));
+      total += bt;
     }
-    HIPCHK(ctx, B.packed.ensure(total));
-    HIPCHK(ctx, hipMemcpyAsync(B.offs.p, ho.data(), 8 * nb, hipMemcpyHostToDevice, st));
-    HIPCHK(ctx, launch_deflate_gather(B.slots.p, B.sizes.p, B.offs.p, nb, B.packed.p, st));
-    HIPCHK(ctx, hipMemcpyAsync(out, B.packed.p, total, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipStreamSynchronize(st));
-    if (deflate_ms) HIPCHK(ctx, hipEventElapsedTime(deflate_ms, B.e0, B.e1));
-  } else if (deflate_ms) {
-    *deflate_ms = 0.f;
   }
+  if (deflate_ms) *deflate_ms = kms;
   static const uint8_t eof[28] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0,
                                   27, 0,   3, 0, 0, 0, 0, 0, 0, 0,   0, 0};
   memcpy(out + total, eof, 28);

@@ -94,11 +94,15 @@ hipError_t launch_compact_u64(const uint64_t *in, const uint64_t *keep, const ui
 hipError_t launch_block_crc(const uint8_t *comp, DevBlocks bl, uint64_t nblocks, const uint8_t *U,
                             unsigned long long *n_bad, unsigned long long *first_bad, hipStream_t st);
 
-// BGZF writer (deflate.hip): k_deflate fills one 64 KiB slot per 65498-byte piece and its
-// member size; k_gather packs the slots at the host-computed file offsets.
+// BGZF writer (deflate.hip): members are coded in batches of at most DEFLATE_BATCH 65498-byte
+// pieces: k_prev (hash chains into prev), k_deflate (tokens into toks, one 64 KiB slot per
+// member and its size), k_footer; k_gather packs the slots at host-computed offsets.
+constexpr uint32_t DEFLATE_BATCH = 2048;
+constexpr uint64_t DEFLATE_PREV_BYTES = 65536ull * 2;  // prev scratch per member
+constexpr uint64_t DEFLATE_TOK_BYTES = 65536ull * 4;   // token scratch per member (256 lanes x 256)
 uint64_t deflate_nblocks(uint64_t n);
-hipError_t launch_deflate(const uint8_t *src, uint64_t n, uint8_t *slots, uint8_t *segbuf, uint16_t *heads,
-                          uint32_t *sizes, hipStream_t st);
+hipError_t launch_deflate(const uint8_t *src, uint64_t n, uint64_t b0, uint32_t nbatch, uint16_t *prev,
+                          uint32_t *toks, uint8_t *slots, uint32_t *sizes, hipStream_t st);
 hipError_t launch_deflate_gather(const uint8_t *slots, const uint32_t *sizes, const uint64_t *offs, uint64_t nblocks,
                                  uint8_t *out, hipStream_t st);
 

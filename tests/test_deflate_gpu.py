@@ -1,7 +1,8 @@
 """BGZF writer on the GPU (sbh_bgzf_compress / htsjdk_rewrite; HTSJDKRewrite.scala:40-67).
-k_deflate runs deflate_core.h one lane per block, so its file must equal the host build's
-byte for byte (test_deflate_cpu.py pins that build against zlib); the rewritten fixtures
-re-inflate (zlib and this library's own GPU inflate + CRC check) to the original stream."""
+k_prev + k_deflate run deflate_core.h's coder one workgroup per member, so the file must
+equal the host build's (tools/deflate_host.cpp) byte for byte (test_deflate_cpu.py pins that
+build against zlib); the rewritten fixtures re-inflate (zlib and this library's own GPU
+inflate + CRC check) to the original stream."""
 import zlib
 
 import numpy as np
@@ -32,6 +33,30 @@ def test_gpu_equals_host_build(ctx, n):
         got, nb, _ = ctx.bgzf_compress(data)
         assert nb == (n + PAYLOAD - 1) // PAYLOAD
         assert got.tobytes() == compress(data.tobytes())
+
+
+def test_batches_of_members(ctx):
+    """More members than one batch (DEFLATE_BATCH = 2048): members are independent, so each
+    equals the host build of its own 65498-byte piece; every member re-inflates (zlib)."""
+    nbatch = 2048
+    nb = nbatch + 3
+    n = (nb - 1) * PAYLOAD + 777
+    rng = np.random.default_rng(11)
+    flat = OracleFile(np.fromfile(golden_bam("5k.bam"), dtype=np.uint8)).uncompressed()
+    data = np.resize(flat, n)
+    data[::4099] = rng.integers(0, 256, data[::4099].size, dtype=np.uint8)  # no two tiles alike
+    got, k, _ = ctx.bgzf_compress(data)
+    assert k == nb
+    m = parse_members(got.tobytes())
+    assert len(m) == nb + 1 and m[-1][2] == 0
+    for b in [0, 1, nbatch - 1, nbatch, nbatch + 1, nb - 1]:
+        piece = data[b * PAYLOAD:(b + 1) * PAYLOAD].tobytes()
+        o, c = m[b][0], m[b][1]
+        assert got[o:o + c].tobytes() + EOF == compress(piece), b
+    assert b"".join(x[3] for x in m) == data.tobytes()
+
+
+EOF = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
 
 
 @pytest.mark.parametrize("name", FIXTURES)
