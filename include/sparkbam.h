@@ -327,10 +327,12 @@ int sbh_records_scan_regions(sbh_shard *sh, const uint64_t *chunk_begin, const u
  * BlockCompressedOutputStream): the uncompressed stream src[0, n) is cut every 65498 bytes,
  * each piece becomes one BGZF member (deflate; stored when it would not fit 64 KiB), CRC32 +
  * ISIZE footer, then the 28-byte empty EOF member.  Member boundaries in uncompressed space
- * match htsjdk's; the deflate bytes are this library's own (greedy LZ77, fixed Huffman), not
- * zlib level 5.  src is a host or device pointer (src_on_device); out is host memory of at
- * least sbh_bgzf_compress_bound(n) bytes.  *deflate_ms (optional): the compress kernel's
- * device time (HIP events on the context's stream). */
+ * match htsjdk's; the deflate bytes are this library's own (hash-chain LZ77 with lazy
+ * matching, one dynamic-Huffman block per member; ratio ~2.9 on BAM streams vs ~3.0 for
+ * htsjdk's zlib level 5), not zlib's.  src is a host or device pointer (src_on_device); out is
+ * host memory of at least sbh_bgzf_compress_bound(n) bytes.  Device scratch is bounded by a
+ * batch of 2048 members (~0.9 GB), whatever n.  *deflate_ms (optional): the compress
+ * kernels' device time, summed over the batches (HIP events on the context's stream). */
 uint64_t sbh_bgzf_compress_bound(uint64_t n);
 int sbh_bgzf_compress(sbh_ctx *ctx, const void *src, uint64_t n, int src_on_device, uint8_t *out,
                       uint64_t out_cap, uint64_t *out_size, uint64_t *n_blocks, float *deflate_ms);

@@ -279,9 +279,10 @@ def htsjdk_rewrite(path_or_bytes, out_path=None, read_ranges=None, ctx=None):
     `index-blocks` / `index-records` run on the result.
 
     Size trade-off: members are cut exactly where htsjdk cuts them (65498 uncompressed
-    bytes), but each is coded by this library's GPU coder (greedy LZ77 + fixed Huffman codes,
-    see deflate_core.h), not zlib level 5, so the compressed bytes -- and therefore the
-    block positions in `.blocks` / `.records` -- differ from htsjdk's output."""
+    bytes), but each is coded by this library's GPU coder (hash-chain LZ77 with lazy matching,
+    one dynamic-Huffman block per member, see deflate_core.h), not zlib level 5, so the
+    compressed bytes -- and therefore the block positions in `.blocks` / `.records` -- differ
+    from htsjdk's output; files come out ~3-5% larger (ratio 2.93 vs ~3.05 on BAM streams)."""
     L = _Loaded(path_or_bytes, ctx)
     try:
         sh = L.shard

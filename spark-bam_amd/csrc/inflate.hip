@@ -1002,12 +1002,16 @@ template <bool LDS, int MODE>
 __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, Src<LDS> src, uint32_t A, uint32_t stop,
                                             uint32_t limit, Ckpt &ck, const LaneRun &sp,
                                             uint32_t *__restrict__ dst, uint32_t out0, uint32_t &bad) {
-  // The only decode state is the bit position: every code reads its 32 bits afresh
-  // (two LDS dwords, one v_alignbit), which is enough for any code plus its extra bits
-  // (<= 28), and the extra bits come out with one v_bfe.  One loop exit, at the end of
+  // The decode state is the bit position and the two stream dwords under it (lo, hi):
+  // a code's 32 bits come from them with one v_alignbit, enough for any code plus its
+  // extra bits (<= 28), and the extra bits come out with one v_bfe.  A code consumes
+  // < 32 bits, so the window moves by at most one dword per code; the dword after it is
+  // loaded at the top of every iteration, beside the table lookup, so each code costs
+  // one LDS round trip on the dependent chain, not two.  One loop exit, at the end of
   // the body; everything else is selects (apart from the rare long code).
   const uint32_t stop2 = stop < limit ? stop : limit;
   uint32_t pos = A;
+  uint32_t wi = pos >> 5, lo = src(wi), hi = src(wi + 1);
   uint32_t ml = 0;  // pending match length: the next code is a distance
   uint32_t ntok = 0, nout = 0;
   uint32_t c1p = NOPOS, c1o = 0, c2p = NOPOS, c2o = 0;
@@ -1015,7 +1019,8 @@ __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, Src<LDS> src, uin
   uint32_t e;
   bool cut;
   for (;;) {
-    const uint32_t bits = src.bits32(pos);
+    const uint32_t bits = __builtin_amdgcn_alignbit(hi, lo, pos & 31);
+    const uint32_t nx = src(wi + 2);
     const bool atb = ml == 0;  // token boundary
     e = t.tab[(bits & ((1u << LIT_FAST) - 1)) | (atb ? 0u : 1u << LIT_FAST)];
     if (e & PE_SLOW) e = slow_lane(t, bits, !atb);
@@ -1035,6 +1040,10 @@ __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, Src<LDS> src, uin
     const uint32_t L = e & 31, x = (e >> 8) & 15;
     const uint32_t val = (e >> 16) + __builtin_amdgcn_ubfe(bits, L, x);
     pos += L + x;
+    const bool adv = (pos >> 5) != wi;
+    lo = adv ? hi : lo;
+    hi = adv ? nx : hi;
+    wi += adv ? 1u : 0u;
     const bool is_tok = (e & PE_LEN) == 0;  // a literal, or the distance completing a match
     if (MODE == RUN_EMIT) {
       if (is_tok) dst[ntok] = atb ? val << 8 : TOK_MATCH | (ml << 16) | val;

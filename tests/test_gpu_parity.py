@@ -445,3 +445,80 @@ def test_verify_crc_synthetic_and_corrupt_footer(ctx, synth_files):
         assert sh.verify_crc() == (1, start)
     finally:
         sh.close()
+
+
+# readsToCheck (CheckerApp / CanLoadBam `--reads-to-check`, default 10) and
+# bgzfBlocksToCheck (`-z`, default 5) away from their defaults: the device honours any value
+# the ABI accepts (rtc 0..1023), bit for bit with the oracle at each.
+RTCS = [0, 1, 2, 3, 25, 100, 1023]
+
+
+@pytest.mark.parametrize("rtc", RTCS)
+@pytest.mark.parametrize("name", ["2.bam", "5k.bam"])
+def test_eager_reads_to_check(golden, name, rtc):
+    data, of, sh = golden[name]
+    end = min(sh.flat_size, 400000)
+    n, bits = sh.check_eager(0, end, reads_to_check=rtc)
+    n_ref, bits_ref = of.eager_range(0, end, reads_to_check=rtc)
+    i = first_diff(np.unpackbits(bits, bitorder="little"), np.unpackbits(bits_ref, bitorder="little"))
+    assert i < 0, f"rtc {rtc}: first differing position {i}"
+    assert n == n_ref
+
+
+@pytest.mark.parametrize("rtc", RTCS)
+def test_full_reads_to_check(golden, rtc):
+    data, of, sh = golden["2.bam"]
+    r = sh.check_full(0, 150000, reads_to_check=rtc, want_words=True)
+    _, counts_ref, rbe_ref, w_ref = of.full_range(0, 150000, reads_to_check=rtc, want_words=True)
+    i = first_diff(r["words"], w_ref)
+    assert i < 0, f"rtc {rtc}: position {i}"
+    assert np.array_equal(r["counts"].astype(np.int64), counts_ref)
+    assert np.array_equal(r["rbe"].astype(np.int64), rbe_ref)
+
+
+@pytest.mark.parametrize("rtc", [0, 1, 3, 100, 1023])
+def test_find_record_start_reads_to_check(golden, rtc):
+    data, of, sh = golden["1.bam"]
+    rng = np.random.default_rng(rtc)
+    for f in rng.integers(0, sh.flat_size - 1, 12).tolist() + [0, sh.flat_of(239479, 0)]:
+        rc, want, d = of.find_record_start(int(f), reads_to_check=rtc)
+        if rc == OR_OK:
+            assert sh.find_record_start(int(f), reads_to_check=rtc) == (want, d), (f, rtc)
+        else:
+            with pytest.raises(sb.SparkBamError):
+                sh.find_record_start(int(f), reads_to_check=rtc)
+
+
+@pytest.mark.parametrize("z", [1, 2, 3, 10])
+def test_find_block_start_blocks_to_check(golden, z):
+    data, of, sh = golden["2.bam"]
+    rng = np.random.default_rng(z)
+    for s in rng.integers(0, data.size - 1, 20).tolist() + [0, 26170, data.size - 28]:
+        rc, want = of.find_block_start(int(s), blocks_to_check=z)
+        if rc == OR_OK:
+            assert sh.find_block_start(int(s), bgzf_blocks_to_check=z) == want, (s, z)
+        else:
+            with pytest.raises(sb.SparkBamError):
+                sh.find_block_start(int(s), bgzf_blocks_to_check=z)
+
+
+@pytest.mark.parametrize("z,rtc", [(1, 1), (2, 0), (10, 3), (5, 100)])
+def test_split_parameters(golden, z, rtc):
+    data, of, sh = golden["1.bam"]
+    for s, e in file_splits(data.size, 100 * 1024):
+        rc, v, n = of.split(s, e, blocks_to_check=z, reads_to_check=rtc)
+        if rc == OR_OK:
+            got = sh.split(s, e, bgzf_blocks_to_check=z, reads_to_check=rtc)
+            assert got[1] == n and (n == 0 or got[0] == v), (s, e, z, rtc)
+        else:
+            with pytest.raises(sb.SparkBamError):
+                sh.split(s, e, bgzf_blocks_to_check=z, reads_to_check=rtc)
+    # the batched path (sbh_split_starts) agrees at the same parameters
+    sp = [(s, e) for s, e in file_splits(data.size, 100 * 1024)]
+    status, v, c, _ = sh.split_starts(sp, bgzf_blocks_to_check=z, reads_to_check=rtc)
+    for k, (s, e) in enumerate(sp):
+        rc, want_v, want_n = of.split(s, e, blocks_to_check=z, reads_to_check=rtc)
+        if rc == OR_OK:
+            assert status[k] == 0 and int(c[k]) == want_n and (want_n == 0 or int(v[k]) == want_v), (s, e, z, rtc)
+        else:
+            assert status[k] != 0, (s, e, z, rtc)
