@@ -9,6 +9,7 @@
 //   spark-bam index-blocks  BAM [OUT]                        (bgzf/index/IndexBlocks.scala)
 //   spark-bam index-records BAM [OUT]                        (check/index/IndexRecords.scala)
 //   spark-bam check-blocks -s [-r RECORDS] [-l N] BAM        (cli/.../check/blocks/CheckBlocks.scala)
+//   spark-bam htsjdk-rewrite [-r READS] [-b] [-i] BAM OUT     (cli/.../rewrite/HTSJDKRewrite.scala)
 //
 // The hadoop-bam ("seqdoop", -u) comparisons are out of scope: hadoop-bam's
 // BAMSplitGuesser is a competitor's algorithm, not part of spark-bam's path.
@@ -236,12 +237,16 @@ struct Args {
   std::vector<std::pair<uint64_t, uint64_t>> ranges;
   bool has_ranges = false;
   int reads_to_check = 10, max_read_size = 100000000, blocks_to_check = 5;
+  // htsjdk-rewrite: -r record-index ranges (IntRanges), -b / -i write OUT.blocks / OUT.records
+  std::vector<std::pair<uint64_t, uint64_t>> read_ranges;
+  bool has_read_ranges = false, idx_blocks = false, idx_records = false;
 };
 
 Args parse(int argc, char **argv) {
   Args a;
   if (argc < 2) throw Error(SBH_E_ARG, "usage: spark-bam <command> [options] <bam>");
   a.cmd = argv[1];
+  const bool rewrite = a.cmd == "htsjdk-rewrite";
   std::vector<std::string> pos;
   for (int i = 2; i < argc; ++i) {
     std::string t = argv[i];
@@ -249,7 +254,10 @@ Args parse(int argc, char **argv) {
       if (i + 1 >= argc) throw Error(SBH_E_ARG, "missing value for " + t);
       return argv[++i];
     };
-    if (t == "-m" || t == "--max-split-size") { a.split = parse_bytes(next()); a.has_split = true; }
+    if (rewrite && (t == "-r" || t == "--read-ranges")) { a.read_ranges = parse_ranges(next()); a.has_read_ranges = true; }
+    else if (rewrite && (t == "-b" || t == "--index-blocks")) a.idx_blocks = true;
+    else if (rewrite && (t == "-i" || t == "--index-records")) a.idx_records = true;
+    else if (t == "-m" || t == "--max-split-size") { a.split = parse_bytes(next()); a.has_split = true; }
     else if (t == "-s" || t == "--spark-bam") a.s = true;
     else if (t == "-u" || t == "--upstream" || t == "--hadoop-bam") a.u = true;
     else if (t == "-l" || t == "--print-limit") a.limit = std::stol(next());
@@ -608,6 +616,58 @@ int index_records(const Args &a) {
   return 0;
 }
 
+// HTSJDKRewrite (cli/.../rewrite/HTSJDKRewrite.scala:40-92): the BAM's uncompressed stream --
+// header, then every record, or only the records whose index is in -r (:48-58) -- re-cut into
+// 65498-byte BGZF members on the GPU (sbh_bgzf_compress) plus the EOF member; -b / -i then
+// index the output like IndexBlocks / IndexRecords (:72-90).  Records pass through byte for
+// byte (htsjdk's decode/re-encode is the identity on a BAM it wrote); the deflate bytes are
+// this library's coder's, not zlib level 5's (include/sparkbam.h).
+int htsjdk_rewrite(const Args &a) {
+  if (a.out.empty()) throw Error(SBH_E_ARG, "htsjdk-rewrite: missing output path");
+  std::vector<uint8_t> payload;
+  {
+    Loaded L(a.path);
+    uint64_t seg_end = L.flat;
+    for (const sbh_block &b : L.blocks)
+      if (b.flags & SBH_BLOCK_EMPTY) { seg_end = b.ustart; break; }
+    std::vector<uint8_t> flat(seg_end);
+    if (seg_end) chk(sbh_read_flat(L.sh, 0, seg_end, flat.data()), "read stream");
+    if (!a.has_read_ranges) {
+      payload.swap(flat);
+    } else {
+      // record starts: the eager calls over the records, proven equal to the record chain
+      std::vector<uint8_t> bits((seg_end - L.hdr.end + 7) / 8);
+      uint64_t n = 0, chain = 0;
+      chk(sbh_check_eager(L.sh, L.hdr.end, seg_end, a.reads_to_check, bits.data(), &n), "eager");
+      chk(sbh_count_records(L.sh, L.hdr.end, seg_end, &chain), "records");
+      if (chain != n) throw Error(SBH_E_STATE, "record chain and eager calls disagree");
+      const std::vector<uint64_t> st = bits_to_positions(bits, L.hdr.end, seg_end - L.hdr.end);
+      payload.assign(flat.begin(), flat.begin() + (ptrdiff_t)L.hdr.end);
+      for (uint64_t i = 0; i < st.size(); ++i) {
+        bool in = false;
+        for (auto &r : a.read_ranges) in |= r.first <= i && i < r.second;
+        if (!in) continue;
+        const uint64_t e = i + 1 < st.size() ? st[i + 1] : seg_end;
+        payload.insert(payload.end(), flat.begin() + (ptrdiff_t)st[i], flat.begin() + (ptrdiff_t)e);
+      }
+    }
+  }
+  std::vector<uint8_t> out(sbh_bgzf_compress_bound(payload.size()));
+  uint64_t size = 0, nb = 0;
+  chk(sbh_bgzf_compress(g_ctx, payload.data(), payload.size(), 0, out.data(), out.size(), &size, &nb, nullptr),
+      "bgzf compress");
+  FILE *f = fopen(a.out.c_str(), "wb");
+  if (!f) throw Error(SBH_E_ARG, "cannot write " + a.out);
+  const bool ok = fwrite(out.data(), 1, size, f) == size;
+  fclose(f);
+  if (!ok) throw Error(SBH_E_ARG, "short write to " + a.out);
+  Args ix = a;
+  ix.path = a.out;
+  ix.out.clear();
+  if (a.idx_blocks) index_blocks(ix);
+  if (a.idx_records) index_records(ix);
+  return 0;
+}
 
 // hammerlab Stats.fromHist rendered with the truncating Show[Double] CheckBlocks installs
 // (CheckBlocks.scala:123-131): N, mean / population sigma, median / MAD, the histogram's
@@ -759,6 +819,7 @@ int main(int argc, char **argv) {
     else if (a.cmd == "index-blocks") rc = index_blocks(a);
     else if (a.cmd == "index-records") rc = index_records(a);
     else if (a.cmd == "check-blocks") rc = check_blocks(a);
+    else if (a.cmd == "htsjdk-rewrite") rc = htsjdk_rewrite(a);
     else throw Error(SBH_E_ARG, "unknown command " + a.cmd);
     sbh_ctx_destroy(g_ctx);
     return rc;

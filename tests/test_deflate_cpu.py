@@ -70,16 +70,41 @@ def test_sizes_random_and_runs(n):
     check_roundtrip(rng.integers(0, 4, n, dtype=np.uint8).tobytes())     # small alphabet
 
 
+def symstats(data):
+    L = host_lib()
+    L.sbh_host_bgzf_symstats.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
+    a = np.frombuffer(bytes(data), dtype=np.uint8)
+    hl, hd = np.zeros(286, np.uint64), np.zeros(30, np.uint64)
+    L.sbh_host_bgzf_symstats(a.ctypes.data, len(a), hl.ctypes.data, hd.ctypes.data)
+    return hl, hd
+
+
 def test_every_length_and_distance_code():
-    # matches of every length 3..258 at distances across every distance code (1..32768)
+    """Matches of every length code and every distance code (0..29, distances 1..32768) are
+    emitted -- counted from the coder's own symbol histogram -- and the stream round-trips
+    through zlib.  Length code 285 (exactly 258) cannot occur: matches end inside their
+    256-byte segment (deflate_core.h), so the longest is 256 (code 284)."""
     rng = np.random.default_rng(7)
     parts = []
-    for d in [1, 2, 3, 4, 5, 7, 8, 9, 13, 17, 33, 65, 129, 257, 513, 1025, 2049, 4097, 8193, 16385, 24577, 32768]:
-        base = rng.integers(0, 256, d, dtype=np.uint8).tobytes()
-        parts.append(base + (base * (300 // d + 2))[:int(rng.integers(3, 259))])
-    data = b"".join(parts)
+    # distance codes: d = 1, 2, 3, 4 and the first distance of every code, and 32768
+    for d in [1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129, 193, 257, 385, 513, 769, 1025, 1537, 2049,
+              3073, 4097, 6145, 8193, 12289, 16385, 24577, 32768]:
+        if d < 64:  # a period-d run: matches at distance d (overlapping)
+            base = rng.integers(0, 256, d, dtype=np.uint8).tobytes()
+            parts.append(rng.integers(0, 256, 300, dtype=np.uint8).tobytes() + base * (200 // d + 2))
+        else:       # a 64-byte block, d - 64 random bytes, the block again
+            blk = rng.integers(0, 256, 64, dtype=np.uint8).tobytes()
+            parts.append(blk + rng.integers(0, 256, d - 64, dtype=np.uint8).tobytes() + blk)
+        parts.append(rng.integers(0, 256, 512, dtype=np.uint8).tobytes())
+        data = b"".join(parts)
+    # length codes: a period-3 run of each length, separated by random bytes
     for L in range(3, 259):
-        data += bytes([L & 0xff, 0xAB, L >> 8]) * (L // 3 + 2)
+        data += rng.integers(0, 256, 64, dtype=np.uint8).tobytes()
+        data += (bytes([0xC3, L & 0xff, 0x5A]) * 100)[:3 + L]
+    hl, hd = symstats(data)
+    assert (hl[257:285] > 0).all(), f"length codes never emitted: {np.flatnonzero(hl[257:285] == 0) + 257}"
+    assert hl[285] == 0
+    assert (hd > 0).all(), f"distance codes never emitted: {np.flatnonzero(hd == 0)}"
     f, _ = check_roundtrip(data)
     assert len(f) < len(data)
 

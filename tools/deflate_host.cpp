@@ -10,8 +10,10 @@
 
 using namespace sbh_deflate;
 
-// One member of n <= PAYLOAD bytes into out (SLOT zeroed bytes); returns its size.
-static uint32_t member(const uint8_t *src, uint32_t n, uint8_t *out, const uint32_t *crctab) {
+// One member of n <= PAYLOAD bytes into out (SLOT zeroed bytes); returns its size.  hl / hd
+// (optional): add the member's lit/len and distance symbol counts when it is coded (not stored).
+static uint32_t member(const uint8_t *src, uint32_t n, uint8_t *out, const uint32_t *crctab, uint64_t *hl = nullptr,
+                       uint64_t *hd = nullptr) {
   std::vector<uint8_t> pad(n + 8, 0);  // 8-byte loads run up to 7 bytes past the data
   memcpy(pad.data(), src, n);
   std::vector<uint16_t> prev(n + 1, NONE16), head(HN, NONE16);
@@ -51,6 +53,10 @@ static uint32_t member(const uint8_t *src, uint32_t n, uint8_t *out, const uint3
   uint8_t *d0 = out + 18;
   uint32_t dsize = (uint32_t)((nbits + 7) / 8);
   if (dsize <= BUDGET) {
+    if (hl && hd) {
+      for (uint32_t i = 0; i < 286; ++i) hl[i] += fl[i];
+      for (uint32_t i = 0; i < 30; ++i) hd[i] += fd[i];
+    }
     Bits b{d0, 0, 0};
     for (uint32_t i = 0; i < hbits; i += 8) b.put(hdr[i / 8], hbits - i < 8 ? hbits - i : 8);
     for (uint32_t t : toks) {
@@ -91,4 +97,20 @@ extern "C" uint64_t sbh_host_bgzf_compress(const uint8_t *src, uint64_t n, uint8
   }
   put_eof(out + o);
   return o + EOF_SIZE;
+}
+
+// Symbol statistics of the coder over src (tests: which length / distance codes it emits).
+extern "C" void sbh_host_bgzf_symstats(const uint8_t *src, uint64_t n, uint64_t *lit_hist, uint64_t *dist_hist) {
+  uint32_t tab[256];
+  for (uint32_t t = 0; t < 256; ++t) {
+    uint32_t c = t;
+    for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+    tab[t] = c;
+  }
+  std::vector<uint8_t> slot(SLOT);
+  for (uint64_t s = 0; s < n; s += PAYLOAD) {
+    const uint32_t len = (uint32_t)(n - s < PAYLOAD ? n - s : PAYLOAD);
+    std::fill(slot.begin(), slot.end(), 0);
+    member(src + s, len, slot.data(), tab, lit_hist, dist_hist);
+  }
 }
