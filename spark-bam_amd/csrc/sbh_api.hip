@@ -1794,13 +1794,14 @@ int sbh_bgzf_compress(sbh_ctx *ctx, const void *src, uint64_t n, int src_on_devi
   if (rc) return rc;
   hipStream_t st = ctx->stream;
   struct Bufs {  // per-call scratch, freed on every return path
-    DBuf<uint8_t> in, slots, packed;
+    DBuf<uint8_t> in, slots, packed, recs;
     DBuf<uint16_t> prev;
     DBuf<uint32_t> toks, sizes;
     DBuf<uint64_t> offs;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     ~Bufs() {
-      in.release(), slots.release(), packed.release(), prev.release(), toks.release(), sizes.release(), offs.release();
+      in.release(), slots.release(), packed.release(), recs.release(), prev.release(), toks.release(), sizes.release(),
+          offs.release();
       if (e0) (void)hipEventDestroy(e0);
       if (e1) (void)hipEventDestroy(e1);
     }
@@ -1820,6 +1821,7 @@ int sbh_bgzf_compress(sbh_ctx *ctx, const void *src, uint64_t n, int src_on_devi
     HIPCHK(ctx, B.packed.ensure(cap * 65536ull));
     HIPCHK(ctx, B.prev.ensure(cap * (DEFLATE_PREV_BYTES / 2)));
     HIPCHK(ctx, B.toks.ensure(cap * (DEFLATE_TOK_BYTES / 4)));
+    HIPCHK(ctx, B.recs.ensure(cap * DEFLATE_REC_BYTES));
     HIPCHK(ctx, B.sizes.ensure(cap));
     HIPCHK(ctx, B.offs.ensure(cap));
     HIPCHK(ctx, hipEventCreate(&B.e0));
@@ -1829,7 +1831,7 @@ int sbh_bgzf_compress(sbh_ctx *ctx, const void *src, uint64_t n, int src_on_devi
     for (uint64_t b0 = 0; b0 < nb; b0 += cap) {
       const uint32_t k = (uint32_t)(nb - b0 < cap ? nb - b0 : cap);
       HIPCHK(ctx, hipEventRecord(B.e0, st));
-      HIPCHK(ctx, launch_deflate(d_src, n, b0, k, B.prev.p, B.toks.p, B.slots.p, B.sizes.p, st));
+      HIPCHK(ctx, launch_deflate(d_src, n, b0, k, B.prev.p, B.toks.p, B.recs.p, B.slots.p, B.sizes.p, st));
       HIPCHK(ctx, hipEventRecord(B.e1, st));
       HIPCHK(ctx, hipMemcpyAsync(hs.data(), B.sizes.p, 4ull * k, hipMemcpyDeviceToHost, st));
       HIPCHK(ctx, hipStreamSynchronize(st));

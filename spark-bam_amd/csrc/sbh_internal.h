@@ -100,9 +100,10 @@ hipError_t launch_block_crc(const uint8_t *comp, DevBlocks bl, uint64_t nblocks,
 constexpr uint32_t DEFLATE_BATCH = 2048;
 constexpr uint64_t DEFLATE_PREV_BYTES = 65536ull * 2;  // prev scratch per member
 constexpr uint64_t DEFLATE_TOK_BYTES = 65536ull * 4;   // token scratch per member (256 lanes x 256)
+constexpr uint64_t DEFLATE_REC_BYTES = 4096;           // per-member record: token counts, histogram, codes
 uint64_t deflate_nblocks(uint64_t n);
 hipError_t launch_deflate(const uint8_t *src, uint64_t n, uint64_t b0, uint32_t nbatch, uint16_t *prev,
-                          uint32_t *toks, uint8_t *slots, uint32_t *sizes, hipStream_t st);
+                          uint32_t *toks, uint8_t *recs, uint8_t *slots, uint32_t *sizes, hipStream_t st);
 hipError_t launch_deflate_gather(const uint8_t *slots, const uint32_t *sizes, const uint64_t *offs, uint64_t nblocks,
                                  uint8_t *out, hipStream_t st);
 
