@@ -90,7 +90,10 @@ def main():
     device = local_rank % ndev
     xdev = "cuda" if backend == "nccl" else "cpu"
     torch.cuda.set_device(device)
-    if world > 1:
+    # SBH_BENCH_COLLECTIVES=1: run the N>1 collectives (RCCL) even at WORLD_SIZE=1, so a
+    # one-GPU box exercises the nccl code path end to end (torch.distributed.run --nproc-per-node 1)
+    coll = world > 1 or os.environ.get("SBH_BENCH_COLLECTIVES") == "1"
+    if coll:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         else:
@@ -125,7 +128,7 @@ def main():
         seg = synth.Segment(p, args.records_per_gpu, world, rank, halo_blocks=64 if streaming else 16, log=log,
                             alloc=pinned if streaming else None)
     own = torch.tensor([seg.own_csize], dtype=torch.int64, device=xdev)
-    if world > 1:
+    if coll:
         gathered = [torch.zeros_like(own) for _ in range(world)]
         dist.all_gather(gathered, own)
         own_sizes = [int(g.item()) for g in gathered]
@@ -166,7 +169,7 @@ def main():
         ex = -1 if ex is None else ex
         r["stages"] = stages
         mine = [r["first_vpos"], r["count"], r["n_true"], r["flat_bytes"], ex]
-        if world > 1:  # RCCL allgather of the per-shard split records (stitching)
+        if coll:  # RCCL allgather of the per-shard split records (stitching)
             result_t.copy_(torch.tensor(mine, dtype=torch.int64))
             out = [torch.zeros_like(result_t) for _ in range(world)]
             dist.all_gather(out, result_t)
@@ -176,7 +179,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if coll:
         dist.barrier()
     torch.cuda.synchronize()
     stage_acc = np.zeros(6)
@@ -185,11 +188,11 @@ def main():
         r, allr = step()
         stage_acc += np.asarray(r["stages"])
     torch.cuda.synchronize()
-    if world > 1:
+    if coll:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
-    if world > 1:
+    if coll:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=xdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
@@ -368,7 +371,7 @@ def main():
     ctx.close()
     for b in pins:
         b.close()
-    if world > 1:
+    if coll:
         dist.destroy_process_group()
     if not ok:
         log(f"STITCH CHECK FAILED: records {total_records} true {total_true} expected {expect}; "

@@ -249,7 +249,12 @@ import torch.distributed as dist
 from __graft_entry__ import load_package
 sb = load_package()
 import spark_bam_amd.sharded as sharded
-dist.init_process_group("gloo")
+if os.environ.get("SBH_TEST_BACKEND", "gloo") == "nccl":  # RCCL on the box's one device
+    import torch
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+else:
+    dist.init_process_group("gloo")
 path, ss = sys.argv[1], (int(sys.argv[2]) or None)
 if os.environ.get("SBH_TEST_FP_RANK"):
     # rank k's chain as if its FindRecordStart had stopped on a false positive one record
@@ -304,6 +309,19 @@ def test_gpu_two_ranks_on_one_device(tmp_path, name, split_size, halo):
         assert r["counts"] == ref_counts
         assert [tuple(s) for s in r["splits"]] == ref_splits
         assert r["ok"], (r, [_oracle_part(of, k, 2, split_size or -(-of.size // 2)) for k in range(2)])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,split_size", [("2.bam", 102400), ("1.bam", 0)])
+def test_gpu_rccl_exchange_one_rank(tmp_path, name, split_size):
+    """The load path's exchange over RCCL (backend "nccl": device tensors, all_gather_object)
+    with the one rank a one-GPU box allows; the splits and counts equal the oracle's."""
+    path = golden_bam(name)
+    res = _run_gpu_ranks(tmp_path, path, split_size, 1 << 20, world=1, env_extra={"SBH_TEST_BACKEND": "nccl"})
+    of = OracleFile.from_path(path)
+    ref_splits, ref_counts = oracle_splits(of, split_size or of.size)
+    assert res[0]["counts"] == ref_counts and [tuple(x) for x in res[0]["splits"]] == ref_splits
+    assert res[0]["ok"]
 
 
 def _synth_file(tmp_path, seed, shape, nrec, name):
