@@ -10,6 +10,9 @@
 // reported.  No CRC is checked (the reference does not check it either).
 //
 // Design (MI355X-first):
+//  * k_hdr -- the first deflate block of a BGZF block starts at its first data bit, so
+//    its dynamic header is decoded and tabled before k_huff, one 64-lane wave per block,
+//    into the end of the block's token region; k_huff copies the tables into LDS.
 //  * k_huff -- Huffman decode to LZ77 tokens.  One 256-lane workgroup per BGZF block
 //    stages the deflate bytes in LDS and decodes lane-parallel: each lane takes a slice
 //    of the bits, decodes speculatively (Huffman/DEFLATE self-synchronises), repairs
@@ -922,7 +925,20 @@ constexpr uint32_t PAR_MIN_USIZE = 4096;     // smaller blocks decode serially
 #endif
 constexpr uint32_t MIN_SLICE = SBH_MIN_SLICE;  // bits per lane at least
 constexpr uint32_t NOPOS = 0xffffffffu;
-constexpr uint32_t CK1 = 6, CK2 = 24;  // pass-1 checkpoints (tokens)
+// k_hdr's output, at the end of a block's token region (dwords)
+constexpr uint32_t HDR_SENT = (1u << LIT_FAST) + (1u << PDIST_FAST);  // after the PAR tables
+constexpr uint32_t HDR_PK = HDR_SENT + 320;
+constexpr uint32_t HDR_PSYM = HDR_PK + 32, HDR_LAST = HDR_PSYM + 1, HDR_STATUS = HDR_PSYM + 2;
+constexpr uint32_t HDR_OUT_DW = HDR_PSYM + 4;
+constexpr uint32_t HDR_OK = 0x48445231u;
+constexpr uint32_t HDR_STAGE_DW = 160;  // deflate dwords k_hdr stages (a header is < 2.5 kbit)
+static_assert(HDR_OUT_DW < PAR_MIN_USIZE, "the header record fits the token region of every parallel block");
+static_assert(HDR_SENT % SBH_HT == 0, "k_huff copies the tables in whole rounds");
+#ifndef SBH_CK1  // (A/B at 4 M records: 4/16, 6/24, 8/32, 10/40 within 2%)
+#define SBH_CK1 8
+#define SBH_CK2 32
+#endif
+constexpr uint32_t CK1 = SBH_CK1, CK2 = SBH_CK2;  // pass-1 checkpoints (tokens)
 constexpr uint32_t LR_RUN = 0, LR_EOB = 1, LR_DEAD = 2, LR_PAST = 3;
 #ifdef SBH_HUFF_PROBE
 // whole-kernel phase sums (cycles): 0 stage, 1 header, 2 pass 1, 3 repair, 4 emit, 5 repair
@@ -1072,6 +1088,86 @@ __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, Src<LDS> src, uin
   return r;
 }
 
+// The code-length part of a dynamic block header (RFC 1951 3.2.7) by one wave: the
+// code-length code, then the nlen + ndist lengths into t.lens ([0, 288) lit/len, [288,
+// 320) dist).  The code-length symbols are decoded 64 bit positions at a time -- lane i
+// decodes the symbol that would start at q + i -- and the wave walks the chain through
+// those with v_readlane, writing each run of lengths with one vector store.  Returns
+// (uniformly) whether the lengths are well formed and include an end-of-block code;
+// q: the bit after the header.  `p` is the block's first bit (BFINAL).
+template <class S>
+__device__ __forceinline__ bool hdr_walk(WaveSmem &t, const S &src, uint32_t p, uint32_t limit, uint32_t nlen,
+                                         uint32_t ndist, uint32_t ncode, uint32_t lane, uint32_t &q_out,
+                                         uint64_t *h1, uint64_t *h2) {
+  if (lane < 19) t.cl_lens[CL_ORDER[lane]] = lane < ncode ? (uint8_t)(src.bits32(p + 17 + 3 * lane) & 7) : 0;
+  __builtin_amdgcn_wave_barrier();
+  bool ok = uni(build_table(t, t.cl_lens, 19, 2, t.lit, CL_FAST, lane)) == 0;
+  if (h1) *h1 = __builtin_readcyclecounter();
+  for (uint32_t w = lane; w < 320 / 4; w += WAVE) reinterpret_cast<uint32_t *>(t.lens)[w] = 0;
+  __builtin_amdgcn_wave_barrier();
+  const uint32_t total = nlen + ndist;
+  uint32_t i = 0, prev = 0, q = p + 17 + 3 * ncode;
+  const uint64_t below = (1ull << lane) - 1;  // lanes under this one
+  while (ok && i < total && q <= limit) {
+    // every lane decodes the symbol that would start at q + lane
+    const uint32_t b = src.bits32(q + lane);
+    const uint32_t e = t.lit[b & ((1u << CL_FAST) - 1)];
+    const uint32_t L = e & 31, sym = (e >> 8) & 31;
+    const uint32_t xb = sym < 16 ? 0 : sym == 16 ? 2 : sym == 17 ? 3 : 7;
+    const uint32_t xv = __builtin_amdgcn_ubfe(b, L, xb);
+    const uint32_t rep = sym < 16 ? 1 : sym == 16 ? 3 + xv : sym == 17 ? 3 + xv : 11 + xv;
+    const uint32_t pack = (L + xb) | (rep << 8);
+    // serial part: the chain of symbol starts through this window
+    uint64_t M = 0;
+    uint32_t o = 0, i0 = i;
+    while (o < WAVE && i < total) {
+      const uint32_t inf = __builtin_amdgcn_readlane(pack, o);
+      M |= 1ull << o;
+      o += inf & 255;
+      i += inf >> 8;
+    }
+    // parallel part: output index and value of each symbol, then its run of lengths
+    const bool mine = (M >> lane) & 1;
+    uint32_t ex;  // exclusive prefix of rep over the window's symbols
+    {
+      const uint32_t x = wave_incl_scan(mine ? rep : 0);
+      ex = x - (mine ? rep : 0);
+    }
+    const uint32_t start = i0 + ex;
+    const uint64_t N = M & __ballot(sym != 16);  // symbols with a value of their own
+    const uint64_t lowN = N & below;
+    const uint32_t own = sym < 16 ? sym : 0;
+    const uint32_t src_lane = lowN ? 63 - (uint32_t)__builtin_clzll(lowN) : 0;
+    const uint32_t from = __shfl(own, src_lane, WAVE);
+    const uint32_t val = sym == 16 ? (lowN ? from : prev) : own;
+    if (M & 1 && __builtin_amdgcn_readfirstlane(sym) == 16 && i0 == 0) ok = false;  // repeat with no previous length
+    if (mine && val != 0) {  // the run [start, start + rep) of lengths (zeros: pre-set); distances at 288
+      const uint32_t e = min(start + rep, total);
+      const uint32_t v4 = val * 0x01010101u;
+      for (uint32_t j = start; j < e;) {
+        const uint32_t d = j < nlen ? j : 288 + j - nlen;
+        const uint32_t seg_end = j < nlen ? min(e, nlen) : e;  // don't cross the lit/dist split
+        if ((d & 3) == 0 && j + 4 <= seg_end) {
+          *reinterpret_cast<uint32_t *>(&t.lens[d]) = v4;
+          j += 4;
+        } else {
+          t.lens[d] = (uint8_t)val;
+          ++j;
+        }
+      }
+    }
+    const uint32_t top = 63 - (uint32_t)__builtin_clzll(M);
+    prev = __builtin_amdgcn_readlane(val, top);
+    q += o;
+  }
+  if (i != total || q > limit) ok = false;  // a repeat past the end, or input ran out
+  __builtin_amdgcn_wave_barrier();
+  if (h2) *h2 = __builtin_readcyclecounter();
+  if (ok && uni(t.lens[256]) == 0) ok = false;  // no end-of-block code
+  q_out = q;
+  return ok;
+}
+
 // Deflate block header and tables for the lane-parallel path, read from the bit source
 // (sm.ctl[5..6] carry wave 0's result to the workgroup).  The code-length symbols are
 // decoded 64 bit positions at a time -- lane i decodes the symbol that would start at
@@ -1129,75 +1225,12 @@ __device__ __forceinline__ bool par_header(HuffSmem &sm, Src<LDS> src, uint32_t 
   uint64_t h1 = 0, h2 = 0;
 #endif
   if (wid == 0) {
-    if (lane < 19) t.cl_lens[CL_ORDER[lane]] = lane < ncode ? (uint8_t)(src.bits32(p + 17 + 3 * lane) & 7) : 0;
-    __builtin_amdgcn_wave_barrier();
-    bool ok = uni(build_table(t, t.cl_lens, 19, 2, t.lit, CL_FAST, lane)) == 0;
+    uint32_t q;
 #ifdef SBH_HUFF_PROBE
-    h1 = __builtin_readcyclecounter();
+    const bool ok = hdr_walk(t, src, p, limit, nlen, ndist, ncode, lane, q, &h1, &h2);
+#else
+    const bool ok = hdr_walk(t, src, p, limit, nlen, ndist, ncode, lane, q, nullptr, nullptr);
 #endif
-    for (uint32_t w = lane; w < 320 / 4; w += WAVE) reinterpret_cast<uint32_t *>(t.lens)[w] = 0;
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t total = nlen + ndist;
-    uint32_t i = 0, prev = 0, q = p + 17 + 3 * ncode;
-    const uint64_t below = (1ull << lane) - 1;  // lanes under this one
-    while (ok && i < total) {
-      // every lane decodes the symbol that would start at q + lane
-      const uint32_t b = src.bits32(q + lane);
-      const uint32_t e = t.lit[b & ((1u << CL_FAST) - 1)];
-      const uint32_t L = e & 31, sym = (e >> 8) & 31;
-      const uint32_t xb = sym < 16 ? 0 : sym == 16 ? 2 : sym == 17 ? 3 : 7;
-      const uint32_t xv = __builtin_amdgcn_ubfe(b, L, xb);
-      const uint32_t rep = sym < 16 ? 1 : sym == 16 ? 3 + xv : sym == 17 ? 3 + xv : 11 + xv;
-      const uint32_t pack = (L + xb) | (rep << 8);
-      // serial part: the chain of symbol starts through this window
-      uint64_t M = 0;
-      uint32_t o = 0, i0 = i;
-      while (o < WAVE && i < total) {
-        const uint32_t inf = __builtin_amdgcn_readlane(pack, o);
-        M |= 1ull << o;
-        o += inf & 255;
-        i += inf >> 8;
-      }
-      // parallel part: output index and value of each symbol, then its run of lengths
-      const bool mine = (M >> lane) & 1;
-      uint32_t ex;  // exclusive prefix of rep over the window's symbols
-      {
-        const uint32_t x = wave_incl_scan(mine ? rep : 0);
-        ex = x - (mine ? rep : 0);
-      }
-      const uint32_t start = i0 + ex;
-      const uint64_t N = M & __ballot(sym != 16);  // symbols with a value of their own
-      const uint64_t lowN = N & below;
-      const uint32_t own = sym < 16 ? sym : 0;
-      const uint32_t src_lane = lowN ? 63 - (uint32_t)__builtin_clzll(lowN) : 0;
-      const uint32_t from = __shfl(own, src_lane, WAVE);
-      const uint32_t val = sym == 16 ? (lowN ? from : prev) : own;
-      if (M & 1 && __builtin_amdgcn_readfirstlane(sym) == 16 && i0 == 0) ok = false;  // repeat with no previous length
-      if (mine && val != 0) {  // the run [start, start + rep) of lengths (zeros: pre-set); distances at 288
-        const uint32_t e = min(start + rep, total);
-        const uint32_t v4 = val * 0x01010101u;
-        for (uint32_t j = start; j < e;) {
-          const uint32_t d = j < nlen ? j : 288 + j - nlen;
-          const uint32_t seg_end = j < nlen ? min(e, nlen) : e;  // don't cross the lit/dist split
-          if ((d & 3) == 0 && j + 4 <= seg_end) {
-            *reinterpret_cast<uint32_t *>(&t.lens[d]) = v4;
-            j += 4;
-          } else {
-            t.lens[d] = (uint8_t)val;
-            ++j;
-          }
-        }
-      }
-      const uint32_t top = 63 - (uint32_t)__builtin_clzll(M);
-      prev = __builtin_amdgcn_readlane(val, top);
-      q += o;
-    }
-    if (i != total || q > limit) ok = false;  // a repeat past the end, or input ran out
-    __builtin_amdgcn_wave_barrier();
-#ifdef SBH_HUFF_PROBE
-    h2 = __builtin_readcyclecounter();
-#endif
-    if (ok && uni(t.lens[256]) == 0) ok = false;  // no end-of-block code
     if (lane == 0) {
       sm.ctl[5] = ok;
       sm.ctl[6] = q;
@@ -1227,7 +1260,7 @@ __device__ __forceinline__ bool par_header(HuffSmem &sm, Src<LDS> src, uint32_t 
 template <bool LDS>
 __device__ __forceinline__ bool inflate_par(HuffSmem &sm, const uint8_t *__restrict__ comp, uint32_t a0, uint32_t skip,
                             uint32_t limit, uint32_t usize, uint32_t *__restrict__ tk, uint32_t tid, uint32_t lane,
-                            uint32_t wid, uint32_t &ntok_out) {
+                            uint32_t wid, uint32_t &ntok_out, bool pre, uint32_t pre_psym, uint32_t pre_last) {
   const Src<LDS> src{LDS ? sm.stage : reinterpret_cast<const uint32_t *>(comp) + a0};
   uint32_t p = skip, out = 0, ntok = 0;
   bool fixed_built = false;  // the tables in sm.t are the fixed code's
@@ -1236,7 +1269,13 @@ __device__ __forceinline__ bool inflate_par(HuffSmem &sm, const uint8_t *__restr
     const uint64_t tp0 = __builtin_readcyclecounter();
 #endif
     uint32_t p0, last;
-    if (!par_header(sm, src, p, limit, fixed_built, wid, lane, p0, last)) return false;
+    if (pre) {  // the first deflate block's tables came from k_hdr (already in sm.t)
+      p0 = pre_psym;
+      last = pre_last;
+      pre = false;
+    } else if (!par_header(sm, src, p, limit, fixed_built, wid, lane, p0, last)) {
+      return false;
+    }
     if (tid == 0) sm.ctl[3] = HT;
 
 #ifdef SBH_HUFF_PROBE
@@ -1250,9 +1289,11 @@ __device__ __forceinline__ bool inflate_par(HuffSmem &sm, const uint8_t *__restr
     Ckpt ck;
     const LaneRun none{};
     LaneRun r = lane_run<LDS, RUN_SPEC>(sm.t, src, A, stop, limit, ck, none, nullptr, 0, nobad);
+    const LaneRun r1 = r;  // the pass-1 chain's result: a redo that joins it at a checkpoint takes its rest
     sm.exitv[tid] = r.st == LR_RUN ? r.exit : NOPOS;
     // pass 2: repair rounds until every lane starts where its left neighbour exits.
-    // A repair run stops as soon as it joins the lane's pass-1 chain (first round only).
+    // A repair run stops as soon as it joins the lane's pass-1 chain (in any round: the
+    // pass-1 result from a checkpoint on holds for every chain that reaches it).
 #ifdef SBH_HUFF_PROBE
     uint32_t nrounds = 0;
     __syncthreads();
@@ -1270,10 +1311,9 @@ __device__ __forceinline__ bool inflate_par(HuffSmem &sm, const uint8_t *__restr
       __syncthreads();
       if (changed) {
         A = nA;
-        r = lane_run<LDS, RUN_REDO>(sm.t, src, A, stop, limit, ck, r, nullptr, 0, nobad);
+        r = lane_run<LDS, RUN_REDO>(sm.t, src, A, stop, limit, ck, r1, nullptr, 0, nobad);
         sm.exitv[tid] = r.st == LR_RUN ? r.exit : NOPOS;
       }
-      ck = Ckpt{NOPOS, 0, NOPOS, 0};  // later rounds: the chain changed, run fully
       const bool again = __syncthreads_or(changed);
 #ifdef SBH_HUFF_PROBE
       if (tid == 0 && nrounds == 1) atomicAdd(&hp_acc[12], __builtin_readcyclecounter() - tp1);
@@ -1322,6 +1362,83 @@ __device__ __forceinline__ bool inflate_par(HuffSmem &sm, const uint8_t *__restr
   return true;
 }
 
+// First-header pre-pass: the first deflate block of every BGZF block starts at the
+// block's first data bit, so its dynamic header (code-length walk, canonical tables) can
+// be decoded before k_huff runs, by one small wave per block at high occupancy, instead
+// of on k_huff's critical path with three of its four waves idle.  The PAR tables, the
+// sorted entries / limits slow_lane reads, the bit after the header and BFINAL go to
+// the end of the block's token region (k_huff copies them into LDS before it writes a
+// token).  Anything this pass does not accept (fixed / stored first block, a header
+// longer than the staged bits, any invalid code) leaves HDR_STATUS != HDR_OK and k_huff
+// decodes that header itself, so results are unchanged.
+struct HdrSrc {  // bits of the staged dwords [0, n) (clamped reads past them are never used)
+  const uint32_t *p;
+  uint32_t n;
+  __device__ __forceinline__ uint32_t bits32(uint32_t pos) const {
+    const uint32_t i = pos >> 5;
+    const uint32_t a = p[i < n ? i : n - 1], b = p[i + 1 < n ? i + 1 : n - 1];
+    return __builtin_amdgcn_alignbit(b, a, pos & 31);
+  }
+};
+
+__device__ __forceinline__ bool huff_serial_block(const DevBlocks &bl, uint64_t b) {
+  const uint32_t csize = bl.csize[b], hsize = bl.hsize[b], usize = bl.usize[b];
+  return (bl.flags[b] & BLK_TRUNCATED) || usize > 65536u || usize < PAR_MIN_USIZE ||
+         (int32_t)csize - (int32_t)hsize - 8 < 0;
+}
+
+__global__ __launch_bounds__(WAVE) void k_hdr(const uint8_t *__restrict__ comp, DevBlocks bl, uint64_t nblocks,
+                                              uint32_t *__restrict__ tok) {
+  __shared__ WaveSmem t;
+  __shared__ uint32_t stage[HDR_STAGE_DW];
+  const uint64_t b = blockIdx.x;
+  if (b >= nblocks || huff_serial_block(bl, b)) return;
+  const uint32_t lane = threadIdx.x;
+  const uint64_t cstart = bl.cstart[b];
+  const uint32_t csize = bl.csize[b], hsize = bl.hsize[b], usize = bl.usize[b];
+  const uint32_t data_len = csize - hsize - 8;
+  const uint64_t dbyte = cstart + hsize;
+  const uint32_t a0 = (uint32_t)(dbyte >> 2), skip = (uint32_t)(dbyte & 3) * 8;
+  const uint32_t limit = skip + data_len * 8;
+  const uint32_t ndw = min((limit + 31) / 32 + 2, HDR_STAGE_DW);
+  const uint32_t *g = reinterpret_cast<const uint32_t *>(comp) + a0;
+  for (uint32_t i = lane; i < ndw; i += WAVE) stage[i] = g[i];
+  __syncthreads();
+  uint32_t *out = tok + bl.ustart[b] + usize - HDR_OUT_DW;
+  const HdrSrc src{stage, ndw};
+  // every code-length symbol start the walk visits keeps its 32-bit reads inside the stage
+  const uint32_t lim = min(limit, ndw * 32 > 96 ? ndw * 32 - 96 : 0u);
+  const uint32_t hb = uni(src.bits32(skip));
+  const uint32_t nlen = ((hb >> 3) & 31) + 257, ndist = ((hb >> 8) & 31) + 1, ncode = ((hb >> 13) & 15) + 4;
+  bool ok = ((hb >> 1) & 3) == 2 && skip + 17 <= lim && nlen <= 286 && ndist <= 30;
+  uint32_t q = 0;
+  if (ok) ok = hdr_walk(t, src, skip, lim, nlen, ndist, ncode, lane, q, nullptr, nullptr);
+  if (ok) {
+    const uint32_t r0 = ptable_meta(t, t.lens, nlen, 0, lane);
+    const uint32_t r1 = ptable_meta(t, t.lens + 288, ndist, 1, lane);
+    ok = r0 != 1 && r1 != 1;
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (ok) {
+    uint32_t lj0[16], lj1[16];
+#pragma unroll
+    for (uint32_t v = 1; v <= 15; ++v) {
+      lj0[v] = t.pk[0][v] >> 16;
+      lj1[v] = t.pk[1][v] >> 16;
+    }
+    for (uint32_t i = lane; i < (1u << LIT_FAST); i += WAVE) out[i] = ptable_entry(t, lj0, 0, LIT_FAST, i);
+    for (uint32_t i = lane; i < (1u << PDIST_FAST); i += WAVE)
+      out[(1u << LIT_FAST) + i] = ptable_entry(t, lj1, 1, PDIST_FAST, i);
+    for (uint32_t i = lane; i < 320; i += WAVE) out[HDR_SENT + i] = t.sent[i];
+    if (lane < 32) out[HDR_PK + lane] = t.pk[lane >> 4][lane & 15];
+    if (lane == 0) {
+      out[HDR_PSYM] = q;
+      out[HDR_LAST] = hb & 1;
+    }
+  }
+  if (lane == 0) out[HDR_STATUS] = ok ? HDR_OK : 0u;
+}
+
 __global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__restrict__ comp, DevBlocks bl, uint64_t nblocks,
                                               uint32_t *__restrict__ tok) {
   __shared__ HuffSmem sm;
@@ -1331,8 +1448,7 @@ __global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__rest
   const uint64_t cstart = bl.cstart[b];
   const uint32_t csize = bl.csize[b], hsize = bl.hsize[b], usize = bl.usize[b];
   const uint64_t G = bl.ustart[b];
-  const bool serial = (bl.flags[b] & BLK_TRUNCATED) || usize > 65536u || usize < PAR_MIN_USIZE ||
-                (int32_t)csize - (int32_t)hsize - 8 < 0;
+  const bool serial = huff_serial_block(bl, b);
 #ifdef SBH_HUFF_PROBE
   const uint64_t hk0 = __builtin_readcyclecounter();
 #endif
@@ -1345,16 +1461,49 @@ __global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__rest
     const uint32_t ndw = (limit + 31) / 32 + 2;
     uint32_t ntok = 0;
     bool ok;
+    // the first deflate block's header, decoded and tabled by k_hdr at the end of this
+    // block's token region (read here before any token is written over it)
+    const uint32_t *hd = tok + G + usize - HDR_OUT_DW;
+    const bool pre = uni(hd[HDR_STATUS]) == HDR_OK;
+    uint32_t pre_psym = 0, pre_last = 0;
+    // the record's dwords go to registers first, so their loads are in flight together
+    // with the stage's and only the LDS stores wait
+    constexpr uint32_t NTV = HDR_SENT / HT, NSV = (320 + 32 + HT - 1) / HT;
+    uint32_t tv[NTV], sv[NSV];
+    if (pre) {
+#pragma unroll
+      for (uint32_t k = 0; k < NTV; ++k) tv[k] = hd[tid + k * HT];
+#pragma unroll
+      for (uint32_t k = 0; k < NSV; ++k) sv[k] = tid + k * HT < 352 ? hd[HDR_SENT + tid + k * HT] : 0u;
+      pre_psym = uni(hd[HDR_PSYM]);
+      pre_last = uni(hd[HDR_LAST]);
+    }
+    auto put_tables = [&]() {
+#pragma unroll
+      for (uint32_t k = 0; k < NTV; ++k) sm.t.tab[tid + k * HT] = tv[k];
+#pragma unroll
+      for (uint32_t k = 0; k < NSV; ++k) {  // sent[320] then pk[2][16]
+        const uint32_t i = tid + k * HT;
+        if (i < 320) sm.t.sent[i] = sv[k];
+        else if (i < 352) sm.t.pk[(i - 320) >> 4][(i - 320) & 15] = sv[k];
+      }
+    };
     if (ndw <= STAGE_DW) {
       const uint32_t *g = reinterpret_cast<const uint32_t *>(comp) + a0;
       for (uint32_t i = tid; i < ndw; i += HT) sm.stage[i] = g[i];
+      if (pre) put_tables();
       __syncthreads();
 #ifdef SBH_HUFF_PROBE
       if (tid == 0) atomicAdd(&hp_acc[0], __builtin_readcyclecounter() - hk0);
 #endif
-      ok = inflate_par<true>(sm, comp, a0, skip, limit, usize, tok + G, tid, lane, wid, ntok);
+      ok = inflate_par<true>(sm, comp, a0, skip, limit, usize, tok + G, tid, lane, wid, ntok, pre, pre_psym, pre_last);
     } else {
-      ok = inflate_par<false>(sm, comp, a0, skip, limit, usize, tok + G, tid, lane, wid, ntok);
+      if (pre) {
+        put_tables();
+        __syncthreads();
+      }
+      ok = inflate_par<false>(sm, comp, a0, skip, limit, usize, tok + G, tid, lane, wid, ntok, pre, pre_psym,
+                              pre_last);
     }
     if (uni(ok)) {
       if (tid == 0) {
@@ -1813,6 +1962,7 @@ hipError_t launch_huff(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, 
   hipLaunchKernelGGL(k_huff_serial<false>, dim3((uint32_t)grid), dim3(WAVES * WAVE), 0, stream, comp, blocks, nblocks,
                      tok);
 #else
+  hipLaunchKernelGGL(k_hdr, dim3((uint32_t)nblocks), dim3(WAVE), 0, stream, comp, blocks, nblocks, tok);
   hipLaunchKernelGGL(k_huff, dim3((uint32_t)nblocks), dim3(HT), 0, stream, comp, blocks, nblocks, tok);
   const uint64_t grid = (nblocks + WAVES - 1) / WAVES;
   hipLaunchKernelGGL(k_huff_serial<true>, dim3((uint32_t)grid), dim3(WAVES * WAVE), 0, stream, comp, blocks, nblocks,
