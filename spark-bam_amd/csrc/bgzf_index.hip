@@ -121,18 +121,27 @@ __global__ __launch_bounds__(256) void k_cand_count(const uint8_t *comp, uint64_
   __syncthreads();
   const uint64_t cbase = (uint64_t)blockIdx.x * CHUNK;
   uint32_t mine = 0, myfirst = ~0u;
+  constexpr uint32_t NV = CHUNK / 4096;
+  // all of the thread's 16-byte loads in flight at once (whole chunks: no per-load test)
+  uint4 vv[NV];
+  if (cbase + CHUNK <= n) {
 #pragma unroll
-  for (uint32_t i = 0; i < CHUNK / 4096; ++i) {
-    const uint32_t o0 = i * 4096 + threadIdx.x * 16;
-    const uint64_t p0 = cbase + o0;
-    uint4 v;
-    if (p0 + 16 <= n) {
-      v = *reinterpret_cast<const uint4 *>(comp + p0);
-    } else {  // ragged end of the shard
+    for (uint32_t i = 0; i < NV; ++i)
+      vv[i] = *reinterpret_cast<const uint4 *>(comp + cbase + i * 4096 + threadIdx.x * 16);
+  } else {  // ragged end of the shard
+#pragma unroll
+    for (uint32_t i = 0; i < NV; ++i) {
+      const uint64_t p0 = cbase + i * 4096 + threadIdx.x * 16;
       uint32_t w[4] = {0, 0, 0, 0};
       for (uint32_t k = 0; k < 16 && p0 + k < n; ++k) w[k >> 2] |= (uint32_t)comp[p0 + k] << (8 * (k & 3));
-      v = make_uint4(w[0], w[1], w[2], w[3]);
+      vv[i] = make_uint4(w[0], w[1], w[2], w[3]);
     }
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < NV; ++i) {
+    const uint32_t o0 = i * 4096 + threadIdx.x * 16;
+    const uint64_t p0 = cbase + o0;
+    const uint4 v = vv[i];
     const uint32_t m[4] = {bytes_eq31(v.x), bytes_eq31(v.y), bytes_eq31(v.z), bytes_eq31(v.w)};
     if (m[0] | m[1] | m[2] | m[3]) {
       for (uint32_t q = 0; q < 4; ++q) {
