@@ -330,30 +330,84 @@ constexpr uint32_t ESTAGE = EW + 512;     // staged bytes (records near the end 
 constexpr uint32_t EQ_CHUNK = 4096;       // survivor-queue capacity
 static_assert(EAGER_REACH >= ESTAGE + 32 + 16, "EAGER_REACH covers the staged window");
 
+// PosChecker.getRefPosError with the contig length already loaded (len_idx: len[idx]
+// when 0 <= idx < n, else unused).
+__device__ __forceinline__ uint32_t ref_pos_error_l(int32_t idx, int32_t pos, int32_t len_idx, const Ctg &c) {
+  if (idx < -1) return pos < -1 ? 5u : 1u;
+  if (idx >= c.n) return pos < -1 ? 6u : 2u;
+  if (pos < -1) return 4u;
+  if (idx >= 0 && (int64_t)pos > (int64_t)len_idx) return 8u;
+  return 0;
+}
+
 // Single-record eager predicate at q, with cur == start == q, reading only the
 // staged window: 0 fail, 1 pass, 2 cannot decide from the window (or EOF edge).
 // On pass, *succ = the next record start (nominal), *normal = nominal >= cursor
 // after name + cigar (so the next record is read at nominal).
+// Latency-shaped: the fixed fields and the first 32 read-name bytes come from one batch
+// of 18 LDS dword reads, and both contig lengths are loaded beside them, so a record
+// costs about three dependent round trips (fields, then CIGAR op bytes) instead of one
+// per field; the tests run in the reference's order on the loaded values.
 __device__ __forceinline__ uint32_t one_record(const Src &s, uint64_t q, uint64_t total, const Ctg &c,
                                                uint64_t *succ, bool *normal) {
   if (q + 36 > total) return 2;                       // EOF rules: exact path
   if (q - s.s0 + 36 + 8 > s.sn) return 2;
+  const uint32_t w = (uint32_t)(q - s.s0), i = w >> 2, k = w & 3;
+  // dwords [i, i + 18): bytes [w, w + 68) (the staged array holds sn + 32 bytes, and
+  // w + 44 <= sn); bytes past sn are read but only used below need <= sn
+  uint32_t d[18];
+#pragma unroll
+  for (uint32_t j = 0; j < 18; ++j) d[j] = s.lds32[i + j];
+  auto fld = [&](uint32_t j) { return __builtin_amdgcn_alignbyte(d[j + 1], d[j], k); };
+  const int32_t ref = (int32_t)fld(1), pos = (int32_t)fld(2), nrf = (int32_t)fld(6), nps = (int32_t)fld(7);
+  const int32_t l1 = ref >= 0 && ref < c.n ? c.len[ref] : 0;
+  const int32_t l2 = nrf >= 0 && nrf < c.n ? c.len[nrf] : 0;
   // most selective predicate first: refID / pos (99% of positions fail here)
-  if (ref_pos_error((int32_t)s.word_at(q + 4), (int32_t)s.word_at(q + 8), c)) return 0;
-  const int32_t rnl = (int32_t)(s.word_at(q + 12) & 0xff);
+  if (ref_pos_error_l(ref, pos, l1, c)) return 0;
+  const int32_t rnl = (int32_t)(fld(3) & 0xff);
   if (rnl < 2) return 0;
-  const uint32_t fnc = s.word_at(q + 16);
+  const uint32_t fnc = fld(4);
   const int32_t nc = (int32_t)(fnc & 0xffff);
-  const int32_t seq_len = (int32_t)s.word_at(q + 20);
+  const int32_t seq_len = (int32_t)fld(5);
   if (((fnc >> 16) & 4) == 0 && (seq_len == 0 || nc == 0)) return 0;
-  const int32_t rem = (int32_t)s.word_at(q);
+  const int32_t rem = (int32_t)fld(0);
   if (rem < implied_min_remaining(rnl, nc, seq_len)) return 0;
-  if (ref_pos_error((int32_t)s.word_at(q + 24), (int32_t)s.word_at(q + 28), c)) return 0;
+  if (ref_pos_error_l(nrf, nps, l2, c)) return 0;
   uint64_t cur = q + 36;
   const uint64_t need = cur + (uint64_t)rnl + 4ull * (uint64_t)nc;
   if (need > total || need - s.s0 > s.sn) return 2;
-  if (s.byte_at(cur + rnl - 1) != 0) return 0;
-  if (!name_bytes_ok(s, cur, (uint32_t)rnl - 1)) return 0;
+  // the name: NUL at rnl - 1, then every byte before it a valid name character
+  const uint32_t nn = (uint32_t)rnl - 1;
+  uint32_t nul;
+  if (nn < 32) {
+    const uint32_t m = nn >> 2;
+    uint32_t x = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) x = j == m ? fld(9 + j) : x;
+    nul = (x >> (8 * (nn & 3))) & 0xff;
+  } else {
+    nul = s.byte_at(cur + nn);
+  }
+  if (nul != 0) return 0;
+  {
+    const uint32_t n0 = nn < 32 ? nn : 32u;
+    uint32_t bad = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+      const uint32_t b0 = 4 * j;
+      uint32_t x = fld(9 + j);
+      if (b0 + 4 > n0) {
+        const uint32_t keep = b0 >= n0 ? 0u : (1u << (8 * (n0 - b0))) - 1u;
+        x = (x & keep) | (0x41414141u & ~keep);
+      }
+      bad |= (x - 0x21212121u) & ~x & 0x80808080u;        // a byte < 0x21
+      bad |= ((x + 0x01010101u) | x) & 0x80808080u;        // a byte > 0x7e
+      const uint32_t y = x ^ 0x40404040u;
+      bad |= (y - 0x01010101u) & ~y & 0x80808080u;         // a byte == 0x40 ('@')
+    }
+    if (bad) return 0;
+    if (nn > 32 && !name_bytes_ok(s, cur + 32, nn - 32)) return 0;
+  }
   cur += rnl;
   if (first_bad_op(s, cur, (uint32_t)nc, cur + 4ull * (uint32_t)nc) < (uint32_t)nc) return 0;
   cur += 4ull * (uint32_t)nc;
@@ -410,7 +464,7 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
   const uint32_t lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
 #ifdef SBH_EPROBE
   const uint64_t c1 = __builtin_readcyclecounter();
-  uint64_t c1a = 0, c1b = 0, c2 = 0;
+  uint64_t c1a = 0, c1b = 0, c2 = 0, c3 = 0, c4 = 0;
 #endif
   // single-record predicate at window position i -> ok / nrm / und bits
   auto eval_one = [&](uint32_t i) {
@@ -648,6 +702,9 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
       else if (g + 1 < nc3 && entry(g + 1) == jn) atomicOr(&lnk[g >> 5], 1u << (g & 31));
     }
     __syncthreads();
+#ifdef SBH_EPROBE
+    c3 = __builtin_readcyclecounter();
+#endif
     const uint32_t need = (uint32_t)rtc - 1;  // steps from a candidate to its rtc-th record
     for (uint32_t g = threadIdx.x; g < nc3; g += T) {
       const uint32_t i = entry(g);
@@ -677,6 +734,9 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
       settle(i, r);
     }
     __syncthreads();
+#ifdef SBH_EPROBE
+    c4 = __builtin_readcyclecounter();
+#endif
     write_res();
   } else {
     // ---- fallback (a survivor list overflowed, or rtc <= 0): per-thread survivor loop
@@ -751,10 +811,12 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
   atomicAdd(&pexact, nexact);
   __syncthreads();
   if (threadIdx.x == 0 && blockIdx.x >= 3000 && blockIdx.x < 3008)
-    printf("eager wg %u fast %d stage %llu A1+2 %llu eval %llu cand %llu B %llu surv %u exactcalls %u true %u exact %u\n",
+    printf("eager wg %u fast %d stage %llu A1+2 %llu eval %llu cand %llu B %llu (links %llu calls %llu tail %llu) surv %u exactcalls %u true %u exact %u\n",
            blockIdx.x, (int)fast, (unsigned long long)(c1 - c0), (unsigned long long)(c1a - c1),
            (unsigned long long)(c1b - c1a), (unsigned long long)(c2 - c1b),
-           (unsigned long long)(__builtin_readcyclecounter() - c2), psurv, pcand, ntrue, pexact);
+           (unsigned long long)(__builtin_readcyclecounter() - c2), (unsigned long long)(c3 - c2),
+           (unsigned long long)(c4 - c3), (unsigned long long)(__builtin_readcyclecounter() - c4), psurv, pcand, ntrue,
+           pexact);
 #endif
 }
 
