@@ -327,7 +327,10 @@ constexpr uint32_t ETILE = SBH_ETILE;     // eager tile: positions per workgroup
 constexpr uint32_t ELA = 4096;            // look-ahead: chains of short reads stay inside
 constexpr uint32_t EW = ETILE + ELA;      // eager window: single-record predicate evaluated here
 constexpr uint32_t ESTAGE = EW + 512;     // staged bytes (records near the end fit)
-constexpr uint32_t EQ_CHUNK = 4096;       // survivor-queue capacity
+#ifndef SBH_EQ_CHUNK
+#define SBH_EQ_CHUNK 4096
+#endif
+constexpr uint32_t EQ_CHUNK = SBH_EQ_CHUNK;  // survivor-queue capacity
 static_assert(EAGER_REACH >= ESTAGE + 32 + 16, "EAGER_REACH covers the staged window");
 
 // PosChecker.getRefPosError with the contig length already loaded (len_idx: len[idx]
@@ -603,6 +606,9 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
       a = b;
     }
   }
+#ifdef SBH_EPROBE
+  const uint64_t c1x = __builtin_readcyclecounter();
+#endif
   // ---- survivor lists: each wave compacts its refID survivors, in position order, into
   // its own queue segment and filters them in place (fixed fields, then the whole
   // single-record predicate), so every step runs one survivor per lane.  The candidate
@@ -643,6 +649,9 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
     return kept;
   };
   uint32_t n2 = 0;
+#ifdef SBH_EPROBE
+  const uint64_t c1y = __builtin_readcyclecounter();
+#endif
   if (wtot1 <= SEGCAP) n2 = compact(wtot1, [&](uint32_t i) { return i >= fast_end || fixed_ok(i); });
   if (lane == 0) wcnt[wid] = wtot1 <= SEGCAP ? n2 : ~0u;
 #ifdef SBH_EPROBE
@@ -811,8 +820,9 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
   atomicAdd(&pexact, nexact);
   __syncthreads();
   if (threadIdx.x == 0 && blockIdx.x >= 3000 && blockIdx.x < 3008)
-    printf("eager wg %u fast %d stage %llu A1+2 %llu eval %llu cand %llu B %llu (links %llu calls %llu tail %llu) surv %u exactcalls %u true %u exact %u\n",
-           blockIdx.x, (int)fast, (unsigned long long)(c1 - c0), (unsigned long long)(c1a - c1),
+    printf("eager wg %u fast %d stage %llu sweep %llu lists %llu A1+2 %llu eval %llu cand %llu B %llu (links %llu calls %llu tail %llu) surv %u exactcalls %u true %u exact %u\n",
+           blockIdx.x, (int)fast, (unsigned long long)(c1 - c0), (unsigned long long)(c1x - c1),
+           (unsigned long long)(c1y - c1x), (unsigned long long)(c1a - c1),
            (unsigned long long)(c1b - c1a), (unsigned long long)(c2 - c1b),
            (unsigned long long)(__builtin_readcyclecounter() - c2), (unsigned long long)(c3 - c2),
            (unsigned long long)(c4 - c3), (unsigned long long)(__builtin_readcyclecounter() - c4), psurv, pcand, ntrue,
@@ -1169,98 +1179,116 @@ __global__ __launch_bounds__(256) void k_first_set(const uint32_t *bits, uint64_
   }
 }
 
-__global__ __launch_bounds__(256) void k_popcount(const uint32_t *bits, uint64_t begin, uint64_t from,
-                                                   uint64_t to, unsigned long long *acc) {
-  __shared__ uint32_t part[4];
-  const uint64_t w0 = (from - begin) / 32;
-  const uint64_t w_end = (to - begin + 31) / 32;
-  uint32_t c = 0;
-  for (uint64_t w = w0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < w_end;
-       w += (uint64_t)gridDim.x * blockDim.x) {
-    uint32_t v = bits[w];
-    const uint64_t p0 = begin + 32 * w;
-    if (p0 < from) v &= ~0u << (uint32_t)(from - p0);
-    if (p0 + 32 > to) v &= (to - p0) >= 32 ? ~0u : ((1u << (uint32_t)(to - p0)) - 1u);
-    c += __popc(v);
-  }
-  for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off);
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t t = part[0] + part[1] + part[2] + part[3];
-    if (t) atomicAdd(acc, (unsigned long long)t);
-  }
-}
-
 // Chain verification over eager-true positions s in [from, E): the record chain
 // (PosStream: next = s + 4 + block_size) must step exactly from each true position
 // to the next true one (or leave [from, E) / reach the stream end).  Any other
 // step is an anomaly (a false positive inside the chain, or a chain record the
 // eager checker rejects); those ranges fall back to an exact sequential walk.
-__global__ __launch_bounds__(256) void k_verify_chain(const uint8_t *U, const uint32_t *bits, uint64_t begin,
-                                                       uint64_t bits_end, uint64_t from, uint64_t E, uint64_t total,
-                                                       unsigned long long *n_anom, unsigned long long *first_anom,
-                                                       unsigned long long *exit_pos) {
-  const uint64_t w = ((from - begin) / 32 & ~3ull) + 4 * ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x);
+// Wave-cooperative, with the popcount of [from, E) folded in (one pass over the bitmap,
+// one host round trip).  A wave covers 64 consecutive 4-word groups: the successor of a lane's last set bit is the first set bit
+// of the next non-empty lane (a readlane), and only the wave's last one looks past the
+// wave -- the whole wave scanning 64 words per step -- so each set bit costs one bitmap
+// load and one U load, and sparse bitmaps (long records) no longer scan word by word.
+__global__ __launch_bounds__(256) void k_verify_chain_w(const uint8_t *U, const uint32_t *bits, uint64_t begin,
+                                                         uint64_t bits_end, uint64_t from, uint64_t E, uint64_t total,
+                                                         unsigned long long *n_anom, unsigned long long *first_anom,
+                                                         unsigned long long *exit_pos, unsigned long long *n_set) {
+  const uint32_t lane = threadIdx.x & (WAVE - 1);
+  const uint64_t W0 = (from - begin) / 32 & ~3ull;
   const uint64_t w_end = (E - begin + 31) / 32;
-  if (w >= w_end) return;
   const uint64_t w_lim = (bits_end - begin + 31) / 32;
-  uint32_t v[4];
-  if (w + 4 <= w_lim) {
-    const uint4 q = *reinterpret_cast<const uint4 *>(bits + w);
-    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
-  } else {
-    for (uint32_t k = 0; k < 4; ++k) v[k] = w + k < w_lim ? bits[w + k] : 0u;
-  }
-  for (uint32_t k = 0; k < 4; ++k) {  // positions outside [from, E)
-    const uint64_t p0 = begin + 32 * (w + k);
-    if (p0 + 32 <= from || p0 >= E) v[k] = 0;
-    else {
-      if (p0 < from) v[k] &= ~0u << (uint32_t)(from - p0);
-      if (p0 + 32 > E) v[k] &= (E - p0) >= 32 ? ~0u : ((1u << (uint32_t)(E - p0)) - 1u);
-    }
-  }
-  // walk the set bits of the 128-position group in order; each one's successor is the
-  // next set bit (in the group, else the first set word after it, bounded by E)
-  uint32_t k = 0;
-  while (k < 4 && !v[k]) ++k;
-  while (k < 4) {
-    const uint32_t b = __builtin_ctz(v[k]);
-    v[k] &= v[k] - 1;
-    const uint64_t s = begin + 32 * (w + k) + b;
-    uint32_t kn = k;
-    while (kn < 4 && !v[kn]) ++kn;
-    uint64_t nxt_set = ~0ull;
-    if (kn < 4) {
-      nxt_set = begin + 32 * (w + kn) + __builtin_ctz(v[kn]);
-    } else {
-      for (uint64_t ww = w + 4; ww < w_lim && begin + 32 * ww < E; ++ww) {
-        const uint32_t x = bits[ww];
-        if (x) { nxt_set = begin + 32 * ww + __builtin_ctz(x); break; }
+  const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / WAVE);
+  uint32_t tot = 0;  // set bits this lane saw (the popcount; one atomic per workgroup)
+  // wave chunks of 64 x 4 words, grid-stride
+  for (uint64_t wc = (uint64_t)blockIdx.x * (blockDim.x / WAVE) + threadIdx.x / WAVE;; wc += nwaves) {
+    const uint64_t wave_w0 = W0 + 4 * WAVE * wc;
+    if (wave_w0 >= w_end) break;
+    const uint64_t w = wave_w0 + 4 * lane;
+    uint32_t v[4] = {0, 0, 0, 0};
+    if (w < w_end) {
+      if (w + 4 <= w_lim) {
+        const uint4 q = *reinterpret_cast<const uint4 *>(bits + w);
+        v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+      } else {
+        for (uint32_t k = 0; k < 4; ++k) v[k] = w + k < w_lim ? bits[w + k] : 0u;
       }
-      if (nxt_set >= E) nxt_set = ~0ull;
+      for (uint32_t k = 0; k < 4; ++k) {  // positions outside [from, E)
+        const uint64_t p0 = begin + 32 * (w + k);
+        if (p0 + 32 <= from || p0 >= E) v[k] = 0;
+        else {
+          if (p0 < from) v[k] &= ~0u << (uint32_t)(from - p0);
+          if (p0 + 32 > E) v[k] &= (E - p0) >= 32 ? ~0u : ((1u << (uint32_t)(E - p0)) - 1u);
+        }
+      }
     }
-    uint64_t step;
-    if (s + 4 > total) {
-      step = ~0ull;  // getInt at EOF: the chain ends here
-    } else {
-      const uint32_t *g = reinterpret_cast<const uint32_t *>(U + (s & ~3ull));
-      const int32_t rem = (int32_t)__builtin_amdgcn_alignbyte(g[1], g[0], (uint32_t)s & 3);
-      step = s + 4 + (int64_t)rem;
+    const uint32_t cnt = __popc(v[0]) + __popc(v[1]) + __popc(v[2]) + __popc(v[3]);
+    tot += cnt;
+    // the lane's first set position (successor of the previous non-empty lane's last bit)
+    uint64_t f = ~0ull;
+    for (int k = 3; k >= 0; --k)
+      if (v[k]) f = begin + 32 * (w + (uint32_t)k) + __builtin_ctz(v[k]);
+    const uint64_t has = __ballot(cnt != 0);
+    if (!has) continue;
+    // next non-empty lane after this one, in this wave
+    const uint64_t after = lane == WAVE - 1 ? 0ull : has & (~0ull << (lane + 1));
+    const uint32_t nl = after ? (uint32_t)__builtin_ctzll(after) : 0u;
+    const uint32_t f_lo = __shfl((uint32_t)f, nl, WAVE), f_hi = __shfl((uint32_t)(f >> 32), nl, WAVE);
+    uint64_t lane_next = after ? ((uint64_t)f_hi << 32 | f_lo) : ~0ull;
+    // past the wave: the first set bit at or after the wave's end (uniform scan; bounded by E)
+    const uint32_t top = 63 - (uint32_t)__builtin_clzll(has);
+    uint64_t past = ~0ull;
+    for (uint64_t ww = wave_w0 + 4 * WAVE; ww < w_end && ww < w_lim; ww += WAVE) {
+      const uint64_t wl = ww + lane;
+      uint32_t x = wl < w_end && wl < w_lim ? bits[wl] : 0u;
+      const uint64_t p0 = begin + 32 * wl;
+      if (x && p0 + 32 > E) x &= (E - p0) >= 32 ? ~0u : ((1u << (uint32_t)(E - p0)) - 1u);
+      const uint64_t b = __ballot(x != 0);
+      if (b) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(b);
+        const uint32_t xl = __shfl(x, l, WAVE);
+        past = begin + 32 * (ww + l) + __builtin_ctz(xl);
+        break;
+      }
     }
-    bool ok;
-    if (nxt_set != ~0ull) ok = step == nxt_set;
-    else ok = step >= E || step + 4 > total;  // leaves the counted range or hits EOF
-    if (!ok) {
-      atomicAdd(n_anom, 1ull);
-      atomicMin(first_anom, (unsigned long long)s);
-    } else if (nxt_set == ~0ull) {
-      // the last record of [from, E): its successor is the chain's exit (the first record
-      // at/after E, or the stream end); atomicMin since FP bits would add more candidates,
-      // and those runs are re-walked exactly anyway
-      atomicMin(exit_pos, (unsigned long long)(step > total ? total : step));
+    if (past >= E) past = ~0ull;
+    if (lane == top) lane_next = past;
+    // walk this lane's set bits in order
+    uint32_t k = 0;
+    while (k < 4 && !v[k]) ++k;
+    while (k < 4) {
+      const uint32_t b = __builtin_ctz(v[k]);
+      v[k] &= v[k] - 1;
+      const uint64_t s = begin + 32 * (w + k) + b;
+      uint32_t kn = k;
+      while (kn < 4 && !v[kn]) ++kn;
+      const uint64_t nxt_set = kn < 4 ? begin + 32 * (w + kn) + __builtin_ctz(v[kn]) : lane_next;
+      uint64_t step;
+      if (s + 4 > total) {
+        step = ~0ull;  // getInt at EOF: the chain ends here
+      } else {
+        const uint32_t *g = reinterpret_cast<const uint32_t *>(U + (s & ~3ull));
+        const int32_t rem = (int32_t)__builtin_amdgcn_alignbyte(g[1], g[0], (uint32_t)s & 3);
+        step = s + 4 + (int64_t)rem;
+      }
+      bool ok;
+      if (nxt_set != ~0ull) ok = step == nxt_set;
+      else ok = step >= E || step + 4 > total;  // leaves the counted range or hits EOF
+      if (!ok) {
+        atomicAdd(n_anom, 1ull);
+        atomicMin(first_anom, (unsigned long long)s);
+      } else if (nxt_set == ~0ull) {
+        atomicMin(exit_pos, (unsigned long long)(step > total ? total : step));
+      }
+      k = kn;
     }
-    k = kn;
+  }
+  __shared__ uint32_t part[4];
+  for (int off = 32; off > 0; off >>= 1) tot += __shfl_down(tot, off);
+  if (lane == 0) part[threadIdx.x / WAVE] = tot;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long t = (unsigned long long)part[0] + part[1] + part[2] + part[3];
+    if (t) atomicAdd(n_set, t);
   }
 }
 
@@ -1569,22 +1597,15 @@ hipError_t launch_first_set(const uint32_t *bits, uint64_t begin, uint64_t from,
   return hipGetLastError();
 }
 
-hipError_t launch_popcount(const uint32_t *bits, uint64_t begin, uint64_t from, uint64_t to,
-                           unsigned long long *acc, hipStream_t st) {
-  if (to <= from) return hipSuccess;
-  const uint64_t nw = (to - begin + 31) / 32 - (from - begin) / 32;
-  const uint32_t grid = (uint32_t)std::min<uint64_t>(ngrid(nw, 256 * 8), 2048);
-  hipLaunchKernelGGL(k_popcount, dim3(grid), dim3(256), 0, st, bits, begin, from, to, acc);
-  return hipGetLastError();
-}
-
-hipError_t launch_verify_chain(const uint8_t *U, const uint32_t *bits, uint64_t begin, uint64_t bits_end,
-                               uint64_t from, uint64_t E, uint64_t total, unsigned long long *n_anom,
-                               unsigned long long *first_anom, unsigned long long *exit_pos, hipStream_t st) {
+hipError_t launch_verify_chain_count(const uint8_t *U, const uint32_t *bits, uint64_t begin, uint64_t bits_end,
+                                     uint64_t from, uint64_t E, uint64_t total, unsigned long long *n_anom,
+                                     unsigned long long *first_anom, unsigned long long *exit_pos,
+                                     unsigned long long *n_set, hipStream_t st) {
   if (E <= from) return hipSuccess;
   const uint64_t nw = (E - begin + 31) / 32 - ((from - begin) / 32 & ~3ull);
-  hipLaunchKernelGGL(k_verify_chain, dim3(ngrid(nw, 1024)), dim3(256), 0, st, U, bits, begin, bits_end, from,
-                     E, total, n_anom, first_anom, exit_pos);
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(ngrid(nw, 1024), 2048);
+  hipLaunchKernelGGL(k_verify_chain_w, dim3(grid), dim3(256), 0, st, U, bits, begin, bits_end, from, E, total,
+                     n_anom, first_anom, exit_pos, n_set);
   return hipGetLastError();
 }
 

@@ -47,11 +47,10 @@ hipError_t launch_full(const uint8_t *U, uint64_t u_pad, uint64_t begin, uint64_
                        uint64_t close_cap, hipStream_t st);
 hipError_t launch_first_set(const uint32_t *bits, uint64_t begin, uint64_t from, uint64_t to,
                             unsigned long long *best, hipStream_t st);
-hipError_t launch_popcount(const uint32_t *bits, uint64_t begin, uint64_t from, uint64_t to,
-                           unsigned long long *acc, hipStream_t st);
-hipError_t launch_verify_chain(const uint8_t *U, const uint32_t *bits, uint64_t begin, uint64_t bits_end,
-                               uint64_t from, uint64_t E, uint64_t total, unsigned long long *n_anom,
-                               unsigned long long *first_anom, unsigned long long *exit_pos, hipStream_t st);
+hipError_t launch_verify_chain_count(const uint8_t *U, const uint32_t *bits, uint64_t begin, uint64_t bits_end,
+                                     uint64_t from, uint64_t E, uint64_t total, unsigned long long *n_anom,
+                                     unsigned long long *first_anom, unsigned long long *exit_pos,
+                                     unsigned long long *n_set, hipStream_t st);
 hipError_t launch_chain_walk(const uint8_t *U, uint64_t first, uint64_t E, uint64_t total,
                              unsigned long long *count, unsigned long long *last, hipStream_t st);
 }  // namespace sbh
@@ -869,7 +868,6 @@ int sbh_find_record_start(sbh_shard *sh, uint64_t from, int32_t rtc, int32_t max
 // Records of the chain from `first` whose start is < E; *exit_flat (optional) = the
 // first chain record at/after E (the successor of the last counted record, clamped to
 // the stream end) -- what the next shard's first record must equal when stitching.
-static constexpr uint64_t CM_SPARSE = 1024;  // positions per set bit above which the chain is marked
 
 static int count_records_impl(sbh_shard *sh, uint64_t first, uint64_t E, uint64_t *count, int32_t *anomalies,
                               uint64_t *exit_flat = nullptr) {
@@ -888,36 +886,32 @@ static int count_records_impl(sbh_shard *sh, uint64_t first, uint64_t E, uint64_
   unsigned long long *c = sh->ctr.p + 16;
   const bool covered = sh->bits_valid && sh->bits_begin <= first && E <= sh->bits_end;
   if (covered) {
-    HIPCHK(ctx, hipMemsetAsync(c, 0, 8, st));
-    HIPCHK(ctx, hipMemsetAsync(c + 1, 0xff, 8, st));
-    HIPCHK(ctx, hipMemsetAsync(c + 2, 0, 8, st));
-    HIPCHK(ctx, hipMemsetAsync(c + 3, 0xff, 8, st));
-    HIPCHK(ctx, launch_popcount(sh->bits.p, sh->bits_begin, first, E, c + 2, st));
-    HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 18, c + 2, 8, hipMemcpyDeviceToHost, st));
+    // counters c[0..3]: anomalies, first anomaly, set bits in [first, E), chain exit
+    unsigned long long *init = sh->h_ctr + 600;  // pinned
+    init[0] = 0;
+    init[1] = ~0ull;
+    init[2] = 0;
+    init[3] = ~0ull;
+    HIPCHK(ctx, hipMemcpyAsync(c, init, 32, hipMemcpyHostToDevice, st));
+    // verify bitmap == chain and count the set bits in one pass (k_verify_chain_w: wave-
+    // cooperative successors, so sparse bitmaps of long records cost no word-by-word scans)
+    HIPCHK(ctx, launch_verify_chain_count(sh->U.p, sh->bits.p, sh->bits_begin, sh->bits_end, first, E, total, c,
+                                          c + 1, c + 3, c + 2, st));
+    HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 16, c, 32, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipStreamSynchronize(st));
-    uint64_t n = sh->h_ctr[18];
-    // dense bits (short records): verify bitmap == chain in one pass; sparse bits (long
-    // records, > CM_SPARSE positions per set bit): the verify pass would scan long runs of
-    // empty words per record, so mark the chain by pointer doubling straight away
-    const bool dense = n == 0 || (E - first) / n <= CM_SPARSE;
-    if (dense) {
-      HIPCHK(ctx, launch_verify_chain(sh->U.p, sh->bits.p, sh->bits_begin, sh->bits_end, first, E, total, c, c + 1,
-                                      c + 3, st));
-      HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 16, c, 32, hipMemcpyDeviceToHost, st));
-      HIPCHK(ctx, hipStreamSynchronize(st));
-      if (sh->h_ctr[16] == 0 && sh->h_ctr[19] != ~0ull) {
-        sh->chain_ok = true;
-        sh->chain_first = first;
-        sh->chain_E = E;
-        *count = sh->h_ctr[18];
-        if (exit_flat) *exit_flat = sh->h_ctr[19];
-        return SBH_OK;
-      }
-      if (anomalies) *anomalies = (int32_t)std::min<uint64_t>(sh->h_ctr[16], INT32_MAX);
+    const uint64_t n = sh->h_ctr[18];
+    if (sh->h_ctr[16] == 0 && sh->h_ctr[19] != ~0ull) {
+      sh->chain_ok = true;
+      sh->chain_first = first;
+      sh->chain_E = E;
+      *count = n;
+      if (exit_flat) *exit_flat = sh->h_ctr[19];
+      return SBH_OK;
     }
-    // the bitmap is not exactly the chain (false positives / rejected chain records), or
-    // it is sparse: mark the chain through the set bits by pointer doubling; the exact
-    // walk only when the chain leaves the set bits
+    if (anomalies) *anomalies = (int32_t)std::min<uint64_t>(sh->h_ctr[16], INT32_MAX);
+    // the bitmap is not exactly the chain (false positives / rejected chain records): mark
+    // the chain through the set bits by pointer doubling; the exact walk only when the
+    // chain leaves the set bits
     if (n > 0 && n < 0xfffffff0ull) {
       const uint64_t nw = (E - sh->bits_begin + 31) / 32 - (first - sh->bits_begin) / 32;
       HIPCHK(ctx, sh->cm_wcnt.ensure(nw));
