@@ -47,7 +47,6 @@ constexpr int WAVES = SBH_HUFF_WAVES;  // waves (blocks) per k_huff workgroup
 #define SBH_LZ_THREADS 512
 #endif
 constexpr uint32_t LZ_THREADS = SBH_LZ_THREADS;
-constexpr uint32_t LZ_LONG = 24;  // longer matches are copied by the whole wave (rounds path)
 #ifndef SBH_LZ_SHORT
 #define SBH_LZ_SHORT 32
 #endif
@@ -890,6 +889,21 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t *wsum, uint3
   return before + x - v;
 }
 
+// Block-wide minimum over NT threads (all threads get it).  wmin: NT/64 words, not
+// read or written by anything else between two calls' barriers.
+template <uint32_t NT>
+__device__ __forceinline__ uint32_t block_min(uint32_t v, uint32_t *wmin) {
+  const uint32_t lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+#pragma unroll
+  for (uint32_t off = WAVE / 2; off > 0; off >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, (int)off, WAVE));
+  if (lane == 0) wmin[w] = v;
+  __syncthreads();
+  uint32_t m = ~0u;
+#pragma unroll
+  for (uint32_t k = 0; k < NT / WAVE; ++k) m = min(m, wmin[k]);
+  return m;
+}
+
 // ---------------------------------------------------------------------------------
 // Lane-parallel Huffman decode (the k_huff fast path).
 //
@@ -1537,29 +1551,22 @@ __global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__rest
 constexpr uint32_t LZ_TPT = SBH_LZ_TPT;                       // tokens per thread per chunk
 constexpr uint32_t LZ_CHUNK = LZ_THREADS * LZ_TPT;      // tokens per chunk
 constexpr uint32_t PTR_HALF = 8;                        // pointer slots per thread and pass
-constexpr uint32_t PTR_CAP = 7552;                      // chunk bytes resolved by pointer chasing
+constexpr uint32_t PTR_CAP = 7552;                      // bytes one pointer-chasing pass resolves
 constexpr uint32_t SB_WORDS = PTR_CAP / 32;             // token-start bitmap words
 constexpr uint32_t NHP = 2;                             // half granules (8 slots) per k_lz thread, at most
 static_assert(PTR_CAP <= NHP * LZ_THREADS * PTR_HALF, "slot pass covers the slots");
 
 struct LzSmem {
   uint8_t img[65536 + 16];  // block image, placed at (ustart & 15) so granules align with HBM
-  union {
-    struct {
-      uint16_t p16[PTR_CAP];     // per chunk byte: its source pointer (token starts first)
-      uint32_t sbits[SB_WORDS];  // per chunk byte: starts a token (every byte of a long match)
-      uint32_t wsum[8];          // block_scan scratch (both paths)
-    } pp;
-    struct {                      // dependency-rounds path, per half chunk
-      uint32_t toff[LZ_THREADS];  // tokens: output offsets (ascending)
-      uint32_t tokv[LZ_THREADS];  // tokens
-      uint32_t done[LZ_THREADS];  // round after which the token's bytes are final (0: pending)
-    } fb;
-  };
+  struct {
+    uint16_t p16[PTR_CAP];     // per pass byte: its source pointer (token starts first)
+    uint32_t sbits[SB_WORDS];  // per pass byte: starts a token (every byte of a long match)
+    uint32_t wsum[8];          // block_scan scratch
+    uint32_t wmin[8];          // block_min scratch (a pass cut)
+  } pp;
 };
 // two workgroups per CU, counting the 256 B of LDS the compiler adds
 static_assert(sizeof(LzSmem) * 2 + 512 <= 160 * 1024, "two k_lz workgroups per CU");
-static_assert(sizeof(LzSmem::fb) <= offsetof(decltype(LzSmem::pp), wsum), "the rounds path keeps wsum");
 
 // k mod d for k < 2^17, d >= 1 (one reciprocal, one correction).
 __device__ __forceinline__ uint32_t mod_small(uint32_t k, uint32_t d) {
@@ -1567,50 +1574,6 @@ __device__ __forceinline__ uint32_t mod_small(uint32_t k, uint32_t d) {
   int32_t r = (int32_t)(k - q * d);
   r = r < 0 ? r + (int32_t)d : r;
   return (uint32_t)(r >= (int32_t)d ? r - (int32_t)d : r);
-}
-
-// Token of the chunk covering output offset q (toff[0] <= q).
-__device__ __forceinline__ uint32_t cover(const uint32_t *toff, uint32_t m, uint32_t q) {
-  uint32_t lo = 0, hi = m;  // toff[lo] <= q < toff[hi]
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (toff[mid] <= q) lo = mid;
-    else hi = mid;
-  }
-  return lo;
-}
-
-// One match into the image: out[off + k] = img[src + (k mod dist)] (src holds bytes
-// equal to out[off - dist ...], already final).  Loads never touch the match's own
-// output.  Non-overlapping matches copy by aligned destination dwords, each assembled
-// from two aligned source dwords with v_alignbyte; the ragged ends go by bytes.
-// `base` is the image's byte offset inside the 16-aligned LDS buffer `img0`.
-__device__ __forceinline__ void lz_match(uint8_t *img0, uint32_t base, uint32_t off, uint32_t src,
-                                         uint32_t dist, uint32_t len) {
-  uint8_t *img = img0 + base;
-  if (dist >= len) {
-    uint32_t k = 0;
-    const uint32_t head = (4u - ((base + off) & 3u)) & 3u;
-    for (; k < len && k < head; ++k) img[off + k] = img[src + k];
-    uint32_t *d32 = reinterpret_cast<uint32_t *>(img0 + base + off + k);
-    const uint32_t *s32 = reinterpret_cast<const uint32_t *>(img0 + ((base + src + k) & ~3u));
-    const uint32_t sh = (base + src + k) & 3u;
-    if (k + 4 <= len) {
-      uint32_t lo = s32[0];
-      for (uint32_t w = 0; k + 4 <= len; k += 4, ++w) {
-        const uint32_t hi = s32[w + 1];
-        d32[w] = __builtin_amdgcn_alignbyte(hi, lo, sh);
-        lo = hi;
-      }
-    }
-    for (; k < len; ++k) img[off + k] = img[src + k];
-  } else {
-    uint32_t s = 0;
-    for (uint32_t k = 0; k < len; ++k) {
-      img[off + k] = img[src + s];
-      s = s + 1 == dist ? 0 : s + 1;
-    }
-  }
 }
 
 // Eight u16 slot values (positions; ones before the block may have wrapped) as a uint4.
@@ -1625,10 +1588,11 @@ __device__ __forceinline__ uint4 pack8_u16(const uint32_t *c) {
 // copies from (itself for a literal; match byte k: off - dist + k mod dist, always
 // earlier), written by its own token; then each thread follows its 16 bytes' pointers to
 // final bytes -- rewriting its slots with the results, which shortens other threads'
-// chases -- and gathers.  Longer chunks (long matches) fall back, per half chunk, to
-// dependency rounds: a match waits only for the matches its (redirected) source overlaps,
-// found by binary search over the half chunk's output offsets.
-__global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblocks,
+// chases -- and gathers.  A longer chunk (long matches) is resolved the same way in
+// passes of at most PTR_CAP bytes, each cut at a token start, so every chunk takes the
+// pointer path (the dependency-rounds fallback this replaced cost ~100 k cycles per
+// overflowing chunk: 2-4 per block of long-read data).
+__global__ __launch_bounds__(LZ_THREADS, 4) void k_lz(DevBlocks bl, uint64_t nblocks,
                                                     const uint32_t *__restrict__ tok, uint8_t *__restrict__ U) {
   __shared__ LzSmem sm;
   uint32_t *wsum = sm.pp.wsum;
@@ -1672,15 +1636,32 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
     off[0] = base + block_scan<LZ_THREADS>(mysum, wsum, &chunk_len);
 #pragma unroll
     for (uint32_t k = 1; k < LZ_TPT; ++k) off[k] = off[k - 1] + len[k - 1];
-    // slots start at the 16-byte LDS granule holding `base`, so that each thread's 16
-    // slots are one granule of the image
-    const uint32_t lead = (sh + base) & 15, abase = base - lead;
+    const uint32_t chunk_end = base + chunk_len;
 #ifdef SBH_LZ_PROBE
     const uint64_t tb = __builtin_readcyclecounter();
     t_pre += tb - ta;
-    nrounds += chunk_len + lead > PTR_CAP;
 #endif
-    if (chunk_len + lead <= PTR_CAP) {
+    // Passes over the chunk's output, each at most PTR_CAP bytes (from its 16-byte granule):
+    // a pass takes the tokens that START in [pb, pe) and pe is the start of the first token
+    // that would end past the pass's slots.  One pass when the chunk fits (the common
+    // case); long-match chunks take a few instead of a slower resolution.
+    uint32_t pb = base;
+    for (;;) {
+      // slots start at the 16-byte LDS granule holding `pb`, so that each thread's 16
+      // slots are one granule of the image
+      const uint32_t lead = (sh + pb) & 15, abase = pb - lead;
+      uint32_t pe = chunk_end;
+      if (chunk_end - abase > PTR_CAP) {  // uniform: cut the chunk
+        uint32_t cut = chunk_end;
+#pragma unroll
+        for (uint32_t k = 0; k < LZ_TPT; ++k)
+          if (i0 + k < n && off[k] >= pb && off[k] + len[k] - abase > PTR_CAP) cut = min(cut, off[k]);
+        pe = block_min<LZ_THREADS>(cut, sm.pp.wmin);
+      }
+      const uint32_t plen = pe - pb;
+#ifdef SBH_LZ_PROBE
+      nrounds += pe != chunk_end || pb != base;
+#endif
       uint16_t *p16 = sm.pp.p16;
       uint32_t *sbits = sm.pp.sbits;
       // Tokens mark their starts: one slot write (a literal points at itself, a short
@@ -1688,7 +1669,7 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
       // their pointers in the slot pass below, from the nearest start.
 #pragma unroll
       for (uint32_t k = 0; k < LZ_TPT; ++k) {
-        if (i0 + k >= n || len[k] > LZ_SHORT) continue;
+        if (i0 + k >= n || len[k] > LZ_SHORT || !(off[k] - pb < plen)) continue;
         const uint32_t d = off[k] - abase;
         p16[d] = (uint16_t)(match[k] ? off[k] - dist[k] : off[k]);
         if (!match[k]) img[off[k]] = (uint8_t)(x[k] >> 8);
@@ -1696,7 +1677,7 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
       }
 #pragma unroll
       for (uint32_t k = 0; k < LZ_TPT; ++k) {  // long matches: the wave writes every byte's pointer
-        uint64_t lm = __ballot(i0 + k < n && match[k] && len[k] > LZ_SHORT);
+        uint64_t lm = __ballot(i0 + k < n && match[k] && len[k] > LZ_SHORT && off[k] - pb < plen);
 #ifdef SBH_LZ_PROBE
         nlong += __builtin_popcountll(lm);
 #endif
@@ -1729,7 +1710,7 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
       // v + j, or v + (j mod (s - v)) when the match overlaps itself (rare); a literal
       // start points at itself.  Each thread owns up to NHP half granules (8 slots) and
       // keeps their pointers in registers for the chase below.
-      const uint32_t nh = (chunk_len + lead + PTR_HALF - 1) / PTR_HALF;
+      const uint32_t nh = (plen + lead + PTR_HALF - 1) / PTR_HALF;
       uint32_t c[NHP][PTR_HALF], pend[NHP];
 #pragma unroll
       for (uint32_t hh = 0; hh < NHP; ++hh) {
@@ -1739,8 +1720,8 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
         const uint32_t s0 = PTR_HALF * h, g0 = abase + s0;  // first slot, its position
         const uint32_t wi = h >> 2, sh8 = (h & 3) * PTR_HALF;
         const uint32_t cur = sbits[wi], prev = wi ? sbits[wi - 1] : 0u;
-        // the window's slots inside the chunk: [klo, khi)
-        const int32_t rlo = (int32_t)lead - (int32_t)s0, rhi = rlo + (int32_t)chunk_len;
+        // the window's slots inside the pass: [klo, khi)
+        const int32_t rlo = (int32_t)lead - (int32_t)s0, rhi = rlo + (int32_t)plen;
         const uint32_t klo = (uint32_t)min(max(rlo, 0), (int32_t)PTR_HALF);
         const uint32_t khi = (uint32_t)min(max(rhi, 0), (int32_t)PTR_HALF);
         // nearest start before the window, then walk the window's start bits
@@ -1769,8 +1750,8 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
             if ((ovl >> k) & 1u) c[hh][k] = v[k] + mod_small(s0 + k - sidx[k], abase + sidx[k] - v[k]);
         }
 #pragma unroll
-        for (uint32_t k = 0; k < PTR_HALF; ++k)  // in the chunk, not a literal, not final yet
-          pend[hh] |= (c[hh][k] != g0 + k && c[hh][k] >= base) ? 1u << k : 0u;
+        for (uint32_t k = 0; k < PTR_HALF; ++k)  // in the pass, not a literal, not final yet
+          pend[hh] |= (c[hh][k] != g0 + k && c[hh][k] >= pb) ? 1u << k : 0u;
         reinterpret_cast<uint4 *>(p16)[h] = pack8_u16(c[hh]);
       }
 #ifdef SBH_LZ_PROBE
@@ -1783,7 +1764,7 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
 #endif
       // chase the pointers of each half granule together, one LDS round trip per round,
       // writing shortened pointers back (other threads' chains pass through them); no
-      // barriers.  A pointer is final when it is before the chunk or names a literal (a
+      // barriers.  A pointer is final when it is before the pass or names a literal (a
       // slot pointing at itself).  Then gather the bytes and store them.
 #pragma unroll
       for (uint32_t hh = 0; hh < NHP; ++hh) {
@@ -1796,33 +1777,33 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
 #ifdef SBH_LZ_DEBUG
         uint32_t guard = 0;
 #endif
-        // Each round replaces every in-chunk pointer by the one stored at its target (a
+        // Each round replaces every in-pass pointer by the one stored at its target (a
         // final slot -- a literal -- stores itself, so it stays); a lane stops once no
-        // pointer of its own moved to another in-chunk position.
+        // pointer of its own moved to another in-pass position.
         bool more = pend[hh] != 0;
         while (__builtin_expect(more, 0)) {
 #ifdef SBH_LZ_DEBUG
           if (++guard > 300) {
             for (uint32_t k = 0; k < PTR_HALF; ++k)
-              printf("lz chase stuck blk %llu pos %u c %u base %u chunk_len %u lead %u\n", (unsigned long long)b,
-                     g0 + k, c[hh][k], base, chunk_len, lead);
+              printf("lz chase stuck blk %llu pos %u c %u base %u plen %u lead %u\n", (unsigned long long)b,
+                     g0 + k, c[hh][k], pb, plen, lead);
             break;
           }
 #endif
           uint32_t v[PTR_HALF];
 #pragma unroll
-          for (uint32_t k = 0; k < PTR_HALF; ++k) v[k] = p16[(c[hh][k] >= base ? c[hh][k] : base) - abase];
+          for (uint32_t k = 0; k < PTR_HALF; ++k) v[k] = p16[(c[hh][k] >= pb ? c[hh][k] : pb) - abase];
 #ifdef SBH_LZ_PROBE
           if (__builtin_amdgcn_readfirstlane(lane) == lane) ++njumps;  // rounds this wave ran
 #endif
           more = false;
 #pragma unroll
           for (uint32_t k = 0; k < PTR_HALF; ++k) {
-            const uint32_t nc = c[hh][k] >= base ? v[k] : c[hh][k];
-            more = more || (nc != c[hh][k] && nc >= base);
+            const uint32_t nc = c[hh][k] >= pb ? v[k] : c[hh][k];
+            more = more || (nc != c[hh][k] && nc >= pb);
             c[hh][k] = nc;
           }
-          // write back: settled and shortened pointers alike (literal and out-of-chunk
+          // write back: settled and shortened pointers alike (literal and out-of-pass
           // slots keep pointing at themselves)
           reinterpret_cast<uint4 *>(p16)[h] = pack8_u16(c[hh]);
         }
@@ -1837,85 +1818,11 @@ __global__ __launch_bounds__(LZ_THREADS) void k_lz(DevBlocks bl, uint64_t nblock
 #ifdef SBH_LZ_PROBE
       t_ch += __builtin_readcyclecounter() - tc;
 #endif
-    } else {
-      // dependency rounds, one half chunk (one token per thread) at a time
-      uint32_t hbase = base;
-      for (uint32_t h = 0; h < LZ_TPT; ++h) {
-        const uint32_t ih = c0 + h * LZ_THREADS + t;
-        const uint32_t m = n > c0 + h * LZ_THREADS ? min(n - (c0 + h * LZ_THREADS), LZ_THREADS) : 0u;
-        const uint32_t xh = ih < n ? tk[ih] : 0;
-        const bool match = ih < n && (xh & TOK_MATCH) != 0;
-        const uint32_t len = ih >= n ? 0 : match ? (xh >> 16) & 0x1ff : 1;
-        const uint32_t dist = xh & 0xffff;
-        uint32_t half_len;
-        __syncthreads();  // wsum / fb arrays free
-        const uint32_t off = hbase + block_scan<LZ_THREADS>(len, wsum, &half_len);
-        const uint32_t base = hbase;
-        if (t < m) {
-          sm.fb.toff[t] = off;
-          sm.fb.tokv[t] = xh;
-          sm.fb.done[t] = match ? 0 : 1;
-          if (!match) img[off] = (uint8_t)(xh >> 8);
-        }
-        __syncthreads();
-        if (m) {
-      uint32_t src = off - dist;  // where the (final-equivalent) source bytes start
-      uint32_t jl = 1, jh = 0;    // chunk tokens the source overlaps (empty: none)
-      if (match) {
-        // external source bytes: [src, src + min(len, dist)) (an overlapping match
-        // re-reads its own output only through the period)
-        const uint32_t ext = len < dist ? len : dist;
-        // Redirect through the chunk's own matches: a source wholly inside one
-        // non-overlapping match M' equals the bytes M' copied, dist' earlier.  This
-        // collapses chains (read names copying the previous read's name ...) so most
-        // matches copy in the first round.
-        for (int hop = 0; hop < 16 && src >= base; ++hop) {
-          const uint32_t j = cover(sm.fb.toff, m, src);
-          const uint32_t y = sm.fb.tokv[j];
-          if (!(y & TOK_MATCH)) break;
-          const uint32_t oj = sm.fb.toff[j], lj = (y >> 16) & 0x1ff, dj = y & 0xffff;
-          if (dj < lj || src + ext > oj + lj) break;  // overlapping M' or source spans tokens
-          src -= dj;
-        }
-        if (src + ext > base) {
-          jl = src < base ? 0 : cover(sm.fb.toff, m, src);
-          jh = cover(sm.fb.toff, m, src + ext - 1);
-        }
-      }
-      bool pending = match;
-      for (uint32_t r = 1;; ++r) {
-        bool go = false;
-        if (pending) {
-          go = true;
-          for (uint32_t j = jl; j <= jh && go; ++j) {
-            const uint32_t dj = sm.fb.done[j];
-            go = dj != 0 && dj <= r;
-          }
-        }
-        // long matches: the whole wave copies each one (byte k by lane k mod 64)
-        uint64_t lm = __ballot(go && len > LZ_LONG);
-        while (lm) {
-          const uint32_t l = (uint32_t)__builtin_ctzll(lm);
-          lm &= lm - 1;
-          const uint32_t o = __builtin_amdgcn_readlane(off, l), sr = __builtin_amdgcn_readlane(src, l);
-          const uint32_t d = __builtin_amdgcn_readlane(dist, l), L = __builtin_amdgcn_readlane(len, l);
-          const uint32_t lane = t & (WAVE - 1);
-          if (d >= L) {
-            for (uint32_t k = lane; k < L; k += WAVE) img[o + k] = img[sr + k];
-          } else {
-            for (uint32_t k = lane; k < L; k += WAVE) img[o + k] = img[sr + k % d];
-          }
-        }
-        if (go && len <= LZ_LONG) lz_match(sm.img, sh, off, src, dist, len);
-        if (go) {
-          sm.fb.done[t] = r + 1;
-          pending = false;
-        }
-        if (!__syncthreads_or(pending)) break;
-      }
-        }
-        hbase += half_len;
-      }
+      if (pe == chunk_end) break;
+      __syncthreads();  // the pass's slots and start bits are reused by the next pass
+      for (uint32_t w = t; w < SB_WORDS; w += LZ_THREADS) sm.pp.sbits[w] = 0;
+      pb = pe;
+      __syncthreads();
     }
     base += chunk_len;
     __syncthreads();  // slots / wsum are reused by the next chunk

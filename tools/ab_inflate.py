@@ -2,7 +2,7 @@
 """A/B the inflate-kernel variants (spark-bam_amd/build/variants/lib_*.so) on one
 synthetic shard: per-variant k_inflate time (HIP events) and output identity vs the
 in-tree library.  Each variant runs in its own process (the library path is bound at
-import).  Usage: python tools/ab_inflate.py [--records N] [variant ...]"""
+import).  Usage: python tools/ab_inflate.py [--records N] [--config B|D|E] [variant ...]"""
 import argparse
 import glob
 import json
@@ -13,7 +13,10 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def child(lib, records, reps):
+CONFIGS = {"B": (0x5B4D0001, 0, 6), "D": (0x5B4D004C, 1, 6), "E": (0x5B4D00AD, 2, -1)}
+
+
+def child(lib, records, reps, config="B"):
     if lib:
         os.environ["SBH_LIB_PATH"] = lib
     sys.path.insert(0, ROOT)
@@ -24,7 +27,8 @@ def child(lib, records, reps):
     import synth
     from __graft_entry__ import load_package
     sb = load_package()
-    p = synth.params(synth.SEEDS["B"])
+    seed, shape, level = CONFIGS[config]
+    p = synth.params(seed, shape=shape, level=level)
     data, usize, nb = synth.make_bam(p, records)
     with sb.Context(0) as ctx:
         sh = ctx.shard(data)
@@ -49,16 +53,18 @@ def main():
     ap.add_argument("--records", type=int, default=2_000_000)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--child", default=None)
+    ap.add_argument("--config", default="B", choices=sorted(CONFIGS))
     ap.add_argument("variants", nargs="*")
     a = ap.parse_args()
     if a.child is not None:
-        return child(a.child, a.records, a.reps)
+        return child(a.child, a.records, a.reps, a.config)
     vdir = os.path.join(ROOT, "spark-bam_amd/build/variants")
     named = [v if v.endswith(".so") else os.path.join(vdir, f"lib_{v}.so") for v in a.variants]
     libs = [""] + (named or sorted(glob.glob(os.path.join(vdir, "lib_*.so"))))
     for lib in libs:
         r = subprocess.run([sys.executable, __file__, "--child", lib, "--records", str(a.records),
-                            "--reps", str(a.reps)], capture_output=True, text=True, timeout=900)
+                            "--reps", str(a.reps), "--config", a.config], capture_output=True, text=True,
+                           timeout=900)
         print(r.stdout.strip() or r.stderr[-2000:], flush=True)
         if r.stderr and r.stdout:  # probe variants print their counters on stderr/stdout
             print(r.stderr[-4000:], flush=True)
