@@ -143,7 +143,8 @@ __device__ __forceinline__ void put_entry(uint32_t *tab, uint32_t kind, uint32_t
 // Canonical Huffman table (zlib inflate_table validity: over-subscribed -> error;
 // incomplete -> error unless type != CODES and max == 1; max == 0 -> all invalid).
 // kind: 0 lit/len, 1 dist, 2 code-length code.  Returns 0 ok, 1 error, 2 empty.
-__device__ __forceinline__ uint32_t build_table(WaveSmem &sm, const uint8_t *lens, uint32_t nsym, uint32_t kind,
+template <class SM>
+__device__ __forceinline__ uint32_t build_table(SM &sm, const uint8_t *lens, uint32_t nsym, uint32_t kind,
                                 uint32_t *tab, int fast, uint32_t lane) {
   const uint32_t w = kind == 1 ? 1 : 0;
   uint16_t *sorted = sm.sorted + (kind == 1 ? 288 : 0);
@@ -255,7 +256,8 @@ __device__ __forceinline__ uint32_t pentry(uint32_t kind, uint32_t sym, uint32_t
 // v occupy [lj[v-1], lj[v]) of the 15-bit left-justified code space, so a reversed
 // index's length is 1 + #{v : lj[v] <= code}.  Entries whose code is longer than
 // `fast` bits are K_SLOW (slow_lane finishes them); prefixes of no code are K_BAD.
-__device__ __forceinline__ uint32_t ptable_meta(WaveSmem &sm, const uint8_t *lens, uint32_t nsym, uint32_t kind,
+template <class SM>
+__device__ __forceinline__ uint32_t ptable_meta(SM &sm, const uint8_t *lens, uint32_t nsym, uint32_t kind,
                                                 uint32_t lane) {
   uint16_t *sorted = sm.sorted + (kind ? 288 : 0);
   uint32_t my_cnt = 0;  // lane v (1..15): count of length v
@@ -314,7 +316,8 @@ __device__ __forceinline__ uint32_t ptable_meta(WaveSmem &sm, const uint8_t *len
 
 // Entry i of the PAR table of `kind` from its limits lj[v] (= pk[kind][v] >> 16) and
 // ptable_meta's canonical order: the code's length is 1 + #{v : lj[v] <= code}.
-__device__ __forceinline__ uint32_t ptable_entry(const WaveSmem &sm, const uint32_t *lj, uint32_t kind, uint32_t fast,
+template <class SM>
+__device__ __forceinline__ uint32_t ptable_entry(const SM &sm, const uint32_t *lj, uint32_t kind, uint32_t fast,
                                                  uint32_t i) {
   const uint32_t c15 = (__builtin_bitreverse32(i) >> (32 - fast)) << (15 - fast);
   uint32_t len = 1;
@@ -1109,8 +1112,8 @@ __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, Src<LDS> src, uin
 // those with v_readlane, writing each run of lengths with one vector store.  Returns
 // (uniformly) whether the lengths are well formed and include an end-of-block code;
 // q: the bit after the header.  `p` is the block's first bit (BFINAL).
-template <class S>
-__device__ __forceinline__ bool hdr_walk(WaveSmem &t, const S &src, uint32_t p, uint32_t limit, uint32_t nlen,
+template <class SM, class S>
+__device__ __forceinline__ bool hdr_walk(SM &t, const S &src, uint32_t p, uint32_t limit, uint32_t nlen,
                                          uint32_t ndist, uint32_t ncode, uint32_t lane, uint32_t &q_out,
                                          uint64_t *h1, uint64_t *h2) {
   if (lane < 19) t.cl_lens[CL_ORDER[lane]] = lane < ncode ? (uint8_t)(src.bits32(p + 17 + 3 * lane) & 7) : 0;
@@ -1378,8 +1381,8 @@ __device__ __forceinline__ bool inflate_par(HuffSmem &sm, const uint8_t *__restr
 
 // First-header pre-pass: the first deflate block of every BGZF block starts at the
 // block's first data bit, so its dynamic header (code-length walk, canonical tables) can
-// be decoded before k_huff runs, by one small wave per block at high occupancy, instead
-// of on k_huff's critical path with three of its four waves idle.  The PAR tables, the
+// be decoded before k_huff runs, by one small wave per block at high occupancy (3.7 KB of
+// LDS: HdrSmem), instead of on k_huff's critical path with three of its four waves idle.  The PAR tables, the
 // sorted entries / limits slow_lane reads, the bit after the header and BFINAL go to
 // the end of the block's token region (k_huff copies them into LDS before it writes a
 // token).  Anything this pass does not accept (fixed / stored first block, a header
@@ -1395,6 +1398,18 @@ struct HdrSrc {  // bits of the staged dwords [0, n) (clamped reads past them ar
   }
 };
 
+// k_hdr's LDS: WaveSmem's header-time members only (the code-length-code table instead of
+// the 8 KB decode tables, which go straight to HBM), so many more headers are in flight.
+struct HdrSmem {
+  uint32_t lit[1 << CL_FAST];  // the code-length-code table (build_table's CL format)
+  uint16_t sorted[320];
+  uint8_t lens[320];
+  uint8_t cl_lens[20];
+  uint32_t cnt[2][16];
+  uint32_t pk[2][16];
+  uint32_t sent[320];
+};
+
 __device__ __forceinline__ bool huff_serial_block(const DevBlocks &bl, uint64_t b) {
   const uint32_t csize = bl.csize[b], hsize = bl.hsize[b], usize = bl.usize[b];
   return (bl.flags[b] & BLK_TRUNCATED) || usize > 65536u || usize < PAR_MIN_USIZE ||
@@ -1403,7 +1418,7 @@ __device__ __forceinline__ bool huff_serial_block(const DevBlocks &bl, uint64_t 
 
 __global__ __launch_bounds__(WAVE) void k_hdr(const uint8_t *__restrict__ comp, DevBlocks bl, uint64_t nblocks,
                                               uint32_t *__restrict__ tok) {
-  __shared__ WaveSmem t;
+  __shared__ HdrSmem t;
   __shared__ uint32_t stage[HDR_STAGE_DW];
   const uint64_t b = blockIdx.x;
   if (b >= nblocks || huff_serial_block(bl, b)) return;
