@@ -1185,6 +1185,21 @@ __device__ __forceinline__ bool hdr_walk(SM &t, const S &src, uint32_t p, uint32
   return ok;
 }
 
+// Both PAR decode tables from ptable_meta's limits (pk) and order (sent), by the HT
+// threads of a k_huff workgroup.
+__device__ __forceinline__ void fill_ptables(WaveSmem &t, uint32_t tid) {
+  uint32_t lj0[16], lj1[16];
+#pragma unroll
+  for (uint32_t v = 1; v <= 15; ++v) {
+    lj0[v] = t.pk[0][v] >> 16;
+    lj1[v] = t.pk[1][v] >> 16;
+  }
+#pragma unroll
+  for (uint32_t i = tid; i < (1u << LIT_FAST); i += HT) t.lit[i] = ptable_entry(t, lj0, 0, LIT_FAST, i);
+#pragma unroll
+  for (uint32_t i = tid; i < (1u << PDIST_FAST); i += HT) t.dist[i] = ptable_entry(t, lj1, 1, PDIST_FAST, i);
+}
+
 // Deflate block header and tables for the lane-parallel path, read from the bit source
 // (sm.ctl[5..6] carry wave 0's result to the workgroup).  The code-length symbols are
 // decoded 64 bit positions at a time -- lane i decodes the symbol that would start at
@@ -1198,19 +1213,7 @@ __device__ __forceinline__ bool par_header(HuffSmem &sm, Src<LDS> src, uint32_t 
                                            uint32_t wid, uint32_t lane, uint32_t &psym, uint32_t &last) {
   WaveSmem &t = sm.t;
   // both decode tables from ptable_meta's limits and order, filled by the whole workgroup
-  auto fill_tables = [&]() {
-    const uint32_t tid = wid * WAVE + lane;
-    uint32_t lj0[16], lj1[16];
-#pragma unroll
-    for (uint32_t v = 1; v <= 15; ++v) {
-      lj0[v] = t.pk[0][v] >> 16;
-      lj1[v] = t.pk[1][v] >> 16;
-    }
-#pragma unroll
-    for (uint32_t i = tid; i < (1u << LIT_FAST); i += HT) t.lit[i] = ptable_entry(t, lj0, 0, LIT_FAST, i);
-#pragma unroll
-    for (uint32_t i = tid; i < (1u << PDIST_FAST); i += HT) t.dist[i] = ptable_entry(t, lj1, 1, PDIST_FAST, i);
-  };
+  auto fill_tables = [&]() { fill_ptables(t, wid * WAVE + lane); };
   const uint32_t hb = uni(src.bits32(p));
   last = hb & 1;
   const uint32_t type = (hb >> 1) & 3;
