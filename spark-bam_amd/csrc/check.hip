@@ -351,8 +351,14 @@ __device__ __forceinline__ uint32_t ref_pos_error_l(int32_t idx, int32_t pos, in
 // of 18 LDS dword reads, and both contig lengths are loaded beside them, so a record
 // costs about three dependent round trips (fields, then CIGAR op bytes) instead of one
 // per field; the tests run in the reference's order on the loaded values.
+// With `cig` set, a record whose CIGAR has more than CIG_WAVE ops returns ONE_CIGAR after
+// every other test passed, with *cig = its first op byte and *ncig = nc: the caller
+// checks those op bytes with the whole wave (one lane walking hundreds of ops would hold
+// the workgroup at its next barrier).
+constexpr uint32_t ONE_CIGAR = 3, CIG_WAVE = 16;
 __device__ __forceinline__ uint32_t one_record(const Src &s, uint64_t q, uint64_t total, const Ctg &c,
-                                               uint64_t *succ, bool *normal) {
+                                               uint64_t *succ, bool *normal, uint64_t *cig = nullptr,
+                                               uint32_t *ncig = nullptr) {
   if (q + 36 > total) return 2;                       // EOF rules: exact path
   if (q - s.s0 + 36 + 8 > s.sn) return 2;
   const uint32_t w = (uint32_t)(q - s.s0), i = w >> 2, k = w & 3;
@@ -412,11 +418,15 @@ __device__ __forceinline__ uint32_t one_record(const Src &s, uint64_t q, uint64_
     if (nn > 32 && !name_bytes_ok(s, cur + 32, nn - 32)) return 0;
   }
   cur += rnl;
-  if (first_bad_op(s, cur, (uint32_t)nc, cur + 4ull * (uint32_t)nc) < (uint32_t)nc) return 0;
-  cur += 4ull * (uint32_t)nc;
   const uint64_t nominal = q + 4 + (int64_t)rem;
   *succ = nominal;
-  *normal = (int64_t)(nominal - cur) >= 0;
+  *normal = (int64_t)(nominal - (cur + 4ull * (uint32_t)nc)) >= 0;
+  if (cig && (uint32_t)nc > CIG_WAVE) {
+    *cig = cur;
+    *ncig = (uint32_t)nc;
+    return ONE_CIGAR;
+  }
+  if (first_bad_op(s, cur, (uint32_t)nc, cur + 4ull * (uint32_t)nc) < (uint32_t)nc) return 0;
   return 1;
 }
 
@@ -476,6 +486,37 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
     uint64_t succ;
     bool normal;
     const uint32_t r = one_record(s, q, total, c, &succ, &normal);
+    if (r == 1) {
+      atomicOr(&ok[i >> 5], 1u << (i & 31));
+      if (normal) atomicOr(&nrm[i >> 5], 1u << (i & 31));
+    } else if (r == 2) {
+      atomicOr(&und[i >> 5], 1u << (i & 31));
+    }
+  };
+  // the same for the wave's lanes together (every lane of the wave must call it; lanes
+  // with has == false only help): long CIGARs are checked 64 ops per step by the wave
+  auto eval_one_w = [&](uint32_t i, bool has) {
+    const uint64_t q = t0 + i;
+    uint64_t succ = 0, cig = 0;
+    uint32_t ncig = 0;
+    bool normal = false;
+    uint32_t r = 0;
+    if (has) {
+      const uint64_t total = q < e0 ? e0 : sg.end[seg_index(sg, q, k0)];
+      r = one_record(s, q, total, c, &succ, &normal, &cig, &ncig);
+    }
+    uint64_t pend = __ballot(r == ONE_CIGAR);
+    while (pend) {
+      const uint32_t l = (uint32_t)__builtin_ctzll(pend);
+      pend &= pend - 1;
+      const uint64_t cl = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(cig >> 32), l) << 32) |
+                          __builtin_amdgcn_readlane((uint32_t)cig, l);
+      const uint32_t nl = __builtin_amdgcn_readlane(ncig, l);
+      bool bad = false;
+      for (uint32_t k = lane; k < nl; k += WAVE) bad = bad || (s.byte_at(cl + 4ull * k) & 0xf) > 8;
+      const bool any = __ballot(bad) != 0;
+      if (lane == l) r = any ? 0u : 1u;
+    }
     if (r == 1) {
       atomicOr(&ok[i >> 5], 1u << (i & 31));
       if (normal) atomicOr(&nrm[i >> 5], 1u << (i & 31));
@@ -676,7 +717,10 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
 #ifdef SBH_EPROBE
     if (threadIdx.x == 0) nsurv = pre[NWV];
 #endif
-    for (uint32_t x = threadIdx.x; x < pre[NWV]; x += T) eval_one(entry(x));
+    for (uint32_t xb = 0; xb < pre[NWV]; xb += T) {  // uniform trip count: eval_one_w uses the whole wave
+      const uint32_t x = xb + threadIdx.x;
+      eval_one_w(x < pre[NWV] ? entry(x) : 0u, x < pre[NWV]);
+    }
 #ifdef SBH_EPROBE
     c1b = __builtin_readcyclecounter();
 #endif
