@@ -509,9 +509,10 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
     while (pend) {
       const uint32_t l = (uint32_t)__builtin_ctzll(pend);
       pend &= pend - 1;
-      const uint64_t cl = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(cig >> 32), l) << 32) |
-                          __builtin_amdgcn_readlane((uint32_t)cig, l);
-      const uint32_t nl = __builtin_amdgcn_readlane(ncig, l);
+      // (readlane returns int: widen through uint32_t, or a flat offset >= 2^31 sign-extends)
+      const uint64_t cl = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(cig >> 32), l) << 32) |
+                          (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)cig, l);
+      const uint32_t nl = (uint32_t)__builtin_amdgcn_readlane(ncig, l);
       bool bad = false;
       for (uint32_t k = lane; k < nl; k += WAVE) bad = bad || (s.byte_at(cl + 4ull * k) & 0xf) > 8;
       const bool any = __ballot(bad) != 0;
