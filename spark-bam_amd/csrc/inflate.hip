@@ -1898,7 +1898,11 @@ hipError_t launch_huff(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, 
 
 hipError_t launch_lz(DevBlocks blocks, uint64_t nblocks, const uint32_t *tok, uint8_t *U, hipStream_t stream) {
   if (nblocks == 0) return hipSuccess;
+#ifdef SBH_LZ_PAD  // occupancy probe: dynamic LDS that leaves one workgroup per CU
+  hipLaunchKernelGGL(k_lz, dim3((uint32_t)nblocks), dim3(LZ_THREADS), SBH_LZ_PAD, stream, blocks, nblocks, tok, U);
+#else
   hipLaunchKernelGGL(k_lz, dim3((uint32_t)nblocks), dim3(LZ_THREADS), 0, stream, blocks, nblocks, tok, U);
+#endif
   return hipGetLastError();
 }
 

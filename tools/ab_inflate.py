@@ -34,6 +34,16 @@ def child(lib, records, reps, config="B"):
         sh = ctx.shard(data)
         names, cl, _ = sb.parse_bam_header(synth.header_bytes())
         sh.set_contigs(cl)
+        if os.environ.get("AB_INFLATE_ONLY"):  # variants whose tokens are wrong: time index + inflate only
+            import time
+            sh.index(0)
+            wall = []
+            for _ in range(reps + 1):
+                t0 = time.perf_counter()
+                sh.inflate()
+                wall.append((time.perf_counter() - t0) * 1e3)
+            print(json.dumps({"lib": os.path.basename(lib or "in-tree"), "inflate_wall_ms": sorted(wall[1:])}))
+            return
         times = []
         for _ in range(reps):
             r = sh.run(0, data.size)
