@@ -52,6 +52,7 @@ constexpr uint32_t LZ_THREADS = SBH_LZ_THREADS;
 #endif
 constexpr uint32_t LZ_SHORT = SBH_LZ_SHORT;  // longer matches get their pointers from the whole wave
 static_assert(LZ_SHORT <= 33, "k_lz finds a short match's start within 32 slots back");
+constexpr uint32_t NTOK_STORED = 0xffffffffu;  // ntok of a block whose payload is one stored deflate block
 constexpr uint32_t TOK_MATCH = 0x80000000u;  // token: literal = byte << 8 (bit 31 clear); match = bit31 | len << 16 | dist
 
 // Table entries (32-bit; laid out so the asm hot loop decodes with few scalar ops):
@@ -1480,6 +1481,21 @@ __global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__rest
   const uint64_t cstart = bl.cstart[b];
   const uint32_t csize = bl.csize[b], hsize = bl.hsize[b], usize = bl.usize[b];
   const uint64_t G = bl.ustart[b];
+  // The payload is one final stored deflate block exactly (BGZF level 0): zlib's output is
+  // the LEN stored bytes, so k_lz copies them (ntok = NTOK_STORED) instead of resolving a
+  // literal token per byte from the serial decoder.
+  if (!(bl.flags[b] & BLK_TRUNCATED) && usize - 1u < 65535u && (int32_t)csize - (int32_t)hsize - 8 == (int32_t)usize + 5) {
+    const uint64_t d = cstart + hsize;
+    const uint32_t b0 = comp[d], len = comp[d + 1] | (uint32_t)comp[d + 2] << 8;
+    const uint32_t nlen = comp[d + 3] | (uint32_t)comp[d + 4] << 8;
+    if ((b0 & 7u) == 1u && len == usize && (len ^ nlen) == 0xffffu) {
+      if (tid == 0) {
+        bl.status[b] = INF_OK;
+        bl.ntok[b] = NTOK_STORED;
+      }
+      return;
+    }
+  }
   const bool serial = huff_serial_block(bl, b);
 #ifdef SBH_HUFF_PROBE
   const uint64_t hk0 = __builtin_readcyclecounter();
@@ -1610,7 +1626,7 @@ __device__ __forceinline__ uint4 pack8_u16(const uint32_t *c) {
 // passes of at most PTR_CAP bytes, each cut at a token start, so every chunk takes the
 // pointer path (the dependency-rounds fallback this replaced cost ~100 k cycles per
 // overflowing chunk: 2-4 per block of long-read data).
-__global__ __launch_bounds__(LZ_THREADS, 4) void k_lz(DevBlocks bl, uint64_t nblocks,
+__global__ __launch_bounds__(LZ_THREADS, 4) void k_lz(const uint8_t *__restrict__ comp, DevBlocks bl, uint64_t nblocks,
                                                     const uint32_t *__restrict__ tok, uint8_t *__restrict__ U) {
   __shared__ LzSmem sm;
   uint32_t *wsum = sm.pp.wsum;
@@ -1620,6 +1636,27 @@ __global__ __launch_bounds__(LZ_THREADS, 4) void k_lz(DevBlocks bl, uint64_t nbl
   const uint32_t n = bl.ntok[b];
   const uint64_t G = bl.ustart[b];
   const uint32_t sh = (uint32_t)(G & 15);
+  if (n == NTOK_STORED) {  // a stored payload: copy it in 16-byte granules aligned to the flat address
+    const uint64_t src = bl.cstart[b] + bl.hsize[b] + 5;
+    const uint32_t usize = bl.usize[b];
+    const uint64_t g0 = G & ~15ull;
+    for (uint32_t lo = 16 * t; lo < sh + usize; lo += 16 * LZ_THREADS) {
+      if (lo >= sh && lo + 16 <= sh + usize) {
+        const uint64_t a = src + (lo - sh);
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(comp + (a & ~3ull));
+        const uint32_t k = (uint32_t)a & 3u, d0 = w[0], d1 = w[1], d2 = w[2], d3 = w[3], d4 = w[4];
+        *reinterpret_cast<uint4 *>(U + g0 + lo) =
+            make_uint4(__builtin_amdgcn_alignbyte(d1, d0, k), __builtin_amdgcn_alignbyte(d2, d1, k),
+                       __builtin_amdgcn_alignbyte(d3, d2, k), __builtin_amdgcn_alignbyte(d4, d3, k));
+      } else {
+        for (uint32_t j = 0; j < 16; ++j) {
+          const uint32_t x = lo + j;
+          if (x >= sh && x < sh + usize) U[g0 + x] = comp[src + (x - sh)];
+        }
+      }
+    }
+    return;
+  }
   uint8_t *img = sm.img + sh;
   const uint32_t *tk = tok + G;
 
@@ -1896,12 +1933,13 @@ hipError_t launch_huff(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, 
   return hipGetLastError();
 }
 
-hipError_t launch_lz(DevBlocks blocks, uint64_t nblocks, const uint32_t *tok, uint8_t *U, hipStream_t stream) {
+hipError_t launch_lz(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, const uint32_t *tok, uint8_t *U,
+                     hipStream_t stream) {
   if (nblocks == 0) return hipSuccess;
 #ifdef SBH_LZ_PAD  // occupancy probe: dynamic LDS that leaves one workgroup per CU
-  hipLaunchKernelGGL(k_lz, dim3((uint32_t)nblocks), dim3(LZ_THREADS), SBH_LZ_PAD, stream, blocks, nblocks, tok, U);
+  hipLaunchKernelGGL(k_lz, dim3((uint32_t)nblocks), dim3(LZ_THREADS), SBH_LZ_PAD, stream, comp, blocks, nblocks, tok, U);
 #else
-  hipLaunchKernelGGL(k_lz, dim3((uint32_t)nblocks), dim3(LZ_THREADS), 0, stream, blocks, nblocks, tok, U);
+  hipLaunchKernelGGL(k_lz, dim3((uint32_t)nblocks), dim3(LZ_THREADS), 0, stream, comp, blocks, nblocks, tok, U);
 #endif
   return hipGetLastError();
 }

@@ -542,7 +542,7 @@ int sbh_inflate(sbh_shard *sh, uint64_t *bad_block) {
   mark(sh, 2);
   HIPCHK(ctx, launch_huff(sh->comp.p, sh->dev_blocks(), sh->nblocks, sh->tok.p, st));
   mark(sh, 7);
-  HIPCHK(ctx, launch_lz(sh->dev_blocks(), sh->nblocks, sh->tok.p, sh->U.p, st));
+  HIPCHK(ctx, launch_lz(sh->comp.p, sh->dev_blocks(), sh->nblocks, sh->tok.p, sh->U.p, st));
   mark(sh, 3);
   std::vector<uint32_t> status(sh->nblocks);
   if (sh->nblocks) HIPCHK(ctx, hipMemcpyAsync(status.data(), sh->b_status.p, sh->nblocks * 4, hipMemcpyDeviceToHost, st));
@@ -1267,7 +1267,7 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
     HIPCHK(ctx, hipEventRecord(e[1], sa));
     HIPCHK(ctx, hipStreamWaitEvent(sl, e[1], 0));
     HIPCHK(ctx, hipEventRecord(e[2], sl));
-    HIPCHK(ctx, launch_lz(d, b1 - b0, sh->tok.p, sh->U.p, sl));
+    HIPCHK(ctx, launch_lz(sh->comp.p, d, b1 - b0, sh->tok.p, sh->U.p, sl));
     HIPCHK(ctx, hipEventRecord(e[3], sl));
     // eager tiles whose staged windows lie below the inflated frontier
     const bool last = i + 1 == nbat;

@@ -59,10 +59,11 @@ constexpr uint64_t EAGER_REACH = SBH_ETILE + 4096 + 512 + 64;
 
 // Launchers (defined in the .hip files, called from sbh_api.hip).
 // Inflate = k_huff (Huffman decode -> LZ77 tokens, block status) then k_lz (tokens ->
-// flat bytes).  tok: scratch of >= 4 B per flat byte (block b's tokens at tok[ustart_b ...]).
+// flat bytes; a block that is one stored deflate block is copied from comp).  tok: scratch
+// of >= 4 B per flat byte (block b's tokens at tok[ustart_b ...]).
 hipError_t launch_huff(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, uint32_t *tok,
                        hipStream_t stream);
-hipError_t launch_lz(DevBlocks blocks, uint64_t nblocks, const uint32_t *tok, uint8_t *U,
+hipError_t launch_lz(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, const uint32_t *tok, uint8_t *U,
                      hipStream_t stream);
 
 // Record field extraction (records.hip): device columns of a decoded batch (the host
