@@ -1914,7 +1914,21 @@ __global__ __launch_bounds__(LZ_THREADS, 4) void k_lz(const uint8_t *__restrict_
   }
 }
 
+// The first block whose inflate status is not INF_OK (atomicMin; *first preset to ~0):
+// the host reads 8 bytes instead of every block's status.
+__global__ void k_first_bad(const uint32_t *status, uint64_t n, unsigned long long *first) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && status[i] != INF_OK) atomicMin(first, (unsigned long long)i);
+}
+
 }  // namespace
+
+hipError_t launch_first_bad(const uint32_t *status, uint64_t n, unsigned long long *first, hipStream_t stream) {
+  hipError_t e = hipMemsetAsync(first, 0xff, sizeof(unsigned long long), stream);
+  if (e != hipSuccess || n == 0) return e;
+  hipLaunchKernelGGL(k_first_bad, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, status, n, first);
+  return hipGetLastError();
+}
 
 hipError_t launch_huff(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, uint32_t *tok,
                        hipStream_t stream) {

@@ -529,6 +529,31 @@ int sbh_get_blocks(sbh_shard *sh, uint64_t first, uint64_t count, sbh_block *out
   return SBH_OK;
 }
 
+// After the inflate kernels on `st`: the first block whose status is not INF_OK decides the
+// error (the reference's exception for that block); 8 bytes come back, not every status.
+// `extra`/`extra_dst`/`extra_n` ride along in the same round trip.
+static int inflate_status(sbh_shard *sh, hipStream_t st, uint64_t *bad_block, const void *extra = nullptr,
+                          void *extra_dst = nullptr, size_t extra_n = 0) {
+  sbh_ctx *ctx = sh->ctx;
+  unsigned long long *fb = sh->ctr.p + 100;
+  HIPCHK(ctx, launch_first_bad(sh->b_status.p, sh->nblocks, fb, st));
+  HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 100, fb, 8, hipMemcpyDeviceToHost, st));
+  if (extra_n) HIPCHK(ctx, hipMemcpyAsync(extra_dst, extra, extra_n, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  const uint64_t i = sh->h_ctr[100];
+  if (i == ~0ull) return SBH_OK;
+  uint32_t *hs = reinterpret_cast<uint32_t *>(sh->h_ctr + 101);
+  HIPCHK(ctx, hipMemcpyAsync(hs, sh->b_status.p + i, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  if (bad_block) *bad_block = i;
+  const sbh_block &b = sh->hb[i];
+  if (*hs == INF_SIZE)
+    return fail(ctx, SBH_E_INFLATE_SIZE, "block %llu: expected %u decompressed bytes", (unsigned long long)b.start,
+                b.usize);
+  if (*hs == INF_BAD_ISIZE) return fail(ctx, SBH_E_BAD_ISIZE, "block %llu: ISIZE %u", (unsigned long long)b.start, b.usize);
+  return fail(ctx, SBH_E_INFLATE_DATA, "block %llu: invalid deflate data", (unsigned long long)b.start);
+}
+
 int sbh_inflate(sbh_shard *sh, uint64_t *bad_block) {
   if (!sh) return SBH_E_ARG;
   sbh_ctx *ctx = sh->ctx;
@@ -544,19 +569,8 @@ int sbh_inflate(sbh_shard *sh, uint64_t *bad_block) {
   mark(sh, 7);
   HIPCHK(ctx, launch_lz(sh->comp.p, sh->dev_blocks(), sh->nblocks, sh->tok.p, sh->U.p, st));
   mark(sh, 3);
-  std::vector<uint32_t> status(sh->nblocks);
-  if (sh->nblocks) HIPCHK(ctx, hipMemcpyAsync(status.data(), sh->b_status.p, sh->nblocks * 4, hipMemcpyDeviceToHost, st));
-  HIPCHK(ctx, hipStreamSynchronize(st));
-  for (uint64_t i = 0; i < sh->nblocks; ++i) {
-    if (status[i] == INF_OK) continue;
-    if (bad_block) *bad_block = i;
-    const sbh_block &b = sh->hb[i];
-    if (status[i] == INF_SIZE)
-      return fail(ctx, SBH_E_INFLATE_SIZE, "block %llu: expected %u decompressed bytes", (unsigned long long)b.start,
-                  b.usize);
-    if (status[i] == INF_BAD_ISIZE) return fail(ctx, SBH_E_BAD_ISIZE, "block %llu: ISIZE %u", (unsigned long long)b.start, b.usize);
-    return fail(ctx, SBH_E_INFLATE_DATA, "block %llu: invalid deflate data", (unsigned long long)b.start);
-  }
+  rc = inflate_status(sh, st, bad_block);
+  if (rc) return rc;
   sh->inflated = true;
   sh->bits_valid = sh->chain_ok = sh->cm_valid = false;
   return SBH_OK;
@@ -1297,18 +1311,9 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
   HIPCHK(ctx, hipEventRecord(ev[6 * nbat + 3], se));
   HIPCHK(ctx, hipEventRecord(ev[6 * nbat + 1], se));
   HIPCHK(ctx, hipStreamWaitEvent(sa, ev[6 * nbat + 1], 0));
-  std::vector<uint32_t> status(nb);
-  if (nb) HIPCHK(ctx, hipMemcpyAsync(status.data(), sh->b_status.p, nb * 4, hipMemcpyDeviceToHost, sa));
-  HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr, c, 48, hipMemcpyDeviceToHost, sa));
-  HIPCHK(ctx, hipStreamSynchronize(sa));
-  for (uint64_t i = 0; i < nb; ++i) {
-    if (status[i] == INF_OK) continue;
-    const sbh_block &b = sh->hb[i];
-    if (status[i] == INF_SIZE)
-      return fail(ctx, SBH_E_INFLATE_SIZE, "block %llu: expected %u decompressed bytes", (unsigned long long)b.start,
-                  b.usize);
-    if (status[i] == INF_BAD_ISIZE) return fail(ctx, SBH_E_BAD_ISIZE, "block %llu: ISIZE %u", (unsigned long long)b.start, b.usize);
-    return fail(ctx, SBH_E_INFLATE_DATA, "block %llu: invalid deflate data", (unsigned long long)b.start);
+  {
+    const int rs = inflate_status(sh, sa, nullptr, c, sh->h_ctr, 48);
+    if (rs) return rs;
   }
   sh->inflated = true;
   if (sh->timing) {

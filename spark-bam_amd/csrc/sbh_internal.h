@@ -65,6 +65,8 @@ hipError_t launch_huff(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, 
                        hipStream_t stream);
 hipError_t launch_lz(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, const uint32_t *tok, uint8_t *U,
                      hipStream_t stream);
+// *first = the first block of [0, n) whose status is not INF_OK (~0 if none).
+hipError_t launch_first_bad(const uint32_t *status, uint64_t n, unsigned long long *first, hipStream_t stream);
 
 // Record field extraction (records.hip): device columns of a decoded batch (the host
 // view is sbh_records_out in sparkbam.h).
