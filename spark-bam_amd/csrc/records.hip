@@ -36,15 +36,63 @@ __global__ void k_bits_positions(const uint32_t *bits, uint64_t begin, uint64_t 
   }
 }
 
-__global__ void k_word_popcounts(const uint32_t *bits, uint64_t begin, uint64_t first, uint64_t E, uint64_t *cnt) {
-  const uint64_t w0 = (first - begin) / 32;
-  const uint64_t w = w0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= (E - begin + 31) / 32) return;
+// Per-word prefix counts in two levels: a workgroup covers WP_CHUNK words (WP_WPT per
+// thread); k_chunk_popcounts sums each chunk, the chunk sums are scanned (a few thousand
+// values), and k_word_prefix re-counts its words, scans them inside the workgroup and
+// writes wpre -- one write pass over the words instead of a multi-pass global scan.
+constexpr uint32_t WP_T = 256, WP_WPT = 16, WP_CHUNK = WP_T * WP_WPT;
+
+__device__ __forceinline__ uint32_t masked_word(const uint32_t *bits, uint64_t begin, uint64_t first, uint64_t E,
+                                                uint64_t w) {
+  if (w >= (E - begin + 31) / 32) return 0;
   uint32_t v = bits[w];
   const uint64_t p0 = begin + 32 * w;
   if (p0 < first) v &= ~0u << (uint32_t)(first - p0);
   if (p0 + 32 > E) v &= (E - p0) >= 32 ? ~0u : ((1u << (uint32_t)(E - p0)) - 1u);
-  cnt[w - w0] = __popc(v);
+  return v;
+}
+
+__global__ __launch_bounds__(WP_T) void k_chunk_popcounts(const uint32_t *bits, uint64_t begin, uint64_t first,
+                                                          uint64_t E, uint64_t *ccnt) {
+  __shared__ uint32_t part[WP_T / WAVE];
+  const uint64_t w0 = (first - begin) / 32 + (uint64_t)blockIdx.x * WP_CHUNK + (uint64_t)threadIdx.x * WP_WPT;
+  uint32_t c = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < WP_WPT; ++k) c += __popc(masked_word(bits, begin, first, E, w0 + k));
+  for (int off = WAVE / 2; off > 0; off >>= 1) c += __shfl_down(c, off);
+  if ((threadIdx.x & (WAVE - 1)) == 0) part[threadIdx.x / WAVE] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (uint32_t k = 0; k < WP_T / WAVE; ++k) t += part[k];
+    ccnt[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(WP_T) void k_word_prefix(const uint32_t *bits, uint64_t begin, uint64_t first,
+                                                      uint64_t E, const uint64_t *cpre, uint64_t *wpre) {
+  __shared__ uint32_t wsum[WP_T / WAVE];
+  const uint64_t wb = (first - begin) / 32;
+  const uint64_t nw = (E - begin + 31) / 32 - wb;
+  const uint64_t r0 = (uint64_t)blockIdx.x * WP_CHUNK + (uint64_t)threadIdx.x * WP_WPT;  // relative word
+  uint32_t cnt[WP_WPT], mine = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < WP_WPT; ++k) {
+    cnt[k] = __popc(masked_word(bits, begin, first, E, wb + r0 + k));
+    mine += cnt[k];
+  }
+  const uint32_t lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
+  const uint32_t incl = wave_incl_scan(mine);
+  if (lane == WAVE - 1) wsum[wv] = incl;
+  __syncthreads();
+  uint32_t before = 0;
+  for (uint32_t k = 0; k < wv; ++k) before += wsum[k];
+  uint64_t o = cpre[blockIdx.x] + before + incl - mine;
+#pragma unroll
+  for (uint32_t k = 0; k < WP_WPT; ++k) {
+    if (r0 + k < nw) wpre[r0 + k] = o;
+    o += cnt[k];
+  }
 }
 
 // Sequential chain from first while the start is < E (fallback when no verified bitmap).
@@ -186,15 +234,18 @@ __global__ __launch_bounds__(256) void k_rec_fields(const uint8_t *__restrict__ 
 
 hipError_t scan_exclusive_u64(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *tmp, hipStream_t st);
 
-// cnt, wpre: one u64 per bitmap word of [first, E); tmp: scan_tmp_words(words)
+// cnt, wpre: one u64 per bitmap word of [first, E) (cnt holds 2 per WP_CHUNK words: chunk
+// sums and their prefix); tmp: scan_tmp_words(words)
 hipError_t launch_rec_positions_bits(const uint32_t *bits, uint64_t begin, uint64_t first, uint64_t E, uint64_t *cnt,
                                      uint64_t *wpre, uint64_t *tmp, uint64_t *pos, hipStream_t st) {
   const uint64_t nw = (E - begin + 31) / 32 - (first - begin) / 32;
   if (!nw) return hipSuccess;
   const uint32_t g = (uint32_t)((nw + 255) / 256);
-  hipLaunchKernelGGL(k_word_popcounts, dim3(g), dim3(256), 0, st, bits, begin, first, E, cnt);
-  hipError_t e = scan_exclusive_u64(cnt, wpre, nw, tmp, st);
+  const uint64_t nch = (nw + WP_CHUNK - 1) / WP_CHUNK;  // cnt: chunk sums, then (cnt + nch) their prefix
+  hipLaunchKernelGGL(k_chunk_popcounts, dim3((uint32_t)nch), dim3(WP_T), 0, st, bits, begin, first, E, cnt);
+  hipError_t e = scan_exclusive_u64(cnt, cnt + nch, nch, tmp, st);
   if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_word_prefix, dim3((uint32_t)nch), dim3(WP_T), 0, st, bits, begin, first, E, cnt + nch, wpre);
   hipLaunchKernelGGL(k_bits_positions, dim3(g), dim3(256), 0, st, bits, begin, first, E, wpre, pos);
   return hipGetLastError();
 }

@@ -928,7 +928,7 @@ static int count_records_impl(sbh_shard *sh, uint64_t first, uint64_t E, uint64_
     // chain leaves the set bits
     if (n > 0 && n < 0xfffffff0ull) {
       const uint64_t nw = (E - sh->bits_begin + 31) / 32 - (first - sh->bits_begin) / 32;
-      HIPCHK(ctx, sh->cm_wcnt.ensure(nw));
+      HIPCHK(ctx, sh->cm_wcnt.ensure(nw + 2));  // (chunk sums + prefix: 2 per 4096 words)
       HIPCHK(ctx, sh->cm_wpre.ensure(nw));
       HIPCHK(ctx, sh->cm_pos.ensure(n));
       HIPCHK(ctx, sh->cm_mark.ensure(n + 1));
@@ -1647,7 +1647,7 @@ static int records_positions(sbh_shard *sh, uint64_t first, uint64_t E, uint64_t
   const bool covered = sh->bits_valid && sh->bits_begin <= first && E <= sh->bits_end && anomalies == 0;
   if (n && covered) {
     const uint64_t nw = (E - sh->bits_begin + 31) / 32 - (first - sh->bits_begin) / 32;
-    HIPCHK(ctx, R.wcnt.ensure(nw));
+    HIPCHK(ctx, R.wcnt.ensure(nw + 2));  // (chunk sums + prefix: 2 per 4096 words)
     HIPCHK(ctx, R.wpre.ensure(nw));
     HIPCHK(ctx, sh->tmp.ensure(scan_tmp_words(nw)));
     HIPCHK(ctx, launch_rec_positions_bits(sh->bits.p, sh->bits_begin, first, E, R.wcnt.p, R.wpre.p, sh->tmp.p, pos, st));
