@@ -1420,13 +1420,20 @@ __device__ __forceinline__ bool huff_serial_block(const DevBlocks &bl, uint64_t 
          (int32_t)csize - (int32_t)hsize - 8 < 0;
 }
 
-__global__ __launch_bounds__(WAVE) void k_hdr(const uint8_t *__restrict__ comp, DevBlocks bl, uint64_t nblocks,
-                                              uint32_t *__restrict__ tok) {
-  __shared__ HdrSmem t;
-  __shared__ uint32_t stage[HDR_STAGE_DW];
-  const uint64_t b = blockIdx.x;
+#ifndef SBH_HDR_WAVES
+#define SBH_HDR_WAVES 4
+#endif
+constexpr uint32_t HDR_WAVES = SBH_HDR_WAVES;  // blocks (one per wave) per k_hdr workgroup
+
+__global__ __launch_bounds__(WAVE * HDR_WAVES) void k_hdr(const uint8_t *__restrict__ comp, DevBlocks bl,
+                                                         uint64_t nblocks, uint32_t *__restrict__ tok) {
+  __shared__ HdrSmem tw[HDR_WAVES];
+  __shared__ uint32_t stagew[HDR_WAVES][HDR_STAGE_DW];
+  const uint32_t lane = threadIdx.x & (WAVE - 1), wid = uni(threadIdx.x / WAVE);
+  const uint64_t b = (uint64_t)blockIdx.x * HDR_WAVES + wid;  // waves work alone: no workgroup barriers
   if (b >= nblocks || huff_serial_block(bl, b)) return;
-  const uint32_t lane = threadIdx.x;
+  HdrSmem &t = tw[wid];
+  uint32_t *stage = stagew[wid];
   const uint64_t cstart = bl.cstart[b];
   const uint32_t csize = bl.csize[b], hsize = bl.hsize[b], usize = bl.usize[b];
   const uint32_t data_len = csize - hsize - 8;
@@ -1436,7 +1443,7 @@ __global__ __launch_bounds__(WAVE) void k_hdr(const uint8_t *__restrict__ comp, 
   const uint32_t ndw = min((limit + 31) / 32 + 2, HDR_STAGE_DW);
   const uint32_t *g = reinterpret_cast<const uint32_t *>(comp) + a0;
   for (uint32_t i = lane; i < ndw; i += WAVE) stage[i] = g[i];
-  __syncthreads();
+  __builtin_amdgcn_wave_barrier();  // (a wave's LDS accesses complete in order)
   uint32_t *out = tok + bl.ustart[b] + usize - HDR_OUT_DW;
   const HdrSrc src{stage, ndw};
   // every code-length symbol start the walk visits keeps its 32-bit reads inside the stage
@@ -1459,7 +1466,9 @@ __global__ __launch_bounds__(WAVE) void k_hdr(const uint8_t *__restrict__ comp, 
       lj0[v] = t.pk[0][v] >> 16;
       lj1[v] = t.pk[1][v] >> 16;
     }
+#pragma unroll 4
     for (uint32_t i = lane; i < (1u << LIT_FAST); i += WAVE) out[i] = ptable_entry(t, lj0, 0, LIT_FAST, i);
+#pragma unroll 4
     for (uint32_t i = lane; i < (1u << PDIST_FAST); i += WAVE)
       out[(1u << LIT_FAST) + i] = ptable_entry(t, lj1, 1, PDIST_FAST, i);
     for (uint32_t i = lane; i < 320; i += WAVE) out[HDR_SENT + i] = t.sent[i];
@@ -1938,7 +1947,8 @@ hipError_t launch_huff(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, 
   hipLaunchKernelGGL(k_huff_serial<false>, dim3((uint32_t)grid), dim3(WAVES * WAVE), 0, stream, comp, blocks, nblocks,
                      tok);
 #else
-  hipLaunchKernelGGL(k_hdr, dim3((uint32_t)nblocks), dim3(WAVE), 0, stream, comp, blocks, nblocks, tok);
+  hipLaunchKernelGGL(k_hdr, dim3((uint32_t)((nblocks + HDR_WAVES - 1) / HDR_WAVES)), dim3(WAVE * HDR_WAVES), 0, stream,
+                     comp, blocks, nblocks, tok);
   hipLaunchKernelGGL(k_huff, dim3((uint32_t)nblocks), dim3(HT), 0, stream, comp, blocks, nblocks, tok);
   const uint64_t grid = (nblocks + WAVES - 1) / WAVES;
   hipLaunchKernelGGL(k_huff_serial<true>, dim3((uint32_t)grid), dim3(WAVES * WAVE), 0, stream, comp, blocks, nblocks,
