@@ -98,16 +98,20 @@ __global__ void k_find_block_start(const uint8_t *comp, uint64_t n, uint64_t sta
 
 // ---------------------------------------------------------------- candidate scan
 // Pass 1 streams every byte once with coalesced 16 B loads (lane t of segment i reads
-// chunk + i*4096 + 16t) and finds the bytes equal to 31 with a SWAR zero-byte test;
-// only those get the full header check.  Per chunk it records the candidate count and
+// chunk + i*4096 + 16t) and finds the BGZF magic (31 139 8 4) with exact SWAR byte tests
+// in registers; only those offsets get the full header check.  Per chunk it records the candidate count and
 // the first candidate's offset.  Pass 2 then needs the bytes again only for the rare
 // chunks holding two or more candidates (blocks are ~20-65 KB apart).
 
-// Bytes of w equal to 31, as bit 7 of each byte (may over-report above a true hit;
-// every reported byte is re-checked exactly).
-__device__ __forceinline__ uint32_t bytes_eq31(uint32_t w) {
-  const uint32_t x = w ^ 0x1f1f1f1fu;
-  return (x - 0x01010101u) & ~x & 0x80808080u;
+// 4-bit mask of the bytes of w equal to the byte replicated in b4 (exact per byte), and
+// the 16-bit mask over a 16-byte vector.
+__device__ __forceinline__ uint32_t eq4(uint32_t w, uint32_t b4) {
+  const uint32_t t = w ^ b4;
+  const uint32_t z = ~(((t & 0x7f7f7f7fu) + 0x7f7f7f7fu) | t) & 0x80808080u;
+  return ((z >> 7) * 0x204081u >> 21) & 0xfu;  // bits 7/15/23/31 -> 0..3
+}
+__device__ __forceinline__ uint32_t eq16(const uint4 &v, uint32_t b4) {
+  return eq4(v.x, b4) | eq4(v.y, b4) << 4 | eq4(v.z, b4) << 8 | eq4(v.w, b4) << 12;
 }
 
 __device__ __forceinline__ bool cand_at(const uint8_t *comp, uint64_t n, uint64_t from, uint64_t p) {
@@ -142,17 +146,19 @@ __global__ __launch_bounds__(256) void k_cand_count(const uint8_t *comp, uint64_
     const uint32_t o0 = i * 4096 + threadIdx.x * 16;
     const uint64_t p0 = cbase + o0;
     const uint4 v = vv[i];
-    const uint32_t m[4] = {bytes_eq31(v.x), bytes_eq31(v.y), bytes_eq31(v.z), bytes_eq31(v.w)};
-    if (m[0] | m[1] | m[2] | m[3]) {
-      for (uint32_t q = 0; q < 4; ++q) {
-        uint32_t mq = m[q];
-        while (mq) {
-          const uint32_t k = 4 * q + (__builtin_ctz(mq) >> 3);
-          mq &= mq - 1;
-          if (cand_at(comp, n, from, p0 + k)) {
-            ++mine;
-            myfirst = min(myfirst, o0 + k);
-          }
+    // the whole 4-byte magic (31 139 8 4) is tested in registers where the vector holds it,
+    // so the header check's dependent loads run only for near-certain headers (and for a
+    // 31 in the vector's last 3 bytes), not for every 31 byte (1 in 256 of deflate data)
+    const uint32_t m31 = eq16(v, 0x1f1f1f1fu);
+    if (m31) {
+      const uint32_t mh = m31 & (eq16(v, 0x8b8b8b8bu) >> 1) & (eq16(v, 0x08080808u) >> 2) & (eq16(v, 0x04040404u) >> 3);
+      uint32_t mq = (mh & 0x1fffu) | (m31 & 0xe000u);
+      while (mq) {
+        const uint32_t k = __builtin_ctz(mq);
+        mq &= mq - 1;
+        if (cand_at(comp, n, from, p0 + k)) {
+          ++mine;
+          myfirst = min(myfirst, o0 + k);
         }
       }
     }
