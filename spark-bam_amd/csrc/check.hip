@@ -300,7 +300,14 @@ struct EagerOut {
   uint64_t *xq_pos;               // long-record candidates for the wave-cooperative exact pass
   unsigned long long *xq_n;
   uint64_t xq_cap;                // 0: every exact check runs inline
+  unsigned long long *true_spread;  // k_eager: per-wave true counts, folded into n_true by k_fold_true
 };
+
+// k_eager's true count goes to TRUE_SLOTS counters TRUE_STRIDE u64 apart (one atomic per
+// wave), not to n_true itself: one address takes every workgroup's atomic in turn at one
+// L2 channel, and the barrier a per-workgroup sum needs waits for the bitmap stores.
+constexpr uint32_t TRUE_SLOTS = 64, TRUE_STRIDE = 16;
+constexpr uint32_t TRUE_SPREAD_OFF = 2048;  // u64 offset of the slots in the counter buffer
 
 // A candidate whose first record is at least this long (block_size) leaves its exact check
 // to k_eager_xq: its name / CIGAR bytes are read by a whole wave instead of one lane.
@@ -445,7 +452,7 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
   __shared__ uint32_t ok[EW / 32], nrm[EW / 32], und[EW / 32];
   __shared__ __attribute__((aligned(16))) uint32_t res[ETILE / 32];
   __shared__ uint32_t lnk[EQ_CHUNK / 32], lfail[EQ_CHUNK / 32];  // per sorted candidate: LINK / FAIL step
-  __shared__ uint32_t seg0, ntrue, nq, wcnt[NWV];
+  __shared__ uint32_t seg0, nq, wcnt[NWV];
   __shared__ uint64_t seg_end0;
   __shared__ uint16_t queue[EQ_CHUNK];
   const uint32_t *lds32 = reinterpret_cast<const uint32_t *>(ldsv);
@@ -463,7 +470,6 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
     const uint32_t k = seg_first(sg, t0);
     seg0 = k;
     seg_end0 = sg.end[k];
-    ntrue = 0;
     nq = 0;
   }
   __syncthreads();
@@ -853,13 +859,16 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
       }
     }
   }
-  if (mytrue) atomicAdd(&ntrue, mytrue);
-  __syncthreads();
-  if (threadIdx.x == 0 && ntrue) atomicAdd(o.n_true, (unsigned long long)ntrue);
+  {
+    const uint32_t wt = (uint32_t)__builtin_amdgcn_readlane(wave_incl_scan(mytrue), WAVE - 1);
+    if (lane == 0 && wt)
+      atomicAdd(o.true_spread + ((blockIdx.x * NWV + wid) % TRUE_SLOTS) * TRUE_STRIDE, (unsigned long long)wt);
+  }
 #ifdef SBH_EPROBE
-  __shared__ uint32_t psurv, pcand, pexact;
-  if (threadIdx.x == 0) { psurv = 0; pcand = 0; pexact = 0; }
+  __shared__ uint32_t psurv, pcand, pexact, ntrue;
+  if (threadIdx.x == 0) { psurv = 0; pcand = 0; pexact = 0; ntrue = 0; }
   __syncthreads();
+  atomicAdd(&ntrue, mytrue);
   atomicAdd(&psurv, nsurv);
   atomicAdd(&pcand, ncand);
   atomicAdd(&pexact, nexact);
@@ -1558,6 +1567,17 @@ __global__ __launch_bounds__(256) void k_eager_xq(const uint8_t *__restrict__ U,
 // Positions the pipelined eager pass deferred (their exact check reached flat bytes that
 // were not inflated yet), re-checked once everything is: bit set atomically over the
 // tile's word, counters as in k_eager.
+// n_true += k_eager's per-wave slots, which are left zero for the next launch (the shard
+// zeroes them once when it allocates the counter buffer).
+__global__ void k_fold_true(unsigned long long *spread, unsigned long long *n_true) {
+  const uint32_t t = threadIdx.x;
+  unsigned long long v = t < TRUE_SLOTS ? spread[t * TRUE_STRIDE] : 0ull;
+  if (t < TRUE_SLOTS) spread[t * TRUE_STRIDE] = 0ull;
+#pragma unroll
+  for (uint32_t d = WAVE / 2; d > 0; d >>= 1) v += __shfl_down(v, d, WAVE);
+  if (t == 0 && v) atomicAdd(n_true, v);
+}
+
 __global__ void k_eager_defer(const uint8_t *__restrict__ U, uint64_t begin, Segs sg, Ctg c, int32_t rtc,
                               const uint64_t *pos, const unsigned long long *n, EagerOut o) {
   const uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1588,10 +1608,11 @@ hipError_t launch_eager(const uint8_t *U, uint64_t u_pad, uint64_t begin, uint64
   if (end <= begin) return hipSuccess;
   Segs sg{seg_end, nseg, open_last};
   Ctg c{ctg, nctg};
-  EagerOut o{bits, counters, counters + 1, counters + 2, front, defer_pos, counters + 3, defer_cap,
-             xq_pos, counters + 4, xq_cap};
+  EagerOut o{bits,   counters,     counters + 1, counters + 2, front, defer_pos, counters + 3, defer_cap,
+             xq_pos, counters + 4, xq_cap,       counters + TRUE_SPREAD_OFF};
   hipLaunchKernelGGL(k_eager, dim3(ngrid(end - begin, ETILE)), dim3(T), 0, st, U, u_pad, begin, end, sg, c,
                      rtc, o);
+  hipLaunchKernelGGL(k_fold_true, dim3(1), dim3(WAVE), 0, st, counters + TRUE_SPREAD_OFF, counters);
   return hipGetLastError();
 }
 

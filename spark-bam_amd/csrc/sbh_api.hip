@@ -329,6 +329,8 @@ int sbh_shard_create(sbh_ctx *ctx, const void *src, uint64_t n, uint64_t file_of
                        ctx->stream);
   if (e == hipSuccess) e = hipMemsetAsync(sh->comp.p + n, 0, sh->pad, ctx->stream);
   if (e == hipSuccess) e = sh->ctr.ensure(4096);
+  // (k_eager's per-wave true-count slots at [2048, 3072) must start zero; k_fold_true keeps them so)
+  if (e == hipSuccess) e = hipMemsetAsync(sh->ctr.p, 0, 4096 * sizeof(unsigned long long), ctx->stream);
   if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&sh->h_ctr), 4096 * sizeof(unsigned long long));
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   if (e != hipSuccess) {
