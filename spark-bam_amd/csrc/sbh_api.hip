@@ -414,16 +414,20 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
   sh->ncand = 0;
   const uint64_t rel = start - sh->file_off;
   const uint64_t n = sh->n;
-  // the start must itself be a header
+  // the start must itself be a header (its 18 bytes come back with the candidate count)
   uint8_t *h18 = reinterpret_cast<uint8_t *>(sh->h_ctr + 512);  // pinned
-  if (rel + 18 <= n) {
-    HIPCHK(ctx, hipMemcpyAsync(h18, sh->comp.p + rel, 18, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipStreamSynchronize(st));
+  auto start_is_header = [&]() -> int {
     if (sbh_header_make(h18, 18, nullptr, nullptr) != SBH_OK)
       return fail(ctx, SBH_E_HEADER_PARSE, "no BGZF header at %llu", (unsigned long long)start);
-  }
+    return SBH_OK;
+  };
+  if (rel + 18 <= n) HIPCHK(ctx, hipMemcpyAsync(h18, sh->comp.p + rel, 18, hipMemcpyDeviceToHost, st));
   const uint64_t nchunks = cand_chunks(n);
   uint64_t nc = 0;
+  if (rel + 18 <= n && !nchunks) {
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    if ((rc = start_is_header()) != SBH_OK) return rc;
+  }
   if (nchunks && rel + 18 <= n) {
     HIPCHK(ctx, sh->counts.ensure(nchunks));
     HIPCHK(ctx, sh->cfirst.ensure(nchunks));
@@ -434,6 +438,7 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
     HIPCHK(ctx, hipMemcpyAsync(&sh->h_ctr[0], sh->offs.p + nchunks - 1, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipMemcpyAsync(&sh->h_ctr[1], sh->counts.p + nchunks - 1, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipStreamSynchronize(st));
+    if ((rc = start_is_header()) != SBH_OK) return rc;
     nc = sh->h_ctr[0] + sh->h_ctr[1];
   }
   uint64_t nchain = 0;
