@@ -259,7 +259,7 @@ __global__ void k_mark_u64(const uint8_t *on, uint64_t *v, uint64_t nc) {
 // Emit the chain as the block table (ordered by position).
 __global__ void k_chain_emit(const uint8_t *comp, uint64_t n, const uint64_t *cand, const uint8_t *on,
                              const uint64_t *rank, uint64_t nc, DevBlocks bl,
-                             uint64_t *usz) {
+                             uint64_t *usz, uint64_t nchain, uint8_t *next18) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nc || !on[i]) return;
   const uint64_t r = rank[i];
@@ -283,6 +283,8 @@ __global__ void k_chain_emit(const uint8_t *comp, uint64_t n, const uint64_t *ca
   // flat sizes: empty or truncated blocks contribute no bytes; ISIZE > 64 KiB is an
   // inflate error (reported by k_inflate), contributes none
   usz[r] = (flags & (BLK_EMPTY | BLK_TRUNCATED)) || us > 65536u ? 0 : us;
+  if (r + 1 == nchain)  // the bytes after the last block: the host checks the next header
+    for (uint32_t j = 0; j < 18; ++j) next18[j] = p + cs + j < n ? comp[p + cs + j] : 0;
 }
 
 __global__ void k_copy_u64(const uint64_t *a, uint64_t *b, uint64_t n) {
@@ -348,7 +350,7 @@ hipError_t launch_cand_write(const uint8_t *comp, uint64_t n, uint64_t from, con
 // usz (u64 per block); returns the block count via *nchain (host).
 hipError_t build_chain(const uint8_t *comp, uint64_t n, const uint64_t *cand, uint64_t nc, int64_t *J0,
                        int64_t *J1, uint8_t *on, uint64_t *v, uint64_t *rank, uint64_t *tmp,
-                       DevBlocks bl, uint64_t *usz, uint64_t *nchain, hipStream_t st) {
+                       DevBlocks bl, uint64_t *usz, uint64_t *nchain, uint8_t *next18, hipStream_t st) {
   *nchain = 0;
   if (nc == 0) return hipSuccess;
   const uint32_t T = 256;
@@ -379,7 +381,7 @@ hipError_t build_chain(const uint8_t *comp, uint64_t n, const uint64_t *cand, ui
   if (e != hipSuccess) return e;
   *nchain = last_rank + last_v;
   hipLaunchKernelGGL(k_chain_emit, dim3(nblk(nc, T)), dim3(T), 0, st, comp, n, cand, on, rank, nc, bl,
-                     usz);
+                     usz, *nchain, next18);
   return hipGetLastError();
 }
 

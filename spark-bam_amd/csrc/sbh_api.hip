@@ -29,7 +29,7 @@ hipError_t launch_cand_write(const uint8_t *comp, uint64_t n, uint64_t from, con
                              hipStream_t st);
 hipError_t build_chain(const uint8_t *comp, uint64_t n, const uint64_t *cand, uint64_t nc, int64_t *J0, int64_t *J1,
                        uint8_t *on, uint64_t *v, uint64_t *rank, uint64_t *tmp, DevBlocks bl, uint64_t *usz,
-                       uint64_t *nchain, hipStream_t st);
+                       uint64_t *nchain, uint8_t *next18, hipStream_t st);
 hipError_t launch_eager(const uint8_t *U, uint64_t u_pad, uint64_t begin, uint64_t end, const uint64_t *seg_end,
                         uint32_t nseg, uint32_t open_last, const int32_t *ctg, int32_t nctg, int32_t rtc,
                         uint32_t *bits, unsigned long long *counters, hipStream_t st, uint64_t front,
@@ -442,6 +442,10 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
     nc = sh->h_ctr[0] + sh->h_ctr[1];
   }
   uint64_t nchain = 0;
+  // the 18 bytes after the last chain block (the next header, checked below), written by
+  // k_chain_emit and copied back with the block table
+  uint8_t *next18_dev = reinterpret_cast<uint8_t *>(sh->ctr.p + 3072);
+  uint8_t *nx = reinterpret_cast<uint8_t *>(sh->h_ctr + 516);  // pinned
   if (nc) {
     HIPCHK(ctx, sh->cand.ensure(nc));
     HIPCHK(ctx, sh->J0.ensure(nc));
@@ -461,7 +465,7 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
     HIPCHK(ctx, sh->b_status.ensure(nc));
     HIPCHK(ctx, sh->b_ntok.ensure(nc));
     HIPCHK(ctx, build_chain(sh->comp.p, n, sh->cand.p, nc, sh->J0.p, sh->J1.p, sh->on.p, sh->v.p, sh->rank.p,
-                            sh->tmp.p, sh->dev_blocks(), sh->usz.p, &nchain, st));
+                            sh->tmp.p, sh->dev_blocks(), sh->usz.p, &nchain, next18_dev, st));
     HIPCHK(ctx, scan_exclusive_u64(sh->usz.p, sh->b_ustart.p, nchain, sh->tmp.p, st));
   }
   sh->ncand = nc;
@@ -487,6 +491,7 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
     HIPCHK(ctx, hipMemcpyAsync(hsz, sh->b_hsize.p, nchain * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipMemcpyAsync(usz, sh->b_usize.p, nchain * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipMemcpyAsync(fl, sh->b_flags.p, nchain * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(nx, next18_dev, 18, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipStreamSynchronize(st));
     for (uint64_t i = 0; i < nchain; ++i)
       sh->hb[i] = sbh_block{cs[i] + sh->file_off, us[i], csz[i], hsz[i], usz[i], fl[i]};
@@ -501,9 +506,6 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
     const sbh_block &l = sh->hb.back();
     const uint64_t q = l.start - sh->file_off + l.csize;
     if (q + 18 <= n) {  // the next header does not parse: HeaderParseException if read
-      uint8_t *nx = reinterpret_cast<uint8_t *>(sh->h_ctr + 516);  // pinned
-      HIPCHK(ctx, hipMemcpyAsync(nx, sh->comp.p + q, 18, hipMemcpyDeviceToHost, st));
-      HIPCHK(ctx, hipStreamSynchronize(st));
       if (sbh_header_make(nx, 18, nullptr, nullptr) != SBH_OK) {
         sh->broken_end = true;
         sh->open_last = false;
