@@ -1220,16 +1220,21 @@ __global__ __launch_bounds__(256) void k_first_set(const uint32_t *bits, uint64_
     } else {
       for (uint32_t k = 0; k < 4; ++k) v[k] = w + k < w_end ? bits[w + k] : 0u;
     }
+    unsigned long long hit = ~0ull;
     for (uint32_t k = 0; k < 4; ++k) {
       uint32_t x = v[k];
       const uint64_t p0 = begin + 32 * (w + k);
       if (p0 < from) x &= ~0u << (uint32_t)(from - p0);
       if (p0 + 32 > to) x &= (to - p0) >= 32 ? ~0u : ((1u << (uint32_t)(to - p0)) - 1u);
       if (x) {
-        atomicMin(best, (unsigned long long)(p0 + __builtin_ctz(x)));
+        hit = p0 + __builtin_ctz(x);
         break;
       }
     }
+    // positions grow with the lane, so the wave's lowest hitting lane holds its minimum:
+    // one atomic per wave (a lane each made ~250 k atomics queue on one address)
+    const uint64_t m = __ballot(hit != ~0ull);
+    if (m && (threadIdx.x & (WAVE - 1)) == (uint32_t)__builtin_ctzll(m)) atomicMin(best, hit);
   }
 }
 
