@@ -620,8 +620,9 @@ int index_records(const Args &a) {
 // header, then every record, or only the records whose index is in -r (:48-58) -- re-cut into
 // 65498-byte BGZF members on the GPU (sbh_bgzf_compress) plus the EOF member; -b / -i then
 // index the output like IndexBlocks / IndexRecords (:72-90).  Records pass through byte for
-// byte (htsjdk's decode/re-encode is the identity on a BAM it wrote); the deflate bytes are
-// this library's coder's, not zlib level 5's (include/sparkbam.h).
+// byte (htsjdk's decode/re-encode is the identity on a BAM it wrote), and each member is
+// deflated exactly as htsjdk's Deflater(5) does (zlib 1.2.11 deflate_slow, include/sparkbam.h),
+// so the output and its .blocks / .records equal htsjdk's (HTSJDKRewriteTest's dirMatch).
 int htsjdk_rewrite(const Args &a) {
   if (a.out.empty()) throw Error(SBH_E_ARG, "htsjdk-rewrite: missing output path");
   std::vector<uint8_t> payload;

@@ -324,18 +324,26 @@ int sbh_records_scan_regions(sbh_shard *sh, const uint64_t *chunk_begin, const u
 /* ---- BGZF writer -------------------------------------------------
  * The block compressor behind HTSJDKRewrite (cli/src/main/scala/org/hammerlab/bam/rewrite/
  * HTSJDKRewrite.scala:62-67: SAMFileWriterFactory.makeBAMWriter -> htsjdk
- * BlockCompressedOutputStream): the uncompressed stream src[0, n) is cut every 65498 bytes,
- * each piece becomes one BGZF member (deflate; stored when it would not fit 64 KiB), CRC32 +
- * ISIZE footer, then the 28-byte empty EOF member.  Member boundaries in uncompressed space
- * match htsjdk's; the deflate bytes are this library's own (hash-chain LZ77 with lazy
- * matching, one dynamic-Huffman block per member; ratio ~2.9 on BAM streams vs ~3.0 for
- * htsjdk's zlib level 5), not zlib's.  src is a host or device pointer (src_on_device); out is
- * host memory of at least sbh_bgzf_compress_bound(n) bytes.  Device scratch is bounded by a
- * batch of 2048 members (~0.9 GB), whatever n.  *deflate_ms (optional): the compress
- * kernels' device time, summed over the batches (HIP events on the context's stream). */
+ * BlockCompressedOutputStream): the uncompressed stream src[0, n) is cut every 65498 bytes and
+ * each piece becomes one BGZF member, CRC32 + ISIZE footer, then the 28-byte empty EOF member.
+ * sbh_bgzf_compress writes exactly htsjdk's bytes: each member is what java.util.zip.Deflater
+ * (level 5, nowrap) = zlib 1.2.11 deflate_slow produces, and a member whose deflate stream does
+ * not finish within htsjdk's 65518-byte buffer is re-deflated at level 0 (one stored block).
+ * sbh_bgzf_compress_level: level 5 (SBH_LEVEL_HTSJDK) as above; 4 and 6..9 the same zlib at
+ * that level (6 is samtools' default); 0 stored members; SBH_LEVEL_FAST this library's own
+ * faster coder (hash-chain LZ77 with lazy matching, one dynamic-Huffman block per member, not
+ * zlib's bytes).  src is a host or device pointer (src_on_device); out is host memory of at
+ * least sbh_bgzf_compress_bound(n) bytes.  Device scratch is bounded by a batch of 2048 members
+ * (~2 GB), whatever n.  *deflate_ms (optional): the compress kernels' device time, summed over
+ * the batches (HIP events on the context's stream). */
+#define SBH_LEVEL_HTSJDK 5
+#define SBH_LEVEL_FAST (-1)
 uint64_t sbh_bgzf_compress_bound(uint64_t n);
 int sbh_bgzf_compress(sbh_ctx *ctx, const void *src, uint64_t n, int src_on_device, uint8_t *out,
                       uint64_t out_cap, uint64_t *out_size, uint64_t *n_blocks, float *deflate_ms);
+int sbh_bgzf_compress_level(sbh_ctx *ctx, const void *src, uint64_t n, int src_on_device, int level,
+                            uint8_t *out, uint64_t out_cap, uint64_t *out_size, uint64_t *n_blocks,
+                            float *deflate_ms);
 
 #ifdef __cplusplus
 }

@@ -38,8 +38,9 @@ EXPORTS = [
     "sbh_find_record_start", "sbh_count_records", "sbh_chain_from", "sbh_split", "sbh_split_starts",
     "sbh_check_records", "sbh_run_shard",
     "sbh_stage_times", "sbh_run_stream", "sbh_records_scan", "sbh_records_fetch", "sbh_records_scan_regions", "sbh_verify_crc",
-    "sbh_bgzf_compress_bound", "sbh_bgzf_compress",
+    "sbh_bgzf_compress_bound", "sbh_bgzf_compress", "sbh_bgzf_compress_level",
 ]
+LEVEL_HTSJDK, LEVEL_FAST = 5, -1  # sbh_bgzf_compress_level: htsjdk's zlib level 5 / this library's own coder
 
 
 class SbhBlock(C.Structure):
@@ -130,6 +131,7 @@ def lib():
         "sbh_records_scan_regions": [P, P, P, U64, P, P, P, C.c_uint32, C.POINTER(SbhRecordsSizes)],
         "sbh_verify_crc": [P, PU64, PU64],
         "sbh_bgzf_compress": [P, P, U64, I32, P, U64, PU64, PU64, C.POINTER(C.c_float)],
+        "sbh_bgzf_compress_level": [P, P, U64, I32, I32, P, U64, PU64, PU64, C.POINTER(C.c_float)],
     }
     for name, args in sig.items():
         f = getattr(L, name)

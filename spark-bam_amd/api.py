@@ -268,7 +268,7 @@ def here():
     return os.path.dirname(os.path.abspath(__file__))
 
 
-def htsjdk_rewrite(path_or_bytes, out_path=None, read_ranges=None, ctx=None):
+def htsjdk_rewrite(path_or_bytes, out_path=None, read_ranges=None, ctx=None, level=5):
     """HTSJDKRewrite (cli/src/main/scala/org/hammerlab/bam/rewrite/HTSJDKRewrite.scala:40-67):
     the BAM's uncompressed stream -- header, then every record (or only those whose index is
     in `read_ranges`, a collection supporting `in`, like the reference's `-r` IntRanges,
@@ -278,16 +278,15 @@ def htsjdk_rewrite(path_or_bytes, out_path=None, read_ranges=None, ctx=None):
     them to out_path when given.  The `-b`/`-i` index side-outputs are the CLI's
     `index-blocks` / `index-records` run on the result.
 
-    Size trade-off: members are cut exactly where htsjdk cuts them (65498 uncompressed
-    bytes), but each is coded by this library's GPU coder (hash-chain LZ77 with lazy matching,
-    one dynamic-Huffman block per member, see deflate_core.h), not zlib level 5, so the
-    compressed bytes -- and therefore the block positions in `.blocks` / `.records` -- differ
-    from htsjdk's output; files come out ~3-5% larger (ratio 2.93 vs ~3.05 on BAM streams)."""
+    The members are byte-identical to htsjdk's: cut at 65498 uncompressed bytes and each
+    deflated as java.util.zip.Deflater(5, nowrap) = zlib 1.2.11 deflate_slow does (zdeflate.hip),
+    so the file, `.blocks` and `.records` equal HTSJDKRewriteTest's fixtures.  `level` picks
+    another zlib level (4..9, 0 = stored) or -1 for this library's faster, non-zlib coder."""
     L = _Loaded(path_or_bytes, ctx)
     try:
         sh = L.shard
         if read_ranges is None:
-            out, _, _ = L.ctx.bgzf_compress(sh.flat_ptr(), sh.flat_size)
+            out, _, _ = L.ctx.bgzf_compress(sh.flat_ptr(), sh.flat_size, level=level)
         else:
             flat = sh.read_flat()
             starts = sh.records(L.header_end, sh.flat_size)["flat"].astype(np.int64)
@@ -297,7 +296,7 @@ def htsjdk_rewrite(path_or_bytes, out_path=None, read_ranges=None, ctx=None):
                 np.fromiter((int(i) for i in read_ranges), dtype=np.int64)  # any collection (IntRanges)
             keep = idx[np.isin(idx, sel)]
             parts = [flat[:L.header_end]] + [flat[starts[i]:ends[i]] for i in keep]
-            out, _, _ = L.ctx.bgzf_compress(np.concatenate(parts))
+            out, _, _ = L.ctx.bgzf_compress(np.concatenate(parts), level=level)
     finally:
         L.close()
     if out_path is not None:

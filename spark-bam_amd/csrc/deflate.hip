@@ -31,35 +31,6 @@ static_assert(4 * QLEN >= PAYLOAD, "four quarters cover a member");
 constexpr uint32_t PREV_STRIDE = 65536;  // u16 prev[] entries per member in the batch scratch
 constexpr uint32_t TOK_STRIDE = LSEG * NLANE;  // u32 tokens per member in the batch scratch
 
-// v from lane ^ M: quad DPP for 1 and 2, ds_swizzle (bit mode, within 32 lanes) for 4..16,
-// ds_bpermute for 32.
-template <uint32_t M>
-__device__ __forceinline__ uint32_t xor_lane(uint32_t v) {
-  if constexpr (M == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false);
-  else if constexpr (M == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false);
-  else if constexpr (M < 32) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (int)((M << 10) | 0x1f));
-  else return (uint32_t)__shfl_xor((int)v, (int)M);
-}
-template <uint32_t SIZE, uint32_t STRIDE>
-__device__ __forceinline__ uint32_t bitonic_step(uint32_t k, uint32_t lane) {
-  const uint32_t o = xor_lane<STRIDE>(k);
-  const bool up = (lane & SIZE) == 0, lower = (lane & STRIDE) == 0;
-  return (lower == up) ? (k < o ? k : o) : (k > o ? k : o);
-}
-// ascending sort of one key per lane across the wave
-__device__ __forceinline__ uint32_t bitonic64(uint32_t k, uint32_t lane) {
-  k = bitonic_step<2, 1>(k, lane);
-  k = bitonic_step<4, 2>(k, lane), k = bitonic_step<4, 1>(k, lane);
-  k = bitonic_step<8, 4>(k, lane), k = bitonic_step<8, 2>(k, lane), k = bitonic_step<8, 1>(k, lane);
-  k = bitonic_step<16, 8>(k, lane), k = bitonic_step<16, 4>(k, lane), k = bitonic_step<16, 2>(k, lane);
-  k = bitonic_step<16, 1>(k, lane);
-  k = bitonic_step<32, 16>(k, lane), k = bitonic_step<32, 8>(k, lane), k = bitonic_step<32, 4>(k, lane);
-  k = bitonic_step<32, 2>(k, lane), k = bitonic_step<32, 1>(k, lane);
-  k = bitonic_step<64, 32>(k, lane), k = bitonic_step<64, 16>(k, lane), k = bitonic_step<64, 8>(k, lane);
-  k = bitonic_step<64, 4>(k, lane), k = bitonic_step<64, 2>(k, lane), k = bitonic_step<64, 1>(k, lane);
-  return k;
-}
-
 // prev[] of one member per workgroup.  Each wave links its quarter 64 positions a step: the
 // step's (hash, lane) keys are sorted across the wave, so a position's predecessor inside
 // the step is its sorted neighbour; the first of a hash in the step takes the wave's head
@@ -409,7 +380,7 @@ __global__ __launch_bounds__(256) void k_deflate_emit(const uint8_t *__restrict_
 constexpr uint32_t CSEG = 1024;
 __global__ __launch_bounds__(256) void k_footer(const uint8_t *__restrict__ src, uint64_t n, uint64_t b0,
                                                 uint64_t nblocks, uint32_t nbatch, uint8_t *__restrict__ slots,
-                                                const uint32_t *__restrict__ sizes) {
+                                                uint64_t stride, const uint32_t *__restrict__ sizes) {
   __shared__ uint32_t tab[256];
   __shared__ uint32_t T[32];
   const uint32_t t = threadIdx.x, lane = t & (WAVE - 1);
@@ -445,24 +416,24 @@ __global__ __launch_bounds__(256) void k_footer(const uint8_t *__restrict__ src,
   }
   if (lane == 0) {
     for (uint32_t k = nseg * CSEG; k < len; ++k) s = tab[(s ^ p[k]) & 0xff] ^ (s >> 8);
-    uint8_t *f = slots + (uint64_t)j * SLOT + sizes[j] - 8;
+    uint8_t *f = slots + (uint64_t)j * stride + sizes[j] - 8;
     put_le32(f, s ^ 0xffffffffu);
     put_le32(f + 4, len);
   }
 }
 
-__global__ __launch_bounds__(256) void k_gather(const uint8_t *__restrict__ slots, const uint32_t *__restrict__ sizes,
-                                                const uint64_t *__restrict__ offs, uint64_t nblocks,
-                                                uint8_t *__restrict__ out) {
+__global__ __launch_bounds__(256) void k_gather(const uint8_t *__restrict__ slots, uint64_t stride,
+                                                const uint32_t *__restrict__ sizes, const uint64_t *__restrict__ offs,
+                                                uint64_t nblocks, uint8_t *__restrict__ out) {
   const uint64_t b = blockIdx.x;
   if (b >= nblocks) return;
-  const uint8_t *s = slots + b * SLOT;
+  const uint8_t *s = slots + b * stride;
   uint8_t *d = out + offs[b];
   const uint32_t m = sizes[b];
   const uint32_t head = (uint32_t)((16 - ((uintptr_t)d & 15)) & 15) < m ? (uint32_t)((16 - ((uintptr_t)d & 15)) & 15) : m;
   for (uint32_t i = threadIdx.x; i < head; i += blockDim.x) d[i] = s[i];
   // destination now 16-byte aligned; the source (slot base + head) is read as bytes packed
-  // into 16-byte vectors (the slot base is 64 KiB aligned, head < 16)
+  // into 16-byte vectors (the slot stride is a multiple of 16, head < 16)
   const uint32_t nv = (m - head) / 16;
   for (uint32_t v = threadIdx.x; v < nv; v += blockDim.x) {
     const uint8_t *q = s + head + 16 * v;
@@ -488,14 +459,20 @@ hipError_t launch_deflate(const uint8_t *src, uint64_t n, uint64_t b0, uint32_t 
   hipLaunchKernelGGL(k_deflate_parse, dim3(nbatch), dim3(256), 0, st, src, n, b0, nb, prev, toks, recs);
   hipLaunchKernelGGL(k_deflate_codes, dim3(nbatch), dim3(128), 0, st, recs, nbatch);
   hipLaunchKernelGGL(k_deflate_emit, dim3(nbatch), dim3(256), 0, st, src, n, b0, nb, toks, recs, slots, sizes);
-  hipLaunchKernelGGL(k_footer, dim3((nbatch + 3) / 4), dim3(256), 0, st, src, n, b0, nb, nbatch, slots, sizes);
+  return launch_member_footer(src, n, b0, nb, nbatch, slots, SLOT, sizes, st);
+}
+
+hipError_t launch_member_footer(const uint8_t *src, uint64_t n, uint64_t b0, uint64_t nblocks, uint32_t nbatch,
+                                uint8_t *slots, uint64_t stride, const uint32_t *sizes, hipStream_t st) {
+  hipLaunchKernelGGL(k_footer, dim3((nbatch + 3) / 4), dim3(256), 0, st, src, n, b0, nblocks, nbatch, slots, stride,
+                     sizes);
   return hipGetLastError();
 }
 
-hipError_t launch_deflate_gather(const uint8_t *slots, const uint32_t *sizes, const uint64_t *offs, uint64_t nblocks,
-                                 uint8_t *out, hipStream_t st) {
+hipError_t launch_deflate_gather(const uint8_t *slots, uint64_t stride, const uint32_t *sizes, const uint64_t *offs,
+                                 uint64_t nblocks, uint8_t *out, hipStream_t st) {
   if (!nblocks) return hipSuccess;
-  hipLaunchKernelGGL(k_gather, dim3((uint32_t)nblocks), dim3(256), 0, st, slots, sizes, offs, nblocks, out);
+  hipLaunchKernelGGL(k_gather, dim3((uint32_t)nblocks), dim3(256), 0, st, slots, stride, sizes, offs, nblocks, out);
   return hipGetLastError();
 }
 

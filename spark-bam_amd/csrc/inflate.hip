@@ -694,9 +694,11 @@ __device__ __forceinline__ void inflate_serial(const uint8_t *__restrict__ comp,
   const uint32_t data_len = csize - hsize - 8;
 
   Bits br;
-  br.c32 = reinterpret_cast<const uint32_t *>(comp);
   const uint64_t dbyte = cstart + hsize;
-  br.a0 = (uint32_t)(dbyte >> 2);
+  // dword indices are relative to the block's first deflate dword (a 32-bit index into
+  // the whole shard would wrap past 16 GiB of compressed bytes)
+  br.c32 = reinterpret_cast<const uint32_t *>(comp + (dbyte & ~3ull));
+  br.a0 = 0;
   const uint32_t skip = (uint32_t)(dbyte & 3) * 8;
   br.limit = skip + data_len * 8;
   br.seek(skip);
@@ -735,7 +737,7 @@ __device__ __forceinline__ void inflate_serial(const uint8_t *__restrict__ comp,
       uint32_t n = len;
       if (n > avail_bytes) n = avail_bytes;
       if (n > usize - out) n = usize - out;
-      const uint8_t *src = comp + (uint64_t)br.a0 * 4 + (p0 >> 3);
+      const uint8_t *src = reinterpret_cast<const uint8_t *>(br.c32) + (p0 >> 3);
       to.drain(lane);
       for (uint32_t i = lane; i < n; i += WAVE) to.dst[i] = (uint32_t)src[i] << 8;  // literal tokens
       to.dst += n;
@@ -1279,10 +1281,10 @@ __device__ __forceinline__ bool par_header(HuffSmem &sm, Src<LDS> src, uint32_t 
 // The deflate blocks of one BGZF block, lane-parallel.  Returns false (uniformly) when
 // the block must be decoded by the serial path instead.
 template <bool LDS>
-__device__ __forceinline__ bool inflate_par(HuffSmem &sm, const uint8_t *__restrict__ comp, uint32_t a0, uint32_t skip,
+__device__ __forceinline__ bool inflate_par(HuffSmem &sm, const uint8_t *__restrict__ dbase, uint32_t skip,
                             uint32_t limit, uint32_t usize, uint32_t *__restrict__ tk, uint32_t tid, uint32_t lane,
                             uint32_t wid, uint32_t &ntok_out, bool pre, uint32_t pre_psym, uint32_t pre_last) {
-  const Src<LDS> src{LDS ? sm.stage : reinterpret_cast<const uint32_t *>(comp) + a0};
+  const Src<LDS> src{LDS ? sm.stage : reinterpret_cast<const uint32_t *>(dbase)};
   uint32_t p = skip, out = 0, ntok = 0;
   bool fixed_built = false;  // the tables in sm.t are the fixed code's
   for (;;) {
@@ -1438,10 +1440,11 @@ __global__ __launch_bounds__(WAVE * HDR_WAVES) void k_hdr(const uint8_t *__restr
   const uint32_t csize = bl.csize[b], hsize = bl.hsize[b], usize = bl.usize[b];
   const uint32_t data_len = csize - hsize - 8;
   const uint64_t dbyte = cstart + hsize;
-  const uint32_t a0 = (uint32_t)(dbyte >> 2), skip = (uint32_t)(dbyte & 3) * 8;
+  const uint32_t skip = (uint32_t)(dbyte & 3) * 8;
   const uint32_t limit = skip + data_len * 8;
   const uint32_t ndw = min((limit + 31) / 32 + 2, HDR_STAGE_DW);
-  const uint32_t *g = reinterpret_cast<const uint32_t *>(comp) + a0;
+  // 64-bit byte address of the block's first deflate dword (no 32-bit dword index)
+  const uint32_t *g = reinterpret_cast<const uint32_t *>(comp + (dbyte & ~3ull));
   for (uint32_t i = lane; i < ndw; i += WAVE) stage[i] = g[i];
   __builtin_amdgcn_wave_barrier();  // (a wave's LDS accesses complete in order)
   uint32_t *out = tok + bl.ustart[b] + usize - HDR_OUT_DW;
@@ -1512,7 +1515,9 @@ __global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__rest
   if (!serial) {
     const uint32_t data_len = csize - hsize - 8;
     const uint64_t dbyte = cstart + hsize;
-    const uint32_t a0 = (uint32_t)(dbyte >> 2);
+    // the block's deflate dwords, addressed from a 64-bit byte base (a 32-bit dword index
+    // into the shard would wrap past 16 GiB of compressed bytes)
+    const uint8_t *dbase = comp + (dbyte & ~3ull);
     const uint32_t skip = (uint32_t)(dbyte & 3) * 8;
     const uint32_t limit = skip + data_len * 8;
     const uint32_t ndw = (limit + 31) / 32 + 2;
@@ -1546,20 +1551,20 @@ __global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__rest
       }
     };
     if (ndw <= STAGE_DW) {
-      const uint32_t *g = reinterpret_cast<const uint32_t *>(comp) + a0;
+      const uint32_t *g = reinterpret_cast<const uint32_t *>(dbase);
       for (uint32_t i = tid; i < ndw; i += HT) sm.stage[i] = g[i];
       if (pre) put_tables();
       __syncthreads();
 #ifdef SBH_HUFF_PROBE
       if (tid == 0) atomicAdd(&hp_acc[0], __builtin_readcyclecounter() - hk0);
 #endif
-      ok = inflate_par<true>(sm, comp, a0, skip, limit, usize, tok + G, tid, lane, wid, ntok, pre, pre_psym, pre_last);
+      ok = inflate_par<true>(sm, dbase, skip, limit, usize, tok + G, tid, lane, wid, ntok, pre, pre_psym, pre_last);
     } else {
       if (pre) {
         put_tables();
         __syncthreads();
       }
-      ok = inflate_par<false>(sm, comp, a0, skip, limit, usize, tok + G, tid, lane, wid, ntok, pre, pre_psym,
+      ok = inflate_par<false>(sm, dbase, skip, limit, usize, tok + G, tid, lane, wid, ntok, pre, pre_psym,
                               pre_last);
     }
     if (uni(ok)) {

@@ -1803,12 +1803,21 @@ int sbh_records_fetch(sbh_shard *sh, const sbh_records_out *o) {
   return SBH_OK;
 }
 
-// ---- BGZF writer (deflate.hip; HTSJDKRewrite.scala:62-67) ----------------------------
-uint64_t sbh_bgzf_compress_bound(uint64_t n) { return deflate_nblocks(n) * 65536ull + 28; }
+// ---- BGZF writer (zdeflate.hip / deflate.hip; HTSJDKRewrite.scala:62-67) ------------------
+uint64_t sbh_bgzf_compress_bound(uint64_t n) { return deflate_nblocks(n) * ZDEFLATE_SLOT + 28; }
 
 int sbh_bgzf_compress(sbh_ctx *ctx, const void *src, uint64_t n, int src_on_device, uint8_t *out,
                       uint64_t out_cap, uint64_t *out_size, uint64_t *n_blocks, float *deflate_ms) {
+  return sbh_bgzf_compress_level(ctx, src, n, src_on_device, SBH_LEVEL_HTSJDK, out, out_cap, out_size, n_blocks,
+                                 deflate_ms);
+}
+
+int sbh_bgzf_compress_level(sbh_ctx *ctx, const void *src, uint64_t n, int src_on_device, int level, uint8_t *out,
+                            uint64_t out_cap, uint64_t *out_size, uint64_t *n_blocks, float *deflate_ms) {
   if (!ctx || !out_size || (!src && n) || !out) return SBH_E_ARG;
+  const bool fast = level == SBH_LEVEL_FAST;
+  if (!fast && (level < 0 || (level > 0 && level < 4) || level > 9))
+    return fail(ctx, SBH_E_ARG, "bgzf_compress: level %d (0, 4..9 or SBH_LEVEL_FAST)", level);
   const uint64_t nb = deflate_nblocks(n);
   if (out_cap < sbh_bgzf_compress_bound(n)) return fail(ctx, SBH_E_ARG, "bgzf_compress: out_cap < bound");
   int rc = set_device(ctx);
@@ -1818,11 +1827,11 @@ int sbh_bgzf_compress(sbh_ctx *ctx, const void *src, uint64_t n, int src_on_devi
     DBuf<uint8_t> in, slots, packed, recs;
     DBuf<uint16_t> prev;
     DBuf<uint32_t> toks, sizes;
-    DBuf<uint64_t> offs;
+    DBuf<uint64_t> offs, info;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     ~Bufs() {
       in.release(), slots.release(), packed.release(), recs.release(), prev.release(), toks.release(), sizes.release(),
-          offs.release();
+          offs.release(), info.release();
       if (e0) (void)hipEventDestroy(e0);
       if (e1) (void)hipEventDestroy(e1);
     }
@@ -1836,13 +1845,22 @@ int sbh_bgzf_compress(sbh_ctx *ctx, const void *src, uint64_t n, int src_on_devi
   uint64_t total = 0;
   float kms = 0.f;
   if (nb) {
-    // members in batches: scratch (prev, slots, packed) bounded by the batch, not the input
-    const uint64_t cap = nb < DEFLATE_BATCH ? nb : DEFLATE_BATCH;
-    HIPCHK(ctx, B.slots.ensure(cap * 65536ull));
-    HIPCHK(ctx, B.packed.ensure(cap * 65536ull));
-    HIPCHK(ctx, B.prev.ensure(cap * (DEFLATE_PREV_BYTES / 2)));
-    HIPCHK(ctx, B.toks.ensure(cap * (DEFLATE_TOK_BYTES / 4)));
-    HIPCHK(ctx, B.recs.ensure(cap * DEFLATE_REC_BYTES));
+    // members in batches: scratch bounded by the batch, not the input
+    const uint64_t bmax = fast ? DEFLATE_BATCH : ZDEFLATE_BATCH;
+    const uint64_t cap = nb < bmax ? nb : bmax;
+    const uint64_t stride = fast ? 65536ull : ZDEFLATE_SLOT;
+    HIPCHK(ctx, B.slots.ensure(cap * stride));
+    HIPCHK(ctx, B.packed.ensure(cap * stride));
+    if (fast) {
+      HIPCHK(ctx, B.prev.ensure(cap * (DEFLATE_PREV_BYTES / 2)));
+      HIPCHK(ctx, B.toks.ensure(cap * (DEFLATE_TOK_BYTES / 4)));
+      HIPCHK(ctx, B.recs.ensure(cap * DEFLATE_REC_BYTES));
+    } else if (level > 0) {
+      HIPCHK(ctx, B.prev.ensure(cap * ZDEFLATE_PREV_ENTRIES));
+      HIPCHK(ctx, B.info.ensure(cap * ZDEFLATE_INFO_ENTRIES));
+      HIPCHK(ctx, B.toks.ensure(cap * ZDEFLATE_TOK_ENTRIES));
+      HIPCHK(ctx, B.recs.ensure(cap * ZDEFLATE_REC_BYTES));
+    }
     HIPCHK(ctx, B.sizes.ensure(cap));
     HIPCHK(ctx, B.offs.ensure(cap));
     HIPCHK(ctx, hipEventCreate(&B.e0));
@@ -1852,7 +1870,11 @@ int sbh_bgzf_compress(sbh_ctx *ctx, const void *src, uint64_t n, int src_on_devi
     for (uint64_t b0 = 0; b0 < nb; b0 += cap) {
       const uint32_t k = (uint32_t)(nb - b0 < cap ? nb - b0 : cap);
       HIPCHK(ctx, hipEventRecord(B.e0, st));
-      HIPCHK(ctx, launch_deflate(d_src, n, b0, k, B.prev.p, B.toks.p, B.recs.p, B.slots.p, B.sizes.p, st));
+      if (fast)
+        HIPCHK(ctx, launch_deflate(d_src, n, b0, k, B.prev.p, B.toks.p, B.recs.p, B.slots.p, B.sizes.p, st));
+      else
+        HIPCHK(ctx, launch_zdeflate(d_src, n, b0, k, level, B.prev.p, B.info.p, B.toks.p, B.recs.p, B.slots.p,
+                                    B.sizes.p, st));
       HIPCHK(ctx, hipEventRecord(B.e1, st));
       HIPCHK(ctx, hipMemcpyAsync(hs.data(), B.sizes.p, 4ull * k, hipMemcpyDeviceToHost, st));
       HIPCHK(ctx, hipStreamSynchronize(st));
@@ -1861,14 +1883,14 @@ int sbh_bgzf_compress(sbh_ctx *ctx, const void *src, uint64_t n, int src_on_devi
       kms += ms;
       uint64_t bt = 0;
       for (uint32_t j = 0; j < k; ++j) {
-        if (hs[j] < 26 || hs[j] > 65536)
+        if (hs[j] < 26 || hs[j] > stride)
           return fail(ctx, SBH_E_HIP, "bgzf_compress: block %llu size %u", (unsigned long long)(b0 + j), hs[j]);
         ho[j] = bt;
         bt += hs[j];
       }
       if (total + bt + 28 > out_cap) return fail(ctx, SBH_E_ARG, "bgzf_compress: out_cap exceeded");
       HIPCHK(ctx, hipMemcpyAsync(B.offs.p, ho.data(), 8ull * k, hipMemcpyHostToDevice, st));
-      HIPCHK(ctx, launch_deflate_gather(B.slots.p, B.sizes.p, B.offs.p, k, B.packed.p, st));
+      HIPCHK(ctx, launch_deflate_gather(B.slots.p, stride, B.sizes.p, B.offs.p, k, B.packed.p, st));
       HIPCHK(ctx, hipMemcpyAsync(out + total, B.packed.p, bt, hipMemcpyDeviceToHost, st));
       HIPCHK(ctx, hipStreamSynchronize(st));
       total += bt;

@@ -23,6 +23,35 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
   return x;
 }
 
+// v from lane ^ M: quad DPP for 1 and 2, ds_swizzle (bit mode, within 32 lanes) for 4..16,
+// ds_bpermute for 32.
+template <uint32_t M>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v) {
+  if constexpr (M == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false);
+  else if constexpr (M == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false);
+  else if constexpr (M < 32) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (int)((M << 10) | 0x1f));
+  else return (uint32_t)__shfl_xor((int)v, (int)M);
+}
+template <uint32_t SIZE, uint32_t STRIDE>
+__device__ __forceinline__ uint32_t bitonic_step(uint32_t k, uint32_t lane) {
+  const uint32_t o = xor_lane<STRIDE>(k);
+  const bool up = (lane & SIZE) == 0, lower = (lane & STRIDE) == 0;
+  return (lower == up) ? (k < o ? k : o) : (k > o ? k : o);
+}
+// ascending sort of one key per lane across the wave
+__device__ __forceinline__ uint32_t bitonic64(uint32_t k, uint32_t lane) {
+  k = bitonic_step<2, 1>(k, lane);
+  k = bitonic_step<4, 2>(k, lane), k = bitonic_step<4, 1>(k, lane);
+  k = bitonic_step<8, 4>(k, lane), k = bitonic_step<8, 2>(k, lane), k = bitonic_step<8, 1>(k, lane);
+  k = bitonic_step<16, 8>(k, lane), k = bitonic_step<16, 4>(k, lane), k = bitonic_step<16, 2>(k, lane);
+  k = bitonic_step<16, 1>(k, lane);
+  k = bitonic_step<32, 16>(k, lane), k = bitonic_step<32, 8>(k, lane), k = bitonic_step<32, 4>(k, lane);
+  k = bitonic_step<32, 2>(k, lane), k = bitonic_step<32, 1>(k, lane);
+  k = bitonic_step<64, 32>(k, lane), k = bitonic_step<64, 16>(k, lane), k = bitonic_step<64, 8>(k, lane);
+  k = bitonic_step<64, 4>(k, lane), k = bitonic_step<64, 2>(k, lane), k = bitonic_step<64, 1>(k, lane);
+  return k;
+}
+
 // Block table (struct of arrays, one entry per BGZF block of the chain, in file
 // order).  Mirrors bgzf Metadata(start, compressedSize, uncompressedSize)
 // (bgzf/.../block/Metadata.scala:6-8) plus the header size and flat start.
@@ -107,8 +136,24 @@ constexpr uint64_t DEFLATE_REC_BYTES = 4096;           // per-member record: tok
 uint64_t deflate_nblocks(uint64_t n);
 hipError_t launch_deflate(const uint8_t *src, uint64_t n, uint64_t b0, uint32_t nbatch, uint16_t *prev,
                           uint32_t *toks, uint8_t *recs, uint8_t *slots, uint32_t *sizes, hipStream_t st);
-hipError_t launch_deflate_gather(const uint8_t *slots, const uint32_t *sizes, const uint64_t *offs, uint64_t nblocks,
-                                 uint8_t *out, hipStream_t st);
+hipError_t launch_deflate_gather(const uint8_t *slots, uint64_t stride, const uint32_t *sizes, const uint64_t *offs,
+                                 uint64_t nblocks, uint8_t *out, hipStream_t st);
+
+// Byte-exact BGZF writer (zdeflate.hip; zlib 1.2.11 deflate_slow at level 4..9, htsjdk's 5 by
+// default): members in batches of at most ZDEFLATE_BATCH, per member prev[] (u16), match
+// records (u64), tokens (u32), a record of blocks / trees / headers, and an output slot.
+constexpr uint32_t ZDEFLATE_BATCH = 2048;
+constexpr uint64_t ZDEFLATE_PREV_ENTRIES = 65536;
+constexpr uint64_t ZDEFLATE_INFO_ENTRIES = 65536;
+constexpr uint64_t ZDEFLATE_TOK_ENTRIES = 65536;
+constexpr uint64_t ZDEFLATE_REC_BYTES = 16384;
+constexpr uint32_t ZDEFLATE_HDR_BYTES = 640;  // a dynamic block header (<= ~4500 bits)
+constexpr uint64_t ZDEFLATE_SLOT = 65536 + 64;  // 18 + (< 65518) + 8 bytes, a multiple of 16
+hipError_t launch_zdeflate(const uint8_t *src, uint64_t n, uint64_t b0, uint32_t nbatch, int level, uint16_t *prev,
+                           uint64_t *info, uint32_t *toks, uint8_t *recs, uint8_t *slots, uint32_t *sizes,
+                           hipStream_t st);
+hipError_t launch_member_footer(const uint8_t *src, uint64_t n, uint64_t b0, uint64_t nblocks, uint32_t nbatch,
+                                uint8_t *slots, uint64_t stride, const uint32_t *sizes, hipStream_t st);
 
 // Batched splits and check-bam truth comparison (splits.hip).
 constexpr uint32_t SPLIT_OK = 0;    // first record and flat end decided on the device

@@ -112,8 +112,10 @@ __global__ __launch_bounds__(64) void k_split_prologue(SplitIn in, const uint64_
       const uint64_t tail = in.n >= 17 ? in.n - 17 : 0;
       if (lim > tail && (best == ~0ull || best >= tail) && best != ~1ull) best = ~1ull;
     }
-    best = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(best >> 32)) << 32) |
-           __builtin_amdgcn_readfirstlane((uint32_t)best);
+    // readfirstlane returns int: widen both halves through uint32_t, or a shard-relative
+    // offset with bit 31 set would sign-extend into the high word
+    best = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(best >> 32)) << 32) |
+           (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)best);
     if (best >= ~1ull) break;
     const uint64_t bi = lower_bound(in.cstart, in.nblocks, best);
     if (bi >= in.nblocks || in.cstart[bi] != best || (in.flags[bi] & BLK_EMPTY)) break;

@@ -80,18 +80,20 @@ class Context:
     def __exit__(self, *a):
         self.close()
 
-    def bgzf_compress(self, data, nbytes=None):
-        """BGZF-compress a flat byte stream (sbh_bgzf_compress; htsjdk BlockCompressedOutputStream as
-        driven by HTSJDKRewrite.scala:62-67).  data: numpy uint8 (host) or a device pointer (int)
-        with nbytes.  Returns (file bytes as numpy uint8, number of data members, kernel ms)."""
+    def bgzf_compress(self, data, nbytes=None, level=5):
+        """BGZF-compress a flat byte stream (sbh_bgzf_compress_level; htsjdk BlockCompressedOutputStream
+        as driven by HTSJDKRewrite.scala:62-67).  level 5 = htsjdk's bytes exactly (zlib 1.2.11
+        deflate_slow), 4 / 6..9 = zlib at that level, 0 = stored, -1 = this library's faster coder.
+        data: numpy uint8 (host) or a device pointer (int) with nbytes.  Returns (file bytes as
+        numpy uint8, number of data members, kernel ms)."""
         on_dev = isinstance(data, int)
         n = int(nbytes) if on_dev else int(data.size)
         cap = lib().sbh_bgzf_compress_bound(n)
         out = np.empty(cap, dtype=np.uint8)
         size, nb, ms = C.c_uint64(), C.c_uint64(), C.c_float()
         src = C.c_void_p(data) if on_dev else _ptr(np.ascontiguousarray(data, dtype=np.uint8))
-        _check(self.h, lib().sbh_bgzf_compress(self.h, src, n, 1 if on_dev else 0, _ptr(out), cap,
-                                               C.byref(size), C.byref(nb), C.byref(ms)))
+        _check(self.h, lib().sbh_bgzf_compress_level(self.h, src, n, 1 if on_dev else 0, int(level), _ptr(out), cap,
+                                                     C.byref(size), C.byref(nb), C.byref(ms)))
         return out[:size.value], nb.value, ms.value
 
     def run_stream(self, comp, contig_len, file_offset=0, file_size=None, own_end=None, index_start=None,

@@ -138,6 +138,11 @@ class OracleFile:
         p = lib().or_stream_data(self._s)
         return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(self.flat_size,)).copy()
 
+    def uncompressed_range(self, a, b):
+        """Flat bytes [a, b) (a copy of just that slice)."""
+        p = lib().or_stream_data(self._s)
+        return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(self.flat_size,))[a:b].copy()
+
     def flat_of(self, block_pos, offset):
         return lib().or_stream_flat_of(self._s, block_pos, offset)
 

@@ -1,8 +1,9 @@
-"""BGZF writer on the GPU (sbh_bgzf_compress / htsjdk_rewrite; HTSJDKRewrite.scala:40-67).
-k_prev + k_deflate run deflate_core.h's coder one workgroup per member, so the file must
-equal the host build's (tools/deflate_host.cpp) byte for byte (test_deflate_cpu.py pins that
-build against zlib); the rewritten fixtures re-inflate (zlib and this library's own GPU
-inflate + CRC check) to the original stream."""
+"""The writer's fast, non-zlib coder on the GPU (sbh_bgzf_compress_level(SBH_LEVEL_FAST);
+the default, byte-exact htsjdk coder is tests/test_zdeflate_gpu.py).  k_prev + k_deflate run
+deflate_core.h's coder one workgroup per member, so the file must equal the host build's
+(tools/deflate_host.cpp) byte for byte (test_deflate_cpu.py pins that build against zlib);
+the rewritten fixtures re-inflate (zlib and this library's own GPU inflate + CRC check) to the
+original stream, with htsjdk's member layout."""
 import zlib
 
 import numpy as np
@@ -14,6 +15,7 @@ from pkg import sb
 from test_deflate_cpu import PAYLOAD, check_roundtrip, compress, parse_members
 
 pytestmark = pytest.mark.gpu
+FAST = -1  # SBH_LEVEL_FAST
 
 FIXTURES = ["2.bam", "1.bam", "5k.bam", "1.2203053-2211029.bam"]
 
@@ -30,7 +32,7 @@ def test_gpu_equals_host_build(ctx, n):
     rng = np.random.default_rng(n)
     for data in (rng.integers(0, 256, n, dtype=np.uint8), np.zeros(n, np.uint8),
                  rng.integers(0, 4, n, dtype=np.uint8)):
-        got, nb, _ = ctx.bgzf_compress(data)
+        got, nb, _ = ctx.bgzf_compress(data, level=FAST)
         assert nb == (n + PAYLOAD - 1) // PAYLOAD
         assert got.tobytes() == compress(data.tobytes())
 
@@ -45,7 +47,7 @@ def test_batches_of_members(ctx):
     flat = OracleFile(np.fromfile(golden_bam("5k.bam"), dtype=np.uint8)).uncompressed()
     data = np.resize(flat, n)
     data[::4099] = rng.integers(0, 256, data[::4099].size, dtype=np.uint8)  # no two tiles alike
-    got, k, _ = ctx.bgzf_compress(data)
+    got, k, _ = ctx.bgzf_compress(data, level=FAST)
     assert k == nb
     m = parse_members(got.tobytes())
     assert len(m) == nb + 1 and m[-1][2] == 0
@@ -63,7 +65,7 @@ EOF = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
 def test_htsjdk_rewrite_fixture(ctx, name):
     data = np.fromfile(golden_bam(name), dtype=np.uint8)
     flat = OracleFile(data).uncompressed().tobytes()
-    out = sb.htsjdk_rewrite(golden_bam(name), ctx=ctx).tobytes()
+    out = sb.htsjdk_rewrite(golden_bam(name), ctx=ctx, level=FAST).tobytes()
     assert out == compress(flat)
     check_roundtrip(flat)
     # the library's own GPU inflate + CRC check reads its writer's output back
@@ -77,7 +79,7 @@ def test_htsjdk_rewrite_fixture(ctx, name):
 def test_rewrite_2bam_blocks_and_records(ctx):
     """2.bam was itself written by htsjdk: the rewrite's members have its usize sequence, and
     every .records position maps to the same (member index, offset)."""
-    out = sb.htsjdk_rewrite(golden_bam("2.bam"), ctx=ctx).tobytes()
+    out = sb.htsjdk_rewrite(golden_bam("2.bam"), ctx=ctx, level=FAST).tobytes()
     m = parse_members(out)
     ref_blocks = read_blocks("2.bam")
     assert [x[2] for x in m[:-1]] == [u for _, _, u in ref_blocks]
@@ -104,7 +106,7 @@ def test_rewrite_read_ranges(ctx):
     ends = np.append(starts[1:], flat.size)
     keep = set(range(10, 20)) | {100, 2499}
     want = flat[:starts[0]].tobytes() + b"".join(flat[starts[i]:ends[i]].tobytes() for i in sorted(keep))
-    out = sb.htsjdk_rewrite(golden_bam("2.bam"), read_ranges=keep, ctx=ctx).tobytes()
+    out = sb.htsjdk_rewrite(golden_bam("2.bam"), read_ranges=keep, ctx=ctx, level=FAST).tobytes()
     got = b"".join(x[3] for x in parse_members(out))
     assert got == want
     assert len(sb.load_reads(out, ctx=ctx)) == len(keep)
@@ -115,12 +117,11 @@ def _vpos_list(records_rows):
 
 
 def test_htsjdk_rewrite_test_slice(ctx):
-    """HTSJDKRewriteTest (cli/src/test/scala/org/hammerlab/bam/rewrite/HTSJDKRewriteTest.scala:14-24):
-    `htsjdk-rewrite -r 100-1000 2.bam` -> slice/2.100-1000.bam{,.blocks,.records}.  The
-    compressed bytes differ (htsjdk's level-5 Deflater vs this coder), so the test pins
-    everything else: the uncompressed stream (header + records [100, 1000)), the member usize
-    column of `.blocks`, and `.records` mapped through (member index, offset)."""
-    out = sb.htsjdk_rewrite(golden_bam("2.bam"), read_ranges=range(100, 1000), ctx=ctx).tobytes()
+    """HTSJDKRewriteTest's `-r 100-1000` slice through the FAST coder: its compressed bytes are
+    not zlib's (the default coder's are: test_zdeflate_gpu.py), everything else is pinned -- the
+    uncompressed stream, the member usize column of `.blocks`, and `.records` mapped through
+    (member index, offset)."""
+    out = sb.htsjdk_rewrite(golden_bam("2.bam"), read_ranges=range(100, 1000), ctx=ctx, level=FAST).tobytes()
     ref = np.fromfile(golden_bam("2.100-1000.bam"), dtype=np.uint8).tobytes()
     m, mr = parse_members(out), parse_members(ref)
     flat, flat_ref = b"".join(x[3] for x in m), b"".join(x[3] for x in mr)
