@@ -273,12 +273,41 @@ typedef struct {
   double ms_h2d;        /* summed host -> HBM copy time (HIP events on the copy stream) */
   double stage_ms[6];   /* sbh_stage_times summed over the windows                   */
   uint64_t halo_final;
+  /* sbh_run_stream2 only (zero otherwise): */
+  uint64_t crc_bad_blocks;  /* owned blocks whose BGZF footer CRC32 differs (opts.verify_crc) */
+  uint64_t crc_first_bad;   /* file offset of the first such block                   */
+  uint64_t splits_host;     /* splits decided by the exact per-split path (sbh_split)  */
+  double ms_splits;         /* device + host time of the per-split work, summed       */
+  double ms_crc;            /* CRC32 kernel time, summed over the windows              */
 } sbh_stream_result;
 int sbh_run_stream(sbh_ctx *ctx, const void *host_comp, uint64_t n, uint64_t file_offset,
                    uint64_t file_size, uint64_t index_start, uint64_t own_end_file, uint64_t window,
                    uint64_t halo, const int32_t *contig_len, int32_t n_contigs, int32_t reads_to_check,
                    int32_t max_read_size, uint8_t *out_bits, uint64_t out_bits_cap,
                    sbh_stream_result *res);
+
+/* sbh_run_stream with per-split results and an in-run CRC check: loadSplitsAndReads' per-split
+ * answer for a shard larger than HBM (CanLoadBam.scala:283-297,316-356 over SplitRDD.scala:
+ * 33-52's partitions).  When n_splits > 0, split i = [split_start[i], split_end[i]) (file
+ * offsets, sorted, split_start[i] < split_end[i] <= split_start[i + 1], every start in
+ * [file_offset, own_end_file), the last end <= own_end_file): windows are cut at split starts,
+ * so every split lies in one window, and each window's splits get sbh_split_starts' (status,
+ * first_vpos, count) -- exactly what sbh_split returns for them on the whole file.
+ * verify_crc: every owned block's inflated bytes against its footer CRC32 (crc_bad_blocks). */
+typedef struct {
+  uint64_t window, halo;
+  int32_t reads_to_check, max_read_size, bgzf_blocks_to_check, verify_crc;
+  const uint64_t *split_start, *split_end; /* n_splits entries, or NULL with n_splits = 0 */
+  uint64_t n_splits;
+  uint64_t *split_first_vpos, *split_count; /* out, n_splits entries                      */
+  int32_t *split_status;                   /* out: SBH_OK or the split's SBH_E_* status */
+  uint8_t *out_bits;
+  uint64_t out_bits_cap;
+} sbh_stream_opts;
+int sbh_run_stream2(sbh_ctx *ctx, const void *host_comp, uint64_t n, uint64_t file_offset,
+                    uint64_t file_size, uint64_t index_start, uint64_t own_end_file,
+                    const int32_t *contig_len, int32_t n_contigs, const sbh_stream_opts *opts,
+                    sbh_stream_result *res);
 
 /* ---- record field extraction ----
  * RecordStream from first_flat while the record start is < end_flat, decoded like

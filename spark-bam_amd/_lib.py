@@ -37,7 +37,7 @@ EXPORTS = [
     "sbh_pos_of", "sbh_flat_bound", "sbh_set_contigs", "sbh_check_eager", "sbh_eager_bits", "sbh_check_full",
     "sbh_find_record_start", "sbh_count_records", "sbh_chain_from", "sbh_split", "sbh_split_starts",
     "sbh_check_records", "sbh_run_shard",
-    "sbh_stage_times", "sbh_run_stream", "sbh_records_scan", "sbh_records_fetch", "sbh_records_scan_regions", "sbh_verify_crc",
+    "sbh_stage_times", "sbh_run_stream", "sbh_run_stream2", "sbh_records_scan", "sbh_records_fetch", "sbh_records_scan_regions", "sbh_verify_crc",
     "sbh_bgzf_compress_bound", "sbh_bgzf_compress", "sbh_bgzf_compress_level",
 ]
 LEVEL_HTSJDK, LEVEL_FAST = 5, -1  # sbh_bgzf_compress_level: htsjdk's zlib level 5 / this library's own coder
@@ -60,7 +60,16 @@ class SbhStreamResult(C.Structure):
                 ("first_vpos", C.c_uint64), ("exit_vpos", C.c_uint64), ("status", C.c_int32),
                 ("rewalks", C.c_int32), ("host_pinned", C.c_int32), ("pad", C.c_int32),
                 ("ms_wall", C.c_double), ("ms_h2d", C.c_double), ("stage_ms", C.c_double * 6),
-                ("halo_final", C.c_uint64)]
+                ("halo_final", C.c_uint64), ("crc_bad_blocks", C.c_uint64), ("crc_first_bad", C.c_uint64),
+                ("splits_host", C.c_uint64), ("ms_splits", C.c_double), ("ms_crc", C.c_double)]
+
+
+class SbhStreamOpts(C.Structure):
+    _fields_ = [("window", C.c_uint64), ("halo", C.c_uint64), ("reads_to_check", C.c_int32),
+                ("max_read_size", C.c_int32), ("bgzf_blocks_to_check", C.c_int32), ("verify_crc", C.c_int32),
+                ("split_start", C.c_void_p), ("split_end", C.c_void_p), ("n_splits", C.c_uint64),
+                ("split_first_vpos", C.c_void_p), ("split_count", C.c_void_p), ("split_status", C.c_void_p),
+                ("out_bits", C.c_void_p), ("out_bits_cap", C.c_uint64)]
 
 
 class SbhRecordsSizes(C.Structure):
@@ -126,6 +135,8 @@ def lib():
         "sbh_run_shard": [P, U64, U64, I32, I32, C.POINTER(SbhShardResult)],
         "sbh_run_stream": [P, P, U64, U64, U64, U64, U64, U64, U64, P, I32, I32, I32, P, U64,
                            C.POINTER(SbhStreamResult)],
+        "sbh_run_stream2": [P, P, U64, U64, U64, U64, U64, P, I32, C.POINTER(SbhStreamOpts),
+                            C.POINTER(SbhStreamResult)],
         "sbh_records_scan": [P, U64, U64, C.POINTER(SbhRecordsSizes)],
         "sbh_records_fetch": [P, C.POINTER(SbhRecordsOut)],
         "sbh_records_scan_regions": [P, P, P, U64, P, P, P, C.c_uint32, C.POINTER(SbhRecordsSizes)],

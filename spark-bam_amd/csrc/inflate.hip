@@ -1944,9 +1944,11 @@ hipError_t launch_first_bad(const uint32_t *status, uint64_t n, unsigned long lo
   return hipGetLastError();
 }
 
-hipError_t launch_huff(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, uint32_t *tok,
+hipError_t launch_huff(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, uint32_t *tok_buf, uint64_t tok_base,
                        hipStream_t stream) {
   if (nblocks == 0) return hipSuccess;
+  // the kernels index tokens by flat offset: tok[ustart_b] is block b's first token slot
+  uint32_t *tok = reinterpret_cast<uint32_t *>(reinterpret_cast<uintptr_t>(tok_buf) - tok_base * 4);
 #ifdef SBH_HUFF_SERIAL
   const uint64_t grid = (nblocks + WAVES - 1) / WAVES;
   hipLaunchKernelGGL(k_huff_serial<false>, dim3((uint32_t)grid), dim3(WAVES * WAVE), 0, stream, comp, blocks, nblocks,
@@ -1962,9 +1964,10 @@ hipError_t launch_huff(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, 
   return hipGetLastError();
 }
 
-hipError_t launch_lz(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, const uint32_t *tok, uint8_t *U,
-                     hipStream_t stream) {
+hipError_t launch_lz(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, const uint32_t *tok_buf,
+                     uint64_t tok_base, uint8_t *U, hipStream_t stream) {
   if (nblocks == 0) return hipSuccess;
+  const uint32_t *tok = reinterpret_cast<const uint32_t *>(reinterpret_cast<uintptr_t>(tok_buf) - tok_base * 4);
 #ifdef SBH_LZ_PAD  // occupancy probe: dynamic LDS that leaves one workgroup per CU
   hipLaunchKernelGGL(k_lz, dim3((uint32_t)nblocks), dim3(LZ_THREADS), SBH_LZ_PAD, stream, comp, blocks, nblocks, tok, U);
 #else

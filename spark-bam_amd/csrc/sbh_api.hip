@@ -563,6 +563,50 @@ static int inflate_status(sbh_shard *sh, hipStream_t st, uint64_t *bad_block, co
   return fail(ctx, SBH_E_INFLATE_DATA, "block %llu: invalid deflate data", (unsigned long long)b.start);
 }
 
+static DevBlocks blocks_from(DevBlocks d, uint64_t b) {
+  return DevBlocks{d.cstart + b, d.csize + b, d.hsize + b, d.usize + b, d.ustart + b, d.flags + b, d.status + b, d.ntok + b};
+}
+
+// Token buffer between k_huff and k_lz: 4 B per flat byte of the blocks inflated at once.  A
+// shard whose flat bytes exceed the budget (SBH_TOK_BUDGET bytes, default 16 GiB) is inflated in
+// consecutive batches of blocks that reuse one buffer, so HBM holds the compressed and flat
+// bytes plus a bounded token buffer whatever the shard size.
+static uint64_t tok_cap_flat() {
+  const char *e = std::getenv("SBH_TOK_BUDGET");
+  const long long v = e ? std::atoll(e) : 0;
+  return (v > 0 ? (uint64_t)v : (16ull << 30)) / 4;
+}
+
+struct TokPlan {
+  std::vector<std::pair<uint64_t, uint64_t>> batches;  // blocks [b0, b1)
+  bool reuse = false;                                  // batches share tok (base = ustart of b0)
+  uint64_t tok_len = 0;                                // tok entries to allocate
+};
+
+// Blocks [0, nblocks) in batches of at most max_blocks blocks and (when the whole shard does
+// not fit the token budget) at most the budget's flat bytes each (one block at least).
+static TokPlan tok_plan(const sbh_shard *sh, uint64_t max_blocks) {
+  TokPlan P;
+  const uint64_t nb = sh->nblocks, cap = tok_cap_flat();
+  P.reuse = sh->utotal + 64 > cap;
+  uint64_t b0 = 0;
+  while (b0 < nb) {
+    uint64_t b1 = b0 + 1;
+    const uint64_t u0 = sh->hb[b0].ustart;
+    while (b1 < nb && b1 - b0 < max_blocks &&
+           (!P.reuse || sh->hb[b1].ustart + sh->hb[b1].usize - u0 <= cap))
+      ++b1;
+    P.batches.emplace_back(b0, b1);
+    const uint64_t ext = sh->hb[b1 - 1].ustart + sh->hb[b1 - 1].usize - u0;
+    P.tok_len = std::max(P.tok_len, ext);
+    b0 = b1;
+  }
+  if (P.batches.empty()) P.batches.emplace_back(0, 0);  // (an empty shard: one empty batch)
+  if (!P.reuse) P.tok_len = sh->utotal;
+  P.tok_len += 64;
+  return P;
+}
+
 int sbh_inflate(sbh_shard *sh, uint64_t *bad_block) {
   if (!sh) return SBH_E_ARG;
   sbh_ctx *ctx = sh->ctx;
@@ -571,12 +615,16 @@ int sbh_inflate(sbh_shard *sh, uint64_t *bad_block) {
   if (rc) return rc;
   hipStream_t st = ctx->stream;
   HIPCHK(ctx, sh->U.ensure(sh->utotal + sh->pad));
-  HIPCHK(ctx, sh->tok.ensure(sh->utotal + 64));
+  const TokPlan P = tok_plan(sh, ~0ull);
+  HIPCHK(ctx, sh->tok.ensure(P.tok_len));
   HIPCHK(ctx, hipMemsetAsync(sh->U.p + sh->utotal, 0, sh->pad, st));
   mark(sh, 2);
-  HIPCHK(ctx, launch_huff(sh->comp.p, sh->dev_blocks(), sh->nblocks, sh->tok.p, st));
-  mark(sh, 7);
-  HIPCHK(ctx, launch_lz(sh->comp.p, sh->dev_blocks(), sh->nblocks, sh->tok.p, sh->U.p, st));
+  for (const auto &bt : P.batches) {  // (one stream: a batch's k_lz finishes before the next k_huff)
+    const DevBlocks d = blocks_from(sh->dev_blocks(), bt.first);
+    const uint64_t base = P.reuse ? sh->hb[bt.first].ustart : 0;
+    HIPCHK(ctx, launch_huff(sh->comp.p, d, bt.second - bt.first, sh->tok.p, base, st));
+    HIPCHK(ctx, launch_lz(sh->comp.p, d, bt.second - bt.first, sh->tok.p, base, sh->U.p, st));
+  }
   mark(sh, 3);
   rc = inflate_status(sh, st, bad_block);
   if (rc) return rc;
@@ -1246,10 +1294,6 @@ static hipEvent_t pev(sbh_shard *sh, size_t i) {
   return sh->pev[i];
 }
 
-static DevBlocks blocks_from(DevBlocks d, uint64_t b) {
-  return DevBlocks{d.cstart + b, d.csize + b, d.hsize + b, d.usize + b, d.ustart + b, d.flags + b, d.status + b, d.ntok + b};
-}
-
 static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_true) {
   sbh_ctx *ctx = sh->ctx;
   if (!sh->indexed) return fail(ctx, SBH_E_STATE, "inflate before index");
@@ -1260,7 +1304,10 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
   if (!sh->s_eg) HIPCHK(ctx, hipStreamCreateWithFlags(&sh->s_eg, hipStreamNonBlocking));
   hipStream_t sl = sh->s_lz, se = sh->s_eg;
   HIPCHK(ctx, sh->U.ensure(sh->utotal + sh->pad));
-  HIPCHK(ctx, sh->tok.ensure(sh->utotal + 64));
+  const uint64_t nb = sh->nblocks;
+  const uint64_t npipe = std::max<uint64_t>(1, std::min<uint64_t>(PIPE_MAX_BATCHES, nb / pipe_min_blocks()));
+  const TokPlan P = tok_plan(sh, (nb + npipe - 1) / std::max<uint64_t>(npipe, 1));
+  HIPCHK(ctx, sh->tok.ensure(P.tok_len));
   HIPCHK(ctx, sh->bits.ensure((E + 31) / 32 + 1));
   HIPCHK(ctx, sh->defer.ensure(DEFER_CAP));
   HIPCHK(ctx, sh->xq.ensure(2 * XQ_CAP_MAX));
@@ -1269,8 +1316,7 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
   HIPCHK(ctx, hipMemsetAsync(c, 0, 48, sa));
   HIPCHK(ctx, hipMemsetAsync(c + 2, 0xff, 8, sa));
   sh->inflated = sh->bits_valid = sh->chain_ok = sh->cm_valid = false;
-  const uint64_t nb = sh->nblocks;
-  const uint64_t nbat = std::max<uint64_t>(1, std::min<uint64_t>(PIPE_MAX_BATCHES, nb / pipe_min_blocks()));
+  const uint64_t nbat = P.batches.size();
   // events: per batch [huff start, huff end, lz start, lz end, eager start, eager end]
   for (size_t i = 0; i < 6 * nbat + 4; ++i)
     if (!pev(sh, i)) return fail(ctx, SBH_E_HIP, "hipEventCreate failed");
@@ -1282,15 +1328,18 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
   uint64_t e_done = 0;
   std::vector<int> eager_launched(nbat, 0);
   for (uint64_t i = 0; i < nbat; ++i) {
-    const uint64_t b0 = nb * i / nbat, b1 = nb * (i + 1) / nbat;
+    const uint64_t b0 = P.batches[i].first, b1 = P.batches[i].second;
     hipEvent_t *e = ev + 6 * i;
     const DevBlocks d = blocks_from(all, b0);
+    const uint64_t base = P.reuse ? sh->hb[b0].ustart : 0;
+    // a reused token buffer: this batch's k_huff overwrites what the previous k_lz reads
+    if (P.reuse && i) HIPCHK(ctx, hipStreamWaitEvent(sa, ev[6 * (i - 1) + 3], 0));
     HIPCHK(ctx, hipEventRecord(e[0], sa));
-    HIPCHK(ctx, launch_huff(sh->comp.p, d, b1 - b0, sh->tok.p, sa));
+    HIPCHK(ctx, launch_huff(sh->comp.p, d, b1 - b0, sh->tok.p, base, sa));
     HIPCHK(ctx, hipEventRecord(e[1], sa));
     HIPCHK(ctx, hipStreamWaitEvent(sl, e[1], 0));
     HIPCHK(ctx, hipEventRecord(e[2], sl));
-    HIPCHK(ctx, launch_lz(sh->comp.p, d, b1 - b0, sh->tok.p, sh->U.p, sl));
+    HIPCHK(ctx, launch_lz(sh->comp.p, d, b1 - b0, sh->tok.p, base, sh->U.p, sl));
     HIPCHK(ctx, hipEventRecord(e[3], sl));
     // eager tiles whose staged windows lie below the inflated frontier
     const bool last = i + 1 == nbat;
@@ -1440,11 +1489,63 @@ int sbh_run_stream(sbh_ctx *ctx, const void *host, uint64_t n, uint64_t file_off
                    uint64_t index_start, uint64_t own_end_file, uint64_t window, uint64_t halo, const int32_t *contigs,
                    int32_t n_contigs, int32_t rtc, int32_t mrs, uint8_t *out_bits, uint64_t out_bits_cap,
                    sbh_stream_result *res) {
-  if (!ctx || !res || (!host && n) || !window || file_offset + n > file_size || own_end_file > file_offset + n ||
-      own_end_file <= file_offset || n_contigs < 0 || (n_contigs && !contigs))
+  sbh_stream_opts o{};
+  o.window = window;
+  o.halo = halo;
+  o.reads_to_check = rtc;
+  o.max_read_size = mrs;
+  o.bgzf_blocks_to_check = 5;
+  o.out_bits = out_bits;
+  o.out_bits_cap = out_bits_cap;
+  return sbh_run_stream2(ctx, host, n, file_offset, file_size, index_start, own_end_file, contigs, n_contigs, &o, res);
+}
+
+// CRC32 of the first nb blocks of the table (a window's owned blocks) against their footers.
+static int verify_crc_prefix(sbh_shard *sh, uint64_t nb, uint64_t *n_bad, uint64_t *first_bad, float *ms) {
+  sbh_ctx *ctx = sh->ctx;
+  hipStream_t st = ctx->stream;
+  unsigned long long *c = sh->ctr.p + 32;
+  HIPCHK(ctx, hipMemsetAsync(c, 0, 8, st));
+  HIPCHK(ctx, hipMemsetAsync(c + 1, 0xff, 8, st));
+  mark(sh, 7);
+  HIPCHK(ctx, launch_block_crc(sh->comp.p, sh->dev_blocks(), nb, sh->U.p, c, c + 1, st));
+  mark(sh, 8);
+  HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 32, c, 16, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, hipStreamSynchronize(st));
+  *n_bad = sh->h_ctr[32];
+  *first_bad = sh->h_ctr[32] ? sh->hb[sh->h_ctr[33]].start : 0;
+  *ms = 0.f;
+  if (sh->ev_ok) (void)hipEventElapsedTime(ms, sh->ev[7], sh->ev[8]);
+  return SBH_OK;
+}
+
+int sbh_run_stream2(sbh_ctx *ctx, const void *host, uint64_t n, uint64_t file_offset, uint64_t file_size,
+                    uint64_t index_start, uint64_t own_end_file, const int32_t *contigs, int32_t n_contigs,
+                    const sbh_stream_opts *opts, sbh_stream_result *res) {
+  if (!ctx || !res || !opts || (!host && n) || !opts->window || file_offset + n > file_size ||
+      own_end_file > file_offset + n || own_end_file <= file_offset || n_contigs < 0 || (n_contigs && !contigs))
     return SBH_E_ARG;
+  const sbh_stream_opts &O = *opts;
+  const uint64_t window = O.window;
+  uint64_t halo = O.halo;
+  const int32_t rtc = O.reads_to_check, mrs = O.max_read_size, kcheck = O.bgzf_blocks_to_check;
+  uint8_t *out_bits = O.out_bits;
+  const uint64_t out_bits_cap = O.out_bits_cap, ns = O.n_splits;
   std::memset(res, 0, sizeof *res);
   res->first_vpos = res->exit_vpos = ~0ull;
+  if (ns) {  // splits: sorted, disjoint, inside the owned range, with their outputs
+    if (!O.split_start || !O.split_end || !O.split_first_vpos || !O.split_count || !O.split_status)
+      return fail(ctx, SBH_E_ARG, "run_stream2: split arrays missing");
+    for (uint64_t i = 0; i < ns; ++i) {
+      const uint64_t a = O.split_start[i], e = O.split_end[i];
+      if (a < file_offset || a >= own_end_file || e <= a || e > own_end_file || (i + 1 < ns && e > O.split_start[i + 1]))
+        return fail(ctx, SBH_E_ARG, "run_stream2: split %llu [%llu, %llu) out of order or outside [%llu, %llu)",
+                    (unsigned long long)i, (unsigned long long)a, (unsigned long long)e,
+                    (unsigned long long)file_offset, (unsigned long long)own_end_file);
+      O.split_first_vpos[i] = O.split_count[i] = 0;
+      O.split_status[i] = SBH_OK;
+    }
+  }
   const auto t_start = std::chrono::steady_clock::now();
   int rc = set_device(ctx);
   if (rc) return res->status = rc;
@@ -1485,19 +1586,35 @@ int sbh_run_stream(sbh_ctx *ctx, const void *host, uint64_t n, uint64_t file_off
   const uint64_t data_end = file_offset + n, pad = sh->pad;
   // the first window is short: its copy is the only one no kernel overlaps
   const uint64_t first_window = std::max<uint64_t>(std::min<uint64_t>(window, 64ull << 20), window / 8);
+  // window ends: split starts when splits are given (a split never straddles two windows)
   auto win_end = [&](uint64_t lo) {
-    uint64_t hi = std::min(lo + (lo == file_offset ? first_window : window), own_end_file);
+    const uint64_t want = lo + (lo == file_offset ? first_window : window);
+    uint64_t hi = std::min(want, own_end_file);
     if (own_end_file - hi < window / 4) hi = own_end_file;  // no sliver of a last window
+    if (ns && hi < own_end_file) {
+      // the last split start in (lo, hi], else the first one after lo
+      const uint64_t *S = O.split_start;
+      const uint64_t k = (uint64_t)(std::upper_bound(S, S + ns, hi) - S);  // starts <= hi: [0, k)
+      if (k > 0 && S[k - 1] > lo) hi = S[k - 1];
+      else if (k < ns) hi = S[k];
+      else hi = own_end_file;
+    }
     return hi;
   };
   auto load_end = [&](uint64_t hi) { return std::min(hi + halo, data_end); };
-  auto size_bufs = [&]() -> hipError_t {
+  auto size_bufs = [&]() -> hipError_t {  // (enqueue grows a buffer for a longer split-aligned window)
     const uint64_t cap = window + window / 4 + halo + pad;
     for (auto &b : R.buf) {
       hipError_t e = b.ensure(cap);
       if (e != hipSuccess) return e;
     }
     return hipSuccess;
+  };
+  auto fit_buf = [&](int b, uint64_t need) -> hipError_t {  // grow buffer b (not in use) to `need` bytes
+    hipError_t e = hipStreamSynchronize(R.cs);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess) e = R.buf[b].ensure(need);
+    return e;
   };
   double h2d_ms = 0;
   bool timed[2] = {false, false};
@@ -1508,7 +1625,12 @@ int sbh_run_stream(sbh_ctx *ctx, const void *host, uint64_t n, uint64_t file_off
     timed[b] = false;
   };
   auto enqueue = [&](int b, uint64_t lo, uint64_t ld) -> hipError_t {
-    hipError_t e = hipEventRecord(R.c0[b], R.cs);
+    hipError_t e = hipSuccess;
+    if (R.buf[b].cap < ld - lo + pad) {  // an oversized (split-aligned) window
+      e = fit_buf(b, ld - lo + pad);
+      if (e != hipSuccess) return e;
+    }
+    e = hipEventRecord(R.c0[b], R.cs);
     if (e == hipSuccess) e = hipMemcpyAsync(R.buf[b].p, src + (lo - file_offset), ld - lo, hipMemcpyHostToDevice, R.cs);
     if (e == hipSuccess) e = hipMemsetAsync(R.buf[b].p + (ld - lo), 0, pad, R.cs);
     if (e == hipSuccess) e = hipEventRecord(R.done[b], R.cs);
@@ -1534,11 +1656,29 @@ int sbh_run_stream(sbh_ctx *ctx, const void *host, uint64_t n, uint64_t file_off
     sh->n = ld - lo;
     sh->at_eof = ld == file_size;
     if (start == ~0ull) {
-      rc = sbh_find_block_start(sh, lo, 5, &start);  // BGZFBlocksToCheck (bgzf/.../block/package.scala:20)
+      rc = sbh_find_block_start(sh, lo, kcheck, &start);  // BGZFBlocksToCheck (bgzf/.../block/package.scala:20)
       if (rc) return res->status = rc;
     }
     sbh_shard_result r{};
     rc = sbh_run_shard(sh, start, hi, rtc, mrs, &r);
+    // this window's splits (every one inside [lo, hi)): the batched per-split path
+    uint64_t k0 = 0, k1 = 0;
+    double split_ms = 0;
+    if (!rc && ns) {
+      k0 = (uint64_t)(std::lower_bound(O.split_start, O.split_start + ns, lo) - O.split_start);
+      k1 = (uint64_t)(std::lower_bound(O.split_start, O.split_start + ns, hi) - O.split_start);
+      if (k1 > k0) {
+        const auto ts0 = std::chrono::steady_clock::now();
+        uint64_t nh = 0;
+        rc = sbh_split_starts(sh, O.split_start + k0, O.split_end + k0, k1 - k0, kcheck, rtc, mrs,
+                              O.split_first_vpos + k0, O.split_count + k0, O.split_status + k0, &nh);
+        if (!rc)
+          for (uint64_t i = k0; i < k1; ++i)
+            if (O.split_status[i] == SBH_E_NEED_HALO) rc = SBH_E_NEED_HALO;
+        res->splits_host += nh;
+        split_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
+      }
+    }
     if (rc == SBH_E_NEED_HALO && ld < data_end) {  // grow the halo and redo this window
       HIPCHK(ctx, hipStreamSynchronize(R.cs));
       HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
@@ -1554,7 +1694,20 @@ int sbh_run_stream(sbh_ctx *ctx, const void *host, uint64_t n, uint64_t file_off
       continue;
     }
     if (rc) return res->status = rc;
+    res->ms_splits += split_ms;
     account(cur);
+    if (O.verify_crc && r.n_blocks) {  // the owned blocks are the block table's prefix
+      uint64_t nbad = 0, fbad = 0;
+      float cms = 0.f;
+      const bool was = sh->timing;
+      sh->timing = true;
+      rc = verify_crc_prefix(sh, std::min<uint64_t>(r.n_blocks, sh->nblocks), &nbad, &fbad, &cms);
+      sh->timing = was;
+      if (rc) return res->status = rc;
+      if (nbad && !res->crc_bad_blocks) res->crc_first_bad = fbad;
+      res->crc_bad_blocks += nbad;
+      res->ms_crc += cms;
+    }
     // this window's chain exit, and the stitch with the previous non-empty window
     uint64_t count = r.count, exit_vpos = ~0ull;
     auto vpos_of = [&](uint64_t flat, uint64_t *v) {

@@ -88,12 +88,14 @@ constexpr uint64_t EAGER_REACH = SBH_ETILE + 4096 + 512 + 64;
 
 // Launchers (defined in the .hip files, called from sbh_api.hip).
 // Inflate = k_huff (Huffman decode -> LZ77 tokens, block status) then k_lz (tokens ->
-// flat bytes; a block that is one stored deflate block is copied from comp).  tok: scratch
-// of >= 4 B per flat byte (block b's tokens at tok[ustart_b ...]).
-hipError_t launch_huff(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, uint32_t *tok,
+// flat bytes; a block that is one stored deflate block is copied from comp).  tok_buf: >= 4 B
+// of token scratch per flat byte of the launched blocks, tok_buf[0] standing for flat offset
+// tok_base (block b's tokens at tok_buf[ustart_b - tok_base ...]), so a shard can be inflated
+// in batches of blocks that reuse one bounded token buffer.
+hipError_t launch_huff(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, uint32_t *tok_buf, uint64_t tok_base,
                        hipStream_t stream);
-hipError_t launch_lz(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, const uint32_t *tok, uint8_t *U,
-                     hipStream_t stream);
+hipError_t launch_lz(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, const uint32_t *tok_buf,
+                     uint64_t tok_base, uint8_t *U, hipStream_t stream);
 // *first = the first block of [0, n) whose status is not INF_OK (~0 if none).
 hipError_t launch_first_bad(const uint32_t *status, uint64_t n, unsigned long long *first, hipStream_t stream);
 

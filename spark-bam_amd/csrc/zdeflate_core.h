@@ -469,8 +469,10 @@ SBH_HD inline uint32_t z_tok_bits_tab(uint32_t t, const uint32_t *lit, const uin
   uint64_t x = l & 0xffff;
   uint32_t n = l >> 16;
   const uint32_t el = (uint32_t)EXTRA_LBITS[code];
-  x |= (uint64_t)(lc - BASE_LENGTH[code]) << n;
-  n += el;
+  if (el) {  // (length 258 is code 28 with base 0 and no extra bits)
+    x |= (uint64_t)(lc - BASE_LENGTH[code]) << n;
+    n += el;
+  }
   x |= (uint64_t)(dd & 0xffff) << n;
   n += dd >> 16;
   x |= (uint64_t)(d - BASE_DIST[dc]) << n;
@@ -554,57 +556,6 @@ SBH_HD inline void z_send_all_trees(const ZTreeState &s, int32_t max_blindex, co
   z_send_tree(s, s.dyn_dtree, dcodes - 1, put);
 }
 
-// A token's bits under the block's trees (compress_block): up to 15 + 5 + 15 + 13 = 48 bits.
-SBH_HD inline uint32_t z_tok_bits(uint32_t t, uint32_t type, const ZTreeState &s, uint64_t *v) {
-  if (!(t & TOK_M)) {
-    const uint32_t c = t & 0xff;
-    if (type == ZB_STATIC) {
-      *v = static_lcode(c);
-      return static_llen(c);
-    }
-    *v = s.dyn_ltree[c].fc;
-    return s.dyn_ltree[c].dl;
-  }
-  const uint32_t lc = (t >> 16) & 0xff, dist = (t & 0xffff) - 1;
-  const uint32_t code = length_code(lc), dc = dist_code(dist);
-  uint64_t x;
-  uint32_t n;
-  if (type == ZB_STATIC) {
-    x = static_lcode(code + 257);
-    n = static_llen(code + 257);
-  } else {
-    x = s.dyn_ltree[code + 257].fc;
-    n = s.dyn_ltree[code + 257].dl;
-  }
-  const uint32_t el = (uint32_t)EXTRA_LBITS[code];
-  if (el) {
-    x |= (uint64_t)(lc - BASE_LENGTH[code]) << n;
-    n += el;
-  }
-  if (type == ZB_STATIC) {
-    x |= (uint64_t)bi_reverse(dc, 5) << n;
-    n += 5;
-  } else {
-    x |= (uint64_t)s.dyn_dtree[dc].fc << n;
-    n += s.dyn_dtree[dc].dl;
-  }
-  const uint32_t ed = (uint32_t)EXTRA_DBITS[dc];
-  if (ed) {
-    x |= (uint64_t)(dist - BASE_DIST[dc]) << n;
-    n += ed;
-  }
-  *v = x;
-  return n;
-}
-SBH_HD inline uint32_t z_eob_bits(uint32_t type, const ZTreeState &s, uint32_t *v) {
-  if (type == ZB_STATIC) {
-    *v = static_lcode(256);
-    return 7;
-  }
-  *v = s.dyn_ltree[256].fc;
-  return s.dyn_ltree[256].dl;
-}
-
 // The whole member serially (host reference of the GPU stages): raw deflate bytes of
 // src[0, N) into out (cap bytes); returns the deflate size, or 0 when it does not fit
 // OUT_CAP - 1 bytes (htsjdk then stores the block at level 0).  tok / prev / info: scratch
@@ -633,11 +584,13 @@ SBH_HD inline void z_emit_block(ZBits &o, const ZTreeState &s, uint32_t type, in
     o.put(~len & 0xffff, 16);
     for (uint32_t i = b.byte0; i < b.byte1; ++i) o.put(byteat(i), 8);
   } else {
+    uint32_t lit[L_CODES], dist[D_CODES];  // (the tables the GPU's k_zemit codes with)
+    z_code_tables(s, type, lit, dist);
     o.put((type == ZB_STATIC ? 2u : 4u) + lb, 3);
     if (type == ZB_DYN) z_send_all_trees(s, mbl, put);
     for (uint32_t k = b.tok0; k < b.tok1; ++k) {
       uint64_t v;
-      const uint32_t n = z_tok_bits(tokat(k), type, s, &v);
+      const uint32_t n = z_tok_bits_tab(tokat(k), lit, dist, &v);
       if (n > 32) {
         o.put((uint32_t)v & 0xffffu, 16);
         o.put((uint32_t)(v >> 16), n - 16);
@@ -645,9 +598,7 @@ SBH_HD inline void z_emit_block(ZBits &o, const ZTreeState &s, uint32_t type, in
         o.put((uint32_t)v, n);
       }
     }
-    uint32_t ev;
-    const uint32_t en = z_eob_bits(type, s, &ev);
-    o.put(ev, en);
+    o.put(lit[256] & 0xffff, lit[256] >> 16);
   }
   if (last) o.windup();
 }

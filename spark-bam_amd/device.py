@@ -4,8 +4,8 @@ import weakref
 
 import numpy as np
 
-from ._lib import (SBH_OK, SbhBlock, SbhRecordsOut, SbhRecordsSizes, SbhShardResult, SbhStreamResult,
-                   SparkBamError, lib)
+from ._lib import (SBH_OK, SbhBlock, SbhRecordsOut, SbhRecordsSizes, SbhShardResult, SbhStreamOpts,
+                   SbhStreamResult, SparkBamError, lib)
 
 
 def _check(ctx_handle, rc):
@@ -97,10 +97,15 @@ class Context:
         return out[:size.value], nb.value, ms.value
 
     def run_stream(self, comp, contig_len, file_offset=0, file_size=None, own_end=None, index_start=None,
-                   window=1 << 30, halo=4 << 20, reads_to_check=10, max_read_size=100000000, want_bits=False):
-        """sbh_run_stream: the per-shard hot path over host-resident compressed bytes `comp`
+                   window=1 << 30, halo=4 << 20, reads_to_check=10, max_read_size=100000000, want_bits=False,
+                   splits=None, verify_crc=False, bgzf_blocks_to_check=5):
+        """sbh_run_stream2: the per-shard hot path over host-resident compressed bytes `comp`
         (numpy uint8, ideally pinned) = file bytes [file_offset, file_offset + comp.size),
-        streamed through HBM in windows.  Returns (result dict, eager bits or None)."""
+        streamed through HBM in windows.  splits = [(start, end), ...] (file offsets inside the
+        owned range): the windows are cut at split starts and every split gets sbh_split's
+        (status, first_vpos, count) -> result["split_status" / "split_first_vpos" /
+        "split_count"].  verify_crc: every owned block's CRC32 (result["crc_bad_blocks"]).
+        Returns (result dict, eager bits or None)."""
         arr = np.ascontiguousarray(comp, dtype=np.uint8) if isinstance(comp, np.ndarray) else comp
         n = int(arr.size)
         file_size = file_offset + n if file_size is None else int(file_size)
@@ -109,17 +114,33 @@ class Context:
         bits = None
         if want_bits:
             bits = np.zeros(max(1, 4 * n + 64), dtype=np.uint8)  # > (flat + 7) / 8 at any ratio <= 32
+        o = SbhStreamOpts()
+        o.window, o.halo = int(window), int(halo)
+        o.reads_to_check, o.max_read_size = reads_to_check, max_read_size
+        o.bgzf_blocks_to_check, o.verify_crc = bgzf_blocks_to_check, 1 if verify_crc else 0
+        keep = []
+        if splits:
+            st = np.ascontiguousarray([a for a, _ in splits], dtype=np.uint64)
+            en = np.ascontiguousarray([b for _, b in splits], dtype=np.uint64)
+            fv = np.zeros(st.size, np.uint64)
+            cn = np.zeros(st.size, np.uint64)
+            ss = np.zeros(st.size, np.int32)
+            keep = [st, en, fv, cn, ss]
+            o.split_start, o.split_end, o.n_splits = _ptr(st).value, _ptr(en).value, st.size
+            o.split_first_vpos, o.split_count, o.split_status = _ptr(fv).value, _ptr(cn).value, _ptr(ss).value
+        if bits is not None:
+            o.out_bits, o.out_bits_cap = _ptr(bits).value, bits.size
         r = SbhStreamResult()
-        _check(self.h, lib().sbh_run_stream(self.h, _ptr(arr), n, int(file_offset), file_size,
-                                            0xFFFFFFFFFFFFFFFF if index_start is None else int(index_start),
-                                            own_end, int(window), int(halo), _ptr(cl), int(cl.size),
-                                            reads_to_check, max_read_size, _ptr(bits),
-                                            0 if bits is None else bits.size, C.byref(r)))
+        _check(self.h, lib().sbh_run_stream2(self.h, _ptr(arr), n, int(file_offset), file_size,
+                                             0xFFFFFFFFFFFFFFFF if index_start is None else int(index_start),
+                                             own_end, _ptr(cl), int(cl.size), C.byref(o), C.byref(r)))
         out = {f: getattr(r, f) for f, _ in SbhStreamResult._fields_ if f != "stage_ms"}
         out["stage_ms"] = list(r.stage_ms)
         for k in ("first_vpos", "exit_vpos"):
             if out[k] == 0xFFFFFFFFFFFFFFFF:
                 out[k] = None
+        if keep:
+            out["split_status"], out["split_first_vpos"], out["split_count"] = keep[4], keep[2], keep[3]
         if bits is not None:
             bits = bits[:(out["flat_bytes"] + 7) // 8]
         return out, bits

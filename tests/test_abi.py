@@ -14,7 +14,7 @@ from pkg import ROOT, sb
 def header_decls():
     with open(os.path.join(ROOT, "include", "sparkbam.h")) as f:
         src = f.read()
-    return sorted(set(re.findall(r"\b(sbh_[a-z_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(sbh_[a-z0-9_]+)\s*\(", src)))
 
 
 def test_library_exports_every_declared_symbol():

@@ -104,3 +104,50 @@ def test_stream_subrange_of_a_file(ctx, files):
     assert np.array_equal(np.unpackbits(got, bitorder="little")[:E - base],
                           np.unpackbits(want, bitorder="little")[:E - base])
     assert s["count"] == n_ref
+
+
+@pytest.mark.parametrize("name", list(CORPORA))
+@pytest.mark.parametrize("window,split", [(150_000, 40_000), (400_000, 97_000), (150_000, 400_000)])
+def test_stream_splits_equal_resident_and_oracle(ctx, files, name, window, split):
+    """loadSplitsAndReads' per-split answer through bounded HBM (sbh_run_stream2): windows cut
+    at split starts, each split decided by the batched split path in its window -- equal to
+    the resident batch (sbh_split_starts on the whole file) and to the oracle
+    (CanLoadBam.scala:283-297,316-356).  A split larger than the window makes its window
+    larger than asked.  The in-run CRC32 check finds no bad block."""
+    from oracle_lib import OR_OK, file_splits
+    data, nrec = files[name]
+    of = OracleFile(data)
+    splits = file_splits(data.size, split)
+    s, _ = ctx.run_stream(data, of.contig_len, index_start=0, window=window, halo=1 << 16, splits=splits,
+                          verify_crc=True)
+    assert s["status"] == 0 and s["crc_bad_blocks"] == 0 and s["count"] == nrec
+    sh = ctx.shard(data)
+    try:
+        sh.index(0)
+        sh.inflate()
+        sh.set_contigs(of.contig_len)
+        st, v, n, _ = sh.split_starts(splits)
+    finally:
+        sh.close()
+    assert s["split_status"].tolist() == st.tolist()
+    assert s["split_count"].tolist() == n.tolist()
+    assert [int(a) for a, c in zip(s["split_first_vpos"], n) if c] == [int(a) for a, c in zip(v, n) if c]
+    assert int(s["split_count"].sum()) == nrec
+    if name != "adversarial":
+        assert s["splits_host"] == 0
+    for i, (a, e) in enumerate(splits):
+        rc, vr, nr = of.split(a, e)
+        if rc == OR_OK:
+            assert int(s["split_status"][i]) == 0 and int(s["split_count"][i]) == nr
+            assert nr == 0 or int(s["split_first_vpos"][i]) == vr
+
+
+def test_stream_crc_detects_a_bad_footer(ctx, files):
+    """A damaged footer CRC32 inside the owned range is counted (the data still inflates)."""
+    data, _ = files["short_l6"]
+    of = OracleFile(data)
+    bad = data.copy()
+    start, csize, _ = of.blocks[7]
+    bad[start + csize - 8] ^= 0xFF
+    s, _ = ctx.run_stream(bad, of.contig_len, index_start=0, window=150_000, halo=1 << 16, verify_crc=True)
+    assert s["crc_bad_blocks"] == 1 and s["crc_first_bad"] == start
