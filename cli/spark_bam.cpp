@@ -26,6 +26,11 @@
 #include <string>
 #include <vector>
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include "../include/sparkbam.h"
 
 namespace {
@@ -284,6 +289,20 @@ struct SplitsResult {
   std::vector<uint64_t> counts;
 };
 
+SplitsResult splits_from(const std::vector<std::pair<uint64_t, uint64_t>> &sp, const std::vector<uint64_t> &v,
+                         const std::vector<uint64_t> &cnt, const std::vector<int32_t> &status, uint64_t file_size) {
+  SplitsResult r;
+  std::vector<Pos> firsts;
+  for (uint64_t i = 0; i < sp.size(); ++i) {
+    if (status[i]) throw Error(status[i], "split " + std::to_string(sp[i].first) + "-" + std::to_string(sp[i].second));
+    r.counts.push_back(cnt[i]);
+    if (cnt[i]) firsts.push_back(Pos{v[i] >> 16, (uint32_t)(v[i] & 0xffff)});
+  }
+  for (size_t i = 0; i < firsts.size(); ++i)
+    r.splits.push_back({firsts[i], i + 1 < firsts.size() ? firsts[i + 1] : Pos{file_size, 0}});
+  return r;
+}
+
 // CanLoadBam.loadSplitsAndReads (load/.../CanLoadBam.scala:268-302)
 SplitsResult spark_bam_splits(Loaded &L, const Args &a, uint64_t split_size) {
   // every split in one batch: FindBlockStart + FindRecordStart + counts on the device
@@ -295,25 +314,98 @@ SplitsResult spark_bam_splits(Loaded &L, const Args &a, uint64_t split_size) {
   chk(sbh_split_starts(L.sh, st.data(), en.data(), n, a.blocks_to_check, a.reads_to_check, a.max_read_size,
                        v.data(), cnt.data(), status.data(), nullptr),
       "splits");
-  SplitsResult r;
-  std::vector<Pos> firsts;
-  for (uint64_t i = 0; i < n; ++i) {
-    if (status[i]) throw Error(status[i], "split " + std::to_string(sp[i].first) + "-" + std::to_string(sp[i].second));
-    r.counts.push_back(cnt[i]);
-    if (cnt[i]) firsts.push_back(Pos{v[i] >> 16, (uint32_t)(v[i] & 0xffff)});
-  }
-  for (size_t i = 0; i < firsts.size(); ++i)
-    r.splits.push_back({firsts[i], i + 1 < firsts.size() ? firsts[i + 1] : Pos{L.data.size(), 0}});
-  return r;
+  return splits_from(sp, v, cnt, status, L.data.size());
 }
 
 uint64_t default_split(const Args &a) { return a.has_split ? a.split : 32ull << 20; }
 
+// A file larger than this many compressed bytes (SBH_RESIDENT_MAX, default 24 GiB) is not held
+// resident: it is memory-mapped and streamed through HBM in windows cut at split starts
+// (sbh_run_stream2), each split decided in its window -- the same per-split answer in bounded
+// HBM, as the reference bounds its memory per split (SplitRDD.scala:33-52, Stream.scala:80-122).
+uint64_t resident_max() {
+  const char *e = std::getenv("SBH_RESIDENT_MAX");
+  return e && *e ? std::strtoull(e, nullptr, 10) : 24ull << 30;
+}
+
+struct Mapped {  // read-only mapping of a whole file
+  const uint8_t *p = nullptr;
+  uint64_t n = 0;
+  explicit Mapped(const std::string &path) {
+    const int fd = open(path.c_str(), O_RDONLY);
+    if (fd < 0) throw Error(SBH_E_ARG, "cannot open " + path);
+    struct stat st;
+    if (fstat(fd, &st) != 0) {
+      close(fd);
+      throw Error(SBH_E_ARG, "cannot stat " + path);
+    }
+    n = (uint64_t)st.st_size;
+    void *m = n ? mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0) : nullptr;
+    close(fd);
+    if (n && m == MAP_FAILED) throw Error(SBH_E_ARG, "cannot map " + path);
+    p = static_cast<const uint8_t *>(m);
+  }
+  ~Mapped() {
+    if (p) munmap(const_cast<uint8_t *>(p), n);
+  }
+};
+
+// Header(path) from the file's leading bytes (grown x4 until the header fits)
+BamHeader header_of(const uint8_t *data, uint64_t size) {
+  for (uint64_t m = std::min<uint64_t>(size, 1 << 20);; m = std::min<uint64_t>(size, m * 4)) {
+    sbh_shard *sh = nullptr;
+    chk(sbh_shard_create(g_ctx, data, m, 0, size, 0, &sh), "shard");
+    uint64_t nb = 0, flat = 0;
+    int rc = sbh_index(sh, 0, &nb, &flat);
+    if (!rc) rc = sbh_inflate(sh, nullptr);
+    try {
+      if (rc) throw Error(rc, "header blocks");
+      BamHeader h = parse_header(sh, flat);
+      sbh_shard_destroy(sh);
+      return h;
+    } catch (const Error &) {
+      sbh_shard_destroy(sh);
+      if (m >= size) throw;
+    }
+  }
+}
+
+// loadSplitsAndReads over a file streamed through HBM (sbh_run_stream2 with every split)
+SplitsResult spark_bam_splits_streamed(const std::string &path, const Args &a, uint64_t split_size) {
+  Mapped f(path);
+  const BamHeader h = header_of(f.p, f.n);
+  const auto sp = file_splits(f.n, split_size);
+  const uint64_t n = sp.size();
+  std::vector<uint64_t> st(n), en(n), v(n), cnt(n);
+  std::vector<int32_t> status(n);
+  for (uint64_t i = 0; i < n; ++i) st[i] = sp[i].first, en[i] = sp[i].second;
+  sbh_stream_opts o{};
+  o.window = 1ull << 30;
+  o.halo = 4ull << 20;
+  o.reads_to_check = a.reads_to_check;
+  o.max_read_size = a.max_read_size;
+  o.bgzf_blocks_to_check = a.blocks_to_check;
+  o.split_start = st.data(), o.split_end = en.data(), o.n_splits = n;
+  o.split_first_vpos = v.data(), o.split_count = cnt.data(), o.split_status = status.data();
+  sbh_stream_result res;
+  chk(sbh_run_stream2(g_ctx, f.p, f.n, 0, f.n, UINT64_MAX, f.n, h.lens.data(), (int32_t)h.lens.size(), &o, &res),
+      "stream");
+  return splits_from(sp, v, cnt, status, f.n);
+}
+
+// the resident path for files that fit, the streamed one otherwise
+SplitsResult spark_bam_splits_any(const Args &a, uint64_t split_size) {
+  struct stat st;
+  if (stat(a.path.c_str(), &st) == 0 && (uint64_t)st.st_size > resident_max())
+    return spark_bam_splits_streamed(a.path, a, split_size);
+  Loaded L(a.path);
+  return spark_bam_splits(L, a, split_size);
+}
+
 int compute_splits(const Args &a) {
   if (a.u && !a.s) no_hadoop_bam();
   auto t0 = std::chrono::steady_clock::now();
-  Loaded L(a.path);
-  SplitsResult r = spark_bam_splits(L, a, default_split(a));
+  SplitsResult r = spark_bam_splits_any(a, default_split(a));
   long ms = (long)std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
   printf("Get spark-bam splits: %ldms\n\n", ms);
   std::vector<double> lens;
@@ -331,8 +423,7 @@ int compute_splits(const Args &a) {
 
 int count_reads(const Args &a) {
   auto t0 = std::chrono::steady_clock::now();
-  Loaded L(a.path);
-  SplitsResult r = spark_bam_splits(L, a, default_split(a));
+  SplitsResult r = spark_bam_splits_any(a, default_split(a));
   uint64_t total = 0;
   for (uint64_t c : r.counts) total += c;
   long ms = (long)std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();

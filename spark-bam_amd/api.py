@@ -137,7 +137,16 @@ def load_splits_and_reads(path_or_bytes, split_size=DEFAULT_SPLIT_SIZE, ctx=None
                           reads_to_check=DEFAULT_READS_TO_CHECK, max_read_size=DEFAULT_MAX_READ_SIZE):
     """CanLoadBam.loadSplitsAndReads (load/.../CanLoadBam.scala:268-302): the splits
     (first record of every non-empty partition, sliding2 with Pos(fileSize, 0)) and
-    the per-partition record counts."""
+    the per-partition record counts.  A file larger than sharded.RESIDENT_MAX compressed bytes
+    is memory-mapped and streamed through HBM (windows cut at split starts, each split decided
+    in its window) instead of being held resident."""
+    from . import sharded  # (sharded builds on this module)
+    size = os.path.getsize(path_or_bytes) if isinstance(path_or_bytes, (str, os.PathLike)) else len(path_or_bytes)
+    if size > sharded.RESIDENT_MAX:
+        splits, counts, _ = sharded.load_splits_and_reads(
+            path_or_bytes, split_size, ctx=ctx, rank=0, world=1, bgzf_blocks_to_check=bgzf_blocks_to_check,
+            reads_to_check=reads_to_check, max_read_size=max_read_size)
+        return splits, counts
     L = _Loaded(path_or_bytes, ctx, reads_to_check)
     try:
         sh = L.shard

@@ -250,6 +250,19 @@ __global__ void k_jump_double(const int64_t *J, int64_t *J2, uint64_t nc) {
   J2[i] = j >= 0 ? J[j] : j;
 }
 
+// The chain starts at the candidate equal to start_rel (the scan may begin before it, so that
+// FindBlockStart from earlier offsets has its candidates): binary search, mark it.
+__global__ void k_mark_start(const uint64_t *cand, uint64_t nc, uint64_t start_rel, uint8_t *on) {
+  if (threadIdx.x != 0) return;
+  uint64_t lo = 0, hi = nc;
+  while (lo < hi) {
+    const uint64_t m = (lo + hi) >> 1;
+    if (cand[m] < start_rel) lo = m + 1;
+    else hi = m;
+  }
+  if (lo < nc && cand[lo] == start_rel) on[lo] = 1;
+}
+
 __global__ void k_mark_u64(const uint8_t *on, uint64_t *v, uint64_t nc) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nc) return;
@@ -348,8 +361,8 @@ hipError_t launch_cand_write(const uint8_t *comp, uint64_t n, uint64_t from, con
 // Build the chain from cand[0] over nc candidates.  Scratch: J0, J1 (int64 x nc),
 // on (u8 x nc), v/rank (u64 x nc each), tmp (scan).  Writes the block table and
 // usz (u64 per block); returns the block count via *nchain (host).
-hipError_t build_chain(const uint8_t *comp, uint64_t n, const uint64_t *cand, uint64_t nc, int64_t *J0,
-                       int64_t *J1, uint8_t *on, uint64_t *v, uint64_t *rank, uint64_t *tmp,
+hipError_t build_chain(const uint8_t *comp, uint64_t n, const uint64_t *cand, uint64_t nc, uint64_t start_rel,
+                       int64_t *J0, int64_t *J1, uint8_t *on, uint64_t *v, uint64_t *rank, uint64_t *tmp,
                        DevBlocks bl, uint64_t *usz, uint64_t *nchain, uint8_t *next18, hipStream_t st) {
   *nchain = 0;
   if (nc == 0) return hipSuccess;
@@ -357,8 +370,7 @@ hipError_t build_chain(const uint8_t *comp, uint64_t n, const uint64_t *cand, ui
   hipLaunchKernelGGL(k_cand_link, dim3(nblk(nc, T)), dim3(T), 0, st, comp, n, cand, nc, J0);
   hipError_t e = hipMemsetAsync(on, 0, nc, st);
   if (e != hipSuccess) return e;
-  e = hipMemsetAsync(on, 1, 1, st);
-  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_mark_start, dim3(1), dim3(64), 0, st, cand, nc, start_rel, on);
   int64_t *a = J0, *b = J1;
   for (uint64_t span = 1; span < nc; span <<= 1) {
     hipLaunchKernelGGL(k_jump_mark, dim3(nblk(nc, T)), dim3(T), 0, st, a, on, nc);

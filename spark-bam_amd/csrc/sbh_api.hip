@@ -27,9 +27,9 @@ hipError_t launch_cand_count(const uint8_t *comp, uint64_t n, uint64_t from, uin
 hipError_t launch_cand_write(const uint8_t *comp, uint64_t n, uint64_t from, const uint64_t *counts,
                              const uint32_t *first, const uint64_t *offs, uint64_t *cand, uint64_t nchunks,
                              hipStream_t st);
-hipError_t build_chain(const uint8_t *comp, uint64_t n, const uint64_t *cand, uint64_t nc, int64_t *J0, int64_t *J1,
-                       uint8_t *on, uint64_t *v, uint64_t *rank, uint64_t *tmp, DevBlocks bl, uint64_t *usz,
-                       uint64_t *nchain, uint8_t *next18, hipStream_t st);
+hipError_t build_chain(const uint8_t *comp, uint64_t n, const uint64_t *cand, uint64_t nc, uint64_t start_rel,
+                       int64_t *J0, int64_t *J1, uint8_t *on, uint64_t *v, uint64_t *rank, uint64_t *tmp, DevBlocks bl,
+                       uint64_t *usz, uint64_t *nchain, uint8_t *next18, hipStream_t st);
 hipError_t launch_eager(const uint8_t *U, uint64_t u_pad, uint64_t begin, uint64_t end, const uint64_t *seg_end,
                         uint32_t nseg, uint32_t open_last, const int32_t *ctg, int32_t nctg, int32_t rtc,
                         uint32_t *bits, unsigned long long *counters, hipStream_t st, uint64_t front,
@@ -105,6 +105,11 @@ struct sbh_shard {
   DBuf<uint64_t> counts, offs, cand, v, rank, tmp;
   DBuf<uint32_t> cfirst;  // per scan chunk: offset of its first candidate
   uint64_t ncand = 0, cand_from = 0;  // header candidates in cand[] (shard-relative, >= cand_from)
+  // sbh_index scans for header candidates from this file offset when it lies in
+  // [file_off, start] (~0: from the shard's first byte), so that every split starting in the
+  // resident bytes -- a rank's or a streamed window's first one included -- has its
+  // FindBlockStart candidates on the device; the block chain still starts at `start`
+  uint64_t scan_from = ~0ull;
   DBuf<int64_t> J0, J1;
   DBuf<uint8_t> on;
   std::vector<sbh_block> hb;
@@ -414,6 +419,7 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
   sh->ncand = 0;
   const uint64_t rel = start - sh->file_off;
   const uint64_t n = sh->n;
+  const uint64_t srel = sh->scan_from >= sh->file_off && sh->scan_from <= start ? sh->scan_from - sh->file_off : 0;
   // the start must itself be a header (its 18 bytes come back with the candidate count)
   uint8_t *h18 = reinterpret_cast<uint8_t *>(sh->h_ctr + 512);  // pinned
   auto start_is_header = [&]() -> int {
@@ -433,7 +439,7 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
     HIPCHK(ctx, sh->cfirst.ensure(nchunks));
     HIPCHK(ctx, sh->offs.ensure(nchunks));
     HIPCHK(ctx, sh->tmp.ensure(scan_tmp_words(nchunks) + scan_tmp_words(1 << 24)));
-    HIPCHK(ctx, launch_cand_count(sh->comp.p, n, rel, sh->counts.p, sh->cfirst.p, nchunks, st));
+    HIPCHK(ctx, launch_cand_count(sh->comp.p, n, srel, sh->counts.p, sh->cfirst.p, nchunks, st));
     HIPCHK(ctx, scan_exclusive_u64(sh->counts.p, sh->offs.p, nchunks, sh->tmp.p, st));
     HIPCHK(ctx, hipMemcpyAsync(&sh->h_ctr[0], sh->offs.p + nchunks - 1, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipMemcpyAsync(&sh->h_ctr[1], sh->counts.p + nchunks - 1, 8, hipMemcpyDeviceToHost, st));
@@ -454,7 +460,7 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
     HIPCHK(ctx, sh->v.ensure(nc));
     HIPCHK(ctx, sh->rank.ensure(nc));
     HIPCHK(ctx, sh->tmp.ensure(scan_tmp_words(nc) + scan_tmp_words(nchunks)));
-    HIPCHK(ctx, launch_cand_write(sh->comp.p, n, rel, sh->counts.p, sh->cfirst.p, sh->offs.p, sh->cand.p, nchunks, st));
+    HIPCHK(ctx, launch_cand_write(sh->comp.p, n, srel, sh->counts.p, sh->cfirst.p, sh->offs.p, sh->cand.p, nchunks, st));
     HIPCHK(ctx, sh->b_cstart.ensure(nc));
     HIPCHK(ctx, sh->b_ustart.ensure(nc));
     HIPCHK(ctx, sh->usz.ensure(nc));
@@ -464,12 +470,12 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
     HIPCHK(ctx, sh->b_flags.ensure(nc));
     HIPCHK(ctx, sh->b_status.ensure(nc));
     HIPCHK(ctx, sh->b_ntok.ensure(nc));
-    HIPCHK(ctx, build_chain(sh->comp.p, n, sh->cand.p, nc, sh->J0.p, sh->J1.p, sh->on.p, sh->v.p, sh->rank.p,
+    HIPCHK(ctx, build_chain(sh->comp.p, n, sh->cand.p, nc, rel, sh->J0.p, sh->J1.p, sh->on.p, sh->v.p, sh->rank.p,
                             sh->tmp.p, sh->dev_blocks(), sh->usz.p, &nchain, next18_dev, st));
     HIPCHK(ctx, scan_exclusive_u64(sh->usz.p, sh->b_ustart.p, nchain, sh->tmp.p, st));
   }
   sh->ncand = nc;
-  sh->cand_from = rel;
+  sh->cand_from = srel;
   // host copy of the block table (Pos mapping, segments)
   sh->hb.assign(nchain, sbh_block{});
   if (nchain) {
@@ -1660,6 +1666,7 @@ int sbh_run_stream2(sbh_ctx *ctx, const void *host, uint64_t n, uint64_t file_of
       if (rc) return res->status = rc;
     }
     sbh_shard_result r{};
+    sh->scan_from = lo;  // header candidates from the window's first byte (its first split's FindBlockStart)
     rc = sbh_run_shard(sh, start, hi, rtc, mrs, &r);
     // this window's splits (every one inside [lo, hi)): the batched per-split path
     uint64_t k0 = 0, k1 = 0;

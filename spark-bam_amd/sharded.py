@@ -34,6 +34,12 @@ from .api import (DEFAULT_BGZF_BLOCKS_TO_CHECK, DEFAULT_MAX_READ_SIZE, DEFAULT_R
 from .device import Context
 
 DEFAULT_HALO = 1 << 20  # compressed bytes past the owned range; grown x4 on SBH_E_NEED_HALO
+# A rank whose compressed shard exceeds this many bytes streams it through HBM in windows
+# (sbh_run_stream2) instead of holding it resident: ~5 B of HBM per compressed byte resident
+# (compressed + flat + bitmap, token buffer bounded), so 24 GiB keeps a resident shard well
+# inside 288 GB; configs[2]'s 100 GB file at N <= 4 streams.  SBH_RESIDENT_MAX overrides.
+RESIDENT_MAX = int(os.environ.get("SBH_RESIDENT_MAX", str(24 << 30)))
+STREAM_WINDOW = int(os.environ.get("SBH_STREAM_WINDOW", str(1 << 30)))
 
 # One rank's contribution to the exchange.  firsts[i] is the htsjdk vpos of split i's
 # first record (None when the split is empty); exit_vpos is the first record of the
@@ -92,18 +98,29 @@ def read_header(ctx, read, file_size, first=DEFAULT_HALO):
 
 
 class RankRun:
-    """One rank's share of the hot path over its splits [lo, hi): the shard +
-    halo stays resident after the run, so the stitch can re-walk its chain later."""
+    """One rank's share of the hot path over its splits [lo, hi).  A shard up to
+    RESIDENT_MAX compressed bytes stays resident after the run, so the stitch can re-walk its
+    chain later; a larger one (or stream=True) is streamed through HBM in windows cut at split
+    starts (sbh_run_stream2, Stream.scala:80-122's bounded memory) and re-walks window by
+    window."""
 
     def __init__(self, ctx, read, file_size, split_index, splits, contig_len, rank=0, halo=DEFAULT_HALO,
                  bgzf_blocks_to_check=DEFAULT_BGZF_BLOCKS_TO_CHECK,
-                 reads_to_check=DEFAULT_READS_TO_CHECK, max_read_size=DEFAULT_MAX_READ_SIZE):
+                 reads_to_check=DEFAULT_READS_TO_CHECK, max_read_size=DEFAULT_MAX_READ_SIZE,
+                 stream=None, window=None):
         self.sh = None
         self.rank = rank
+        self.ctx, self.read, self.file_size, self.contig_len = ctx, read, file_size, contig_len
+        self.rtc, self.mrs = reads_to_check, max_read_size
         if not splits:
             self.part = RankPart(rank, split_index, [], [], None, 0, None)
             return
         lo, hi = splits[0][0], splits[-1][1]
+        self.lo, self.hi = lo, hi
+        self.streamed = (hi - lo > RESIDENT_MAX) if stream is None else bool(stream)
+        if self.streamed:
+            self._run_streamed(split_index, splits, halo, window or STREAM_WINDOW, bgzf_blocks_to_check)
+            return
         while True:
             end = min(file_size, hi + halo)
             sh = ctx.shard(read(lo, end), file_offset=lo, file_size=file_size)
@@ -114,13 +131,9 @@ class RankRun:
                 # every split of the rank in one batch (FindBlockStart + FindRecordStart +
                 # counts on the device; CanLoadBam.scala:283-297, 316-356)
                 status, v, n, _ = sh.split_starts(splits, bgzf_blocks_to_check, reads_to_check, max_read_size)
-                for k in np.flatnonzero((status != 0) & (status != SBH_E_NO_READ_FOUND)):
-                    raise SparkBamError(int(status[k]), f"split {splits[k][0]}-{splits[k][1]}")
-                counts = [int(c) if st == 0 else 0 for st, c in zip(status, n)]
-                firsts = [int(x) if c else None for x, c in zip(v, counts)]
-                self.part = RankPart(rank, split_index, firsts, counts,
-                                     r["first_vpos"] if r["count"] else None, r["count"], sh.exit_vpos(r))
-                self.sh, self.hi = sh, hi
+                self.part = self._part(split_index, splits, status, v, n, r["first_vpos"] if r["count"] else None,
+                                       r["count"], sh.exit_vpos(r))
+                self.sh = sh
                 return
             except SparkBamError as err:
                 sh.close()
@@ -131,13 +144,81 @@ class RankRun:
                 sh.close()
                 raise
 
+    def _part(self, split_index, splits, status, v, n, first, count, exit_vpos):
+        for k in np.flatnonzero((status != 0) & (status != SBH_E_NO_READ_FOUND)):
+            raise SparkBamError(int(status[k]), f"split {splits[k][0]}-{splits[k][1]}")
+        counts = [int(c) if st == 0 else 0 for st, c in zip(status, n)]
+        firsts = [int(x) if c else None for x, c in zip(v, counts)]
+        return RankPart(self.rank, split_index, firsts, counts, first, count, exit_vpos)
+
+    def _run_streamed(self, split_index, splits, halo, window, kcheck):
+        lo, hi = self.lo, self.hi
+        while True:
+            end = min(self.file_size, hi + halo)
+            comp = self.read(lo, end)
+            try:
+                r, _ = self.ctx.run_stream(comp, self.contig_len, file_offset=lo, file_size=self.file_size,
+                                           own_end=hi, window=window, halo=min(halo, 4 << 20),
+                                           reads_to_check=self.rtc, max_read_size=self.mrs, splits=splits,
+                                           bgzf_blocks_to_check=kcheck)
+            except SparkBamError as err:
+                if err.code != SBH_E_NEED_HALO or end >= self.file_size:
+                    raise
+                halo *= 4
+                continue
+            self.stream_result = r
+            self.halo = halo
+            self.part = self._part(split_index, splits, r["split_status"], r["split_first_vpos"], r["split_count"],
+                                   r["first_vpos"] if r["count"] else None, r["count"], r["exit_vpos"])
+            return
+
     def rewalk(self, from_vpos):
         """The chain from the upstream rank's exit (SURVEY 8e stitch fix-up): (records from
         from_vpos that start before the owned end, the chain's exit vpos or None)."""
+        if self.streamed:
+            return self._rewalk_streamed(from_vpos)
         sh = self.sh
         f = sh.flat_of(from_vpos >> 16, from_vpos & 0xFFFF)
         n, x = sh.chain_from(f, sh.flat_bound(self.hi))
         return n, sh.exit_vpos({"count": n, "exit_flat": x})
+
+    def _rewalk_streamed(self, from_vpos, window=None):
+        """The re-walk through bounded HBM: window by window from the entry record's block, the
+        eager bitmap of the window first (so the chain is proven against it, not walked one
+        record at a time), then the chain to the window's end; its exit enters the next."""
+        window = window or STREAM_WINDOW
+        total, v = 0, from_vpos
+        while True:
+            blo = v >> 16
+            if blo >= self.hi:
+                return total, v
+            whi = min(self.hi, blo + window)
+            halo = max(self.halo, 1 << 20)
+            while True:
+                end = min(self.file_size, whi + halo)
+                sh = self.ctx.shard(self.read(blo, end), file_offset=blo, file_size=self.file_size)
+                try:
+                    sh.index(blo)
+                    sh.inflate()
+                    sh.set_contigs(self.contig_len)
+                    f = sh.flat_of(blo, v & 0xFFFF)
+                    E = sh.flat_bound(whi)
+                    sh.check_eager(f, E, self.rtc, want_bits=False)
+                    n, x = sh.chain_from(f, E)
+                    ex = sh.exit_vpos({"count": n, "exit_flat": x}) if n else v
+                    break
+                except SparkBamError as err:
+                    if err.code != SBH_E_NEED_HALO or end >= self.file_size:
+                        raise
+                    halo *= 4
+                finally:
+                    sh.close()
+            total += n
+            if ex is None or whi >= self.hi:
+                return total, ex
+            if ex == v:  # no record started in this window: continue after it
+                ex = whi << 16
+            v = ex
 
     def close(self):
         if self.sh is not None:

@@ -36,6 +36,20 @@ def test_compute_splits_240k():
         "\t0:45846-263656:191", "\t263656:191-508565:287", "\t508565:287-597482:0", ""]
 
 
+def test_compute_splits_and_count_streamed():
+    # the same ComputeSplitsTest / CountReadsTest answers when the file is streamed through
+    # HBM (SBH_RESIDENT_MAX below the file size: sbh_run_stream2 with every split)
+    env = dict(os.environ, SBH_RESIDENT_MAX="1")
+    r = subprocess.run([CLI, "compute-splits", "-s", "-m", "230k", os.path.join(BAMS, "1.bam")], capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.splitlines()[-4:] == ["\t0:45846-239479:312", "\t239479:312-484396:25", "\t484396:25-597482:0", ""]
+    r = subprocess.run([CLI, "count-reads", "-m", "100k", os.path.join(BAMS, "1.bam")], capture_output=True, text=True,
+                       timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    assert "spark-bam found 4917 reads" in r.stdout
+
+
 def test_check_bam_eager_1bam():
     # CheckBamTest "eager 1.bam"
     out = run("check-bam", "-s", "-m", "200k", os.path.join(BAMS, "1.bam"))

@@ -266,10 +266,18 @@ if os.environ.get("SBH_TEST_FP_RANK"):
             super().__init__(*a, **kw)
             p = self.part
             if self.rank == fp_rank and p.count > 1:
-                sh = self.sh
-                f = sh.flat_of(p.first_vpos >> 16, p.first_vpos & 0xFFFF)
-                nxt = f + 4 + int(sh.read_flat(f, 4).view("<i4")[0])
-                bp, off = sh.pos_of(nxt)
+                if self.sh is not None:
+                    sh = self.sh
+                    f = sh.flat_of(p.first_vpos >> 16, p.first_vpos & 0xFFFF)
+                    nxt = f + 4 + int(sh.read_flat(f, 4).view("<i4")[0])
+                    bp, off = sh.pos_of(nxt)
+                else:  # a streamed rank keeps no shard: the checker's view of the file
+                    sys.path.insert(0, os.path.join(os.environ["SBH_ROOT"], "tests"))
+                    from oracle_lib import OracleFile
+                    of = OracleFile.from_path(path)
+                    f = of.flat_of(p.first_vpos >> 16, p.first_vpos & 0xFFFF)
+                    nxt = f + 4 + int(of.uncompressed_range(f, f + 4).view("<i4")[0])
+                    bp, off = of.pos_of(nxt)
                 self.true_count = p.count
                 self.part = p._replace(first_vpos=(bp << 16) | off, count=p.count - 1)
     sharded.RankRun = FPRun
@@ -392,4 +400,46 @@ def test_gpu_stitch_rewalk_after_false_positive(tmp_path):
     res = _run_gpu_ranks(tmp_path, path, 0, 1 << 20, world=3, env_extra={"SBH_TEST_FP_RANK": "1"})
     for r in res:
         assert not r["ok"] and r["chain_ok"] and r["chain_count"] == 2500
+        assert r["rewalk"]["1"]["count"] == r["rank_counts"][1] + 1
+
+
+STREAMED = {"SBH_RESIDENT_MAX": "1", "SBH_STREAM_WINDOW": "150000"}
+
+
+@pytest.mark.gpu
+def test_gpu_four_ranks_wgs_shape_streamed(tmp_path):
+    """The same 4-rank configs[2] run with every rank streamed through HBM (RankRun over
+    sbh_run_stream2: windows of 150 KB cut at split starts, per-split results per window)."""
+    path, data = _synth_file(tmp_path, 0x5B4D0030, 0, 50000, "wgs.bam")
+    of = OracleFile(data)
+    ss = data.size // 23
+    res = _run_gpu_ranks(tmp_path, path, ss, 1 << 18, world=4, env_extra=STREAMED)
+    ref_splits, ref_counts = oracle_splits(of, ss)
+    for r in res:
+        assert r["counts"] == ref_counts and [tuple(s) for s in r["splits"]] == ref_splits
+        assert r["ok"] and r["chain_ok"] and r["chain_count"] == 50000
+
+
+@pytest.mark.gpu
+def test_gpu_long_reads_streamed_edges_inside_records(tmp_path):
+    path, data = _synth_file(tmp_path, 0x5B4D004C, 1, 500, "long.bam")
+    of = OracleFile(data)
+    ss = _edges_inside_long_records(of, 2)
+    assert ss is not None
+    res = _run_gpu_ranks(tmp_path, path, ss, 4096, world=2, env_extra=STREAMED)
+    ref_splits, ref_counts = oracle_splits(of, ss)
+    for r in res:
+        assert r["counts"] == ref_counts and [tuple(s) for s in r["splits"]] == ref_splits
+        assert r["ok"] and r["chain_ok"] and r["chain_count"] == 500
+
+
+@pytest.mark.gpu
+def test_gpu_stitch_rewalk_streamed(tmp_path):
+    """The stitch fix-up on streamed ranks: rank 1 re-walks window by window (each window's
+    eager bitmap, then the chain) from rank 0's exit."""
+    path, data = _synth_file(tmp_path, 0x5B4D0030, 0, 20000, "wgs_fp.bam")
+    res = _run_gpu_ranks(tmp_path, path, 0, 1 << 20, world=3,
+                         env_extra=dict(STREAMED, SBH_TEST_FP_RANK="1"))
+    for r in res:
+        assert not r["ok"] and r["chain_ok"] and r["chain_count"] == 20000
         assert r["rewalk"]["1"]["count"] == r["rank_counts"][1] + 1

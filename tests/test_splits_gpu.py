@@ -171,3 +171,19 @@ def test_check_bam_api_golden(ctx):
     r = sb.check_bam(golden_bam("1.bam"), records=recs[:100] + recs[101:], ctx=ctx)
     assert r["false_positives"] == 1 and r["false_negatives"] == 0
     assert r["fp_positions"] == [sb.Pos(*recs[100])]
+
+
+@pytest.mark.parametrize("name,split_size", [("1.bam", 230 * 1024), ("2.bam", 102400)])
+def test_load_splits_and_reads_streamed(ctx, monkeypatch, name, split_size):
+    """api.load_splits_and_reads on a file over the resident budget: streamed through HBM in
+    windows (sharded.RankRun over sbh_run_stream2), same splits and counts as the oracle."""
+    import spark_bam_amd.sharded as sharded
+    from conftest import golden_bam
+    from oracle_lib import load_splits_and_reads as oracle_load
+    monkeypatch.setattr(sharded, "RESIDENT_MAX", 1)
+    monkeypatch.setattr(sharded, "STREAM_WINDOW", 120_000)
+    splits, counts = sb.load_splits_and_reads(golden_bam(name), split_size, ctx=ctx)
+    of = OracleFile.from_path(golden_bam(name))
+    ref_splits, ref_counts = oracle_load(of, split_size)
+    assert counts == ref_counts
+    assert [(a.to_htsjdk(), b.to_htsjdk()) for a, b in splits] == ref_splits
