@@ -69,6 +69,12 @@ def main():
     ap.add_argument("--e2e-window", type=int, default=256 << 20,
                     help="window of the H2D-inclusive side measurement of the resident configs")
     ap.add_argument("--no-e2e", action="store_true", help="skip the H2D-inclusive side measurement")
+    ap.add_argument("--file-gib", type=float, default=None,
+                    help="strong scaling over ONE file of this many GiB compressed (configs[2]: --config C "
+                         "--file-gib 100): the N ranks split its Hadoop splits and stream their ranges")
+    ap.add_argument("--split-mib", type=float, default=32.0, help="Hadoop split size of the --file-gib file")
+    ap.add_argument("--no-crc", action="store_true", help="--file-gib: skip the in-run CRC32 check")
+    ap.add_argument("--no-pin", action="store_true", help="--file-gib: pageable host memory for the rank's bytes")
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes per launch of the dominant kernel (default: the committed "
                          "rocprofv3 --pmc summary, profiles/*_pmc_traffic.json)")
@@ -105,6 +111,10 @@ def main():
 
     sb = load_package()
     import spark_bam_amd.sharded as sharded
+
+    if args.file_gib is not None:
+        return main_strong(args, rank, world, local_rank, device, backend, xdev, coll, dist, torch, synth, sb,
+                           sharded)
 
     # ---- input generation (not timed) ----
     t0 = time.time()
@@ -150,11 +160,18 @@ def main():
     result_t = torch.zeros(5, dtype=torch.int64, device=xdev)
     stream_last = {}
 
+    # the streamed shard's Hadoop splits (32 MiB, SplitRDD's partitions): per-split first record
+    # and count come back from every window (sbh_run_stream2)
+    stream_splits = None
+    if streaming:
+        sp = sb.file_splits(seg.own_end - seg.file_offset, 32 << 20)
+        stream_splits = [(seg.file_offset + x, seg.file_offset + y) for x, y in sp]
+
     def run_once():
         if streaming:  # windows through HBM; copies of window w+1 overlap window w's kernels
             r, _ = ctx.run_stream(seg.comp, contig_len, file_offset=seg.file_offset, file_size=seg.file_size,
                                   own_end=seg.own_end, index_start=seg.file_offset, window=args.window,
-                                  halo=4 << 20)
+                                  halo=4 << 20, splits=stream_splits, verify_crc=True)
             stream_last.update(r)
             first = r["first_vpos"] or 0
             ex = r["exit_vpos"]
@@ -209,8 +226,14 @@ def main():
     # bait (config E), whose exact bits are pinned by the parity tests, not here
     # every inflated block of the last step against its BGZF footer CRC32 (full-size
     # bit-exactness of the inflate), outside the timed region
-    crc_bad = shard.verify_crc()[0] if shard is not None else 0  # (stream mode: windows are gone)
-    ok = total_records == expect and (total_true == expect or not cfg["fp_free"]) and stitch["ok"] and crc_bad == 0
+    # (stream mode: every window's owned blocks were CRC-checked in the run, sbh_run_stream2)
+    crc_bad = shard.verify_crc()[0] if shard is not None else stream_last.get("crc_bad_blocks", 0)
+    split_ok = True
+    if streaming:
+        split_ok = (int(np.count_nonzero(stream_last["split_status"])) == 0
+                    and int(stream_last["split_count"].sum()) == r["count"])
+    ok = (total_records == expect and (total_true == expect or not cfg["fp_free"]) and stitch["ok"] and crc_bad == 0
+          and split_ok)
     firsts = [x[0] for x in allr if x[1] > 0]
 
     stage_ms = stage_acc / args.steps
@@ -230,21 +253,16 @@ def main():
     alg_bytes, dom_ms, dom_units = kern[dom]
     achieved = alg_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
 
-    traffic, traffic_src = args.traffic, "--traffic" if args.traffic is not None else None
+    traffic, traffic_src, traffic_fresh = args.traffic, "--traffic" if args.traffic is not None else None, None
     if traffic is None:
-        import glob
-        files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
-        if files:
-            with open(files[-1]) as fh:
-                kt = json.load(fh)["kernels"].get(dom)
-            if kt:
-                traffic, traffic_src = kt["hbm_bytes"], os.path.relpath(files[-1], ROOT)
-                # k_huff's timed stage is launch_huff: the k_hdr header pre-pass, then k_huff
-                if dom == "k_huff":
-                    with open(files[-1]) as fh:
-                        kh = json.load(fh)["kernels"].get("k_hdr")
-                    if kh:
-                        traffic += kh["hbm_bytes"]
+        tj, tsrc = latest_pmc("traffic.json")
+        kt = tj["kernels"].get(dom) if tj else None
+        if kt:
+            traffic, traffic_src = kt["hbm_bytes"], tsrc
+            traffic_fresh = tj.get("src_hash") == kernel_src_hash()
+            # k_huff's timed stage is launch_huff: the k_hdr header pre-pass, then k_huff
+            if dom == "k_huff" and tj["kernels"].get("k_hdr"):
+                traffic += tj["kernels"]["k_hdr"]["hbm_bytes"]
 
     def gbps(nbytes, ms):
         return round(nbytes / (ms * 1e-3) / 1e9, 2) if ms > 0 else None
@@ -282,7 +300,11 @@ def main():
                if stream_last.get("ms_h2d") else None,
                "device_ms_per_step": round(float(stage_acc[1] + stage_acc[0] + stage_acc[3]) / args.steps, 3),
                "host_pinned": bool(stream_last.get("host_pinned")),
-               "note": "value IS the streamed rate here: shard in pinned host memory, windows through HBM"}
+               "crc_ms_per_step": round(stream_last.get("ms_crc", 0), 3),
+               "splits": len(stream_splits), "splits_host_path": int(stream_last.get("splits_host", 0)),
+               "split_counts_sum": int(stream_last["split_count"].sum()),
+               "note": "value IS the streamed rate here: shard in pinned host memory, windows through HBM cut at "
+                       "split starts; per-split first record + count and every block's CRC32 in the timed run"}
     elif not args.no_e2e and seg.file_offset is not None:
         buf = sb.PinnedBuffer(seg.comp.size)
         buf.array[:] = seg.comp
@@ -357,9 +379,10 @@ def main():
                 "traffic": traffic,
                 "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                 "traffic_source": traffic_src,
+                "traffic_matches_kernels": traffic_fresh,  # collected from these kernel sources (hash)
                 "alg_bytes_per_step": int(alg_bytes),
                 "alg_units": dom_units,
-                "limiter": limiter_text(dom),
+                "limiter": limiter_text(dom, dom_ms, traffic),
                 "path": {  # B_alg = C + U (inflate write) + U (checker read) + U/8 (bitmap) per step
                     "alg_bytes_per_step": int(sum(own_sizes) / world + 2.125 * flat_bytes),
                     "achieved": round((sum(own_sizes) / world + 2.125 * flat_bytes) * args.steps / elapsed / 1e9, 2),
@@ -386,22 +409,191 @@ def main():
         sys.exit(3)
 
 
-def limiter_text(kernel):
-    """What bounds `kernel`, from the committed counter ratios (tools/pmc_derived.py over the
-    rocprofv3 passes of tools/pmc_collect.sh)."""
+def main_strong(args, rank, world, local_rank, device, backend, xdev, coll, dist, torch, synth, sb, sharded):
+    """configs[2] as BASELINE.json states it: ONE file of --file-gib GiB compressed, its Hadoop
+    splits dealt to the N ranks as contiguous runs (sharded.rank_splits), every rank streaming
+    its byte range from pinned host memory through HBM (sbh_run_stream2: windows cut at split
+    starts, per-split first record + count, in-run CRC32 of every owned block), one RCCL
+    allgather of the per-rank chain records per step.  Strong scaling: total work is fixed."""
+    cfg = CONFIGS[args.config]
+    if cfg["level"] < 0:
+        raise SystemExit("--file-gib needs a single-level config (B, C or D)")
+    t0 = time.time()
+    p = synth.params(cfg["seed"], shape=cfg["shape"], level=cfg["level"], threads=min(16, os.cpu_count() or 1))
+    seg_records = args.records_per_gpu or CONFIGS["B"]["records"]  # ~1 GiB compressed canonical segment
+    F = synth.Replicated(p, seg_records, int(args.file_gib * 2**30))
+    split = int(args.split_mib * 2**20)
+    a, mine = sharded.rank_splits(F.size, split, world, rank)
+    nsplits = len(sharded.rank_splits(F.size, split, 1, 0)[1])
+    lo, hi = mine[0][0], mine[-1][1]
+    end = min(F.size, hi + (64 << 20))
+    pins = []
+    if args.no_pin:
+        comp = np.empty(end - lo, dtype=np.uint8)
+    else:
+        pins.append(sb.PinnedBuffer(end - lo))
+        comp = pins[-1].array
+    F.read_into(lo, end, comp)
+    log(f"[rank {rank}] file {F.size / 2**30:.2f} GiB ({F.copies} x {F.seg_comp.size / 2**30:.3f} GiB segment, "
+        f"{F.records} records, {nsplits} splits); rank range [{lo}, {hi}) = {(hi - lo) / 2**30:.2f} GiB, "
+        f"{len(mine)} splits; ready in {time.time() - t0:.1f}s")
+    ctx = sb.Context(device)
+    _, contig_len, _ = sb.parse_bam_header(synth.header_bytes())
+    res_t = torch.zeros(5, dtype=torch.int64, device=xdev)
+    last = {}
+
+    def step():
+        r, _ = ctx.run_stream(comp, contig_len, file_offset=lo, file_size=F.size, own_end=hi, window=args.window,
+                              halo=4 << 20, splits=mine, verify_crc=not args.no_crc)
+        last.clear()
+        last.update(r)
+        mine_rec = [r["first_vpos"] or 0, r["count"], r["n_true"], r["flat_bytes"],
+                    -1 if r["exit_vpos"] is None else r["exit_vpos"]]
+        if coll:
+            res_t.copy_(torch.tensor(mine_rec, dtype=torch.int64))
+            out = [torch.zeros_like(res_t) for _ in range(world)]
+            dist.all_gather(out, res_t)
+            return [o.cpu().tolist() for o in out]
+        return [mine_rec]
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if coll:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        allr = step()
+    torch.cuda.synchronize()
+    if coll:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    if coll:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=xdev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    # per-split results -> the reference's splits (sliding2 over non-empty firsts) and counts
+    r = last
+    part = sharded.RankPart(rank, a, [int(v) if c else None for v, c in zip(r["split_first_vpos"], r["split_count"])],
+                            [int(c) for c in r["split_count"]], r["first_vpos"] if r["count"] else None, r["count"],
+                            r["exit_vpos"])
+    parts = sharded.exchange(part) if coll else [part]
+    splits, counts, st = sharded.stitch(parts, F.size)
+    crc_bad = [r["crc_bad_blocks"]]
+    split_bad = int(np.count_nonzero(r["split_status"]))
+    if coll:
+        g = [None] * world
+        dist.all_gather_object(g, (int(r["crc_bad_blocks"]), split_bad, int(r["splits_host"])))
+        crc_bad, split_bad, host = [x[0] for x in g], sum(x[1] for x in g), sum(x[2] for x in g)
+    else:
+        host = int(r["splits_host"])
+    total_records = sum(x[1] for x in allr)
+    total_flat = sum(x[3] for x in allr)
+    ok = (total_records == F.records and sum(counts) == F.records and st["ok"] and sum(crc_bad) == 0
+          and split_bad == 0 and len(counts) == nsplits)
+    if rank == 0:
+        value = total_flat * args.steps / elapsed / 1e9
+        out = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "GB/s decompressed (whole job)",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": (f"synthetic (tools/synth_bam.c seed {cfg['seed']:#x}): one {seg_records}-record segment "
+                     f"replicated x{F.copies} into one file (synth.Replicated)"),
+            "config": {
+                "workload": (f"configs[2]: ONE {F.size / 2**30:.1f} GiB-compressed WGS-shaped BAM ({F.records} records,"
+                             f" {F.flat_size / 1e9:.1f} GB flat), its {nsplits} Hadoop splits of {args.split_mib:g} MiB "
+                             f"dealt to {world} rank(s), each streamed from {'pinned' if not args.no_pin else 'pageable'}"
+                             f" host memory through HBM in {args.window / 2**30:g} GiB windows"),
+                "file_bytes": F.size, "decompressed_bytes": int(total_flat), "splits": nsplits,
+                "parallelism": f"dp{world} byte-range shards (Hadoop split runs) + "
+                               f"{'RCCL' if backend == 'nccl' else 'gloo'} allgather stitch",
+            },
+            "records_per_s": round(total_records * args.steps / elapsed, 1),
+            "compressed_GBps": round(F.size * args.steps / elapsed / 1e9, 3),
+            "correct": bool(ok),
+            "stitch_ok": bool(st["ok"]),
+            "records": int(total_records),
+            "splits_nonempty": len(splits),
+            "split_counts_sum": int(sum(counts)),
+            "splits_host_path": int(host),
+            "crc_bad_blocks": int(sum(crc_bad)),
+            "crc_checked": not args.no_crc,
+            "rank0": {"windows": r["n_windows"], "h2d_ms": round(r["ms_h2d"], 2), "wall_ms": round(r["ms_wall"], 2),
+                      "crc_ms": round(r["ms_crc"], 2), "splits_ms": round(r["ms_splits"], 2),
+                      "stages_ms": [round(x, 2) for x in r["stage_ms"]], "host_pinned": bool(r["host_pinned"])},
+        }
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    for b in pins:
+        b.close()
+    if coll:
+        dist.destroy_process_group()
+    if not ok:
+        log(f"CHECK FAILED: records {total_records}/{F.records}, counts {sum(counts)}, stitch {st['ok']}, "
+            f"crc {crc_bad}, split errors {split_bad}, splits {len(counts)}/{nsplits}")
+        sys.exit(3)
+
+
+def kernel_src_hash():
+    """Content hash of the kernel sources (spark-bam_amd/csrc/*.hip, *.h): counter summaries
+    record it when collected (tools/pmc_collect.sh), so a bench line can tell whether its
+    `traffic` / `limiter` still describe the kernels it ran."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc", "derived.json")))
+    import hashlib
+    h = hashlib.sha256()
+    for f in sorted(glob.glob(os.path.join(ROOT, "spark-bam_amd", "csrc", "*.hip")) +
+                    glob.glob(os.path.join(ROOT, "spark-bam_amd", "csrc", "*.h"))):
+        h.update(os.path.basename(f).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
+def latest_pmc(name):
+    """The newest committed counter summary `profiles/r*_pmc/<name>` (tools/pmc_collect.sh)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc", name)))
     if not files:
-        return "no counter data committed"
+        return None, None
     with open(files[-1]) as fh:
-        k = json.load(fh)["kernels"].get(kernel)
+        return json.load(fh), os.path.relpath(files[-1], ROOT)
+
+
+def limiter_text(kernel, ms=None, traffic=None):
+    """What bounds `kernel`, worded from its own counters (tools/pmc_derived.py over the
+    rocprofv3 passes of tools/pmc_collect.sh) and its measured HBM traffic."""
+    d, src = latest_pmc("derived.json")
+    if not d:
+        return "no counter data committed"
+    k = d["kernels"].get(kernel)
     if not k:
-        return f"no counter data for {kernel}"
-    return (f"not HBM: {kernel} issues on {100 * k['issuing_frac']:.0f}% of wave cycles and is parked on "
-            f"s_waitcnt/barrier {100 * k['parked_waitcnt_barrier_frac']:.0f}% (LDS round trips of the per-lane "
-            f"decode chains, repair-round barriers), VALU active {100 * k['valu_active_frac']:.0f}%, LDS bank "
-            f"conflicts {100 * k['lds_bank_conflict_frac']:.0f}% of LDS-array cycles (random table lookups) -- "
-            f"{os.path.relpath(files[-1], ROOT)} from sq_lds.csv / sq_wait.csv")
+        return f"no counter data for {kernel} in {src}"
+    parts = []
+    if traffic and ms:
+        bw = traffic / (ms * 1e-3) / 1e9
+        parts.append(f"{'HBM-bound' if bw > 0.6 * HBM_PEAK_GBPS else 'not HBM-bound'}: its measured traffic "
+                     f"moves at {bw:.0f} GB/s ({100 * bw / HBM_PEAK_GBPS:.0f}% of peak) while it runs")
+    parked, issuing = k.get("parked_waitcnt_barrier_frac") or 0, k.get("issuing_frac") or 0
+    if parked >= 0.4:
+        parts.append(f"latency-bound: waves parked on s_waitcnt/barrier {100 * parked:.0f}% of wave cycles, "
+                     f"issuing {100 * issuing:.0f}%")
+    else:
+        parts.append(f"issue-bound: waves issuing {100 * issuing:.0f}% of wave cycles, parked {100 * parked:.0f}%")
+    bc = k.get("lds_bank_conflict_frac")
+    if bc is not None:
+        parts.append(f"LDS bank conflicts {100 * bc:.0f}% of LDS-array cycles")
+    parts.append(f"VALU active {100 * k['valu_active_frac']:.0f}%")
+    fresh = d.get("src_hash") == kernel_src_hash()
+    return "; ".join(parts) + f" -- {src}" + ("" if fresh else " (collected before the last kernel change)")
 
 
 def host_cores():

@@ -48,7 +48,31 @@ static int failed(JNIEnv *env, jlong ctx, int rc) {
   return 1;
 }
 
-static void *direct(JNIEnv *env, jobject buf) { return buf ? (*env)->GetDirectBufferAddress(env, buf) : NULL; }
+static void throw_arg(JNIEnv *env, const char *msg) {
+  jclass c = (*env)->FindClass(env, "java/lang/IllegalArgumentException");
+  if (c) (*env)->ThrowNew(env, c, msg);
+}
+
+/* The address of a direct ByteBuffer the library will read or write `need` bytes of.  A null
+ * buffer gives NULL (an optional output is skipped, a required input is rejected by the
+ * library).  A heap buffer (no address) or one shorter than `need` throws
+ * IllegalArgumentException and sets *bad: the library never writes past the JVM's buffer. */
+static void *direct_n(JNIEnv *env, jobject buf, uint64_t need, int *bad) {
+  if (!buf) return NULL;
+  void *p = (*env)->GetDirectBufferAddress(env, buf);
+  const jlong cap = (*env)->GetDirectBufferCapacity(env, buf);
+  if (!p || cap < 0) {
+    throw_arg(env, "libsparkbam_hip needs a direct ByteBuffer");
+    *bad = 1;
+    return NULL;
+  }
+  if ((uint64_t)cap < need) {
+    throw_arg(env, "ByteBuffer smaller than the bytes libsparkbam_hip reads or writes");
+    *bad = 1;
+    return NULL;
+  }
+  return p;
+}
 
 static int put_longs(JNIEnv *env, jlongArray out, const jlong *v, jsize n) {
   if ((*env)->GetArrayLength(env, out) < n) {
@@ -86,7 +110,7 @@ JNIEXPORT jobject JNICALL Java_org_hammerlab_bam_gpu_Native_00024_hostAlloc(JNIE
 }
 
 JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_hostFree(JNIEnv *env, jobject self, jobject buf) {
-  sbh_host_free(direct(env, buf));
+  sbh_host_free(buf ? (*env)->GetDirectBufferAddress(env, buf) : NULL);
 }
 
 /* ---- shards: compressed bytes [fileOffset, fileOffset + n) of a BGZF file ---- */
@@ -94,8 +118,11 @@ JNIEXPORT jlong JNICALL Java_org_hammerlab_bam_gpu_Native_00024_shardCreate(JNIE
                                                                             jobject buf, jlong n, jlong fileOffset,
                                                                             jlong fileSize) {
   sbh_shard *sh = NULL;
-  if (failed(env, ctx, sbh_shard_create(CTX(ctx), direct(env, buf), (uint64_t)n, (uint64_t)fileOffset,
-                                        (uint64_t)fileSize, 0, &sh)))
+  int bad = 0;
+  const void *comp = direct_n(env, buf, (uint64_t)n, &bad);
+  if (bad) return 0;
+  if (failed(env, ctx, sbh_shard_create(CTX(ctx), comp, (uint64_t)n, (uint64_t)fileOffset, (uint64_t)fileSize, 0,
+                                        &sh)))
     return 0;
   return (jlong)(intptr_t)sh;
 }
@@ -149,7 +176,10 @@ JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_blocks(JNIEnv *en
 /* Block.bytes on demand: flat [flat, flat + n) into a direct ByteBuffer */
 JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_readFlat(JNIEnv *env, jobject self, jlong ctx,
                                                                         jlong sh, jlong flat, jlong n, jobject buf) {
-  failed(env, ctx, sbh_read_flat(SH(sh), (uint64_t)flat, (uint64_t)n, (uint8_t *)direct(env, buf)));
+  int bad = 0;
+  uint8_t *out = (uint8_t *)direct_n(env, buf, (uint64_t)n, &bad);
+  if (bad) return;
+  failed(env, ctx, sbh_read_flat(SH(sh), (uint64_t)flat, (uint64_t)n, out));
 }
 
 JNIEXPORT jlong JNICALL Java_org_hammerlab_bam_gpu_Native_00024_flatOf(JNIEnv *env, jobject self, jlong ctx,
@@ -183,10 +213,22 @@ JNIEXPORT jlong JNICALL Java_org_hammerlab_bam_gpu_Native_00024_checkEager(JNIEn
                                                                            jlong sh, jlong begin, jlong end,
                                                                            jint readsToCheck, jobject bits) {
   uint64_t n_true = 0;
-  if (failed(env, ctx, sbh_check_eager(SH(sh), (uint64_t)begin, (uint64_t)end, readsToCheck,
-                                       (uint8_t *)direct(env, bits), &n_true)))
+  int bad = 0;
+  uint8_t *out = (uint8_t *)direct_n(env, bits, end > begin ? ((uint64_t)(end - begin) + 7) / 8 : 0, &bad);
+  if (bad) return -1;
+  if (failed(env, ctx, sbh_check_eager(SH(sh), (uint64_t)begin, (uint64_t)end, readsToCheck, out, &n_true)))
     return -1;
   return (jlong)n_true;
+}
+
+/* the eager bitmap the last checkEager / runShard left on the device, [begin, end) */
+JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_eagerBits(JNIEnv *env, jobject self, jlong ctx,
+                                                                         jlong sh, jlong begin, jlong end,
+                                                                         jobject bits) {
+  int bad = 0;
+  uint8_t *out = (uint8_t *)direct_n(env, bits, end > begin ? ((uint64_t)(end - begin) + 7) / 8 : 0, &bad);
+  if (bad) return;
+  failed(env, ctx, sbh_eager_bits(SH(sh), (uint64_t)begin, (uint64_t)end, out));
 }
 
 /* full.Checker over flat [begin, end): words (may be null), counts 21*19, rbe 21*64, close
@@ -198,10 +240,16 @@ JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_checkFull(JNIEnv 
                                                                          jobject closeFlat, jobject closeWord,
                                                                          jlong closeCap, jlongArray out) {
   uint64_t ns = 0, nclose = 0;
-  if (failed(env, ctx, sbh_check_full(SH(sh), (uint64_t)begin, (uint64_t)end, readsToCheck,
-                                      (uint32_t *)direct(env, words), (uint64_t *)direct(env, counts),
-                                      (uint64_t *)direct(env, rbe), &ns, (uint64_t *)direct(env, closeFlat),
-                                      (uint32_t *)direct(env, closeWord), (uint64_t)closeCap, &nclose)))
+  const uint64_t npos = end > begin ? (uint64_t)(end - begin) : 0, cc = closeCap > 0 ? (uint64_t)closeCap : 0;
+  int bad = 0;
+  uint32_t *w = (uint32_t *)direct_n(env, words, 4 * npos, &bad);
+  uint64_t *c = bad ? NULL : (uint64_t *)direct_n(env, counts, 8ull * SBH_NNZ_MAX * 19, &bad);
+  uint64_t *r = bad ? NULL : (uint64_t *)direct_n(env, rbe, 8ull * SBH_NNZ_MAX * SBH_RBE_MAX, &bad);
+  uint64_t *cf = bad ? NULL : (uint64_t *)direct_n(env, closeFlat, 8 * cc, &bad);
+  uint32_t *cw = bad ? NULL : (uint32_t *)direct_n(env, closeWord, 4 * cc, &bad);
+  if (bad) return;
+  if (failed(env, ctx, sbh_check_full(SH(sh), (uint64_t)begin, (uint64_t)end, readsToCheck, w, c, r, &ns, cf, cw,
+                                      (cf || cw) ? cc : 0, &nclose)))
     return;
   jlong v[2] = {(jlong)ns, (jlong)nclose};
   put_longs(env, out, v, 2);
@@ -282,10 +330,17 @@ JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_checkRecords(JNIE
     re[i] = (uint64_t)ab[1];
   }
   uint64_t o[4] = {0, 0, 0, 0};
-  if (!failed(env, ctx, sbh_check_records(SH(sh), rb, re, (uint64_t)nr, readsToCheck,
-                                          (const uint64_t *)direct(env, recVpos), (uint64_t)nRec, o,
-                                          (uint64_t *)direct(env, fpFlat), (uint64_t)cap,
-                                          (uint64_t *)direct(env, fnFlat), (uint64_t)cap))) {
+  const uint64_t cp = cap > 0 ? (uint64_t)cap : 0, nv = nRec > 0 ? (uint64_t)nRec : 0;
+  int bad = 0;
+  const uint64_t *rv = (const uint64_t *)direct_n(env, recVpos, 8 * nv, &bad);
+  uint64_t *fp = bad ? NULL : (uint64_t *)direct_n(env, fpFlat, 8 * cp, &bad);
+  uint64_t *fn = bad ? NULL : (uint64_t *)direct_n(env, fnFlat, 8 * cp, &bad);
+  if (bad) {
+    free(r);
+    return;
+  }
+  if (!failed(env, ctx, sbh_check_records(SH(sh), rb, re, (uint64_t)nr, readsToCheck, rv, nv, o, fp, fp ? cp : 0, fn,
+                                          fn ? cp : 0))) {
     jlong v[4] = {(jlong)o[0], (jlong)o[1], (jlong)o[2], (jlong)o[3]};
     put_longs(env, out, v, 4);
   }
@@ -314,11 +369,14 @@ JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_runStream(JNIEnv 
                                                                          jlong ownEnd, jlong window, jlong halo,
                                                                          jintArray contigs, jint readsToCheck,
                                                                          jint maxReadSize, jlongArray out) {
+  int bad = 0;
+  const void *src = direct_n(env, comp, (uint64_t)n, &bad);
+  if (bad) return;
   const jsize nc = (*env)->GetArrayLength(env, contigs);
   jint *cl = (*env)->GetIntArrayElements(env, contigs, NULL);
   if (!cl) return;
   sbh_stream_result r;
-  const int rc = sbh_run_stream(CTX(ctx), direct(env, comp), (uint64_t)n, (uint64_t)fileOffset, (uint64_t)fileSize,
+  const int rc = sbh_run_stream(CTX(ctx), src, (uint64_t)n, (uint64_t)fileOffset, (uint64_t)fileSize,
                                 (uint64_t)indexStart, (uint64_t)ownEnd, (uint64_t)window, (uint64_t)halo,
                                 (const int32_t *)cl, (int32_t)nc, readsToCheck, maxReadSize, NULL, 0, &r);
   (*env)->ReleaseIntArrayElements(env, contigs, cl, JNI_ABORT);
@@ -340,13 +398,100 @@ JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_recordsScan(JNIEn
 }
 
 JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_recordsFetch(JNIEnv *env, jobject self, jlong ctx,
-                                                                            jlong sh, jobjectArray cols) {
-  /* 18 direct buffers in sbh_records_out field order */
+                                                                            jlong sh, jlongArray sizes,
+                                                                            jobjectArray cols) {
+  /* 18 direct buffers in sbh_records_out field order, each checked against the bytes of its
+   * column for the sizes recordsScan returned ({n, nameBytes, cigarOps, bases, auxBytes}) */
+  jlong z[5];
+  if ((*env)->GetArrayLength(env, sizes) < 5) {
+    throw_arg(env, "recordsFetch: sizes must hold recordsScan's 5 values");
+    return;
+  }
+  (*env)->GetLongArrayRegion(env, sizes, 0, 5, z);
+  const uint64_t n = (uint64_t)z[0], nm = (uint64_t)z[1], cg = (uint64_t)z[2], bs = (uint64_t)z[3], ax = (uint64_t)z[4];
+  const uint64_t need[18] = {8 * n, 4 * n, 4 * n, 4 * n, 4 * n, 4 * n, 2 * n, 2 * n, n, 8 * (n + 1), 8 * (n + 1),
+                             8 * (n + 1), 8 * (n + 1), nm, 4 * cg, bs, bs, ax};
   void *p[18];
-  for (jsize i = 0; i < 18; ++i) p[i] = direct(env, (*env)->GetObjectArrayElement(env, cols, i));
+  int bad = 0;
+  for (jsize i = 0; i < 18 && !bad; ++i) p[i] = direct_n(env, (*env)->GetObjectArrayElement(env, cols, i), need[i], &bad);
+  if (bad) return;
   sbh_records_out o = {(uint64_t *)p[0], (int32_t *)p[1],  (int32_t *)p[2],  (int32_t *)p[3],  (int32_t *)p[4],
                        (int32_t *)p[5],  (uint16_t *)p[6], (uint16_t *)p[7], (uint8_t *)p[8],  (uint64_t *)p[9],
                        (uint64_t *)p[10], (uint64_t *)p[11], (uint64_t *)p[12], (char *)p[13], (uint32_t *)p[14],
                        (char *)p[15], (uint8_t *)p[16], (uint8_t *)p[17]};
   failed(env, ctx, sbh_records_fetch(SH(sh), &o));
+}
+
+/* sbh_run_stream2: a shard streamed through HBM with per-split results; splitOut = 3 longs per
+ * split {status, firstVpos, count}; out = {nWindows, compBytes, flatBytes, nTrue, count,
+ * firstVpos, exitVpos, crcBadBlocks} */
+JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_runStreamSplits(
+    JNIEnv *env, jobject self, jlong ctx, jobject comp, jlong n, jlong fileOffset, jlong fileSize, jlong indexStart,
+    jlong ownEnd, jlong window, jlong halo, jintArray contigs, jint blocksToCheck, jint readsToCheck,
+    jint maxReadSize, jboolean verifyCrc, jlongArray splitStarts, jlongArray splitEnds, jlongArray splitOut,
+    jlongArray out) {
+  int bad = 0;
+  const void *src = direct_n(env, comp, (uint64_t)n, &bad);
+  if (bad) return;
+  const jsize ns = (*env)->GetArrayLength(env, splitStarts);
+  if ((*env)->GetArrayLength(env, splitEnds) != ns || (*env)->GetArrayLength(env, splitOut) < 3 * ns) {
+    throw_arg(env, "runStreamSplits: split arrays of different lengths");
+    return;
+  }
+  uint64_t *buf = (uint64_t *)malloc(sizeof(uint64_t) * 4 * (size_t)(ns > 0 ? ns : 1));
+  int32_t *status = (int32_t *)malloc(sizeof(int32_t) * (size_t)(ns > 0 ? ns : 1));
+  jlong *v = (jlong *)malloc(sizeof(jlong) * 3 * (size_t)(ns > 0 ? ns : 1));
+  const jsize nc = (*env)->GetArrayLength(env, contigs);
+  jint *cl = (*env)->GetIntArrayElements(env, contigs, NULL);
+  if (!buf || !status || !v || !cl) {
+    if (cl) (*env)->ReleaseIntArrayElements(env, contigs, cl, JNI_ABORT);
+    free(buf), free(status), free(v);
+    if (!cl) return;
+    throw_status(env, NULL, SBH_E_NOMEM);
+    return;
+  }
+  uint64_t *st = buf, *en = buf + ns, *first = buf + 2 * ns, *cnt = buf + 3 * ns;
+  (*env)->GetLongArrayRegion(env, splitStarts, 0, ns, (jlong *)st);
+  (*env)->GetLongArrayRegion(env, splitEnds, 0, ns, (jlong *)en);
+  sbh_stream_opts o = {0};
+  o.window = (uint64_t)window;
+  o.halo = (uint64_t)halo;
+  o.reads_to_check = readsToCheck;
+  o.max_read_size = maxReadSize;
+  o.bgzf_blocks_to_check = blocksToCheck;
+  o.verify_crc = verifyCrc ? 1 : 0;
+  o.split_start = st, o.split_end = en, o.n_splits = (uint64_t)ns;
+  o.split_first_vpos = first, o.split_count = cnt, o.split_status = status;
+  sbh_stream_result r;
+  const int rc = sbh_run_stream2(CTX(ctx), src, (uint64_t)n, (uint64_t)fileOffset, (uint64_t)fileSize,
+                                 (uint64_t)indexStart, (uint64_t)ownEnd, (const int32_t *)cl, (int32_t)nc, &o, &r);
+  (*env)->ReleaseIntArrayElements(env, contigs, cl, JNI_ABORT);
+  if (!failed(env, ctx, rc)) {
+    for (jsize i = 0; i < ns; ++i) v[3 * i] = status[i], v[3 * i + 1] = (jlong)first[i], v[3 * i + 2] = (jlong)cnt[i];
+    if (!put_longs(env, splitOut, v, 3 * ns)) {
+      jlong w[8] = {(jlong)r.n_windows, (jlong)r.comp_bytes, (jlong)r.flat_bytes, (jlong)r.n_true,
+                    (jlong)r.count, (jlong)r.first_vpos, (jlong)r.exit_vpos, (jlong)r.crc_bad_blocks};
+      put_longs(env, out, w, 8);
+    }
+  }
+  free(buf), free(status), free(v);
+}
+
+/* The BGZF writer (sbh_bgzf_compress_level; level 5 = htsjdk's exact bytes) */
+JNIEXPORT jlong JNICALL Java_org_hammerlab_bam_gpu_Native_00024_bgzfBound(JNIEnv *env, jobject self, jlong n) {
+  return (jlong)sbh_bgzf_compress_bound((uint64_t)n);
+}
+
+JNIEXPORT jlong JNICALL Java_org_hammerlab_bam_gpu_Native_00024_bgzfCompress(JNIEnv *env, jobject self, jlong ctx,
+                                                                             jobject src, jlong n, jint level,
+                                                                             jobject out) {
+  const uint64_t cap = sbh_bgzf_compress_bound((uint64_t)n);
+  int bad = 0;
+  const void *in = direct_n(env, src, (uint64_t)n, &bad);
+  uint8_t *o = bad ? NULL : (uint8_t *)direct_n(env, out, cap, &bad);
+  if (bad) return -1;
+  uint64_t size = 0, nb = 0;
+  if (failed(env, ctx, sbh_bgzf_compress_level(CTX(ctx), in, (uint64_t)n, 0, level, o, cap, &size, &nb, NULL)))
+    return -1;
+  return (jlong)size;
 }

@@ -7,6 +7,7 @@
 #include <stdint.h>
 typedef int32_t jint;
 typedef int64_t jlong;
+typedef unsigned char jboolean;
 typedef jint jsize;
 typedef struct _jobject *jobject;
 typedef jobject jclass, jarray, jlongArray, jintArray, jobjectArray;
@@ -19,6 +20,7 @@ struct JNINativeInterface_ {
   jclass (*FindClass)(JNIEnv *, const char *);
   jint (*ThrowNew)(JNIEnv *, jclass, const char *);
   void *(*GetDirectBufferAddress)(JNIEnv *, jobject);
+  jlong (*GetDirectBufferCapacity)(JNIEnv *, jobject);
   jobject (*NewDirectByteBuffer)(JNIEnv *, void *, jlong);
   jsize (*GetArrayLength)(JNIEnv *, jarray);
   void (*SetLongArrayRegion)(JNIEnv *, jlongArray, jsize, jsize, const jlong *);

@@ -23,7 +23,9 @@ pass sq_lds SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_I
 pass sq_wait SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES
 pass fetch FETCH_SIZE
 pass write WRITE_SIZE
+python3 -c "import bench; print(bench.kernel_src_hash())" > "$OUT/src_hash"
 python3 tools/pmc_summary.py "$OUT/sq_lds.csv" > "$OUT/sq_lds.txt"
 python3 tools/pmc_summary.py "$OUT/sq_wait.csv" > "$OUT/sq_wait.txt"
 python3 tools/pmc_traffic.py "$OUT/fetch.csv" "$OUT/write.csv" > "$OUT/traffic.json"
+python3 tools/pmc_derived.py "$OUT" > "$OUT/derived.json"
 echo "pmc ok"

@@ -42,7 +42,9 @@ def main(d):
             "lds_insts_per_wave": round(x.get("SQ_INSTS_LDS", 0) / y["SQ_WAVES"], 1) if y.get("SQ_WAVES") else None,
             "salu_insts_per_wave": round(y.get("SQ_INSTS_SALU", 0) / y["SQ_WAVES"], 1) if y.get("SQ_WAVES") else None,
         }
-    json.dump({"source": f"rocprofv3 --pmc passes in {d} (tools/pmc_collect.sh over bench.py)", "kernels": out},
+    hp = os.path.join(d, "src_hash")
+    json.dump({"source": f"rocprofv3 --pmc passes in {d} (tools/pmc_collect.sh over bench.py)",
+               "src_hash": open(hp).read().strip() if os.path.exists(hp) else None, "kernels": out},
               sys.stdout, indent=1)
     print()
 

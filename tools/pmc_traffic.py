@@ -12,8 +12,15 @@ usage: python tools/pmc_traffic.py FETCH.csv WRITE.csv > profiles/rNN_pmc_traffi
 import collections
 import csv
 import json
+import os
 import re
 import sys
+
+
+def src_hash(d):
+    """bench.kernel_src_hash() of the kernels the passes ran (tools/pmc_collect.sh writes it)."""
+    p = os.path.join(d, "src_hash")
+    return open(p).read().strip() if os.path.exists(p) else None
 
 
 def per_kernel(path):
@@ -34,7 +41,7 @@ def main(fetch, write):
         out[k] = {"read_bytes": int(rd), "write_bytes": int(wr), "hbm_bytes": int(rd + wr)}
     json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE over `bench.py --no-cpu-baseline "
                          "--steps 2 --warmup 1` (median launch; FETCH_SIZE doubled, gfx950)",
-               "kernels": out}, sys.stdout, indent=1)
+               "src_hash": src_hash(os.path.dirname(fetch)), "kernels": out}, sys.stdout, indent=1)
     print()
 
 

@@ -215,3 +215,58 @@ class WholeFile:
         self.file_offset = 0
         self.own_end = self.file_size = int(self.comp.size)
         return self
+
+
+class Replicated:
+    """configs[2]'s one big file, strong scaling: the BAM header's block(s), then one canonical
+    segment of records repeated `copies` times, then the EOF block.  The segment is `records`
+    records BGZF-compressed on the htsjdk payload grid with a short last block, so it starts
+    with a record at a block start and ends with a record at a block end: the copies join into
+    a valid BAM (record chain unbroken across them) whose compressed bytes are a periodic
+    pattern.  Any rank materializes its byte range [lo, hi) without generating the rest --
+    100 GB of file in seconds of memcpy instead of ~20 minutes of generation.  Block contents
+    repeat every segment (~1 GiB compressed, far beyond any cache), so every window still
+    inflates and checks its own bytes."""
+
+    def __init__(self, p, records, file_bytes):
+        if p.level < 0:
+            raise ValueError("a replicated file needs one zlib level")
+        hdr = header_bytes()
+        self.hdr_comp, _ = bgzf(p, hdr, 0, False)
+        recs = records_(p, 0, records)
+        self.seg_comp, self.seg_blocks = bgzf(p, recs, 1, False)
+        self.seg_flat = int(recs.size)
+        del recs
+        self.hdr_flat = int(hdr.size)
+        self.seg_records = int(records)
+        self.copies = max(1, -(-(int(file_bytes) - self.hdr_comp.size - 28) // self.seg_comp.size))
+        self.records = self.seg_records * self.copies
+        self.eof = np.frombuffer(bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000"),
+                                 dtype=np.uint8)
+        self.size = int(self.hdr_comp.size + self.copies * self.seg_comp.size + 28)
+        self.flat_size = self.hdr_flat + self.copies * self.seg_flat
+
+    def read_into(self, lo, hi, out):
+        """Compressed bytes [lo, hi) of the file into out[0: hi - lo]."""
+        h, s = self.hdr_comp.size, self.seg_comp.size
+        body_end = h + self.copies * s
+        o = 0
+        p = lo
+        while p < hi:
+            if p < h:
+                n = min(hi, h) - p
+                out[o:o + n] = self.hdr_comp[p:p + n]
+            elif p < body_end:
+                k, r = divmod(p - h, s)
+                n = min(hi - p, s - r)
+                out[o:o + n] = self.seg_comp[r:r + n]
+            else:
+                r = p - body_end
+                n = min(hi, self.size) - p
+                out[o:o + n] = self.eof[r:r + n]
+            o += n
+            p += n
+        return out
+
+
+records_ = records  # (Replicated's __init__ has a `records` argument)
