@@ -215,7 +215,8 @@ int sbh_split_starts(sbh_shard *sh, const uint64_t *starts, const uint64_t *ends
  * htsjdk virtual positions (the `.records` lines, any order).  out[0..3] = true positives,
  * false positives, false negatives, truth records whose block is not in the shard.  fp_flat /
  * fn_flat (optional) receive up to fp_cap / fn_cap mismatching flat positions, sorted (all of
- * them when out[1] <= fp_cap, resp. out[2] <= fn_cap). */
+ * them when out[1] <= fp_cap, resp. out[2] <= fn_cap; past the cap an arbitrary subset, not
+ * the first ones by position). */
 int sbh_check_records(sbh_shard *sh, const uint64_t *range_begin, const uint64_t *range_end,
                       uint64_t n_ranges, int32_t reads_to_check, const uint64_t *rec_vpos,
                       uint64_t n_rec, uint64_t *out, uint64_t *fp_flat, uint64_t fp_cap,

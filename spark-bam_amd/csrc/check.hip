@@ -307,7 +307,8 @@ struct EagerOut {
 // wave), not to n_true itself: one address takes every workgroup's atomic in turn at one
 // L2 channel, and the barrier a per-workgroup sum needs waits for the bitmap stores.
 constexpr uint32_t TRUE_SLOTS = 64, TRUE_STRIDE = 16;
-constexpr uint32_t TRUE_SPREAD_OFF = 2048;  // u64 offset of the slots in the counter buffer
+constexpr uint32_t TRUE_SPREAD_OFF = CTR_TRUE_SPREAD;  // u64 offset of the slots in the counter buffer
+static_assert(TRUE_SLOTS * TRUE_STRIDE == CTR_TRUE_WORDS, "true-count slots fill their region");
 
 // A candidate whose first record is at least this long (block_size) leaves its exact check
 // to k_eager_xq: its name / CIGAR bytes are read by a whole wave instead of one lane.
@@ -1057,7 +1058,11 @@ __device__ uint32_t chain_full(const Src &s, const uint32_t *bname, const uint32
 
 __global__ __launch_bounds__(T, 5) void k_full(const uint8_t *__restrict__ U, uint64_t u_pad, uint64_t begin,
                                             uint64_t end, Segs sg, Ctg c, int32_t rtc, FullOut o) {
-  constexpr uint32_t NREP = 4, REP = 21 * 19 + 2;  // histogram replicas (stride coprime to 32 banks)
+#ifndef SBH_FULL_NREP
+#define SBH_FULL_NREP 4
+#endif
+  constexpr uint32_t NREP = SBH_FULL_NREP, REP = 21 * 19 + 2;  // histogram replicas (odd stride: replica
+                                                                 // bases on distinct banks)
   constexpr uint32_t SLOWCAP = 512;
   __shared__ uint4 ldsv[FNV];
   __shared__ uint32_t bname[FBW], bop[FBW];
@@ -1606,6 +1611,8 @@ __global__ void k_eager_defer(const uint8_t *__restrict__ U, uint64_t begin, Seg
 
 static inline uint32_t ngrid(uint64_t n, uint32_t t) { return (uint32_t)((n + t - 1) / t); }
 
+// counters: a shard's counter buffer (CTR_WORDS u64, layout in sbh_internal.h) -- the
+// true-count slots at CTR_TRUE_SPREAD must be zero on entry; k_fold_true leaves them zero.
 hipError_t launch_eager(const uint8_t *U, uint64_t u_pad, uint64_t begin, uint64_t end, const uint64_t *seg_end,
                         uint32_t nseg, uint32_t open_last, const int32_t *ctg, int32_t nctg, int32_t rtc,
                         uint32_t *bits, unsigned long long *counters, hipStream_t st, uint64_t front,

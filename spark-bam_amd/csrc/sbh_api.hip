@@ -333,10 +333,10 @@ int sbh_shard_create(sbh_ctx *ctx, const void *src, uint64_t n, uint64_t file_of
     e = hipMemcpyAsync(sh->comp.p, src, n, comp_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
                        ctx->stream);
   if (e == hipSuccess) e = hipMemsetAsync(sh->comp.p + n, 0, sh->pad, ctx->stream);
-  if (e == hipSuccess) e = sh->ctr.ensure(4096);
-  // (k_eager's per-wave true-count slots at [2048, 3072) must start zero; k_fold_true keeps them so)
-  if (e == hipSuccess) e = hipMemsetAsync(sh->ctr.p, 0, 4096 * sizeof(unsigned long long), ctx->stream);
-  if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&sh->h_ctr), 4096 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = sh->ctr.ensure(CTR_WORDS);
+  // (layout: sbh_internal.h; k_eager's true-count slots must start zero, k_fold_true keeps them so)
+  if (e == hipSuccess) e = hipMemsetAsync(sh->ctr.p, 0, CTR_WORDS * sizeof(unsigned long long), ctx->stream);
+  if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&sh->h_ctr), CTR_WORDS * sizeof(unsigned long long));
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   if (e != hipSuccess) {
     sbh_shard_destroy(sh);
@@ -450,7 +450,7 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
   uint64_t nchain = 0;
   // the 18 bytes after the last chain block (the next header, checked below), written by
   // k_chain_emit and copied back with the block table
-  uint8_t *next18_dev = reinterpret_cast<uint8_t *>(sh->ctr.p + 3072);
+  uint8_t *next18_dev = reinterpret_cast<uint8_t *>(sh->ctr.p + CTR_NEXT18);
   uint8_t *nx = reinterpret_cast<uint8_t *>(sh->h_ctr + 516);  // pinned
   if (nc) {
     HIPCHK(ctx, sh->cand.ensure(nc));
@@ -1209,7 +1209,9 @@ int sbh_split_starts(sbh_shard *sh, const uint64_t *starts, const uint64_t *ends
 // check-bam's comparison with the `.records` truth (CheckerApp.scala:65-227) on the device:
 // the eager bitmap over the hull of the selected flat ranges, the truth (htsjdk vpos of every
 // record) scattered into a second bitmap, and one word-parallel compare.  fp_flat / fn_flat
-// (optional) receive the first fp_cap / fn_cap mismatching flat positions in order.
+// (optional) receive up to fp_cap / fn_cap mismatching flat positions, sorted: all of them
+// when there are at most that many, otherwise an arbitrary subset (the compaction is in
+// atomic order), not the first ones by position.
 int sbh_check_records(sbh_shard *sh, const uint64_t *range_begin, const uint64_t *range_end, uint64_t n_ranges,
                       int32_t rtc, const uint64_t *rec_vpos, uint64_t n_rec, uint64_t *out /*tp, fp, fn, unknown*/,
                       uint64_t *fp_flat, uint64_t fp_cap, uint64_t *fn_flat, uint64_t fn_cap) {

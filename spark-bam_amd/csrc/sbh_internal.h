@@ -158,6 +158,25 @@ hipError_t launch_member_footer(const uint8_t *src, uint64_t n, uint64_t b0, uin
                                 uint8_t *slots, uint64_t stride, const uint32_t *sizes, hipStream_t st);
 
 // Batched splits and check-bam truth comparison (splits.hip).
+// The shard's counter buffer (sbh_shard::ctr, device, CTR_WORDS u64, zeroed by
+// sbh_shard_create) and its pinned host mirror h_ctr.  Entry points run one at a time on the
+// shard's stream and copy their results out before returning, so the per-call regions
+// below may overlap each other; the persistent regions may not overlap anything.
+//   per call  [0, CTR_CALL_END)   k_eager (n_true, deferred, xq) / k_full (n_success,
+//                                 n_unknown, min_unknown, close_n, Counts [4, 403),
+//                                 rbe [403, 1747)); FindRecordStart best [8]; chain walk
+//                                 [16, 20); chain marks [20, 26); block CRCs [32, 34);
+//                                 check-records [40, 46); first bad block [100]
+//   persistent [CTR_TRUE_SPREAD, +CTR_TRUE_WORDS)  k_eager's per-wave true counts: must be
+//                                 zero before every k_eager launch; k_fold_true folds them
+//                                 into n_true and zeroes them again
+//   per call  [CTR_NEXT18, +3)    the 18 bytes after an index's last chained block
+constexpr uint32_t CTR_WORDS = 4096;
+constexpr uint32_t CTR_CALL_END = 4 + 21 * 19 + 21 * 64;
+constexpr uint32_t CTR_TRUE_SPREAD = 2048, CTR_TRUE_WORDS = 64 * 16;
+constexpr uint32_t CTR_NEXT18 = CTR_TRUE_SPREAD + CTR_TRUE_WORDS;
+static_assert(CTR_CALL_END <= CTR_TRUE_SPREAD && CTR_NEXT18 + 3 <= CTR_WORDS, "counter buffer layout");
+
 constexpr uint32_t SPLIT_OK = 0;    // first record and flat end decided on the device
 constexpr uint32_t SPLIT_HOST = 1;  // off the common path: the exact per-split host path decides
 struct SplitArgs {
