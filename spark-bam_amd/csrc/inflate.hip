@@ -329,27 +329,6 @@ __device__ __forceinline__ uint32_t ptable_entry(const SM &sm, const uint32_t *l
   return sm.sent[(kind ? 288 : 0) + (((sm.pk[kind][len] & 0xffffu) + (c15 >> (15 - len))) & 0xffffu)];
 }
 
-#ifndef SBH_LIT2
-#define SBH_LIT2 1
-#endif
-// Literal/length entry i with literal pairs (SBH_LIT2): when the table's bits hold a literal
-// code of length L1 followed by a whole second literal code of length L2, the entry decodes
-// both -- [4:0] L1 + L2, [15:12] L1 (non-zero marks a pair), [23:16] first byte, [31:24]
-// second byte -- so literal runs (quality strings) cost one LDS round trip per two symbols.
-// The second code's length is decided with the unknown bits past the table taken as zero:
-// a prefix code's first L2 bits decide it, so L2 <= LIT_FAST - L1 means it is fully known.
-template <class SM>
-__device__ __forceinline__ uint32_t ptable_lit_entry(const SM &sm, const uint32_t *lj, uint32_t i) {
-  const uint32_t e = ptable_entry(sm, lj, 0, LIT_FAST, i);
-  if (!SBH_LIT2) return e;
-  const uint32_t L1 = e & 31;
-  if ((e & 0xff00ffe0u) != 0 || L1 >= (uint32_t)LIT_FAST) return e;  // not a literal, or no bits left
-  const uint32_t e2 = ptable_entry(sm, lj, 0, LIT_FAST, i >> L1);
-  const uint32_t L2 = e2 & 31;
-  if ((e2 & 0xff00ffe0u) != 0 || L2 > (uint32_t)LIT_FAST - L1) return e;
-  return (L1 + L2) | (L1 << 12) | (e & 0x00ff0000u) | ((e2 & 0x00ff0000u) << 8);
-}
-
 // Canonical table in the PAR format (kind 0 lit/len, 1 dist), same validity rules as
 // build_table, built by one wave.  Returns 0 ok, 1 error, 2 empty.
 __device__ __forceinline__ uint32_t build_ptable(WaveSmem &sm, const uint8_t *lens, uint32_t nsym, uint32_t kind,
@@ -987,19 +966,10 @@ constexpr uint32_t LR_RUN = 0, LR_EOB = 1, LR_DEAD = 2, LR_PAST = 3;
 __device__ unsigned long long hp_acc[16];
 __device__ unsigned int hp_done;
 #endif
-#ifndef SBH_HUFF_ILP
-#define SBH_HUFF_ILP 2
-#endif
-// Slices per lane: a lane decodes slices tid and tid + HT as two interleaved chains, so two
-// table lookups are in flight per lane (k_huff is bound by the latency of each code's LDS
-// round trip, not by issue).
-constexpr uint32_t HILP = SBH_HUFF_ILP;
-static_assert(HILP == 1 || HILP == 2, "one or two chains per lane");
-constexpr uint32_t NSLICE = HILP * HT;
 struct HuffSmem {
   WaveSmem t;                    // tables (built by wave 0; the serial fallback's too)
   uint32_t stage[STAGE_DW + 8];  // the block's deflate dwords, from dword a0
-  uint32_t exitv[NSLICE];        // slice exits (NOPOS: the chain ended in the slice)
+  uint32_t exitv[HT];            // lane exits (NOPOS: the chain ended in the lane)
   uint32_t wsum[HT / WAVE];
   uint32_t ctl[8];
 };
@@ -1057,19 +1027,6 @@ struct Ckpt {
 };
 constexpr int RUN_SPEC = 0, RUN_REDO = 1, RUN_EMIT = 2;
 
-// A literal-pair entry taken as its first literal alone when the boundary between the two
-// is one the chain must stop at: the first boundary at or past stop2 (the exit), the
-// boundary after exactly ck_next tokens (a RUN_SPEC checkpoint) or a checkpoint a RUN_REDO
-// chain joins at.  So every chain stops at the same boundaries as a symbol-at-a-time decode.
-template <int MODE>
-__device__ __forceinline__ uint32_t lit2_split(uint32_t e, uint32_t pos, uint32_t stop2, uint32_t ntok,
-                                               uint32_t ck_next, const Ckpt &ck) {
-  const uint32_t L1 = (e >> 12) & 15, mid = pos + L1;
-  const bool half = L1 != 0 && (mid >= stop2 || (MODE == RUN_SPEC && ntok + 1 == ck_next) ||
-                                (MODE == RUN_REDO && (mid == ck.p1 || mid == ck.p2)));
-  return half ? (L1 | (e & 0x00ff0000u)) : e;
-}
-
 // Decode tokens from bit A while the position is below `stop`, as a two-state machine
 // (literal/length code, then distance code) so every lane runs the same instructions:
 // one table lookup per code, the extra bits taken straight from the entry.
@@ -1116,8 +1073,6 @@ __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, Src<LDS> src, uin
     }
     cut = atb && (pos >= stop2 || (MODE == RUN_REDO && (pos == ck.p1 || pos == ck.p2)));
     if (cut || (e & PE_SPECIAL)) break;
-    if (SBH_LIT2) e = lit2_split<MODE>(e, pos, stop2, ntok, ck_next, ck);
-    const uint32_t pair = ((e >> 12) & 15) != 0;  // L1 > 0: two literals
     const uint32_t L = e & 31, x = (e >> 8) & 15;
     const uint32_t val = (e >> 16) + __builtin_amdgcn_ubfe(bits, L, x);
     pos += L + x;
@@ -1125,14 +1080,13 @@ __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, Src<LDS> src, uin
     lo = adv ? hi : lo;
     hi = adv ? nx : hi;
     wi += adv ? 1u : 0u;
-    const bool is_tok = (e & PE_LEN) == 0;  // a literal (pair), or the distance completing a match
+    const bool is_tok = (e & PE_LEN) == 0;  // a literal, or the distance completing a match
     if (MODE == RUN_EMIT) {
-      if (is_tok) dst[ntok] = atb ? (val & 0xffu) << 8 : TOK_MATCH | (ml << 16) | val;
-      if (pair) dst[ntok + 1] = val & 0xff00u;
+      if (is_tok) dst[ntok] = atb ? val << 8 : TOK_MATCH | (ml << 16) | val;
       bad |= (!atb && val > out0 + nout) ? 1u : 0u;
     }
-    ntok += is_tok ? 1u + pair : 0u;
-    nout += is_tok ? (ml > 1u ? ml : 1u) + pair : 0u;
+    ntok += is_tok ? 1u : 0u;
+    nout += is_tok ? (ml > 1u ? ml : 1u) : 0u;
     ml = is_tok ? 0u : val;
   }
   if (MODE == RUN_SPEC) ck = Ckpt{c1p, c1o, c2p, c2o};
@@ -1152,112 +1106,6 @@ __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, Src<LDS> src, uin
     r.exit = pos + (e & 31);
   }
   return r;
-}
-
-// lane_run on two independent chains of one lane (slices tid and tid + HT), interleaved:
-// both chains' stream dword and table lookups are issued before either is used, so each
-// iteration waits for one LDS round trip for two codes.  on[k] = chain k runs at all; a
-// chain that stops keeps its state while the other finishes.  Same results as two
-// lane_run calls.
-template <bool LDS, int MODE>
-__device__ __forceinline__ void lane_run2(const WaveSmem &t, Src<LDS> src, const uint32_t (&A)[2],
-                                          const uint32_t (&stop)[2], const bool (&on)[2], uint32_t limit,
-                                          Ckpt (&ck)[2], const LaneRun (&sp)[2], uint32_t *__restrict__ dst0,
-                                          uint32_t *__restrict__ dst1, uint32_t out00, uint32_t out01, uint32_t &bad,
-                                          LaneRun (&res)[2]) {
-  uint32_t pos[2], wi[2], lo[2], hi[2], ml[2], ntok[2], nout[2], stop2[2];
-  uint32_t c1p[2], c1o[2], c2p[2], c2o[2], ckn[2], e[2];
-  bool live[2], cut[2];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    stop2[k] = stop[k] < limit ? stop[k] : limit;
-    pos[k] = A[k];
-    wi[k] = pos[k] >> 5;
-    lo[k] = src(wi[k]);
-    hi[k] = src(wi[k] + 1);
-    ml[k] = ntok[k] = nout[k] = 0;
-    c1p[k] = c2p[k] = NOPOS;
-    c1o[k] = c2o[k] = 0;
-    ckn[k] = CK1;
-    e[k] = 0;
-    live[k] = on[k];
-    cut[k] = false;
-  }
-  while (live[0] || live[1]) {
-    uint32_t bits[2], nx[2], en[2];
-    bool atb[2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {  // both lookups in flight before either is used
-      bits[k] = __builtin_amdgcn_alignbit(hi[k], lo[k], pos[k] & 31);
-      nx[k] = src(wi[k] + 2);
-      atb[k] = ml[k] == 0;
-      en[k] = t.tab[(bits[k] & ((1u << LIT_FAST) - 1)) | (atb[k] ? 0u : 1u << LIT_FAST)];
-    }
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      if (!live[k]) continue;
-      uint32_t ek = en[k];
-      if (ek & PE_SLOW) ek = slow_lane(t, bits[k], !atb[k]);
-      if (MODE == RUN_SPEC && atb[k] && ntok[k] == ckn[k]) {
-        if (ckn[k] == CK1) {
-          c1p[k] = pos[k];
-          c1o[k] = nout[k];
-          ckn[k] = CK2;
-        } else {
-          c2p[k] = pos[k];
-          c2o[k] = nout[k];
-          ckn[k] = ~0u;
-        }
-      }
-      cut[k] = atb[k] && (pos[k] >= stop2[k] || (MODE == RUN_REDO && (pos[k] == ck[k].p1 || pos[k] == ck[k].p2)));
-      e[k] = ek;
-      if (cut[k] || (ek & PE_SPECIAL)) {
-        live[k] = false;
-        continue;
-      }
-      if (SBH_LIT2) ek = lit2_split<MODE>(ek, pos[k], stop2[k], ntok[k], ckn[k], ck[k]);
-      const uint32_t pair = ((ek >> 12) & 15) != 0;
-      const uint32_t L = ek & 31, x = (ek >> 8) & 15;
-      const uint32_t val = (ek >> 16) + __builtin_amdgcn_ubfe(bits[k], L, x);
-      pos[k] += L + x;
-      const bool adv = (pos[k] >> 5) != wi[k];
-      lo[k] = adv ? hi[k] : lo[k];
-      hi[k] = adv ? nx[k] : hi[k];
-      wi[k] += adv ? 1u : 0u;
-      const bool is_tok = (ek & PE_LEN) == 0;
-      if (MODE == RUN_EMIT) {
-        uint32_t *dst = k == 0 ? dst0 : dst1;
-        const uint32_t o0 = k == 0 ? out00 : out01;
-        if (is_tok) dst[ntok[k]] = atb[k] ? (val & 0xffu) << 8 : TOK_MATCH | (ml[k] << 16) | val;
-        if (pair) dst[ntok[k] + 1] = val & 0xff00u;
-        bad |= (!atb[k] && val > o0 + nout[k]) ? 1u : 0u;
-      }
-      ntok[k] += is_tok ? 1u + pair : 0u;
-      nout[k] += is_tok ? (ml[k] > 1u ? ml[k] : 1u) + pair : 0u;
-      ml[k] = is_tok ? 0u : val;
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    if (!on[k]) continue;
-    if (MODE == RUN_SPEC) ck[k] = Ckpt{c1p[k], c1o[k], c2p[k], c2o[k]};
-    LaneRun r{LR_RUN, pos[k], ntok[k], nout[k]};
-    if (cut[k]) {
-      if (MODE == RUN_REDO && pos[k] < stop2[k]) {  // joined the pass-1 chain at a checkpoint
-        const bool one = pos[k] == ck[k].p1;
-        r.ntok += sp[k].ntok - (one ? CK1 : CK2);
-        r.nout += sp[k].nout - (one ? ck[k].o1 : ck[k].o2);
-        r.st = sp[k].st;
-        r.exit = sp[k].exit;
-      } else if (pos[k] >= limit) {
-        r.st = LR_PAST;
-      }
-    } else {
-      r.st = (ml[k] == 0 && (e[k] & PE_EOB)) ? LR_EOB : LR_DEAD;
-      r.exit = pos[k] + (e[k] & 31);
-    }
-    res[k] = r;
-  }
 }
 
 // The code-length part of a dynamic block header (RFC 1951 3.2.7) by one wave: the
@@ -1350,7 +1198,7 @@ __device__ __forceinline__ void fill_ptables(WaveSmem &t, uint32_t tid) {
     lj1[v] = t.pk[1][v] >> 16;
   }
 #pragma unroll
-  for (uint32_t i = tid; i < (1u << LIT_FAST); i += HT) t.lit[i] = ptable_lit_entry(t, lj0, i);
+  for (uint32_t i = tid; i < (1u << LIT_FAST); i += HT) t.lit[i] = ptable_entry(t, lj0, 0, LIT_FAST, i);
 #pragma unroll
   for (uint32_t i = tid; i < (1u << PDIST_FAST); i += HT) t.dist[i] = ptable_entry(t, lj1, 1, PDIST_FAST, i);
 }
@@ -1430,88 +1278,6 @@ __device__ __forceinline__ bool par_header(HuffSmem &sm, Src<LDS> src, uint32_t 
   return true;
 }
 
-// One deflate block's symbols (from p0, tables in sm.t), lane-parallel with two slices per
-// lane (slice j = [p0 + j S, p0 + (j + 1) S), lane tid owns slices tid and tid + HT): pass 1
-// speculates both, repair rounds restart every slice whose left neighbour's exit moved, the
-// first slice whose chain ends decides the block, and the emit pass writes the tokens at
-// their prefix-sum offsets.  ntok / out advance; p = the bit after the end-of-block code.
-// Returns false (uniformly) when the serial decoder must decide the BGZF block.
-template <bool LDS>
-__device__ __forceinline__ bool par_slices2(HuffSmem &sm, Src<LDS> src, uint32_t p0, uint32_t limit, uint32_t usize,
-                                            uint32_t *__restrict__ tk, uint32_t tid, uint32_t &ntok, uint32_t &out,
-                                            uint32_t &p) {
-  uint32_t S = (limit > p0 ? limit - p0 : 0) / NSLICE + 1;
-  if (S < MIN_SLICE) S = MIN_SLICE;
-  uint32_t A[2] = {p0 + tid * S, p0 + (tid + HT) * S};
-  const uint32_t stop[2] = {A[0] + S, A[1] + S};
-  uint32_t nobad = 0;
-  Ckpt ck[2];
-  LaneRun r[2], r1[2];
-  const LaneRun none2[2] = {};
-  {
-    const bool on[2] = {true, true};
-    lane_run2<LDS, RUN_SPEC>(sm.t, src, A, stop, on, limit, ck, none2, nullptr, nullptr, 0, 0, nobad, r);
-  }
-  r1[0] = r[0];
-  r1[1] = r[1];
-  sm.exitv[tid] = r[0].st == LR_RUN ? r[0].exit : NOPOS;
-  sm.exitv[tid + HT] = r[1].st == LR_RUN ? r[1].exit : NOPOS;
-  for (;;) {
-    __syncthreads();
-    // a slice keeps its speculation while its left neighbour's chain has ended
-    const uint32_t nA0 = tid == 0 ? p0 : sm.exitv[tid - 1], nA1 = sm.exitv[tid + HT - 1];
-    const bool ch[2] = {nA0 != NOPOS && nA0 != A[0], nA1 != NOPOS && nA1 != A[1]};
-    __syncthreads();
-    if (ch[0] || ch[1]) {
-      if (ch[0]) A[0] = nA0;
-      if (ch[1]) A[1] = nA1;
-      LaneRun rr[2];
-      lane_run2<LDS, RUN_REDO>(sm.t, src, A, stop, ch, limit, ck, r1, nullptr, nullptr, 0, 0, nobad, rr);
-      if (ch[0]) {
-        r[0] = rr[0];
-        sm.exitv[tid] = r[0].st == LR_RUN ? r[0].exit : NOPOS;
-      }
-      if (ch[1]) {
-        r[1] = rr[1];
-        sm.exitv[tid + HT] = r[1].st == LR_RUN ? r[1].exit : NOPOS;
-      }
-    }
-    if (!__syncthreads_or(ch[0] || ch[1])) break;
-  }
-  // the first slice whose chain ends decides the deflate block
-  if (r[0].st != LR_RUN) atomicMin(&sm.ctl[3], tid);
-  if (r[1].st != LR_RUN) atomicMin(&sm.ctl[3], tid + HT);
-  __syncthreads();
-  const uint32_t k = uni(sm.ctl[3]);
-  if (tid == k) sm.ctl[4] = (r[0].st == LR_EOB && r[0].exit <= limit) ? r[0].exit : NOPOS;
-  if (tid + HT == k) sm.ctl[4] = (r[1].st == LR_EOB && r[1].exit <= limit) ? r[1].exit : NOPOS;
-  const bool in0 = tid <= k, in1 = tid + HT <= k;
-  uint32_t t0, t1, o0, o1;
-  const uint32_t tp0 = block_scan<HT>(in0 ? r[0].ntok : 0, sm.wsum, &t0);  // (syncs: ctl[4] visible)
-  __syncthreads();
-  const uint32_t tp1 = block_scan<HT>(in1 ? r[1].ntok : 0, sm.wsum, &t1);
-  __syncthreads();
-  const uint32_t op0 = block_scan<HT>(in0 ? r[0].nout : 0, sm.wsum, &o0);
-  __syncthreads();
-  const uint32_t op1 = block_scan<HT>(in1 ? r[1].nout : 0, sm.wsum, &o1);
-  const uint32_t eob_end = uni(sm.ctl[4]);
-  const uint32_t ttot = uni(t0 + t1), otot = uni(o0 + o1);
-  if (k >= NSLICE || eob_end == NOPOS || otot > usize - out) return false;
-  // emit
-  uint32_t bad = 0;
-  {
-    const bool on[2] = {in0, in1};
-    LaneRun re[2];
-    lane_run2<LDS, RUN_EMIT>(sm.t, src, A, stop, on, limit, ck, none2, tk + ntok + tp0, tk + ntok + t0 + tp1,
-                             out + op0, out + o0 + op1, bad, re);
-  }
-  if (__syncthreads_or(bad)) return false;
-  ntok += ttot;
-  out += otot;
-  p = eob_end;
-  return true;
-}
-
 // The deflate blocks of one BGZF block, lane-parallel.  Returns false (uniformly) when
 // the block must be decoded by the serial path instead.
 template <bool LDS>
@@ -1533,15 +1299,10 @@ __device__ __forceinline__ bool inflate_par(HuffSmem &sm, const uint8_t *__restr
     } else if (!par_header(sm, src, p, limit, fixed_built, wid, lane, p0, last)) {
       return false;
     }
-    if (tid == 0) sm.ctl[3] = NSLICE;
+    if (tid == 0) sm.ctl[3] = HT;
 
 #ifdef SBH_HUFF_PROBE
     const uint64_t tph = __builtin_readcyclecounter();
-#endif
-#if SBH_HUFF_ILP == 2
-    if (!par_slices2<LDS>(sm, src, p0, limit, usize, tk, tid, ntok, out, p)) return false;
-    if (last) break;
-    continue;
 #endif
     // pass 1: speculative decode of every lane's slice
     uint32_t S = (limit > p0 ? limit - p0 : 0) / HT + 1;
@@ -1709,7 +1470,7 @@ __global__ __launch_bounds__(WAVE * HDR_WAVES) void k_hdr(const uint8_t *__restr
       lj1[v] = t.pk[1][v] >> 16;
     }
 #pragma unroll 4
-    for (uint32_t i = lane; i < (1u << LIT_FAST); i += WAVE) out[i] = ptable_lit_entry(t, lj0, i);
+    for (uint32_t i = lane; i < (1u << LIT_FAST); i += WAVE) out[i] = ptable_entry(t, lj0, 0, LIT_FAST, i);
 #pragma unroll 4
     for (uint32_t i = lane; i < (1u << PDIST_FAST); i += WAVE)
       out[(1u << LIT_FAST) + i] = ptable_entry(t, lj1, 1, PDIST_FAST, i);
