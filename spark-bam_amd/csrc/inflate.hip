@@ -958,7 +958,11 @@ static_assert(HDR_SENT % SBH_HT == 0, "k_huff copies the tables in whole rounds"
 #define SBH_CK1 8
 #define SBH_CK2 32
 #endif
+#ifndef SBH_CK3
+#define SBH_CK3 64
+#endif
 constexpr uint32_t CK1 = SBH_CK1, CK2 = SBH_CK2;  // pass-1 checkpoints (tokens)
+constexpr uint32_t CK3 = SBH_CK3;                 // a third, for chains that sync late (0: none)
 constexpr uint32_t LR_RUN = 0, LR_EOB = 1, LR_DEAD = 2, LR_PAST = 3;
 #ifdef SBH_HUFF_PROBE
 // whole-kernel phase sums (cycles): 0 stage, 1 header, 2 pass 1, 3 repair, 4 emit, 5 repair
@@ -1019,11 +1023,13 @@ struct LaneRun {
   uint32_t nout;  // bytes
 };
 
-// Checkpoints of a lane's pass-1 chain: the boundaries after CK1 and CK2 tokens and
+// Checkpoints of a lane's pass-1 chain: the boundaries after CK1, CK2 and CK3 tokens and
 // the bytes produced up to them.  A repair run that lands on one of them has joined
-// that chain, so the rest of the pass-1 result holds.
+// that chain, so the rest of the pass-1 result holds.  (A chain that synchronises with the
+// true one only after CK2 tokens would otherwise be redone to its slice end, and the
+// slowest lane of a wave sets the repair round's time.)
 struct Ckpt {
-  uint32_t p1, o1, p2, o2;
+  uint32_t p1, o1, p2, o2, p3, o3;
 };
 constexpr int RUN_SPEC = 0, RUN_REDO = 1, RUN_EMIT = 2;
 
@@ -1050,7 +1056,7 @@ __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, Src<LDS> src, uin
   uint32_t wi = pos >> 5, lo = src(wi), hi = src(wi + 1);
   uint32_t ml = 0;  // pending match length: the next code is a distance
   uint32_t ntok = 0, nout = 0;
-  uint32_t c1p = NOPOS, c1o = 0, c2p = NOPOS, c2o = 0;
+  uint32_t c1p = NOPOS, c1o = 0, c2p = NOPOS, c2o = 0, c3p = NOPOS, c3o = 0;
   uint32_t ck_next = CK1;  // RUN_SPEC: token count of the next checkpoint
   uint32_t e;
   bool cut;
@@ -1065,13 +1071,17 @@ __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, Src<LDS> src, uin
         c1p = pos;
         c1o = nout;
         ck_next = CK2;
-      } else {
+      } else if (ck_next == CK2) {
         c2p = pos;
         c2o = nout;
+        ck_next = CK3 > CK2 ? CK3 : ~0u;
+      } else {
+        c3p = pos;
+        c3o = nout;
         ck_next = ~0u;
       }
     }
-    cut = atb && (pos >= stop2 || (MODE == RUN_REDO && (pos == ck.p1 || pos == ck.p2)));
+    cut = atb && (pos >= stop2 || (MODE == RUN_REDO && (pos == ck.p1 || pos == ck.p2 || pos == ck.p3)));
     if (cut || (e & PE_SPECIAL)) break;
     const uint32_t L = e & 31, x = (e >> 8) & 15;
     const uint32_t val = (e >> 16) + __builtin_amdgcn_ubfe(bits, L, x);
@@ -1089,13 +1099,14 @@ __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, Src<LDS> src, uin
     nout += is_tok ? (ml > 1u ? ml : 1u) : 0u;
     ml = is_tok ? 0u : val;
   }
-  if (MODE == RUN_SPEC) ck = Ckpt{c1p, c1o, c2p, c2o};
+  if (MODE == RUN_SPEC) ck = Ckpt{c1p, c1o, c2p, c2o, c3p, c3o};
   LaneRun r{LR_RUN, pos, ntok, nout};
   if (cut) {
     if (MODE == RUN_REDO && pos < stop2) {  // joined the pass-1 chain at a checkpoint
       const bool one = pos == ck.p1;
-      r.ntok += sp.ntok - (one ? CK1 : CK2);
-      r.nout += sp.nout - (one ? ck.o1 : ck.o2);
+      const bool two = pos == ck.p2;
+      r.ntok += sp.ntok - (one ? CK1 : two ? CK2 : CK3);
+      r.nout += sp.nout - (one ? ck.o1 : two ? ck.o2 : ck.o3);
       r.st = sp.st;
       r.exit = sp.exit;
     } else if (pos >= limit) {

@@ -1198,7 +1198,17 @@ int sbh_split_starts(sbh_shard *sh, const uint64_t *starts, const uint64_t *ends
       status[i] = SBH_OK;
       continue;
     }
+    if (code[i] == SPLIT_NOREAD) {  // as sbh_split: the split starts at an empty block
+      first_vpos[i] = counts[i] = 0;
+      status[i] = SBH_E_NO_READ_FOUND;
+      continue;
+    }
     ++nh;
+    if (std::getenv("SBH_SPLIT_DEBUG"))
+      fprintf(stderr, "[sbh] split %llu [%llu, %llu) host path: shard [%llu, +%llu) first %llu E %llu dense %d marked %d code %#x\n",
+              (unsigned long long)i, (unsigned long long)starts[i], (unsigned long long)ends[i],
+              (unsigned long long)sh->file_off, (unsigned long long)sh->n, (unsigned long long)first[i],
+              (unsigned long long)E[i], (int)dense, (int)marked, code[i]);
     first_vpos[i] = counts[i] = 0;
     status[i] = sbh_split(sh, starts[i], ends[i], k, rtc, mrs, &first_vpos[i], &counts[i]);
   }
@@ -1671,20 +1681,18 @@ int sbh_run_stream2(sbh_ctx *ctx, const void *host, uint64_t n, uint64_t file_of
     sh->scan_from = lo;  // header candidates from the window's first byte (its first split's FindBlockStart)
     rc = sbh_run_shard(sh, start, hi, rtc, mrs, &r);
     // this window's splits (every one inside [lo, hi)): the batched per-split path
-    uint64_t k0 = 0, k1 = 0;
+    uint64_t k0 = 0, k1 = 0, nh = 0;
     double split_ms = 0;
     if (!rc && ns) {
       k0 = (uint64_t)(std::lower_bound(O.split_start, O.split_start + ns, lo) - O.split_start);
       k1 = (uint64_t)(std::lower_bound(O.split_start, O.split_start + ns, hi) - O.split_start);
       if (k1 > k0) {
         const auto ts0 = std::chrono::steady_clock::now();
-        uint64_t nh = 0;
         rc = sbh_split_starts(sh, O.split_start + k0, O.split_end + k0, k1 - k0, kcheck, rtc, mrs,
                               O.split_first_vpos + k0, O.split_count + k0, O.split_status + k0, &nh);
         if (!rc)
           for (uint64_t i = k0; i < k1; ++i)
             if (O.split_status[i] == SBH_E_NEED_HALO) rc = SBH_E_NEED_HALO;
-        res->splits_host += nh;
         split_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
       }
     }
@@ -1704,6 +1712,7 @@ int sbh_run_stream2(sbh_ctx *ctx, const void *host, uint64_t n, uint64_t file_of
     }
     if (rc) return res->status = rc;
     res->ms_splits += split_ms;
+    res->splits_host += nh;  // (a window redone with a larger halo counts its final attempt only)
     account(cur);
     if (O.verify_crc && r.n_blocks) {  // the owned blocks are the block table's prefix
       uint64_t nbad = 0, fbad = 0;

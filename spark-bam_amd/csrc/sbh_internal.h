@@ -179,6 +179,7 @@ static_assert(CTR_CALL_END <= CTR_TRUE_SPREAD && CTR_NEXT18 + 3 <= CTR_WORDS, "c
 
 constexpr uint32_t SPLIT_OK = 0;    // first record and flat end decided on the device
 constexpr uint32_t SPLIT_HOST = 1;  // off the common path: the exact per-split host path decides
+constexpr uint32_t SPLIT_NOREAD = 2;  // FindBlockStart lands on an empty block: NoReadFoundException (no records)
 struct SplitArgs {
   const uint8_t *comp;
   uint64_t n;

@@ -92,10 +92,12 @@ __global__ __launch_bounds__(64) void k_split_prologue(SplitIn in, const uint64_
   if (i >= nsplit) return;
   const uint32_t lane = threadIdx.x;
   const uint64_t s = starts[i];
-  uint32_t code = SPLIT_HOST;
+  // off the common path: SPLIT_HOST | why << 4 (why: the step that gave up, for diagnostics)
+  uint32_t code = SPLIT_HOST | 1u << 4;
   uint64_t first = 0, E = 0;
   do {
     if (s < in.cand_from) break;
+    code = SPLIT_HOST | 2u << 4;
     // FindBlockStart: the first candidate in [s, s + 64 KiB) whose attempt is not a
     // HeaderParseException; positions within 18 bytes of the resident end are attempts
     // that never parse a header, so they end the search too (host path decides them).
@@ -117,15 +119,22 @@ __global__ __launch_bounds__(64) void k_split_prologue(SplitIn in, const uint64_
     best = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(best >> 32)) << 32) |
            (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)best);
     if (best >= ~1ull) break;
+    code = SPLIT_HOST | 3u << 4;
     const uint64_t bi = lower_bound(in.cstart, in.nblocks, best);
-    if (bi >= in.nblocks || in.cstart[bi] != best || (in.flags[bi] & BLK_EMPTY)) break;
+    if (bi >= in.nblocks || in.cstart[bi] != best) break;
+    if (in.flags[bi] & BLK_EMPTY) {  // the stream from an empty block ends at once (sbh_split)
+      code = SPLIT_NOREAD;
+      break;
+    }
     const uint64_t from = in.ustart[bi];
     // the stream segment holding `from` (an empty block ends the stream) and maxReadSize
     uint64_t seg = in.seg_end[in.nseg - 1];
     for (uint32_t k = 0; k < in.nseg; ++k)
       if (in.seg_end[k] > from) { seg = in.seg_end[k]; break; }
     const uint64_t limit = min(seg, from + (uint64_t)in.mrs);
+    code = SPLIT_HOST | 4u << 4;
     if (from < in.bits_begin) break;
+    code = SPLIT_HOST | 5u << 4;
     const uint64_t hi = min(limit, in.bits_end);
     // FindRecordStart: first set bit in [from, hi), 64 words per step
     uint64_t found = ~0ull;
@@ -145,6 +154,7 @@ __global__ __launch_bounds__(64) void k_split_prologue(SplitIn in, const uint64_
     }
     if (found == ~0ull) break;  // no read start in the bitmap: the host path decides
     first = found;
+    code = SPLIT_HOST | 6u << 4;
     // flat bound of Pos(end, 0): the first block starting at/after end
     const uint64_t e = ends[i];
     const uint64_t bj = lower_bound(in.cstart, in.nblocks, e);
