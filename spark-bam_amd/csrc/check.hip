@@ -920,6 +920,10 @@ constexpr uint32_t FNV = FTILE / 16 + 256;    // staged 16-byte vectors: tile + 
 constexpr uint32_t FSN = FNV * 16;            // staged bytes
 constexpr uint32_t FBW = FSN / 32;            // bitmap words
 constexpr uint32_t FCCAP = 256;               // close calls buffered per workgroup
+#ifndef SBH_FULL_CTG_LDS
+#define SBH_FULL_CTG_LDS 1
+#endif
+constexpr uint32_t FCTG = 1024;               // contig lengths staged in LDS (more: read from global)
 constexpr uint32_t FULL_SLOW = 0xFFFFFFFFu;   // "take the exact path" (no valid word has all bits)
 constexpr uint32_t FULL_PASS = 0xFFFFFFFEu;   // the first record passes: the chain decides
 static_assert(FTILE % (FPL * T) == 0 && FSN % 32 == 0 && FSN >= FTILE + 36 + 255 + 16, "full tile layout");
@@ -1073,6 +1077,15 @@ __global__ __launch_bounds__(T, 5) void k_full(const uint8_t *__restrict__ U, ui
   __shared__ uint32_t seg0, nsucc, ncl, nslow;
   __shared__ uint64_t e0;
   __shared__ unsigned long long cbase;
+#if SBH_FULL_CTG_LDS
+  // contig lengths in LDS (getRefPosError reads one for every position whose refID is valid:
+  // inside records that is several per record, each an L1/L2 round trip from global memory)
+  __shared__ int32_t ctgl[FCTG];
+  if (c.n <= (int32_t)FCTG) {
+    for (int32_t i = threadIdx.x; i < c.n; i += T) ctgl[i] = c.len[i];
+    c.len = ctgl;
+  }
+#endif
   const uint32_t *lds32 = reinterpret_cast<const uint32_t *>(ldsv);
   const uint64_t s0 = (begin & ~15ull) + (uint64_t)blockIdx.x * FTILE;  // 16-aligned tile start
   stage_vec<FNV>(ldsv, U, s0, u_pad);
