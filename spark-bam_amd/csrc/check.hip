@@ -976,6 +976,9 @@ __device__ __forceinline__ uint32_t full_first(const Src &s, const uint32_t *bna
   uint32_t f = ref_pos_error(x.idx, x.pos, c) << 1;
   if (x.rem < implied_min_remaining(rnl, nc, x.seq_len)) f |= 1u << 18;
   f |= ref_pos_error(x.nidx, x.npos, c) << 5;
+#ifdef SBH_FULL_FIXEDONLY  // A/B probe (timing only, results wrong): no read-name / CIGAR tests
+  if (f) return f;
+#endif
   uint64_t cur = p + 36;
   uint32_t a = q + 36;  // window offset of cur
   if (rnl == 0) {
@@ -1190,7 +1193,11 @@ __global__ __launch_bounds__(T, 5) void k_full(const uint8_t *__restrict__ U, ui
     }
   }
   __syncthreads();
+#ifdef SBH_FULL_NOCHAIN  // A/B probe (timing only, results wrong): queued record starts not walked
+  const uint32_t ns = 0;
+#else
   const uint32_t ns = nslow < SLOWCAP ? nslow : SLOWCAP;
+#endif
   for (uint32_t i = threadIdx.x; i < ns; i += T) {
     const uint64_t p = s0 + slowq[i];
     uint64_t total;

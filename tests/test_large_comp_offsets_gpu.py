@@ -121,8 +121,10 @@ def test_split_starts_past_2g(big, loaded):
 
 
 def test_run_shard_past_2g(big, loaded):
+    """The whole per-shard path indexed from the records' first block (compressed offset past
+    2^31; from offset 0 the first record lies 2 GiB past the start, beyond maxReadSize)."""
     comp, of, r0, rec_comp = big
     sh = loaded
-    r = sh.run(0, comp.size)
+    r = sh.run(rec_comp, comp.size)
     assert r["status"] == 0 and r["count"] == N_SHORT + N_LONG
     assert r["first_vpos"] == (rec_comp << 16)
