@@ -119,6 +119,57 @@ __device__ __forceinline__ uint32_t first_bad_op(const Src &s, uint64_t q, uint3
   return lim;
 }
 
+// Bad-CIGAR-op index for the full checker over flat bytes [base, end) (base 1024-aligned):
+// ob word w holds one bit per byte of [base + 32 w, +32) -- (b & 0xf) > 8, an op code no CIGAR
+// has -- and os[r] (r = flat position mod 4) one bit per ob word that holds such a byte at a
+// position of residue r.  A record's first invalid op is the first set bit at stride 4 from its
+// CIGAR start: a scan across kilobytes of valid-looking op bytes (the packed bases of a long
+// read, whose low nibbles are all valid op codes) costs a few summary words instead of one
+// byte per op.
+struct OpIdx {
+  const uint32_t *ob;
+  const uint32_t *os;  // four arrays of nsw words, residue-major
+  uint64_t base, end;
+  uint64_t nsw;
+};
+
+// First y in [x, lim) with y = x (mod 4) and a bad op byte at y; lim if none
+// (base <= x, lim <= end).
+__device__ __forceinline__ uint64_t op_scan(const OpIdx &oi, uint64_t x, uint64_t lim) {
+  if (x >= lim) return lim;
+  const uint32_t pat = 0x11111111u << ((uint32_t)x & 3);
+  uint64_t w = (x - oi.base) >> 5;
+  uint32_t m = oi.ob[w] & pat & (~0u << ((uint32_t)(x - oi.base) & 31));
+  if (!m) {
+    const uint32_t *os = oi.os + ((uint32_t)x & 3) * oi.nsw;
+    const uint64_t gl = (lim - oi.base + 31) >> 5;  // ob words below lim
+    uint64_t g = w + 1;
+    for (;;) {
+      if (g >= gl) return lim;
+      const uint32_t sm = os[g >> 5] & (~0u << (g & 31));
+      if (sm) {
+        w = (g & ~31ull) + __builtin_ctz(sm);
+        break;
+      }
+      g = (g | 31) + 1;
+    }
+    if (w >= gl) return lim;
+    m = oi.ob[w] & pat;
+  }
+  const uint64_t y = oi.base + 32 * w + __builtin_ctz(m);
+  return y < lim ? y : lim;
+}
+
+// first_bad_op through the index when it covers the ops, else byte by byte
+__device__ __forceinline__ uint32_t first_bad_op_ix(const Src &s, const OpIdx &oi, uint64_t q, uint32_t nc,
+                                                    uint64_t bound) {
+  const uint64_t fit = bound >= q ? (bound - q) / 4 : 0;
+  const uint32_t lim = fit < (uint64_t)nc ? (uint32_t)fit : nc;
+  if (oi.ob && q >= oi.base && q + 4ull * lim <= oi.end)
+    return (uint32_t)((op_scan(oi, q, q + 4ull * lim) - q + 3) / 4);
+  return first_bad_op(s, q, nc, bound);
+}
+
 // Eager check at p: 0 false, 1 true, 2 unknown (needs bytes past an open end), 3 deferred
 // (needs flat bytes at or past `front`, which are not inflated yet: the pipelined run
 // re-checks the position once they are).
@@ -177,7 +228,7 @@ __device__ uint32_t eager_at(const Src s, uint64_t p, uint64_t total, bool open,
 
 // Full check at p: result word (see include/sparkbam.h), or FULL_UNKNOWN.
 __device__ uint32_t full_at(const Src s, uint64_t p, uint64_t total, bool open, const Ctg c,
-                            int32_t rtc) {
+                            int32_t rtc, const OpIdx oi) {
   uint64_t cur = p, start = p;
   for (int32_t n = 0;; ++n) {
     if (n == rtc) return FULL_SUCCESS | ((uint32_t)n << N_SHIFT);
@@ -216,7 +267,7 @@ __device__ uint32_t full_at(const Src s, uint64_t p, uint64_t total, bool open, 
     }
     if (!name_eof) {
       bool cig_err = false;
-      const uint32_t kb = first_bad_op(s, cur, (uint32_t)nc, total);
+      const uint32_t kb = first_bad_op_ix(s, oi, cur, (uint32_t)nc, total);
       if (kb < (uint32_t)nc) {  // past the stream end first, else an invalid op
         cig_err = true;
         if (cur + 4ull * kb + 4 > total) {
@@ -969,7 +1020,7 @@ struct Fixed {  // the 36-byte fixed part of a record (tlen unused by the checke
 // rules), FULL_PASS when it passes, FULL_SLOW when the window cannot decide it.
 __device__ __forceinline__ uint32_t full_first(const Src &s, const uint32_t *bname, const uint32_t *bop, uint64_t p,
                                                uint32_t q, const Fixed &x, uint64_t total, bool open, const Ctg &c,
-                                               int32_t rtc) {
+                                               int32_t rtc, const OpIdx &oi) {
   if (rtc == 0) return FULL_SUCCESS;
   if (p + 36 > total) return open ? FULL_UNKNOWN : 1u;
   const int32_t rnl = (int32_t)(x.bmn & 0xff), nc = (int32_t)(x.fnc & 0xffff);
@@ -1001,12 +1052,14 @@ __device__ __forceinline__ uint32_t full_first(const Src &s, const uint32_t *bna
   const uint64_t stop = (uint64_t)a + 4ull * lim;  // window offset past the ops to test
   const uint32_t hi = stop < FSN ? (uint32_t)stop : FSN;
   const uint32_t y = next_set(bop, a, hi, 0x11111111u << (a & 3));
-  bool cig_err = false;
-  if (y < hi) {
+  bool cig_err = false, beyond = false;
+  if (y >= hi && stop > hi) {  // ops past the window: the op index, else the exact path
+    if (!(oi.ob && s.s0 + a >= oi.base && s.s0 + stop <= oi.end)) return FULL_SLOW;
+    beyond = op_scan(oi, s.s0 + a, s.s0 + stop) < s.s0 + stop;
+  }
+  if (y < hi || beyond) {
     cig_err = true;
     f |= 1u << 15;
-  } else if (stop > hi) {
-    return FULL_SLOW;  // ops past the window: exact path
   } else if (lim < (uint32_t)nc) {
     if (open) return FULL_UNKNOWN;
     cig_err = true;
@@ -1042,7 +1095,7 @@ __device__ __forceinline__ Fixed fixed_at(const uint32_t *lds32, uint32_t q) {
 // Anything else -- an abnormal record, a nominal end past the stream, a record the window
 // does not hold -- returns FULL_SLOW for the exact full_at().
 __device__ uint32_t chain_full(const Src &s, const uint32_t *bname, const uint32_t *bop, uint64_t p, uint64_t total,
-                               bool open, const Ctg &c, int32_t rtc) {
+                               bool open, const Ctg &c, int32_t rtc, const OpIdx &oi) {
   uint64_t q = p;
   for (uint32_t n = 0;; ++n) {
     if ((int32_t)n == rtc) return FULL_SUCCESS | (n << N_SHIFT);
@@ -1053,7 +1106,7 @@ __device__ uint32_t chain_full(const Src &s, const uint32_t *bname, const uint32
     if (q - s.s0 + 36 + 255 + 8 > FSN) return FULL_SLOW;  // fixed fields + the longest name staged
     const uint32_t qw = (uint32_t)(q - s.s0);
     const Fixed x = fixed_at(s.lds32, qw);
-    const uint32_t r = full_first(s, bname, bop, q, qw, x, total, open, c, 1);
+    const uint32_t r = full_first(s, bname, bop, q, qw, x, total, open, c, 1, oi);
     if (r == FULL_SLOW || r == FULL_UNKNOWN) return r;
     if (r != FULL_PASS) return r | (n << N_SHIFT);
     const uint64_t nominal = q + 4 + (int64_t)x.rem;
@@ -1064,7 +1117,7 @@ __device__ uint32_t chain_full(const Src &s, const uint32_t *bname, const uint32
 }
 
 __global__ __launch_bounds__(T, 5) void k_full(const uint8_t *__restrict__ U, uint64_t u_pad, uint64_t begin,
-                                            uint64_t end, Segs sg, Ctg c, int32_t rtc, FullOut o) {
+                                            uint64_t end, Segs sg, Ctg c, int32_t rtc, FullOut o, OpIdx oi) {
 #ifndef SBH_FULL_NREP
 #define SBH_FULL_NREP 4
 #endif
@@ -1178,15 +1231,15 @@ __global__ __launch_bounds__(T, 5) void k_full(const uint8_t *__restrict__ U, ui
       uint64_t total;
       bool open;
       where(p, &total, &open);
-      const uint32_t r = full_first(s, bname, bop, p, q, x, total, open, c, rtc);
+      const uint32_t r = full_first(s, bname, bop, p, q, x, total, open, c, rtc, oi);
       if (r == FULL_SLOW || r == FULL_PASS) {  // record starts, long CIGARs: the balanced pass below
         const uint32_t qi = atomicAdd(&nslow, 1u);
         if (qi < SLOWCAP) {
           slowq[qi] = q;
           continue;
         }
-        const uint32_t rc = chain_full(s, bname, bop, p, total, open, c, rtc);
-        account(p, rc == FULL_SLOW ? full_at(s, p, total, open, c, rtc) : rc);
+        const uint32_t rc = chain_full(s, bname, bop, p, total, open, c, rtc, oi);
+        account(p, rc == FULL_SLOW ? full_at(s, p, total, open, c, rtc, oi) : rc);
         continue;
       }
       account(p, r);
@@ -1203,8 +1256,8 @@ __global__ __launch_bounds__(T, 5) void k_full(const uint8_t *__restrict__ U, ui
     uint64_t total;
     bool open;
     where(p, &total, &open);
-    const uint32_t rc = chain_full(s, bname, bop, p, total, open, c, rtc);
-    account(p, rc == FULL_SLOW ? full_at(s, p, total, open, c, rtc) : rc);
+    const uint32_t rc = chain_full(s, bname, bop, p, total, open, c, rtc, oi);
+    account(p, rc == FULL_SLOW ? full_at(s, p, total, open, c, rtc, oi) : rc);
   }
   if (mysucc) atomicAdd(&nsucc, mysucc);
   __syncthreads();
@@ -1627,6 +1680,34 @@ __global__ void k_eager_defer(const uint8_t *__restrict__ U, uint64_t begin, Seg
   }
 }
 
+// The full checker's bad-CIGAR-op index (OpIdx) over [base, base + 32 nw): a thread per
+// 32-byte group (two 16-byte loads, SWAR byte classes), the residue summaries from ballots
+// (a wave's 64 groups are two summary words per residue).
+__global__ __launch_bounds__(256) void k_op_index(const uint8_t *__restrict__ U, uint64_t u_pad, uint64_t base,
+                                                 uint64_t nw, uint32_t *__restrict__ ob, uint32_t *__restrict__ os,
+                                                 uint64_t nsw) {
+  const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  uint32_t v = 0;
+  if (w < nw) {
+    const uint64_t p = base + 32 * w;
+    const uint4 *g = reinterpret_cast<const uint4 *>(U + p);
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    const uint4 a = p + 16 <= u_pad ? g[0] : z, b = p + 32 <= u_pad ? g[1] : z;
+    v = bad_op4(a.x) | bad_op4(a.y) << 4 | bad_op4(a.z) << 8 | bad_op4(a.w) << 12 | bad_op4(b.x) << 16 |
+        bad_op4(b.y) << 20 | bad_op4(b.z) << 24 | bad_op4(b.w) << 28;
+    ob[w] = v;
+  }
+  const uint64_t w0 = w & ~63ull;  // the wave's first group
+#pragma unroll
+  for (uint32_t r = 0; r < 4; ++r) {
+    const uint64_t m = __ballot((v & (0x11111111u << r)) != 0);
+    if ((threadIdx.x & 63) == 0 && w0 < nw) {
+      os[r * nsw + w0 / 32] = (uint32_t)m;
+      if (w0 / 32 + 1 < nsw) os[r * nsw + w0 / 32 + 1] = (uint32_t)(m >> 32);
+    }
+  }
+}
+
 }  // namespace
 
 static inline uint32_t ngrid(uint64_t n, uint32_t t) { return (uint32_t)((n + t - 1) / t); }
@@ -1666,10 +1747,31 @@ hipError_t launch_eager_defer(const uint8_t *U, uint64_t begin, const uint64_t *
 hipError_t launch_full(const uint8_t *U, uint64_t u_pad, uint64_t begin, uint64_t end, const uint64_t *seg_end,
                        uint32_t nseg, uint32_t open_last, const int32_t *ctg, int32_t nctg, int32_t rtc,
                        uint32_t *words, unsigned long long *counters /* [2+21*19+21*64+2] */,
-                       uint64_t *close_pos, uint32_t *close_word, uint64_t close_cap, hipStream_t st) {
+                       uint64_t *close_pos, uint32_t *close_word, uint64_t close_cap, uint32_t *op_words,
+                       uint64_t op_cap_words, hipStream_t st) {
   if (end <= begin) return hipSuccess;
   Segs sg{seg_end, nseg, open_last};
   Ctg c{ctg, nctg};
+  // the op index over [begin rounded down to 1 KiB, the last byte a CIGAR of a position
+  // before `end` can reach), clipped to the resident bytes and to op_cap_words
+  OpIdx oi{nullptr, nullptr, 0, 0, 0};
+#ifdef SBH_FULL_NOOPIX  // A/B: every CIGAR past the staged window takes the exact path
+  op_words = nullptr;
+#endif
+  if (op_words) {
+    const uint64_t base = begin & ~1023ull;
+    uint64_t top = end + 36 + 255 + 4ull * 65535 + 4;
+    const uint64_t u_total = u_pad;  // (bytes past the stream are padding: never bad ops)
+    if (top > u_total) top = u_total;
+    uint64_t nw = (top - base + 31) / 32;
+    nw = (nw + 63) & ~63ull;
+    const uint64_t nsw = nw / 32;
+    if (nw + 4 * nsw <= op_cap_words) {
+      uint32_t *ob = op_words, *os = op_words + nw;
+      hipLaunchKernelGGL(k_op_index, dim3(ngrid(nw, 256)), dim3(256), 0, st, U, u_pad, base, nw, ob, os, nsw);
+      oi = OpIdx{ob, os, base, base + 32 * nw, nsw};
+    }
+  }
   FullOut o;
   o.words = words;
   o.n_success = counters + 0;
@@ -1682,7 +1784,7 @@ hipError_t launch_full(const uint8_t *U, uint64_t u_pad, uint64_t begin, uint64_
   o.close_word = close_word;
   o.close_cap = close_cap;
   hipLaunchKernelGGL(k_full, dim3(ngrid(end - (begin & ~15ull), FTILE)), dim3(T), 0, st, U, u_pad, begin, end, sg, c, rtc,
-                     o);
+                     o, oi);
   return hipGetLastError();
 }
 

@@ -19,6 +19,33 @@ constexpr uint32_t CRC_SEG = 1024;  // bytes per lane
 constexpr uint32_t CRC_POW = 17;    // T_{2^j}, j < 17 (a block holds at most 65536 bytes)
 constexpr uint32_t CRC_T = 256;
 
+// The slicing-by-8 tables (tab[k][b]: the register after byte b, then k zero bytes) and the
+// shift matrices P[j] = T_{2^j}, computed at compile time; each workgroup copies them to LDS.
+struct CrcTabs {
+  uint32_t tab[8][256];
+  uint32_t P[CRC_POW][32];
+};
+constexpr CrcTabs make_crc_tabs() {
+  CrcTabs z{};
+  for (uint32_t n = 0; n < 256; ++n) {
+    uint32_t c = n;
+    for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+    z.tab[0][n] = c;
+  }
+  for (uint32_t k = 1; k < 8; ++k)
+    for (uint32_t n = 0; n < 256; ++n) z.tab[k][n] = z.tab[0][z.tab[k - 1][n] & 0xff] ^ (z.tab[k - 1][n] >> 8);
+  for (uint32_t j = 0; j < 32; ++j) z.P[0][j] = z.tab[0][(1u << j) & 0xff] ^ ((1u << j) >> 8);  // one zero byte
+  for (uint32_t l = 1; l < CRC_POW; ++l)  // T_{2L} = T_L o T_L
+    for (uint32_t j = 0; j < 32; ++j) {
+      uint32_t r = 0;
+      for (uint32_t i = 0; i < 32; ++i)
+        if ((z.P[l - 1][j] >> i) & 1u) r ^= z.P[l - 1][i];
+      z.P[l][j] = r;
+    }
+  return z;
+}
+__device__ const CrcTabs kCrcTabs = make_crc_tabs();
+
 // s -> T(s) for the matrix whose column j (the image of state bit j) is M[j]
 __device__ __forceinline__ uint32_t gf2_apply(const uint32_t *M, uint32_t s) {
   uint32_t r = 0;
@@ -37,26 +64,12 @@ __device__ __forceinline__ uint32_t gf2_shift(const uint32_t (*P)[32], uint32_t 
 __global__ __launch_bounds__(CRC_T) void k_block_crc(const uint8_t *__restrict__ comp, DevBlocks bl, uint64_t nblocks,
                                                      const uint8_t *__restrict__ U, unsigned long long *n_bad,
                                                      unsigned long long *first_bad) {
-  __shared__ uint32_t tab[8][256];   // slicing-by-8: tab[k][b] = the register after byte b, then k zero bytes
+  __shared__ uint32_t tab[8][256];
   __shared__ uint32_t P[CRC_POW][32];  // P[j] = T_{2^j} (columns)
   const uint32_t t = threadIdx.x, lane = t & (WAVE - 1);
-  {
-    uint32_t c = t;
-    for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
-    tab[0][t] = c;  // blockDim.x == 256
-  }
+  for (uint32_t i = t; i < 8 * 256; i += CRC_T) (&tab[0][0])[i] = (&kCrcTabs.tab[0][0])[i];
+  for (uint32_t i = t; i < CRC_POW * 32; i += CRC_T) (&P[0][0])[i] = (&kCrcTabs.P[0][0])[i];
   __syncthreads();
-  for (uint32_t k = 1; k < 8; ++k) {
-    const uint32_t p = tab[k - 1][t];
-    tab[k][t] = tab[0][p & 0xff] ^ (p >> 8);
-    __syncthreads();
-  }
-  if (t < 32) P[0][t] = tab[0][(1u << t) & 0xff] ^ ((1u << t) >> 8);  // one zero byte
-  __syncthreads();
-  for (uint32_t j = 1; j < CRC_POW; ++j) {  // T_{2L} = T_L o T_L
-    if (t < 32) P[j][t] = gf2_apply(P[j - 1], P[j - 1][t]);
-    __syncthreads();
-  }
   const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / WAVE);
   for (uint64_t b = (uint64_t)blockIdx.x * (blockDim.x / WAVE) + t / WAVE; b < nblocks; b += nw) {
     if (bl.flags[b] & BLK_TRUNCATED) continue;

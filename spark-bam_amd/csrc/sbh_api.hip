@@ -44,7 +44,7 @@ hipError_t launch_eager_defer(const uint8_t *U, uint64_t begin, const uint64_t *
 hipError_t launch_full(const uint8_t *U, uint64_t u_pad, uint64_t begin, uint64_t end, const uint64_t *seg_end,
                        uint32_t nseg, uint32_t open_last, const int32_t *ctg, int32_t nctg, int32_t rtc,
                        uint32_t *words, unsigned long long *counters, uint64_t *close_pos, uint32_t *close_word,
-                       uint64_t close_cap, hipStream_t st);
+                       uint64_t close_cap, uint32_t *op_words, uint64_t op_cap_words, hipStream_t st);
 hipError_t launch_first_set(const uint32_t *bits, uint64_t begin, uint64_t from, uint64_t to,
                             unsigned long long *best, hipStream_t st);
 hipError_t launch_verify_chain_count(const uint8_t *U, const uint32_t *bits, uint64_t begin, uint64_t bits_end,
@@ -137,6 +137,7 @@ struct sbh_shard {
   uint64_t bits_begin = 0, bits_end = 0;
   int32_t bits_rtc = 0;
   DBuf<uint32_t> words;
+  DBuf<uint32_t> opix;  // the full checker's bad-CIGAR-op index (launch_full)
   DBuf<uint64_t> close_pos;
   DBuf<uint32_t> close_word;
   DBuf<unsigned long long> ctr;  // scratch counters
@@ -359,7 +360,7 @@ int sbh_shard_destroy(sbh_shard *sh) {
   sh->counts.release(); sh->cfirst.release(); sh->offs.release(); sh->cand.release(); sh->v.release(); sh->rank.release();
   sh->tmp.release(); sh->J0.release(); sh->J1.release(); sh->on.release(); sh->d_seg.release();
   sh->U.release(); sh->ctg.release(); sh->bits.release(); sh->words.release(); sh->close_pos.release();
-  sh->close_word.release(); sh->ctr.release();
+  sh->close_word.release(); sh->ctr.release(); sh->opix.release();
   for (hipEvent_t &e : sh->ev)
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t &e : sh->pev)
@@ -837,9 +838,15 @@ int sbh_check_full(sbh_shard *sh, uint64_t begin, uint64_t end, int32_t rtc, uin
   const uint64_t cap = close_cap;
   HIPCHK(ctx, sh->close_pos.ensure(cap + 1));
   HIPCHK(ctx, sh->close_word.ensure(cap + 1));
-  HIPCHK(ctx, launch_full(sh->U.p, sh->utotal + sh->pad, begin, end, sh->d_seg.p, (uint32_t)sh->seg_end.size(),
+  // the op index launch_full builds: one bit per byte from begin (1 KiB-aligned) to the
+  // farthest CIGAR byte a position before `end` can name, plus four residue summaries
+  const uint64_t u_pad = sh->utotal + sh->pad, ob0 = begin & ~1023ull;
+  const uint64_t ob_top = std::min<uint64_t>(end + 36 + 255 + 4ull * 65535 + 4, u_pad);
+  const uint64_t ob_nw = (((ob_top - ob0 + 31) / 32) + 63) & ~63ull;
+  HIPCHK(ctx, sh->opix.ensure(ob_nw + ob_nw / 8));
+  HIPCHK(ctx, launch_full(sh->U.p, u_pad, begin, end, sh->d_seg.p, (uint32_t)sh->seg_end.size(),
                           sh->open_last ? 1 : 0, sh->ctg.p, sh->nctg, rtc, words, c, sh->close_pos.p,
-                          sh->close_word.p, cap, st));
+                          sh->close_word.p, cap, sh->opix.p, sh->opix.cap, st));
   HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr, c, nctr * 8, hipMemcpyDeviceToHost, st));
   HIPCHK(ctx, hipStreamSynchronize(st));
   if (sh->h_ctr[1])

@@ -16,11 +16,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--records", type=int, default=2_000_000)
     ap.add_argument("--rtc", default="10,1")
+    ap.add_argument("--config", default="B", choices=["B", "D", "E"])
     a = ap.parse_args()
     import synth
     from __graft_entry__ import load_package
     sb = load_package()
-    p = synth.params(synth.SEEDS["B"])
+    seed, shape, level = {"B": (0x5B4D0001, 0, 6), "D": (0x5B4D004C, 1, 6), "E": (0x5B4D00AD, 2, -1)}[a.config]
+    p = synth.params(seed, shape=shape, level=level)
     data, usize, nb = synth.make_bam(p, a.records)
     with sb.Context(0) as ctx:
         sh = ctx.shard(data)
@@ -35,7 +37,7 @@ def main():
                 r = sh.check_full(0, sh.flat_size, reads_to_check=rtc, close_cap=1 << 10)
                 dt = time.perf_counter() - t0
                 best = dt if best is None else min(best, dt)
-            print(f"{os.path.basename(os.environ.get('SBH_LIB_PATH', 'main'))} rtc {rtc}: {best * 1e3:.2f} ms for "
+            print(f"{os.path.basename(os.environ.get('SBH_LIB_PATH', '') or 'in-tree')} config {a.config} rtc {rtc}: {best * 1e3:.2f} ms for "
                   f"{sh.flat_size} positions ({sh.flat_size / best / 1e9:.1f} GB/s), success {r['n_success']}",
                   flush=True)
 
