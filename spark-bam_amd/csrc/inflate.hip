@@ -961,6 +961,9 @@ static_assert(HDR_SENT % SBH_HT == 0, "k_huff copies the tables in whole rounds"
 #ifndef SBH_CK3
 #define SBH_CK3 64
 #endif
+#ifndef SBH_MARGIN
+#define SBH_MARGIN 256  // pass-1 warm-up bits before each slice (0: none)
+#endif
 constexpr uint32_t CK1 = SBH_CK1, CK2 = SBH_CK2;  // pass-1 checkpoints (tokens)
 constexpr uint32_t CK3 = SBH_CK3;                 // a third, for chains that sync late (0: none)
 constexpr uint32_t LR_RUN = 0, LR_EOB = 1, LR_DEAD = 2, LR_PAST = 3;
@@ -1322,6 +1325,18 @@ __device__ __forceinline__ bool inflate_par(HuffSmem &sm, const uint8_t *__restr
     uint32_t A = s, nobad = 0;
     Ckpt ck;
     const LaneRun none{};
+#if SBH_MARGIN
+    // warm-up: decode from SBH_MARGIN bits before the slice, so that by the slice start the
+    // chain has (very likely) fallen onto the true token boundaries; the speculative start is
+    // then the first boundary at or past the slice start -- usually exactly where the left
+    // neighbour's chain exits, so the first repair round has nothing to redo for that lane
+    if (tid) {
+      Ckpt nock{NOPOS, 0, NOPOS, 0, NOPOS, 0};
+      const uint32_t w0 = s - p0 > SBH_MARGIN ? s - SBH_MARGIN : p0;
+      const LaneRun rw = lane_run<LDS, RUN_REDO>(sm.t, src, w0, s, limit, nock, none, nullptr, 0, nobad);
+      if (rw.st == LR_RUN && rw.exit < stop) A = rw.exit;
+    }
+#endif
     LaneRun r = lane_run<LDS, RUN_SPEC>(sm.t, src, A, stop, limit, ck, none, nullptr, 0, nobad);
     const LaneRun r1 = r;  // the pass-1 chain's result: a redo that joins it at a checkpoint takes its rest
     sm.exitv[tid] = r.st == LR_RUN ? r.exit : NOPOS;
