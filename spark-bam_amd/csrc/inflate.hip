@@ -962,7 +962,7 @@ static_assert(HDR_SENT % SBH_HT == 0, "k_huff copies the tables in whole rounds"
 #define SBH_CK3 64
 #endif
 #ifndef SBH_MARGIN
-#define SBH_MARGIN 256  // pass-1 warm-up bits before each slice (0: none)
+#define SBH_MARGIN 0  // pass-1 warm-up bits before each slice (A/B: 128-384 bits measured neutral)
 #endif
 constexpr uint32_t CK1 = SBH_CK1, CK2 = SBH_CK2;  // pass-1 checkpoints (tokens)
 constexpr uint32_t CK3 = SBH_CK3;                 // a third, for chains that sync late (0: none)

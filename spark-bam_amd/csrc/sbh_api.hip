@@ -2024,7 +2024,9 @@ int sbh_bgzf_compress_level(sbh_ctx *ctx, const void *src, uint64_t n, int src_o
   float kms = 0.f;
   if (nb) {
     // members in batches: scratch bounded by the batch, not the input
-    const uint64_t bmax = fast ? DEFLATE_BATCH : ZDEFLATE_BATCH;
+    uint64_t bmax = fast ? DEFLATE_BATCH : ZDEFLATE_BATCH;
+    if (const char *e = std::getenv("SBH_ZDEFLATE_BATCH"))
+      if (!fast && std::strtoull(e, nullptr, 10) > 0) bmax = std::strtoull(e, nullptr, 10);
     const uint64_t cap = nb < bmax ? nb : bmax;
     const uint64_t stride = fast ? 65536ull : ZDEFLATE_SLOT;
     HIPCHK(ctx, B.slots.ensure(cap * stride));

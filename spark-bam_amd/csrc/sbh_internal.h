@@ -142,9 +142,12 @@ hipError_t launch_deflate_gather(const uint8_t *slots, uint64_t stride, const ui
                                  uint64_t nblocks, uint8_t *out, hipStream_t st);
 
 // Byte-exact BGZF writer (zdeflate.hip; zlib 1.2.11 deflate_slow at level 4..9, htsjdk's 5 by
-// default): members in batches of at most ZDEFLATE_BATCH, per member prev[] (u16), match
-// records (u64), tokens (u32), a record of blocks / trees / headers, and an output slot.
-constexpr uint32_t ZDEFLATE_BATCH = 2048;
+// default): members in batches of at most ZDEFLATE_BATCH (env SBH_ZDEFLATE_BATCH overrides),
+// per member prev[] (u16), match records (u64), tokens (u32), a record of blocks / trees /
+// headers, and an output slot: ~1 MB of scratch per member, 8 GB at 8192 members.  The batch
+// is large because k_zparse runs one serial wave per member: 8192 members keep 8 of them per
+// SIMD in flight.
+constexpr uint32_t ZDEFLATE_BATCH = 8192;
 constexpr uint64_t ZDEFLATE_PREV_ENTRIES = 65536;
 constexpr uint64_t ZDEFLATE_INFO_ENTRIES = 65536;
 constexpr uint64_t ZDEFLATE_TOK_ENTRIES = 65536;

@@ -95,9 +95,11 @@ def test_synthetic_bam_streams(ctx):
         assert got.tobytes() == htsjdk_bgzf(flat.tobytes()), seed
 
 
-def test_batches_of_members(ctx):
-    """More members than one batch (2048): each member equals htsjdk's for its own piece; the
-    input sits on the device (an inflated shard's flat bytes go in this way)."""
+def test_batches_of_members(ctx, monkeypatch):
+    """More members than one batch (here 2048, SBH_ZDEFLATE_BATCH): each member equals htsjdk's
+    for its own piece; the input sits on the device (an inflated shard's flat bytes go in this
+    way)."""
+    monkeypatch.setenv("SBH_ZDEFLATE_BATCH", "2048")
     nb = 2048 + 3
     n = (nb - 1) * PAYLOAD + 777
     rng = np.random.default_rng(11)
