@@ -961,6 +961,9 @@ static_assert(HDR_SENT % SBH_HT == 0, "k_huff copies the tables in whole rounds"
 #ifndef SBH_CK3
 #define SBH_CK3 64
 #endif
+#ifndef SBH_NX_PRED
+#define SBH_NX_PRED 1  // stream dword reloads only in lanes that crossed a dword (A/B: 0 = every code)
+#endif
 #ifndef SBH_MARGIN
 #define SBH_MARGIN 0  // pass-1 warm-up bits before each slice (A/B: 128-384 bits measured neutral)
 #endif
@@ -1050,13 +1053,18 @@ __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, Src<LDS> src, uin
   // The decode state is the bit position and the two stream dwords under it (lo, hi):
   // a code's 32 bits come from them with one v_alignbit, enough for any code plus its
   // extra bits (<= 28), and the extra bits come out with one v_bfe.  A code consumes
-  // < 32 bits, so the window moves by at most one dword per code; the dword after it is
-  // loaded at the top of every iteration, beside the table lookup, so each code costs
-  // one LDS round trip on the dependent chain, not two.  One loop exit, at the end of
-  // the body; everything else is selects (apart from the rare long code).
+  // < 32 bits, so the window moves by at most one dword per code; the dword after it (nx)
+  // is already in a register when the window moves, and only the lanes that moved reload
+  // the next one, so each code costs one LDS round trip on the dependent chain and the
+  // LDS pipe serves one table lookup per code plus one stream dword per ~32 bits.  One
+  // loop exit, at the end of the body; everything else is selects (apart from the rare
+  // long code).
   const uint32_t stop2 = stop < limit ? stop : limit;
   uint32_t pos = A;
   uint32_t wi = pos >> 5, lo = src(wi), hi = src(wi + 1);
+#if SBH_NX_PRED
+  uint32_t nx = src(wi + 2);
+#endif
   uint32_t ml = 0;  // pending match length: the next code is a distance
   uint32_t ntok = 0, nout = 0;
   uint32_t c1p = NOPOS, c1o = 0, c2p = NOPOS, c2o = 0, c3p = NOPOS, c3o = 0;
@@ -1065,7 +1073,9 @@ __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, Src<LDS> src, uin
   bool cut;
   for (;;) {
     const uint32_t bits = __builtin_amdgcn_alignbit(hi, lo, pos & 31);
+#if !SBH_NX_PRED
     const uint32_t nx = src(wi + 2);
+#endif
     const bool atb = ml == 0;  // token boundary
     e = t.tab[(bits & ((1u << LIT_FAST) - 1)) | (atb ? 0u : 1u << LIT_FAST)];
     if (e & PE_SLOW) e = slow_lane(t, bits, !atb);
@@ -1093,6 +1103,11 @@ __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, Src<LDS> src, uin
     lo = adv ? hi : lo;
     hi = adv ? nx : hi;
     wi += adv ? 1u : 0u;
+#if SBH_NX_PRED
+    // only a lane that moved into the next dword refills (one code in four or five): its load
+    // is in flight during the next code's table lookup, which LDS returns after it
+    if (adv) nx = src(wi + 2);
+#endif
     const bool is_tok = (e & PE_LEN) == 0;  // a literal, or the distance completing a match
     if (MODE == RUN_EMIT) {
       if (is_tok) dst[ntok] = atb ? val << 8 : TOK_MATCH | (ml << 16) | val;
