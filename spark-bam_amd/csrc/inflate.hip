@@ -962,7 +962,7 @@ static_assert(HDR_SENT % SBH_HT == 0, "k_huff copies the tables in whole rounds"
 #define SBH_CK3 64
 #endif
 #ifndef SBH_NX_PRED
-#define SBH_NX_PRED 1  // stream dword reloads only in lanes that crossed a dword (A/B: 0 = every code)
+#define SBH_NX_PRED 0  // 1: stream dword reloads only in lanes that crossed a dword (A/B: 6% slower)
 #endif
 #ifndef SBH_MARGIN
 #define SBH_MARGIN 0  // pass-1 warm-up bits before each slice (A/B: 128-384 bits measured neutral)
@@ -1053,11 +1053,11 @@ __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, Src<LDS> src, uin
   // The decode state is the bit position and the two stream dwords under it (lo, hi):
   // a code's 32 bits come from them with one v_alignbit, enough for any code plus its
   // extra bits (<= 28), and the extra bits come out with one v_bfe.  A code consumes
-  // < 32 bits, so the window moves by at most one dword per code; the dword after it (nx)
-  // is already in a register when the window moves, and only the lanes that moved reload
-  // the next one, so each code costs one LDS round trip on the dependent chain and the
-  // LDS pipe serves one table lookup per code plus one stream dword per ~32 bits.  One
-  // loop exit, at the end of the body; everything else is selects (apart from the rare
+  // < 32 bits, so the window moves by at most one dword per code; the dword after it is
+  // loaded at the top of every iteration, beside the table lookup, so each code costs
+  // one LDS round trip on the dependent chain, not two (SBH_NX_PRED=1 instead reloads it
+  // only in the lanes that moved: fewer LDS reads, but the branch made k_huff 6% slower).
+  // One loop exit, at the end of the body; everything else is selects (apart from the rare
   // long code).
   const uint32_t stop2 = stop < limit ? stop : limit;
   uint32_t pos = A;
