@@ -970,26 +970,33 @@ static_assert(HDR_SENT % SBH_HT == 0, "k_huff copies the tables in whole rounds"
 constexpr uint32_t CK1 = SBH_CK1, CK2 = SBH_CK2;  // pass-1 checkpoints (tokens)
 constexpr uint32_t CK3 = SBH_CK3;                 // a third, for chains that sync late (0: none)
 constexpr uint32_t LR_RUN = 0, LR_EOB = 1, LR_DEAD = 2, LR_PAST = 3;
+#ifndef SBH_TAIL
+#define SBH_TAIL 1  // short final deflate blocks left to k_huff_tail (0: k_huff decodes them)
+#endif
+constexpr uint32_t INF_TAIL = 0xfeu;  // (inside inflate only) k_huff_tail finishes the block
 #ifdef SBH_HUFF_PROBE
 // whole-kernel phase sums (cycles): 0 stage, 1 header, 2 pass 1, 3 repair, 4 emit, 5 repair
 // rounds, 6 deflate blocks, 7 whole block, 8-10 header: CL table / walk / tables, 11 tokens
 __device__ unsigned long long hp_acc[16];
 __device__ unsigned int hp_done;
 #endif
-struct HuffSmem {
-  WaveSmem t;                    // tables (built by wave 0; the serial fallback's too)
-  uint32_t stage[STAGE_DW + 8];  // the block's deflate dwords, from dword a0
-  uint32_t exitv[HT];            // lane exits (NOPOS: the chain ended in the lane)
-  uint32_t wsum[HT / WAVE];
+template <uint32_t NT_, uint32_t SDW_>
+struct HuffSmemT {
+  static constexpr uint32_t NT = NT_, SDW = SDW_;
+  WaveSmem t;               // tables (built by wave 0; the serial fallback's too)
+  uint32_t stage[SDW + 8];  // the block's deflate dwords, from dword a0
+  uint32_t exitv[NT];       // lane exits (NOPOS: the chain ended in the lane)
+  uint32_t wsum[NT / WAVE];
   uint32_t ctl[8];
 };
+using HuffSmem = HuffSmemT<HT, STAGE_DW>;
 
 // Bit source of a lane: the LDS stage or (blocks too large to stage) global memory.
-template <bool LDS>
+template <bool LDS, uint32_t SDW = STAGE_DW>
 struct Src {
   const uint32_t *p;
   __device__ __forceinline__ uint32_t operator()(uint32_t i) const {
-    if (LDS) return p[i < STAGE_DW + 7 ? i : STAGE_DW + 7];
+    if (LDS) return p[i < SDW + 7 ? i : SDW + 7];
     return p[i];
   }
   // 32 stream bits starting at bit position `pos`
@@ -1046,8 +1053,8 @@ constexpr int RUN_SPEC = 0, RUN_REDO = 1, RUN_EMIT = 2;
 //   RUN_REDO: stop early on reaching one of ck's boundaries (sp: that chain's result).
 //   RUN_EMIT: store tokens at dst, flag a distance reaching before the block's first
 //             byte (out0: bytes before A).
-template <bool LDS, int MODE>
-__device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, Src<LDS> src, uint32_t A, uint32_t stop,
+template <int MODE, class S>
+__device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, S src, uint32_t A, uint32_t stop,
                                             uint32_t limit, Ckpt &ck, const LaneRun &sp,
                                             uint32_t *__restrict__ dst, uint32_t out0, uint32_t &bad) {
   // The decode state is the bit position and the two stream dwords under it (lo, hi):
@@ -1217,8 +1224,9 @@ __device__ __forceinline__ bool hdr_walk(SM &t, const S &src, uint32_t p, uint32
   return ok;
 }
 
-// Both PAR decode tables from ptable_meta's limits (pk) and order (sent), by the HT
+// Both PAR decode tables from ptable_meta's limits (pk) and order (sent), by the NT
 // threads of a k_huff workgroup.
+template <uint32_t NT>
 __device__ __forceinline__ void fill_ptables(WaveSmem &t, uint32_t tid) {
   uint32_t lj0[16], lj1[16];
 #pragma unroll
@@ -1226,10 +1234,10 @@ __device__ __forceinline__ void fill_ptables(WaveSmem &t, uint32_t tid) {
     lj0[v] = t.pk[0][v] >> 16;
     lj1[v] = t.pk[1][v] >> 16;
   }
-#pragma unroll
-  for (uint32_t i = tid; i < (1u << LIT_FAST); i += HT) t.lit[i] = ptable_entry(t, lj0, 0, LIT_FAST, i);
-#pragma unroll
-  for (uint32_t i = tid; i < (1u << PDIST_FAST); i += HT) t.dist[i] = ptable_entry(t, lj1, 1, PDIST_FAST, i);
+#pragma unroll 4
+  for (uint32_t i = tid; i < (1u << LIT_FAST); i += NT) t.lit[i] = ptable_entry(t, lj0, 0, LIT_FAST, i);
+#pragma unroll 4
+  for (uint32_t i = tid; i < (1u << PDIST_FAST); i += NT) t.dist[i] = ptable_entry(t, lj1, 1, PDIST_FAST, i);
 }
 
 // Deflate block header and tables for the lane-parallel path, read from the bit source
@@ -1240,12 +1248,13 @@ __device__ __forceinline__ void fill_ptables(WaveSmem &t, uint32_t tid) {
 // wave 1 the distance table, concurrently.  Returns false (uniformly) for anything
 // the serial decoder must judge: stored/invalid block types, invalid or incomplete
 // codes, a header running past the input.
-template <bool LDS>
-__device__ __forceinline__ bool par_header(HuffSmem &sm, Src<LDS> src, uint32_t p, uint32_t limit, bool &fixed_built,
+template <class SM, class S>
+__device__ __forceinline__ bool par_header(SM &sm, S src, uint32_t p, uint32_t limit, bool &fixed_built,
                                            uint32_t wid, uint32_t lane, uint32_t &psym, uint32_t &last) {
+  constexpr uint32_t NT = SM::NT;
   WaveSmem &t = sm.t;
   // both decode tables from ptable_meta's limits and order, filled by the whole workgroup
-  auto fill_tables = [&]() { fill_ptables(t, wid * WAVE + lane); };
+  auto fill_tables = [&]() { fill_ptables<NT>(t, wid * WAVE + lane); };
   const uint32_t hb = uni(src.bits32(p));
   last = hb & 1;
   const uint32_t type = (hb >> 1) & 3;
@@ -1257,7 +1266,8 @@ __device__ __forceinline__ bool par_header(HuffSmem &sm, Src<LDS> src, uint32_t 
         for (uint32_t s = lane; s < 288; s += WAVE) t.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
         __builtin_amdgcn_wave_barrier();
         ptable_meta(t, t.lens, 288, 0, lane);
-      } else if (wid == 1) {
+      }
+      if (wid == (NT > WAVE ? 1u : 0u)) {  // (one wave: it builds both)
         if (lane < 32) t.lens[288 + lane] = 5;
         __builtin_amdgcn_wave_barrier();
         ptable_meta(t, t.lens + 288, 32, 1, lane);
@@ -1291,10 +1301,10 @@ __device__ __forceinline__ bool par_header(HuffSmem &sm, Src<LDS> src, uint32_t 
   __syncthreads();
   if (!uni(sm.ctl[5])) return false;
   psym = uni(sm.ctl[6]);
-  uint32_t rc = 0;
-  if (wid == 0) rc = ptable_meta(t, t.lens, nlen, 0, lane);
-  else if (wid == 1) rc = ptable_meta(t, t.lens + 288, ndist, 1, lane);
-  if (__syncthreads_or(rc == 1)) return false;
+  bool bad = false;
+  if (wid == 0) bad = ptable_meta(t, t.lens, nlen, 0, lane) == 1;
+  if (wid == (NT > WAVE ? 1u : 0u)) bad = bad || ptable_meta(t, t.lens + 288, ndist, 1, lane) == 1;
+  if (__syncthreads_or(bad)) return false;
   fill_tables();
   __syncthreads();
 #ifdef SBH_HUFF_PROBE
@@ -1307,13 +1317,22 @@ __device__ __forceinline__ bool par_header(HuffSmem &sm, Src<LDS> src, uint32_t 
   return true;
 }
 
-// The deflate blocks of one BGZF block, lane-parallel.  Returns false (uniformly) when
-// the block must be decoded by the serial path instead.
-template <bool LDS>
-__device__ __forceinline__ bool inflate_par(HuffSmem &sm, const uint8_t *__restrict__ dbase, uint32_t skip,
+// The deflate blocks of one BGZF block (from bit `skip` of dbase's dwords), lane-parallel
+// over SM::NT lanes.  Returns (uniformly) PAR_OK, PAR_FAIL when the block must be decoded
+// by the serial path instead, or -- with `tail_ok` -- PAR_TAIL after a non-final deflate
+// block when the bits left are few (< a quarter of the block's): *tail_p / *tail_out get
+// the next block's first bit and the bytes produced, and k_huff_tail finishes the block
+// with one wave, instead of this workgroup decoding a short final block (zlib's level-6
+// BGZF member: 16383 symbols, then ~1 k) with most of its lanes idle.  `out_before`:
+// bytes of the BGZF block before this call (for the too-far-back distance check).
+constexpr uint32_t PAR_OK = 0, PAR_FAIL = 1, PAR_TAIL = 2;
+template <bool LDS, class SM>
+__device__ __forceinline__ uint32_t inflate_par(SM &sm, const uint8_t *__restrict__ dbase, uint32_t skip,
                             uint32_t limit, uint32_t usize, uint32_t *__restrict__ tk, uint32_t tid, uint32_t lane,
-                            uint32_t wid, uint32_t &ntok_out, bool pre, uint32_t pre_psym, uint32_t pre_last) {
-  const Src<LDS> src{LDS ? sm.stage : reinterpret_cast<const uint32_t *>(dbase)};
+                            uint32_t wid, uint32_t &ntok_out, bool pre, uint32_t pre_psym, uint32_t pre_last,
+                            uint32_t out_before, bool tail_ok, uint32_t *tail_p, uint32_t *tail_out) {
+  constexpr uint32_t NT = SM::NT;
+  const Src<LDS, SM::SDW> src{LDS ? sm.stage : reinterpret_cast<const uint32_t *>(dbase)};
   uint32_t p = skip, out = 0, ntok = 0;
   bool fixed_built = false;  // the tables in sm.t are the fixed code's
   for (;;) {
@@ -1326,15 +1345,15 @@ __device__ __forceinline__ bool inflate_par(HuffSmem &sm, const uint8_t *__restr
       last = pre_last;
       pre = false;
     } else if (!par_header(sm, src, p, limit, fixed_built, wid, lane, p0, last)) {
-      return false;
+      return PAR_FAIL;
     }
-    if (tid == 0) sm.ctl[3] = HT;
+    if (tid == 0) sm.ctl[3] = NT;
 
 #ifdef SBH_HUFF_PROBE
     const uint64_t tph = __builtin_readcyclecounter();
 #endif
     // pass 1: speculative decode of every lane's slice
-    uint32_t S = (limit > p0 ? limit - p0 : 0) / HT + 1;
+    uint32_t S = (limit > p0 ? limit - p0 : 0) / NT + 1;
     if (S < MIN_SLICE) S = MIN_SLICE;  // short streams: fewer, longer slices (sync needs bits)
     const uint32_t s = p0 + tid * S, stop = s + S;
     uint32_t A = s, nobad = 0;
@@ -1348,11 +1367,11 @@ __device__ __forceinline__ bool inflate_par(HuffSmem &sm, const uint8_t *__restr
     if (tid) {
       Ckpt nock{NOPOS, 0, NOPOS, 0, NOPOS, 0};
       const uint32_t w0 = s - p0 > SBH_MARGIN ? s - SBH_MARGIN : p0;
-      const LaneRun rw = lane_run<LDS, RUN_REDO>(sm.t, src, w0, s, limit, nock, none, nullptr, 0, nobad);
+      const LaneRun rw = lane_run<RUN_REDO>(sm.t, src, w0, s, limit, nock, none, nullptr, 0, nobad);
       if (rw.st == LR_RUN && rw.exit < stop) A = rw.exit;
     }
 #endif
-    LaneRun r = lane_run<LDS, RUN_SPEC>(sm.t, src, A, stop, limit, ck, none, nullptr, 0, nobad);
+    LaneRun r = lane_run<RUN_SPEC>(sm.t, src, A, stop, limit, ck, none, nullptr, 0, nobad);
     const LaneRun r1 = r;  // the pass-1 chain's result: a redo that joins it at a checkpoint takes its rest
     sm.exitv[tid] = r.st == LR_RUN ? r.exit : NOPOS;
     // pass 2: repair rounds until every lane starts where its left neighbour exits.
@@ -1375,7 +1394,7 @@ __device__ __forceinline__ bool inflate_par(HuffSmem &sm, const uint8_t *__restr
       __syncthreads();
       if (changed) {
         A = nA;
-        r = lane_run<LDS, RUN_REDO>(sm.t, src, A, stop, limit, ck, r1, nullptr, 0, nobad);
+        r = lane_run<RUN_REDO>(sm.t, src, A, stop, limit, ck, r1, nullptr, 0, nobad);
         sm.exitv[tid] = r.st == LR_RUN ? r.exit : NOPOS;
       }
       const bool again = __syncthreads_or(changed);
@@ -1391,9 +1410,9 @@ __device__ __forceinline__ bool inflate_par(HuffSmem &sm, const uint8_t *__restr
     const uint32_t k = uni(sm.ctl[3]);
     if (tid == k) sm.ctl[4] = (r.st == LR_EOB && r.exit <= limit) ? r.exit : NOPOS;
     uint32_t ttot, otot;
-    const uint32_t tpre = block_scan<HT>(tid <= k ? r.ntok : 0, sm.wsum, &ttot);  // (syncs: ctl[4] visible)
+    const uint32_t tpre = block_scan<NT>(tid <= k ? r.ntok : 0, sm.wsum, &ttot);  // (syncs: ctl[4] visible)
     __syncthreads();
-    const uint32_t opre = block_scan<HT>(tid <= k ? r.nout : 0, sm.wsum, &otot);
+    const uint32_t opre = block_scan<NT>(tid <= k ? r.nout : 0, sm.wsum, &otot);
     const uint32_t eob_end = uni(sm.ctl[4]);
     ttot = uni(ttot);
     otot = uni(otot);
@@ -1408,22 +1427,35 @@ __device__ __forceinline__ bool inflate_par(HuffSmem &sm, const uint8_t *__restr
       atomicAdd(&hp_acc[11], (unsigned long long)ttot);
     }
 #endif
-    if (k >= HT || eob_end == NOPOS || otot > usize - out) return false;
+    if (k >= NT || eob_end == NOPOS || otot > usize - out) return PAR_FAIL;
     // pass 3: emit
     uint32_t bad = 0;
-    if (tid <= k) lane_run<LDS, RUN_EMIT>(sm.t, src, A, stop, limit, ck, none, tk + ntok + tpre, out + opre, bad);
-    if (__syncthreads_or(bad)) return false;
+    if (tid <= k)
+      lane_run<RUN_EMIT>(sm.t, src, A, stop, limit, ck, none, tk + ntok + tpre, out_before + out + opre, bad);
+    if (__syncthreads_or(bad)) return PAR_FAIL;
 #ifdef SBH_HUFF_PROBE
     if (tid == 0) atomicAdd(&hp_acc[4], __builtin_readcyclecounter() - tp3);
 #endif
     ntok += ttot;
     out += otot;
     p = eob_end;
+#ifdef SBH_HUFF_FIRST_ONLY  // A/B probe (timing only, results wrong): the first deflate block alone
+    ntok_out = ntok;
+    return PAR_OK;
+#endif
     if (last) break;
+    // (the tail's two words go where its tokens will start: ntok + 2 <= usize keeps them
+    // inside the block's token region)
+    if (tail_ok && (limit - p) * 4 < limit && ntok + 2 <= usize) {
+      *tail_p = p;
+      *tail_out = out;
+      ntok_out = ntok;
+      return PAR_TAIL;
+    }
   }
-  if (out != usize) return false;
+  if (out != usize) return PAR_FAIL;
   ntok_out = ntok;
-  return true;
+  return PAR_OK;
 }
 
 // First-header pre-pass: the first deflate block of every BGZF block starts at the
@@ -1562,8 +1594,7 @@ __global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__rest
     const uint32_t skip = (uint32_t)(dbyte & 3) * 8;
     const uint32_t limit = skip + data_len * 8;
     const uint32_t ndw = (limit + 31) / 32 + 2;
-    uint32_t ntok = 0;
-    bool ok;
+    uint32_t ntok = 0, rc, tail_p = 0, tail_out = 0;
     // the first deflate block's header, decoded and tabled by k_hdr at the end of this
     // block's token region (read here before any token is written over it)
     const uint32_t *hd = tok + G + usize - HDR_OUT_DW;
@@ -1599,16 +1630,26 @@ __global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__rest
 #ifdef SBH_HUFF_PROBE
       if (tid == 0) atomicAdd(&hp_acc[0], __builtin_readcyclecounter() - hk0);
 #endif
-      ok = inflate_par<true>(sm, dbase, skip, limit, usize, tok + G, tid, lane, wid, ntok, pre, pre_psym, pre_last);
+      rc = inflate_par<true>(sm, dbase, skip, limit, usize, tok + G, tid, lane, wid, ntok, pre, pre_psym, pre_last, 0,
+                             SBH_TAIL != 0, &tail_p, &tail_out);
     } else {
       if (pre) {
         put_tables();
         __syncthreads();
       }
-      ok = inflate_par<false>(sm, dbase, skip, limit, usize, tok + G, tid, lane, wid, ntok, pre, pre_psym,
-                              pre_last);
+      rc = inflate_par<false>(sm, dbase, skip, limit, usize, tok + G, tid, lane, wid, ntok, pre, pre_psym, pre_last,
+                              0, SBH_TAIL != 0, &tail_p, &tail_out);
     }
-    if (uni(ok)) {
+    if (uni(rc) == PAR_TAIL) {  // k_huff_tail decodes the rest: its start bit and bytes so far at tok[ntok..]
+      if (tid == 0) {
+        tok[G + ntok] = tail_p;
+        tok[G + ntok + 1] = tail_out;
+        bl.ntok[b] = ntok;
+        bl.status[b] = INF_TAIL;
+      }
+      return;
+    }
+    if (uni(rc) == PAR_OK) {
       if (tid == 0) {
         bl.status[b] = INF_OK;
         bl.ntok[b] = ntok;
@@ -1632,6 +1673,49 @@ __global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__rest
     }
   }
   if (tid == 0) bl.status[b] = INF_SERIAL;  // k_huff_serial<true> decodes it
+}
+
+// The rest of a block k_huff deferred (INF_TAIL: a short final deflate block, typically),
+// by one wave per block: that block's header and the lane-parallel passes over 64 lanes,
+// with the remaining compressed bytes staged from the tail's first dword (4 KiB; longer
+// tails read global memory).  The tokens continue at tok[ntok]; anything the fast path
+// does not prove leaves INF_SERIAL, and the serial decoder redoes the whole block.
+constexpr uint32_t TAIL_DW = 1024;
+using TailSmem = HuffSmemT<WAVE, TAIL_DW>;
+__global__ __launch_bounds__(WAVE) void k_huff_tail(const uint8_t *__restrict__ comp, DevBlocks bl, uint64_t nblocks,
+                                                    uint32_t *__restrict__ tok) {
+  __shared__ TailSmem sm;
+  const uint64_t b = blockIdx.x;
+  if (b >= nblocks || uni(bl.status[b]) != INF_TAIL) return;
+  const uint32_t lane = threadIdx.x;
+  const uint64_t cstart = bl.cstart[b];
+  const uint32_t csize = bl.csize[b], hsize = bl.hsize[b], usize = bl.usize[b];
+  const uint64_t G = bl.ustart[b];
+  const uint32_t n1 = uni(bl.ntok[b]);
+  uint32_t *tk = tok + G + n1;
+  const uint32_t p = uni(tk[0]), out1 = uni(tk[1]);  // (read before any token overwrites them)
+  const uint64_t dbyte = cstart + hsize;
+  const uint32_t limit0 = (uint32_t)(dbyte & 3) * 8 + (csize - hsize - 8) * 8;
+  // rebased at the dword holding the tail's first bit
+  const uint32_t pd = p >> 5;
+  const uint8_t *dbase = comp + (dbyte & ~3ull) + 4ull * pd;
+  const uint32_t skip = p & 31, limit = limit0 - 32 * pd;
+  const uint32_t ndw = (limit + 31) / 32 + 2;
+  uint32_t n2 = 0, rc;
+  if (ndw <= TAIL_DW) {
+    const uint32_t *g = reinterpret_cast<const uint32_t *>(dbase);
+    for (uint32_t i = lane; i < ndw; i += WAVE) sm.stage[i] = g[i];
+    __syncthreads();
+    rc = inflate_par<true>(sm, dbase, skip, limit, usize - out1, tk, lane, lane, 0, n2, false, 0, 0, out1, false,
+                           nullptr, nullptr);
+  } else {
+    rc = inflate_par<false>(sm, dbase, skip, limit, usize - out1, tk, lane, lane, 0, n2, false, 0, 0, out1, false,
+                            nullptr, nullptr);
+  }
+  if (lane == 0) {
+    bl.status[b] = uni(rc) == PAR_OK ? INF_OK : INF_SERIAL;
+    bl.ntok[b] = n1 + n2;
+  }
 }
 
 #ifndef SBH_LZ_TPT
@@ -1998,6 +2082,9 @@ hipError_t launch_huff(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, 
   hipLaunchKernelGGL(k_hdr, dim3((uint32_t)((nblocks + HDR_WAVES - 1) / HDR_WAVES)), dim3(WAVE * HDR_WAVES), 0, stream,
                      comp, blocks, nblocks, tok);
   hipLaunchKernelGGL(k_huff, dim3((uint32_t)nblocks), dim3(HT), 0, stream, comp, blocks, nblocks, tok);
+#if SBH_TAIL
+  hipLaunchKernelGGL(k_huff_tail, dim3((uint32_t)nblocks), dim3(WAVE), 0, stream, comp, blocks, nblocks, tok);
+#endif
   const uint64_t grid = (nblocks + WAVES - 1) / WAVES;
   hipLaunchKernelGGL(k_huff_serial<true>, dim3((uint32_t)grid), dim3(WAVES * WAVE), 0, stream, comp, blocks, nblocks,
                      tok);
