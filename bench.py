@@ -162,10 +162,11 @@ def main():
 
     # the streamed shard's Hadoop splits (32 MiB, SplitRDD's partitions): per-split first record
     # and count come back from every window (sbh_run_stream2)
-    stream_splits = None
-    if streaming:
-        sp = sb.file_splits(seg.own_end - seg.file_offset, 32 << 20)
-        stream_splits = [(seg.file_offset + x, seg.file_offset + y) for x, y in sp]
+    # (resident shards too: the step returns every owned split's first record and count, the
+    # north star's "split virtual offsets", from sbh_split_starts on the run's bitmap)
+    sp = sb.file_splits(seg.own_end - seg.file_offset, 32 << 20)
+    stream_splits = [(seg.file_offset + x, seg.file_offset + y) for x, y in sp]
+    split_last = {}
 
     def run_once():
         if streaming:  # windows through HBM; copies of window w+1 overlap window w's kernels
@@ -177,7 +178,10 @@ def main():
             ex = r["exit_vpos"]
             return dict(r, first_vpos=first), r["stage_ms"], ex
         r = shard.run(seg.file_offset, seg.own_end)
-        return r, shard.stage_times(), shard.exit_vpos(r)  # exit: None when the chain hit the stream end
+        stages = shard.stage_times()
+        st, v, n, nh = shard.split_starts(stream_splits)
+        split_last.update(split_status=st, split_vpos=v, split_count=n, splits_host=nh)
+        return r, stages, shard.exit_vpos(r)  # exit: None when the chain hit the stream end
 
     def step():
         r, stages, ex = run_once()
@@ -228,10 +232,8 @@ def main():
     # bit-exactness of the inflate), outside the timed region
     # (stream mode: every window's owned blocks were CRC-checked in the run, sbh_run_stream2)
     crc_bad = shard.verify_crc()[0] if shard is not None else stream_last.get("crc_bad_blocks", 0)
-    split_ok = True
-    if streaming:
-        split_ok = (int(np.count_nonzero(stream_last["split_status"])) == 0
-                    and int(stream_last["split_count"].sum()) == r["count"])
+    sl = stream_last if streaming else split_last
+    split_ok = (int(np.count_nonzero(sl["split_status"])) == 0 and int(sl["split_count"].sum()) == r["count"])
     ok = (total_records == expect and (total_true == expect or not cfg["fp_free"]) and stitch["ok"] and crc_bad == 0
           and split_ok)
     firsts = [x[0] for x in allr if x[1] > 0]
@@ -360,6 +362,11 @@ def main():
             "compressed_GBps": round(sum(own_sizes) * args.steps / elapsed / 1e9, 3),
             "correct": bool(ok),
             "stitch_ok": bool(stitch["ok"]),
+            "splits_rank0": {"n": len(stream_splits), "split_bytes": 32 << 20,
+                             "host_path": int(sl.get("splits_host", 0)),
+                             "counts_sum": int(sl["split_count"].sum()),
+                             "note": "every owned Hadoop split's first-record vpos and count "
+                                     "(sbh_split_starts) inside the timed step"},
             "crc_bad_blocks_rank0": int(crc_bad),
             "records": int(total_records),
             "eager_true": int(total_true),

@@ -78,10 +78,11 @@ __constant__ uint8_t CL_ORDER[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12
 static_assert((1 << PDIST_FAST) >= (2 << DIST_FAST), "the serial distance table fits the PAR one");
 
 // PAR-format entry flags (see pentry)
-constexpr uint32_t PE_LEN = 1u << 5;      // a length code: a distance code follows
-constexpr uint32_t PE_SPECIAL = 1u << 6;  // not a token: end of block, invalid, or long code
-constexpr uint32_t PE_SLOW = 1u << 7;     // (with PE_SPECIAL) code longer than the table: slow_lane
-constexpr uint32_t PE_EOB = 1u << 12;     // (with PE_SPECIAL) end of block
+constexpr uint32_t PE_LEN = 1u << 12;      // a length code: a distance code follows (= the distance
+                                           // table's byte offset in WaveSmem::tab)
+constexpr uint32_t PE_EOB = 1u << 13;      // (with PE_SPECIAL) end of block
+constexpr uint32_t PE_SLOW = 1u << 14;     // (with PE_SPECIAL) code longer than the table: slow_lane
+constexpr uint32_t PE_SPECIAL = 1u << 31;  // not a token: end of block, invalid, or long code
 
 struct __attribute__((aligned(16))) WaveSmem {
   union {
@@ -226,10 +227,10 @@ __device__ __forceinline__ uint32_t build_table(SM &sm, const uint8_t *lens, uin
   return 0;
 }
 
-// PAR-format entries (the lane-parallel decoder): [4:0] code length L, [5] PE_LEN,
-// [6] PE_SPECIAL, [7] PE_SLOW, [11:8] extra bits, [12] PE_EOB, [31:16] base (a literal's
-// byte; a length or distance base), so any token code decodes as base + bits(L, extra)
-// and "completes a token" is simply "neither PE_LEN nor PE_SPECIAL" in either table.
+// PAR-format entries (the lane-parallel decoder): [4:0] code length L, [8:5] extra bits,
+// [12] PE_LEN, [13] PE_EOB, [14] PE_SLOW, [30:16] base (a literal's byte; a length's base
+// MINUS ONE; a distance base), [31] PE_SPECIAL, so any code decodes as base + bits(L, extra),
+// a special entry is a negative one, and PE_LEN doubles as the distance table's offset.
 __device__ __forceinline__ uint32_t pentry(uint32_t kind, uint32_t sym, uint32_t L) {
   // base / extra bits of length symbols 257 + i and distance symbols i, computed
   // (RFC 1951 3.2.5) rather than looked up: no constant-memory loads in the table build
@@ -240,14 +241,14 @@ __device__ __forceinline__ uint32_t pentry(uint32_t kind, uint32_t sym, uint32_t
       const uint32_t i = sym - 257;
       const uint32_t x = (i < 8 || i == 28) ? 0u : (i - 4) >> 2;
       const uint32_t base = i < 8 ? 3 + i : i == 28 ? 258u : ((4 + (i & 3)) << x) + 3;
-      return L | PE_LEN | (x << 8) | (base << 16);
+      return L | PE_LEN | (x << 5) | ((base - 1) << 16);
     }
     return L | PE_SPECIAL;
   }
   if (sym < 30) {
     const uint32_t x = sym < 4 ? 0u : (sym - 2) >> 1;
     const uint32_t base = sym < 4 ? sym + 1 : ((2 + (sym & 1)) << x) + 1;
-    return L | (x << 8) | (base << 16);
+    return L | (x << 5) | (base << 16);
   }
   return L | PE_SPECIAL;
 }
@@ -961,9 +962,6 @@ static_assert(HDR_SENT % SBH_HT == 0, "k_huff copies the tables in whole rounds"
 #ifndef SBH_CK3
 #define SBH_CK3 64
 #endif
-#ifndef SBH_NX_PRED
-#define SBH_NX_PRED 0  // 1: stream dword reloads only in lanes that crossed a dword (A/B: 6% slower)
-#endif
 #ifndef SBH_MARGIN
 #define SBH_MARGIN 0  // pass-1 warm-up bits before each slice (A/B: 128-384 bits measured neutral)
 #endif
@@ -998,6 +996,10 @@ struct Src {
   __device__ __forceinline__ uint32_t operator()(uint32_t i) const {
     if (LDS) return p[i < SDW + 7 ? i : SDW + 7];
     return p[i];
+  }
+  // the dword at byte offset b (4-aligned; callers keep it inside the staged dwords)
+  __device__ __forceinline__ uint32_t at_byte(uint32_t b) const {
+    return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(p) + b);
   }
   // 32 stream bits starting at bit position `pos`
   // (no clamp: a lane never reads past dword (limit + 48) / 32 + 1, and staged blocks
@@ -1053,78 +1055,90 @@ constexpr int RUN_SPEC = 0, RUN_REDO = 1, RUN_EMIT = 2;
 //   RUN_REDO: stop early on reaching one of ck's boundaries (sp: that chain's result).
 //   RUN_EMIT: store tokens at dst, flag a distance reaching before the block's first
 //             byte (out0: bytes before A).
+// k_huff's passes are bound by VALU issue (each SIMD issues VALU on ~80% of its cycles at 4
+// waves: r03n PMC), so the loop is written for few vector instructions per code:
+//  * the decode state is the bit position and the two stream dwords under it (lo, hi): a
+//    code's 32 bits come from them with one v_alignbit, enough for any code plus its extra
+//    bits (<= 28); a code consumes < 32 bits, so the window moves by at most one dword per
+//    code, and the dword after it is loaded at the top of every iteration beside the table
+//    lookup (its byte address straight from the position: no dword index to maintain);
+//  * `tsel` (0, or PE_LEN = the distance table's byte offset) is both the table select and
+//    the state; a token is counted at its first code (a match at its length code), and the
+//    bytes as acc = 4096 * sum(match length - 1), one v_mad_u32_u24 per code -- both equal
+//    the per-token counts at every token boundary, where they are read;
+//  * one sign test per code catches every special entry (EOB, invalid, long code);
+//  * checkpoint recording and the loop exit are branches (scalar ops, off the VALU).
 template <int MODE, class S>
 __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, S src, uint32_t A, uint32_t stop,
                                             uint32_t limit, Ckpt &ck, const LaneRun &sp,
                                             uint32_t *__restrict__ dst, uint32_t out0, uint32_t &bad) {
-  // The decode state is the bit position and the two stream dwords under it (lo, hi):
-  // a code's 32 bits come from them with one v_alignbit, enough for any code plus its
-  // extra bits (<= 28), and the extra bits come out with one v_bfe.  A code consumes
-  // < 32 bits, so the window moves by at most one dword per code; the dword after it is
-  // loaded at the top of every iteration, beside the table lookup, so each code costs
-  // one LDS round trip on the dependent chain, not two (SBH_NX_PRED=1 instead reloads it
-  // only in the lanes that moved: fewer LDS reads, but the branch made k_huff 6% slower).
-  // One loop exit, at the end of the body; everything else is selects (apart from the rare
-  // long code).
   const uint32_t stop2 = stop < limit ? stop : limit;
+  if (MODE == RUN_SPEC) ck = Ckpt{NOPOS, 0, NOPOS, 0, NOPOS, 0};
+  // a lane starting at or past its stop ends there (a slice past the stream's end; its
+  // stream reads would leave the stage)
+  if (A >= stop2) return LaneRun{A >= limit ? LR_PAST : LR_RUN, A, 0, 0};
+  const char *tab = reinterpret_cast<const char *>(t.tab);
   uint32_t pos = A;
-  uint32_t wi = pos >> 5, lo = src(wi), hi = src(wi + 1);
-#if SBH_NX_PRED
-  uint32_t nx = src(wi + 2);
-#endif
-  uint32_t ml = 0;  // pending match length: the next code is a distance
-  uint32_t ntok = 0, nout = 0;
+  uint32_t lo = src((pos >> 5)), hi = src((pos >> 5) + 1);
+  uint32_t tsel = 0;             // 0: at a token boundary (literal/length table); PE_LEN: a distance follows
+  uint32_t ntok = 0, acc = 0;    // tokens started; 4096 * sum over matches of (length - 1)
+  uint32_t ml = 0;               // RUN_EMIT: the pending match's length - 1
   uint32_t c1p = NOPOS, c1o = 0, c2p = NOPOS, c2o = 0, c3p = NOPOS, c3o = 0;
   uint32_t ck_next = CK1;  // RUN_SPEC: token count of the next checkpoint
   uint32_t e;
   bool cut;
   for (;;) {
-    const uint32_t bits = __builtin_amdgcn_alignbit(hi, lo, pos & 31);
-#if !SBH_NX_PRED
-    const uint32_t nx = src(wi + 2);
-#endif
-    const bool atb = ml == 0;  // token boundary
-    e = t.tab[(bits & ((1u << LIT_FAST) - 1)) | (atb ? 0u : 1u << LIT_FAST)];
-    if (e & PE_SLOW) e = slow_lane(t, bits, !atb);
+    const uint32_t bits = __builtin_amdgcn_alignbit(hi, lo, pos);
+    const uint32_t nx = src.at_byte(((pos >> 3) & ~3u) + 8);  // dword (pos >> 5) + 2
+    e = *reinterpret_cast<const uint32_t *>(tab + (((bits & ((1u << LIT_FAST) - 1)) << 2) | tsel));
+    bool special = (int32_t)e < 0;
+    if (special && (e & PE_SLOW)) {  // rare: a code longer than the table
+      e = slow_lane(t, bits, tsel != 0);
+      special = (int32_t)e < 0;
+    }
+    const bool atb = tsel == 0;  // token boundary
     if (MODE == RUN_SPEC && atb && ntok == ck_next) {  // rare: a branch, not per-code selects
+      const uint32_t o = ntok + (acc >> 12);
       if (ck_next == CK1) {
         c1p = pos;
-        c1o = nout;
+        c1o = o;
         ck_next = CK2;
       } else if (ck_next == CK2) {
         c2p = pos;
-        c2o = nout;
+        c2o = o;
         ck_next = CK3 > CK2 ? CK3 : ~0u;
       } else {
         c3p = pos;
-        c3o = nout;
+        c3o = o;
         ck_next = ~0u;
       }
     }
     cut = atb && (pos >= stop2 || (MODE == RUN_REDO && (pos == ck.p1 || pos == ck.p2 || pos == ck.p3)));
-    if (cut || (e & PE_SPECIAL)) break;
-    const uint32_t L = e & 31, x = (e >> 8) & 15;
-    const uint32_t val = (e >> 16) + __builtin_amdgcn_ubfe(bits, L, x);
-    pos += L + x;
-    const bool adv = (pos >> 5) != wi;
+    if (cut || special) break;
+    const uint32_t L = e & 31, x = __builtin_amdgcn_ubfe(e, 5, 4);
+    const uint32_t val = (e >> 16) + __builtin_amdgcn_ubfe(bits, e, x);  // (offset: e's low 5 bits = L)
+    const uint32_t np = pos + L + x;
+    const bool adv = (np ^ pos) >= 32u;
+    pos = np;
     lo = adv ? hi : lo;
     hi = adv ? nx : hi;
-    wi += adv ? 1u : 0u;
-#if SBH_NX_PRED
-    // only a lane that moved into the next dword refills (one code in four or five): its load
-    // is in flight during the next code's table lookup, which LDS returns after it
-    if (adv) nx = src(wi + 2);
-#endif
-    const bool is_tok = (e & PE_LEN) == 0;  // a literal, or the distance completing a match
+    const uint32_t tnew = e & PE_LEN;
     if (MODE == RUN_EMIT) {
-      if (is_tok) dst[ntok] = atb ? val << 8 : TOK_MATCH | (ml << 16) | val;
-      bad |= (!atb && val > out0 + nout) ? 1u : 0u;
+      if (atb && !tnew) {
+        dst[ntok] = val << 8;  // a literal
+      } else if (!atb) {       // a distance completing a match (started at token ntok - 1)
+        dst[ntok - 1] = TOK_MATCH | ((ml + 1) << 16) | val;
+        // bytes before the match: out0 + tokens before it + the earlier matches' extra bytes
+        bad |= val > out0 + ntok - 1 + ((acc >> 12) - ml) ? 1u : 0u;
+      }
+      ml = tnew ? val : ml;
     }
-    ntok += is_tok ? 1u : 0u;
-    nout += is_tok ? (ml > 1u ? ml : 1u) : 0u;
-    ml = is_tok ? 0u : val;
+    ntok += atb ? 1u : 0u;
+    acc += (uint32_t)__umul24(tnew, val);  // (tnew: 0 or 4096; one v_mad_u32_u24)
+    tsel = tnew;
   }
   if (MODE == RUN_SPEC) ck = Ckpt{c1p, c1o, c2p, c2o, c3p, c3o};
+  const uint32_t nout = ntok + (acc >> 12);
   LaneRun r{LR_RUN, pos, ntok, nout};
   if (cut) {
     if (MODE == RUN_REDO && pos < stop2) {  // joined the pass-1 chain at a checkpoint
@@ -1138,7 +1152,7 @@ __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, S src, uint32_t A
       r.st = LR_PAST;
     }
   } else {  // end of block, or an invalid code
-    r.st = (ml == 0 && (e & PE_EOB)) ? LR_EOB : LR_DEAD;
+    r.st = (tsel == 0 && (e & PE_EOB)) ? LR_EOB : LR_DEAD;
     r.exit = pos + (e & 31);
   }
   return r;
@@ -1382,6 +1396,9 @@ __device__ __forceinline__ uint32_t inflate_par(SM &sm, const uint8_t *__restric
     __syncthreads();
     const uint64_t tp1 = __builtin_readcyclecounter();
 #endif
+#if defined(SBH_HUFF_TIMING) && (SBH_HUFF_TIMING & 1)
+    if (false)  // timing probe: no repair rounds
+#endif
     for (;;) {
 #ifdef SBH_HUFF_PROBE
       ++nrounds;
@@ -1425,6 +1442,17 @@ __device__ __forceinline__ uint32_t inflate_par(SM &sm, const uint8_t *__restric
       atomicAdd(&hp_acc[5], (unsigned long long)nrounds);
       atomicAdd(&hp_acc[6], 1ull);
       atomicAdd(&hp_acc[11], (unsigned long long)ttot);
+    }
+#endif
+#ifdef SBH_HUFF_TIMING  // A/B phase-cost probe (timing only, results wrong): the first deflate block's
+                        // passes, none of the checks; bit 0: no repair rounds, bit 1: no emit pass
+    {
+      uint32_t bad = 0;
+      if ((SBH_HUFF_TIMING & 2) == 0)
+        lane_run<RUN_EMIT>(sm.t, src, A, stop, limit, ck, none, tk + ((tid * 16) & 2047), opre, bad);  // (in bounds)
+      __syncthreads();
+      ntok_out = 0;
+      return PAR_OK;
     }
 #endif
     if (k >= NT || eob_end == NOPOS || otot > usize - out) return PAR_FAIL;
