@@ -1098,20 +1098,14 @@ __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, S src, uint32_t A
     }
     const bool atb = tsel == 0;  // token boundary
     if (MODE == RUN_SPEC && atb && ntok == ck_next) {  // rare: a branch, not per-code selects
-      const uint32_t o = ntok + (acc >> 12);
-      if (ck_next == CK1) {
-        c1p = pos;
-        c1o = o;
-        ck_next = CK2;
-      } else if (ck_next == CK2) {
-        c2p = pos;
-        c2o = o;
-        ck_next = CK3 > CK2 ? CK3 : ~0u;
-      } else {
-        c3p = pos;
-        c3o = o;
-        ck_next = ~0u;
-      }
+      // shift register: the newest checkpoint in c1 (the order is restored after the loop)
+      c3p = c2p;
+      c3o = c2o;
+      c2p = c1p;
+      c2o = c1o;
+      c1p = pos;
+      c1o = ntok + (acc >> 12);
+      ck_next = ck_next == CK1 ? CK2 : ck_next == CK2 && CK3 > CK2 ? CK3 : ~0u;
     }
     cut = atb && (pos >= stop2 || (MODE == RUN_REDO && (pos == ck.p1 || pos == ck.p2 || pos == ck.p3)));
     if (cut || special) break;
@@ -1137,7 +1131,13 @@ __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, S src, uint32_t A
     acc += (uint32_t)__umul24(tnew, val);  // (tnew: 0 or 4096; one v_mad_u32_u24)
     tsel = tnew;
   }
-  if (MODE == RUN_SPEC) ck = Ckpt{c1p, c1o, c2p, c2o, c3p, c3o};
+  if (MODE == RUN_SPEC) {  // oldest first: CK1's boundary in p1
+    const uint32_t nck = ck_next == CK1 ? 0u : ck_next == CK2 ? 1u : ck_next == CK3 && CK3 > CK2 ? 2u : CK3 > CK2 ? 3u : 2u;
+    ck = nck == 3 ? Ckpt{c3p, c3o, c2p, c2o, c1p, c1o}
+       : nck == 2 ? Ckpt{c2p, c2o, c1p, c1o, NOPOS, 0}
+       : nck == 1 ? Ckpt{c1p, c1o, NOPOS, 0, NOPOS, 0}
+                  : Ckpt{NOPOS, 0, NOPOS, 0, NOPOS, 0};
+  }
   const uint32_t nout = ntok + (acc >> 12);
   LaneRun r{LR_RUN, pos, ntok, nout};
   if (cut) {
@@ -1156,6 +1156,492 @@ __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, S src, uint32_t A
     r.exit = pos + (e & 31);
   }
   return r;
+}
+
+#ifndef SBH_ASM_SPEC
+#define SBH_ASM_SPEC 1  // pass 1 (RUN_SPEC over the LDS stage) as the hand-written loop below
+#endif
+// RUN_SPEC over the LDS stage as hand-written code: lane_run<RUN_SPEC>'s loop with the same
+// results, in ~33 instructions per code instead of the compiler's ~57 (whose structurized loop
+// spends ~25 scalar instructions per code on exit masks and phi copies, and waves of k_huff
+// wait on their own issue: PMC r03n, 32% of wave cycles issuing, 54% parked).  Per code: the
+// entry's LDS address from the stream bits, the next stream dword beside it; the token-boundary,
+// checkpoint and cut tests as lane masks while the entry is in flight; lanes that reach their
+// cut or a special entry leave the loop (exec shrinks) with their state as it was; long codes
+// (> LIT_FAST bits) resolve in place through the PAR limits (slow_lane's arithmetic).  The
+// checkpoints go into a shift register (newest in c1), reordered after the loop.
+static_assert(CK1 == 8 && CK2 == 32 && CK3 == 64, "the asm pass-1 loop hard-codes the checkpoint schedule");
+static_assert(LIT_FAST == 10 && PDIST_FAST == 10, "the asm pass-1 loop indexes 10-bit tables");
+__device__ __forceinline__ LaneRun spec_asm(const WaveSmem &t, const uint32_t *stage, uint32_t A, uint32_t stop,
+                                            uint32_t limit, Ckpt &ck) {
+  const uint32_t stop2 = stop < limit ? stop : limit;
+  ck = Ckpt{NOPOS, 0, NOPOS, 0, NOPOS, 0};
+  if (A >= stop2) return LaneRun{A >= limit ? LR_PAST : LR_RUN, A, 0, 0};
+  const uint32_t tabb = uni((uint32_t)reinterpret_cast<uintptr_t>(t.tab));
+  const uint32_t stb = uni((uint32_t)reinterpret_cast<uintptr_t>(stage) + 8u);  // + dword 2 of the window
+  const uint32_t pkb = uni((uint32_t)reinterpret_cast<uintptr_t>(&t.pk[0][11]));
+  const uint32_t sentb = uni((uint32_t)reinterpret_cast<uintptr_t>(t.sent));
+  const uint32_t sentd = sentb + 288u * 4u;
+  uint32_t pos = A, lo = stage[A >> 5], hi = stage[(A >> 5) + 1];
+  uint32_t vt = 0, tselb = tabb, ntok = 0, acc = 0, ckn = CK1;
+  uint32_t c1p = NOPOS, c1o = 0, c2p = NOPOS, c2o = 0, c3p = NOPOS, c3o = 0;
+  const uint32_t bad_e = 1u | PE_SPECIAL;
+  uint32_t e = 0, bits, a, nx, x, ex, val, np, tmp, r15, q, p11, p12, p13, p14, p15, d, sh;
+  uint64_t sA, sB, sC, sD, sE, sv;
+  asm volatile(
+      "s_mov_b64 %[sv], exec\n"
+      "L_top%=:\n\t"
+      "v_alignbit_b32 %[bits], %[hi], %[lo], %[pos]\n\t"
+      "v_and_b32 %[a], 0x3ff, %[bits]\n\t"
+      "v_lshl_add_u32 %[a], %[a], 2, %[tselb]\n\t"
+      "ds_read_b32 %[e], %[a]\n\t"
+      "v_lshrrev_b32 %[a], 3, %[pos]\n\t"
+      "v_and_b32 %[a], -4, %[a]\n\t"
+      "v_add_u32 %[a], %[stb], %[a]\n\t"
+      "ds_read_b32 %[nx], %[a]\n\t"
+      // while the entry is in flight: token boundary (sA), cut (sC), checkpoint hit (sB)
+      "v_cmp_eq_u32 %[sA], 0, %[vt]\n\t"
+      "v_cmp_ge_u32 %[sC], %[pos], %[stop]\n\t"
+      "s_and_b64 %[sC], %[sC], %[sA]\n\t"
+      "v_cmp_eq_u32 %[sB], %[ntok], %[ckn]\n\t"
+      "s_and_b64 %[sB], %[sB], %[sA]\n\t"
+      "s_cbranch_scc0 L_nock%=\n\t"
+      // checkpoint (hit lanes): shift in (pos, bytes), next threshold 8 -> 32 -> 64 -> never
+      "s_and_saveexec_b64 %[sD], %[sB]\n\t"
+      "v_mov_b32 %[c3p], %[c2p]\n\t"
+      "v_mov_b32 %[c3o], %[c2o]\n\t"
+      "v_mov_b32 %[c2p], %[c1p]\n\t"
+      "v_mov_b32 %[c2o], %[c1o]\n\t"
+      "v_mov_b32 %[c1p], %[pos]\n\t"
+      "v_lshrrev_b32 %[c1o], 12, %[acc]\n\t"
+      "v_add_u32 %[c1o], %[c1o], %[ntok]\n\t"
+      "v_cmp_eq_u32 %[sB], 32, %[ckn]\n\t"
+      "v_cmp_eq_u32 %[sE], 8, %[ckn]\n\t"
+      "s_nop 1\n\t"
+      "v_cndmask_b32_e64 %[tmp], -1, 64, %[sB]\n\t"
+      "v_cndmask_b32_e64 %[ckn], %[tmp], 32, %[sE]\n\t"
+      "s_mov_b64 exec, %[sD]\n"
+      "L_nock%=:\n\t"
+      "s_waitcnt lgkmcnt(1)\n\t"
+      "v_cmp_gt_i32 %[sD], 0, %[e]\n\t"  // special entries
+      "s_and_b64 %[sD], %[sD], exec\n\t"
+      "s_cbranch_scc0 L_nosp%=\n\t"
+      "v_and_b32 %[tmp], 0x4000, %[e]\n\t"  // PE_SLOW
+      "v_cmp_ne_u32 %[sB], 0, %[tmp]\n\t"
+      "s_and_b64 %[sB], %[sB], %[sD]\n\t"
+      "s_cbranch_scc0 L_nosp%=\n\t"
+      // long codes: the length is 11 + #{v in 11..14 : limit(v) <= rev15}; invalid past limit(15)
+      "s_and_saveexec_b64 %[sB], %[sB]\n\t"
+      "v_bfrev_b32 %[r15], %[bits]\n\t"
+      "v_lshrrev_b32 %[r15], 17, %[r15]\n\t"
+      "v_lshrrev_b32 %[q], 6, %[vt]\n\t"  // pk[kind]: 64 bytes per kind
+      "v_add_u32 %[q], %[pkb], %[q]\n\t"
+      "ds_read_b32 %[p11], %[q]\n\t"  // pk[kind][11..15]
+      "ds_read_b32 %[p12], %[q] offset:4\n\t"
+      "ds_read_b32 %[p13], %[q] offset:8\n\t"
+      "ds_read_b32 %[p14], %[q] offset:12\n\t"
+      "ds_read_b32 %[p15], %[q] offset:16\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "v_mov_b32 %[d], %[p11]\n\t"
+      "v_mov_b32 %[sh], 4\n\t"
+      "v_lshrrev_b32 %[tmp], 16, %[p11]\n\t"
+      "v_cmp_le_u32 vcc, %[tmp], %[r15]\n\t"
+      "s_nop 1\n\t"
+      "v_cndmask_b32_e32 %[d], %[d], %[p12], vcc\n\t"
+      "v_cndmask_b32_e64 %[sh], %[sh], 3, vcc\n\t"
+      "v_lshrrev_b32 %[tmp], 16, %[p12]\n\t"
+      "v_cmp_le_u32 vcc, %[tmp], %[r15]\n\t"
+      "s_nop 1\n\t"
+      "v_cndmask_b32_e32 %[d], %[d], %[p13], vcc\n\t"
+      "v_cndmask_b32_e64 %[sh], %[sh], 2, vcc\n\t"
+      "v_lshrrev_b32 %[tmp], 16, %[p13]\n\t"
+      "v_cmp_le_u32 vcc, %[tmp], %[r15]\n\t"
+      "s_nop 1\n\t"
+      "v_cndmask_b32_e32 %[d], %[d], %[p14], vcc\n\t"
+      "v_cndmask_b32_e64 %[sh], %[sh], 1, vcc\n\t"
+      "v_lshrrev_b32 %[tmp], 16, %[p14]\n\t"
+      "v_cmp_le_u32 vcc, %[tmp], %[r15]\n\t"
+      "s_nop 1\n\t"
+      "v_cndmask_b32_e32 %[d], %[d], %[p15], vcc\n\t"
+      "v_cndmask_b32_e64 %[sh], %[sh], 0, vcc\n\t"
+      "v_lshrrev_b32 %[tmp], %[sh], %[r15]\n\t"  // (d + (rev15 >> (15 - len))) & 0xffff
+      "v_add_u32 %[tmp], %[tmp], %[d]\n\t"
+      "v_and_b32 %[tmp], 0xffff, %[tmp]\n\t"
+      "v_min_u32 %[tmp], 0x13f, %[tmp]\n\t"  // (inside sent[]; an index past it is an invalid code, replaced below)
+      "v_cmp_ne_u32 vcc, 0, %[vt]\n\t"
+      "v_mov_b32 %[q], %[sentd]\n\t"
+      "v_mov_b32 %[d], %[sentb]\n\t"
+      "v_cndmask_b32_e32 %[q], %[d], %[q], vcc\n\t"
+      "v_lshl_add_u32 %[tmp], %[tmp], 2, %[q]\n\t"
+      "ds_read_b32 %[e], %[tmp]\n\t"
+      "v_lshrrev_b32 %[tmp], 16, %[p15]\n\t"
+      "v_cmp_ge_u32 vcc, %[r15], %[tmp]\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_nop 1\n\t"
+      "v_cndmask_b32_e32 %[e], %[e], %[bad_e], vcc\n\t"
+      "s_mov_b64 exec, %[sB]\n\t"
+      "v_cmp_gt_i32 %[sD], 0, %[e]\n"  // special after the long-code lookup
+      "L_nosp%=:\n\t"
+      // lanes at their cut or a special entry leave the loop
+      "s_or_b64 %[sD], %[sD], %[sC]\n\t"
+      "s_andn2_b64 exec, exec, %[sD]\n\t"
+      "s_cbranch_execz L_end%=\n\t"
+      "v_and_b32 %[tmp], 31, %[e]\n\t"
+      "v_bfe_u32 %[x], %[e], 5, 4\n\t"
+      "v_bfe_u32 %[ex], %[bits], %[e], %[x]\n\t"
+      "v_add3_u32 %[np], %[pos], %[tmp], %[x]\n\t"
+      "v_add_u32_sdwa %[val], %[ex], %[e] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+      "v_xor_b32 %[tmp], %[np], %[pos]\n\t"
+      "v_cmp_lt_u32 vcc, 31, %[tmp]\n\t"
+      "v_and_b32 %[vt], 0x1000, %[e]\n\t"
+      "v_mov_b32 %[pos], %[np]\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "v_cndmask_b32_e32 %[lo], %[lo], %[hi], vcc\n\t"
+      "v_cndmask_b32_e32 %[hi], %[hi], %[nx], vcc\n\t"
+      "v_addc_co_u32_e64 %[ntok], vcc, 0, %[ntok], %[sA]\n\t"
+      "v_add_u32 %[tselb], %[tabb], %[vt]\n\t"
+      "v_mad_u32_u24 %[acc], %[vt], %[val], %[acc]\n\t"
+      "s_branch L_top%=\n"
+      "L_end%=:\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_mov_b64 exec, %[sv]"
+      : [pos] "+v"(pos), [lo] "+v"(lo), [hi] "+v"(hi), [vt] "+v"(vt), [tselb] "+v"(tselb), [ntok] "+v"(ntok),
+        [acc] "+v"(acc), [ckn] "+v"(ckn), [c1p] "+v"(c1p), [c1o] "+v"(c1o), [c2p] "+v"(c2p), [c2o] "+v"(c2o),
+        [c3p] "+v"(c3p), [c3o] "+v"(c3o), [e] "+v"(e), [bits] "=&v"(bits), [a] "=&v"(a), [nx] "=&v"(nx),
+        [x] "=&v"(x), [ex] "=&v"(ex), [val] "=&v"(val), [np] "=&v"(np), [tmp] "=&v"(tmp), [r15] "=&v"(r15),
+        [q] "=&v"(q), [p11] "=&v"(p11), [p12] "=&v"(p12), [p13] "=&v"(p13), [p14] "=&v"(p14), [p15] "=&v"(p15),
+        [d] "=&v"(d), [sh] "=&v"(sh), [sA] "=&s"(sA),
+        [sB] "=&s"(sB), [sC] "=&s"(sC), [sD] "=&s"(sD), [sE] "=&s"(sE), [sv] "=&s"(sv)
+      : [stop] "v"(stop2), [tabb] "s"(tabb), [stb] "s"(stb), [pkb] "s"(pkb), [sentb] "s"(sentb),
+        [sentd] "s"(sentd), [bad_e] "v"(bad_e)
+      : "vcc", "scc", "memory");
+  const uint32_t nck = ckn == CK1 ? 0u : ckn == CK2 ? 1u : ckn == CK3 ? 2u : 3u;
+  ck = nck == 3 ? Ckpt{c3p, c3o, c2p, c2o, c1p, c1o}
+     : nck == 2 ? Ckpt{c2p, c2o, c1p, c1o, NOPOS, 0}
+     : nck == 1 ? Ckpt{c1p, c1o, NOPOS, 0, NOPOS, 0}
+                : Ckpt{NOPOS, 0, NOPOS, 0, NOPOS, 0};
+  LaneRun r{LR_RUN, pos, ntok, ntok + (acc >> 12)};
+  if (vt == 0 && pos >= stop2) {  // cut at a token boundary
+    if (pos >= limit) r.st = LR_PAST;
+  } else {  // end of block, or an invalid code
+    r.st = (vt == 0 && (e & PE_EOB)) ? LR_EOB : LR_DEAD;
+    r.exit = pos + (e & 31);
+  }
+  return r;
+}
+
+#ifndef SBH_ASM_REDO
+#define SBH_ASM_REDO 1  // repair runs (RUN_REDO over the LDS stage) as the hand-written loop below
+#endif
+// RUN_REDO over the LDS stage as hand-written code (lane_run<RUN_REDO>'s results): spec_asm's
+// loop with the checkpoint recording replaced by the join test -- a run also stops at a token
+// boundary that is one of its pass-1 checkpoints (ck), and then takes that chain's rest (sp).
+__device__ __forceinline__ LaneRun redo_asm(const WaveSmem &t, const uint32_t *stage, uint32_t A, uint32_t stop,
+                                            uint32_t limit, const Ckpt &ck, const LaneRun &sp) {
+  const uint32_t stop2 = stop < limit ? stop : limit;
+  if (A >= stop2) return LaneRun{A >= limit ? LR_PAST : LR_RUN, A, 0, 0};
+  const uint32_t tabb = uni((uint32_t)reinterpret_cast<uintptr_t>(t.tab));
+  const uint32_t stb = uni((uint32_t)reinterpret_cast<uintptr_t>(stage) + 8u);
+  const uint32_t pkb = uni((uint32_t)reinterpret_cast<uintptr_t>(&t.pk[0][11]));
+  const uint32_t sentb = uni((uint32_t)reinterpret_cast<uintptr_t>(t.sent));
+  const uint32_t sentd = sentb + 288u * 4u;
+  uint32_t pos = A, lo = stage[A >> 5], hi = stage[(A >> 5) + 1];
+  uint32_t vt = 0, tselb = tabb, ntok = 0, acc = 0;
+  const uint32_t bad_e = 1u | PE_SPECIAL;
+  const uint32_t k1 = ck.p1, k2 = ck.p2, k3 = ck.p3;
+  uint32_t e = 0, bits, a, nx, x, ex, val, np, tmp, r15, q, p11, p12, p13, p14, p15, d, sh;
+  uint64_t sA, sB, sC, sD, sE, sv;
+  asm volatile(
+      "s_mov_b64 %[sv], exec\n"
+      "L_top%=:\n\t"
+      "v_alignbit_b32 %[bits], %[hi], %[lo], %[pos]\n\t"
+      "v_and_b32 %[a], 0x3ff, %[bits]\n\t"
+      "v_lshl_add_u32 %[a], %[a], 2, %[tselb]\n\t"
+      "ds_read_b32 %[e], %[a]\n\t"
+      "v_lshrrev_b32 %[a], 3, %[pos]\n\t"
+      "v_and_b32 %[a], -4, %[a]\n\t"
+      "v_add_u32 %[a], %[stb], %[a]\n\t"
+      "ds_read_b32 %[nx], %[a]\n\t"
+      // while the entry is in flight: token boundary (sA), cut (sC), checkpoint hit (sB)
+      "v_cmp_eq_u32 %[sA], 0, %[vt]\n\t"
+      "v_cmp_ge_u32 %[sC], %[pos], %[stop]\n\t"
+      "v_cmp_eq_u32 %[sB], %[pos], %[k1]\n\t"
+      "v_cmp_eq_u32 %[sE], %[pos], %[k2]\n\t"
+      "s_or_b64 %[sC], %[sC], %[sB]\n\t"
+      "v_cmp_eq_u32 %[sB], %[pos], %[k3]\n\t"
+      "s_or_b64 %[sC], %[sC], %[sE]\n\t"
+      "s_or_b64 %[sC], %[sC], %[sB]\n\t"
+      "s_and_b64 %[sC], %[sC], %[sA]\n"
+      "L_nock%=:\n\t"
+      "s_waitcnt lgkmcnt(1)\n\t"
+      "v_cmp_gt_i32 %[sD], 0, %[e]\n\t"  // special entries
+      "s_and_b64 %[sD], %[sD], exec\n\t"
+      "s_cbranch_scc0 L_nosp%=\n\t"
+      "v_and_b32 %[tmp], 0x4000, %[e]\n\t"  // PE_SLOW
+      "v_cmp_ne_u32 %[sB], 0, %[tmp]\n\t"
+      "s_and_b64 %[sB], %[sB], %[sD]\n\t"
+      "s_cbranch_scc0 L_nosp%=\n\t"
+      // long codes: the length is 11 + #{v in 11..14 : limit(v) <= rev15}; invalid past limit(15)
+      "s_and_saveexec_b64 %[sB], %[sB]\n\t"
+      "v_bfrev_b32 %[r15], %[bits]\n\t"
+      "v_lshrrev_b32 %[r15], 17, %[r15]\n\t"
+      "v_lshrrev_b32 %[q], 6, %[vt]\n\t"  // pk[kind]: 64 bytes per kind
+      "v_add_u32 %[q], %[pkb], %[q]\n\t"
+      "ds_read_b32 %[p11], %[q]\n\t"  // pk[kind][11..15]
+      "ds_read_b32 %[p12], %[q] offset:4\n\t"
+      "ds_read_b32 %[p13], %[q] offset:8\n\t"
+      "ds_read_b32 %[p14], %[q] offset:12\n\t"
+      "ds_read_b32 %[p15], %[q] offset:16\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "v_mov_b32 %[d], %[p11]\n\t"
+      "v_mov_b32 %[sh], 4\n\t"
+      "v_lshrrev_b32 %[tmp], 16, %[p11]\n\t"
+      "v_cmp_le_u32 vcc, %[tmp], %[r15]\n\t"
+      "s_nop 1\n\t"
+      "v_cndmask_b32_e32 %[d], %[d], %[p12], vcc\n\t"
+      "v_cndmask_b32_e64 %[sh], %[sh], 3, vcc\n\t"
+      "v_lshrrev_b32 %[tmp], 16, %[p12]\n\t"
+      "v_cmp_le_u32 vcc, %[tmp], %[r15]\n\t"
+      "s_nop 1\n\t"
+      "v_cndmask_b32_e32 %[d], %[d], %[p13], vcc\n\t"
+      "v_cndmask_b32_e64 %[sh], %[sh], 2, vcc\n\t"
+      "v_lshrrev_b32 %[tmp], 16, %[p13]\n\t"
+      "v_cmp_le_u32 vcc, %[tmp], %[r15]\n\t"
+      "s_nop 1\n\t"
+      "v_cndmask_b32_e32 %[d], %[d], %[p14], vcc\n\t"
+      "v_cndmask_b32_e64 %[sh], %[sh], 1, vcc\n\t"
+      "v_lshrrev_b32 %[tmp], 16, %[p14]\n\t"
+      "v_cmp_le_u32 vcc, %[tmp], %[r15]\n\t"
+      "s_nop 1\n\t"
+      "v_cndmask_b32_e32 %[d], %[d], %[p15], vcc\n\t"
+      "v_cndmask_b32_e64 %[sh], %[sh], 0, vcc\n\t"
+      "v_lshrrev_b32 %[tmp], %[sh], %[r15]\n\t"  // (d + (rev15 >> (15 - len))) & 0xffff
+      "v_add_u32 %[tmp], %[tmp], %[d]\n\t"
+      "v_and_b32 %[tmp], 0xffff, %[tmp]\n\t"
+      "v_min_u32 %[tmp], 0x13f, %[tmp]\n\t"  // (inside sent[]; an index past it is an invalid code, replaced below)
+      "v_cmp_ne_u32 vcc, 0, %[vt]\n\t"
+      "v_mov_b32 %[q], %[sentd]\n\t"
+      "v_mov_b32 %[d], %[sentb]\n\t"
+      "v_cndmask_b32_e32 %[q], %[d], %[q], vcc\n\t"
+      "v_lshl_add_u32 %[tmp], %[tmp], 2, %[q]\n\t"
+      "ds_read_b32 %[e], %[tmp]\n\t"
+      "v_lshrrev_b32 %[tmp], 16, %[p15]\n\t"
+      "v_cmp_ge_u32 vcc, %[r15], %[tmp]\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_nop 1\n\t"
+      "v_cndmask_b32_e32 %[e], %[e], %[bad_e], vcc\n\t"
+      "s_mov_b64 exec, %[sB]\n\t"
+      "v_cmp_gt_i32 %[sD], 0, %[e]\n"  // special after the long-code lookup
+      "L_nosp%=:\n\t"
+      // lanes at their cut or a special entry leave the loop
+      "s_or_b64 %[sD], %[sD], %[sC]\n\t"
+      "s_andn2_b64 exec, exec, %[sD]\n\t"
+      "s_cbranch_execz L_end%=\n\t"
+      "v_and_b32 %[tmp], 31, %[e]\n\t"
+      "v_bfe_u32 %[x], %[e], 5, 4\n\t"
+      "v_bfe_u32 %[ex], %[bits], %[e], %[x]\n\t"
+      "v_add3_u32 %[np], %[pos], %[tmp], %[x]\n\t"
+      "v_add_u32_sdwa %[val], %[ex], %[e] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+      "v_xor_b32 %[tmp], %[np], %[pos]\n\t"
+      "v_cmp_lt_u32 vcc, 31, %[tmp]\n\t"
+      "v_and_b32 %[vt], 0x1000, %[e]\n\t"
+      "v_mov_b32 %[pos], %[np]\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "v_cndmask_b32_e32 %[lo], %[lo], %[hi], vcc\n\t"
+      "v_cndmask_b32_e32 %[hi], %[hi], %[nx], vcc\n\t"
+      "v_addc_co_u32_e64 %[ntok], vcc, 0, %[ntok], %[sA]\n\t"
+      "v_add_u32 %[tselb], %[tabb], %[vt]\n\t"
+      "v_mad_u32_u24 %[acc], %[vt], %[val], %[acc]\n\t"
+      "s_branch L_top%=\n"
+      "L_end%=:\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_mov_b64 exec, %[sv]"
+      : [pos] "+v"(pos), [lo] "+v"(lo), [hi] "+v"(hi), [vt] "+v"(vt), [tselb] "+v"(tselb), [ntok] "+v"(ntok),
+        [acc] "+v"(acc), [e] "+v"(e), [bits] "=&v"(bits), [a] "=&v"(a), [nx] "=&v"(nx), [x] "=&v"(x),
+        [ex] "=&v"(ex), [val] "=&v"(val), [np] "=&v"(np), [tmp] "=&v"(tmp), [r15] "=&v"(r15), [q] "=&v"(q),
+        [p11] "=&v"(p11), [p12] "=&v"(p12), [p13] "=&v"(p13), [p14] "=&v"(p14), [p15] "=&v"(p15), [d] "=&v"(d),
+        [sh] "=&v"(sh), [sA] "=&s"(sA), [sB] "=&s"(sB), [sC] "=&s"(sC), [sD] "=&s"(sD), [sE] "=&s"(sE),
+        [sv] "=&s"(sv)
+      : [stop] "v"(stop2), [k1] "v"(k1), [k2] "v"(k2), [k3] "v"(k3), [tabb] "s"(tabb), [stb] "s"(stb),
+        [pkb] "s"(pkb), [sentb] "s"(sentb), [sentd] "s"(sentd), [bad_e] "v"(bad_e)
+      : "vcc", "scc", "memory");
+  LaneRun r{LR_RUN, pos, ntok, ntok + (acc >> 12)};
+  if (vt == 0 && (pos >= stop2 || pos == k1 || pos == k2 || pos == k3)) {  // cut at a token boundary
+    if (pos < stop2) {  // joined the pass-1 chain at a checkpoint
+      const bool one = pos == k1;
+      const bool two = pos == k2;
+      r.ntok += sp.ntok - (one ? CK1 : two ? CK2 : CK3);
+      r.nout += sp.nout - (one ? ck.o1 : two ? ck.o2 : ck.o3);
+      r.st = sp.st;
+      r.exit = sp.exit;
+    } else if (pos >= limit) {
+      r.st = LR_PAST;
+    }
+  } else {  // end of block, or an invalid code
+    r.st = (vt == 0 && (e & PE_EOB)) ? LR_EOB : LR_DEAD;
+    r.exit = pos + (e & 31);
+  }
+  return r;
+}
+
+#ifndef SBH_ASM_EMIT
+#define SBH_ASM_EMIT 1  // pass 3 (RUN_EMIT over the LDS stage) as the hand-written loop below
+#endif
+// RUN_EMIT over the LDS stage as hand-written code (lane_run<RUN_EMIT>'s results): the decode
+// loop of spec_asm without the checkpoints, each token stored once (a literal at its code, a
+// match at its distance code) through a 32-bit offset from the block's token base `tk` (wave-
+// uniform), and the too-far-back test of every distance accumulated as a lane mask.
+__device__ __forceinline__ void emit_asm(const WaveSmem &t, const uint32_t *stage, uint32_t A, uint32_t stop,
+                                         uint32_t limit, uint32_t *tk, uint32_t tidx, uint32_t out0, uint32_t &bad) {
+  const uint32_t stop2 = stop < limit ? stop : limit;
+  if (A >= stop2) return;
+  const uint32_t tabb = uni((uint32_t)reinterpret_cast<uintptr_t>(t.tab));
+  const uint32_t stb = uni((uint32_t)reinterpret_cast<uintptr_t>(stage) + 8u);
+  const uint32_t pkb = uni((uint32_t)reinterpret_cast<uintptr_t>(&t.pk[0][11]));
+  const uint32_t sentb = uni((uint32_t)reinterpret_cast<uintptr_t>(t.sent));
+  const uint32_t sentd = sentb + 288u * 4u;
+  const uint64_t tkp = reinterpret_cast<uint64_t>(tk);
+  const uint64_t tkb = (uint64_t)uni((uint32_t)tkp) | (uint64_t)uni((uint32_t)(tkp >> 32)) << 32;
+  uint32_t pos = A, lo = stage[A >> 5], hi = stage[(A >> 5) + 1];
+  uint32_t vt = 0, tselb = tabb, ntok = 0, acc = 0, ml = 0, voff = tidx * 4u, badv = 0;
+  const uint32_t om1 = out0 - 1u;
+  const uint32_t bad_e = 1u | PE_SPECIAL;
+  uint32_t e = 0, bits, a, nx, x, ex, val, np, tmp, r15, q, p11, p12, p13, p14, p15, d, sh, vtn, vtok, vb;
+  uint64_t sA, sB, sC, sD, sE, sL, sBad, sv;
+  asm volatile(
+      "s_mov_b64 %[sv], exec\n\t"
+      "s_mov_b64 %[sBad], 0\n"
+      "L_top%=:\n\t"
+      "v_alignbit_b32 %[bits], %[hi], %[lo], %[pos]\n\t"
+      "v_and_b32 %[a], 0x3ff, %[bits]\n\t"
+      "v_lshl_add_u32 %[a], %[a], 2, %[tselb]\n\t"
+      "ds_read_b32 %[e], %[a]\n\t"
+      "v_lshrrev_b32 %[a], 3, %[pos]\n\t"
+      "v_and_b32 %[a], -4, %[a]\n\t"
+      "v_add_u32 %[a], %[stb], %[a]\n\t"
+      "ds_read_b32 %[nx], %[a]\n\t"
+      // while the entry is in flight: token boundary (sA), cut (sC), checkpoint hit (sB)
+      "v_cmp_eq_u32 %[sA], 0, %[vt]\n\t"
+      "v_cmp_ge_u32 %[sC], %[pos], %[stop]\n\t"
+      "s_and_b64 %[sC], %[sC], %[sA]\n"
+      "L_nock%=:\n\t"
+      "s_waitcnt lgkmcnt(1)\n\t"
+      "v_cmp_gt_i32 %[sD], 0, %[e]\n\t"  // special entries
+      "s_and_b64 %[sD], %[sD], exec\n\t"
+      "s_cbranch_scc0 L_nosp%=\n\t"
+      "v_and_b32 %[tmp], 0x4000, %[e]\n\t"  // PE_SLOW
+      "v_cmp_ne_u32 %[sB], 0, %[tmp]\n\t"
+      "s_and_b64 %[sB], %[sB], %[sD]\n\t"
+      "s_cbranch_scc0 L_nosp%=\n\t"
+      // long codes: the length is 11 + #{v in 11..14 : limit(v) <= rev15}; invalid past limit(15)
+      "s_and_saveexec_b64 %[sB], %[sB]\n\t"
+      "v_bfrev_b32 %[r15], %[bits]\n\t"
+      "v_lshrrev_b32 %[r15], 17, %[r15]\n\t"
+      "v_lshrrev_b32 %[q], 6, %[vt]\n\t"  // pk[kind]: 64 bytes per kind
+      "v_add_u32 %[q], %[pkb], %[q]\n\t"
+      "ds_read_b32 %[p11], %[q]\n\t"  // pk[kind][11..15]
+      "ds_read_b32 %[p12], %[q] offset:4\n\t"
+      "ds_read_b32 %[p13], %[q] offset:8\n\t"
+      "ds_read_b32 %[p14], %[q] offset:12\n\t"
+      "ds_read_b32 %[p15], %[q] offset:16\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "v_mov_b32 %[d], %[p11]\n\t"
+      "v_mov_b32 %[sh], 4\n\t"
+      "v_lshrrev_b32 %[tmp], 16, %[p11]\n\t"
+      "v_cmp_le_u32 vcc, %[tmp], %[r15]\n\t"
+      "s_nop 1\n\t"
+      "v_cndmask_b32_e32 %[d], %[d], %[p12], vcc\n\t"
+      "v_cndmask_b32_e64 %[sh], %[sh], 3, vcc\n\t"
+      "v_lshrrev_b32 %[tmp], 16, %[p12]\n\t"
+      "v_cmp_le_u32 vcc, %[tmp], %[r15]\n\t"
+      "s_nop 1\n\t"
+      "v_cndmask_b32_e32 %[d], %[d], %[p13], vcc\n\t"
+      "v_cndmask_b32_e64 %[sh], %[sh], 2, vcc\n\t"
+      "v_lshrrev_b32 %[tmp], 16, %[p13]\n\t"
+      "v_cmp_le_u32 vcc, %[tmp], %[r15]\n\t"
+      "s_nop 1\n\t"
+      "v_cndmask_b32_e32 %[d], %[d], %[p14], vcc\n\t"
+      "v_cndmask_b32_e64 %[sh], %[sh], 1, vcc\n\t"
+      "v_lshrrev_b32 %[tmp], 16, %[p14]\n\t"
+      "v_cmp_le_u32 vcc, %[tmp], %[r15]\n\t"
+      "s_nop 1\n\t"
+      "v_cndmask_b32_e32 %[d], %[d], %[p15], vcc\n\t"
+      "v_cndmask_b32_e64 %[sh], %[sh], 0, vcc\n\t"
+      "v_lshrrev_b32 %[tmp], %[sh], %[r15]\n\t"  // (d + (rev15 >> (15 - len))) & 0xffff
+      "v_add_u32 %[tmp], %[tmp], %[d]\n\t"
+      "v_and_b32 %[tmp], 0xffff, %[tmp]\n\t"
+      "v_min_u32 %[tmp], 0x13f, %[tmp]\n\t"  // (inside sent[]; an index past it is an invalid code, replaced below)
+      "v_cmp_ne_u32 vcc, 0, %[vt]\n\t"
+      "v_mov_b32 %[q], %[sentd]\n\t"
+      "v_mov_b32 %[d], %[sentb]\n\t"
+      "v_cndmask_b32_e32 %[q], %[d], %[q], vcc\n\t"
+      "v_lshl_add_u32 %[tmp], %[tmp], 2, %[q]\n\t"
+      "ds_read_b32 %[e], %[tmp]\n\t"
+      "v_lshrrev_b32 %[tmp], 16, %[p15]\n\t"
+      "v_cmp_ge_u32 vcc, %[r15], %[tmp]\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_nop 1\n\t"
+      "v_cndmask_b32_e32 %[e], %[e], %[bad_e], vcc\n\t"
+      "s_mov_b64 exec, %[sB]\n\t"
+      "v_cmp_gt_i32 %[sD], 0, %[e]\n"  // special after the long-code lookup
+      "L_nosp%=:\n\t"
+      "s_or_b64 %[sD], %[sD], %[sC]\n\t"
+      "s_andn2_b64 exec, exec, %[sD]\n\t"
+      "s_cbranch_execz L_end%=\n\t"
+      "v_and_b32 %[tmp], 31, %[e]\n\t"
+      "v_bfe_u32 %[x], %[e], 5, 4\n\t"
+      "v_bfe_u32 %[ex], %[bits], %[e], %[x]\n\t"
+      "v_add3_u32 %[np], %[pos], %[tmp], %[x]\n\t"
+      "v_add_u32_sdwa %[val], %[ex], %[e] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+      "v_and_b32 %[vtn], 0x1000, %[e]\n\t"
+      "v_xor_b32 %[tmp], %[np], %[pos]\n\t"
+      "v_cmp_ne_u32 %[sL], 0, %[vtn]\n\t"  // a length code
+      "v_cmp_lt_u32 vcc, 31, %[tmp]\n\t"
+      "v_mov_b32 %[pos], %[np]\n\t"
+      // the token: a literal (byte << 8) or the match completed by this distance code
+      "v_lshlrev_b32 %[vtok], 8, %[val]\n\t"
+      "v_add_u32 %[tmp], 1, %[ml]\n\t"
+      "v_lshl_or_b32 %[np], %[tmp], 16, %[val]\n\t"
+      "v_or_b32 %[np], 0x80000000, %[np]\n\t"
+      "v_cndmask_b32_e64 %[vtok], %[np], %[vtok], %[sA]\n\t"
+      // too far back: a distance past the bytes before its match
+      "v_lshrrev_b32 %[vb], 12, %[acc]\n\t"
+      "v_sub_u32 %[vb], %[vb], %[ml]\n\t"
+      "v_add3_u32 %[vb], %[vb], %[ntok], %[om1]\n\t"
+      "v_cmp_gt_u32 %[sB], %[val], %[vb]\n\t"
+      "s_andn2_b64 %[sB], %[sB], %[sA]\n\t"
+      "s_or_b64 %[sBad], %[sBad], %[sB]\n\t"
+      "v_cndmask_b32_e64 %[ml], %[ml], %[val], %[sL]\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "v_cndmask_b32_e32 %[lo], %[lo], %[hi], vcc\n\t"
+      "v_cndmask_b32_e32 %[hi], %[hi], %[nx], vcc\n\t"
+      // store every code but a length code
+      "s_and_b64 %[sE], %[sA], %[sL]\n\t"
+      "s_mov_b64 %[sB], exec\n\t"
+      "s_andn2_b64 exec, exec, %[sE]\n\t"
+      "global_store_dword %[voff], %[vtok], %[tkb]\n\t"
+      "v_add_u32 %[voff], 4, %[voff]\n\t"
+      "s_mov_b64 exec, %[sB]\n\t"
+      "v_addc_co_u32_e64 %[ntok], vcc, 0, %[ntok], %[sA]\n\t"
+      "v_mov_b32 %[vt], %[vtn]\n\t"
+      "v_add_u32 %[tselb], %[tabb], %[vt]\n\t"
+      "v_mad_u32_u24 %[acc], %[vt], %[val], %[acc]\n\t"
+      "s_branch L_top%=\n"
+      "L_end%=:\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_mov_b64 exec, %[sv]\n\t"
+      "v_cndmask_b32_e64 %[badv], 0, 1, %[sBad]"
+      : [pos] "+v"(pos), [lo] "+v"(lo), [hi] "+v"(hi), [vt] "+v"(vt), [tselb] "+v"(tselb), [ntok] "+v"(ntok),
+        [acc] "+v"(acc), [ml] "+v"(ml), [voff] "+v"(voff), [badv] "+v"(badv), [e] "+v"(e), [bits] "=&v"(bits),
+        [a] "=&v"(a), [nx] "=&v"(nx), [x] "=&v"(x), [ex] "=&v"(ex), [val] "=&v"(val), [np] "=&v"(np),
+        [tmp] "=&v"(tmp), [r15] "=&v"(r15), [q] "=&v"(q), [p11] "=&v"(p11), [p12] "=&v"(p12), [p13] "=&v"(p13),
+        [p14] "=&v"(p14), [p15] "=&v"(p15), [d] "=&v"(d), [sh] "=&v"(sh), [vtn] "=&v"(vtn), [vtok] "=&v"(vtok),
+        [vb] "=&v"(vb), [sA] "=&s"(sA), [sB] "=&s"(sB), [sC] "=&s"(sC), [sD] "=&s"(sD), [sE] "=&s"(sE),
+        [sL] "=&s"(sL), [sBad] "=&s"(sBad), [sv] "=&s"(sv)
+      : [stop] "v"(stop2), [tabb] "s"(tabb), [stb] "s"(stb), [pkb] "s"(pkb), [sentb] "s"(sentb),
+        [sentd] "s"(sentd), [bad_e] "v"(bad_e), [om1] "v"(om1), [tkb] "s"(tkb)
+      : "vcc", "scc", "memory");
+  bad |= badv;
 }
 
 // The code-length part of a dynamic block header (RFC 1951 3.2.7) by one wave: the
@@ -1385,7 +1871,12 @@ __device__ __forceinline__ uint32_t inflate_par(SM &sm, const uint8_t *__restric
       if (rw.st == LR_RUN && rw.exit < stop) A = rw.exit;
     }
 #endif
+#if SBH_ASM_SPEC
+    LaneRun r = LDS ? spec_asm(sm.t, sm.stage, A, stop, limit, ck)
+                    : lane_run<RUN_SPEC>(sm.t, src, A, stop, limit, ck, none, nullptr, 0, nobad);
+#else
     LaneRun r = lane_run<RUN_SPEC>(sm.t, src, A, stop, limit, ck, none, nullptr, 0, nobad);
+#endif
     const LaneRun r1 = r;  // the pass-1 chain's result: a redo that joins it at a checkpoint takes its rest
     sm.exitv[tid] = r.st == LR_RUN ? r.exit : NOPOS;
     // pass 2: repair rounds until every lane starts where its left neighbour exits.
@@ -1411,7 +1902,12 @@ __device__ __forceinline__ uint32_t inflate_par(SM &sm, const uint8_t *__restric
       __syncthreads();
       if (changed) {
         A = nA;
+#if SBH_ASM_REDO
+        r = LDS ? redo_asm(sm.t, sm.stage, A, stop, limit, ck, r1)
+                : lane_run<RUN_REDO>(sm.t, src, A, stop, limit, ck, r1, nullptr, 0, nobad);
+#else
         r = lane_run<RUN_REDO>(sm.t, src, A, stop, limit, ck, r1, nullptr, 0, nobad);
+#endif
         sm.exitv[tid] = r.st == LR_RUN ? r.exit : NOPOS;
       }
       const bool again = __syncthreads_or(changed);
@@ -1458,8 +1954,14 @@ __device__ __forceinline__ uint32_t inflate_par(SM &sm, const uint8_t *__restric
     if (k >= NT || eob_end == NOPOS || otot > usize - out) return PAR_FAIL;
     // pass 3: emit
     uint32_t bad = 0;
-    if (tid <= k)
-      lane_run<RUN_EMIT>(sm.t, src, A, stop, limit, ck, none, tk + ntok + tpre, out_before + out + opre, bad);
+    if (tid <= k) {
+#if SBH_ASM_EMIT
+      if (LDS)
+        emit_asm(sm.t, sm.stage, A, stop, limit, tk + ntok, tpre, out_before + out + opre, bad);
+      else
+#endif
+        lane_run<RUN_EMIT>(sm.t, src, A, stop, limit, ck, none, tk + ntok + tpre, out_before + out + opre, bad);
+    }
     if (__syncthreads_or(bad)) return PAR_FAIL;
 #ifdef SBH_HUFF_PROBE
     if (tid == 0) atomicAdd(&hp_acc[4], __builtin_readcyclecounter() - tp3);

@@ -13,6 +13,6 @@ step() {  # name, seconds, command...
 }
 A=spark-bam_amd/build/ab
 step gputests 400 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
-step abB 300 python -u tools/ab_inflate.py --records 4000000 $A/lib_base.so "$@"
-step abD 200 python -u tools/ab_inflate.py --config D --records 25000 $A/lib_base.so
-step abE 200 python -u tools/ab_inflate.py --config E --records 2000000 $A/lib_base.so
+step abB 300 python -u tools/ab_inflate.py --records 4000000 $A/lib_v2.so $A/lib_sp.so
+step abD 200 python -u tools/ab_inflate.py --config D --records 25000 $A/lib_v2.so
+step abE 200 python -u tools/ab_inflate.py --config E --records 2000000 $A/lib_v2.so
