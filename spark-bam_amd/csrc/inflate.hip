@@ -2285,6 +2285,63 @@ __device__ __forceinline__ uint4 pack8_u16(const uint32_t *c) {
                     __builtin_amdgcn_perm(c[5], c[4], 0x05040100u), __builtin_amdgcn_perm(c[7], c[6], 0x05040100u));
 }
 
+#ifndef SBH_ASM_CHASE
+#define SBH_ASM_CHASE 1  // k_lz's pointer chase as the hand-written loop below
+#endif
+// k_lz's pointer chase for one half granule (8 slots) as hand-written code, the same rounds as
+// the C++ loop: every pointer at or past the pass start pb is replaced by its target's slot
+// value (u16 LDS reads at 2 * max(c, pb) + p16 - 2 * abase), the 8 slots written back as
+// 16 bytes, until no pointer of the lane moved to another in-pass position.  5 vector + 3
+// scalar instructions per pointer and round (the compiler's version: ~9 and ~3, plus a
+// register rotation of the 8 pointers every round).
+__device__ __forceinline__ void chase8_asm(uint32_t (&c)[8], uint32_t pend, uint32_t pb, uint32_t off,
+                                           uint32_t waddr) {
+  const uint32_t sel = 0x05040100u;  // v_perm: the low halves of two dwords
+  uint32_t a0, a1, a2, a3, a4, a5, a6, a7, r0, r1, r2, r3, r4, r5, r6, r7;
+  uint64_t sv, sm, sx, sy, sc;
+#define SBH_CH_ADDR(k) "v_max_u32 %[a" #k "], %[pb], %[c" #k "]\n\t" \
+                       "v_lshl_add_u32 %[a" #k "], %[a" #k "], 1, %[off]\n\t" \
+                       "ds_read_u16 %[r" #k "], %[a" #k "]\n\t"
+#define SBH_CH_STEP(k, w) "s_waitcnt lgkmcnt(" #w ")\n\t" \
+                          "v_cmp_le_u32 vcc, %[pb], %[c" #k "]\n\t" \
+                          "v_cmp_ne_u32 %[sx], %[r" #k "], %[c" #k "]\n\t" \
+                          "v_cmp_le_u32 %[sy], %[pb], %[r" #k "]\n\t" \
+                          "s_and_b64 %[sx], %[sx], vcc\n\t" \
+                          "s_and_b64 %[sx], %[sx], %[sy]\n\t" \
+                          "s_or_b64 %[sc], %[sc], %[sx]\n\t" \
+                          "v_cndmask_b32_e32 %[c" #k "], %[c" #k "], %[r" #k "], vcc\n\t"
+  asm volatile(
+      "s_mov_b64 %[sv], exec\n\t"
+      "v_cmp_ne_u32 %[sm], 0, %[pend]\n\t"
+      "s_and_b64 exec, exec, %[sm]\n\t"
+      "s_cbranch_execz L_chend%=\n"
+      "L_round%=:\n\t"
+      SBH_CH_ADDR(0) SBH_CH_ADDR(1) SBH_CH_ADDR(2) SBH_CH_ADDR(3)
+      SBH_CH_ADDR(4) SBH_CH_ADDR(5) SBH_CH_ADDR(6) SBH_CH_ADDR(7)
+      "s_mov_b64 %[sc], 0\n\t"
+      SBH_CH_STEP(0, 7) SBH_CH_STEP(1, 6) SBH_CH_STEP(2, 5) SBH_CH_STEP(3, 4)
+      SBH_CH_STEP(4, 3) SBH_CH_STEP(5, 2) SBH_CH_STEP(6, 1) SBH_CH_STEP(7, 0)
+      "v_perm_b32 %[a0], %[c1], %[c0], %[sel]\n\t"
+      "v_perm_b32 %[a1], %[c3], %[c2], %[sel]\n\t"
+      "v_perm_b32 %[a2], %[c5], %[c4], %[sel]\n\t"
+      "v_perm_b32 %[a3], %[c7], %[c6], %[sel]\n\t"
+      "ds_write2_b32 %[waddr], %[a0], %[a1] offset1:1\n\t"
+      "ds_write2_b32 %[waddr], %[a2], %[a3] offset0:2 offset1:3\n\t"
+      "s_and_b64 exec, exec, %[sc]\n\t"
+      "s_cbranch_execnz L_round%=\n"
+      "L_chend%=:\n\t"
+      "s_mov_b64 exec, %[sv]"
+      : [c0] "+v"(c[0]), [c1] "+v"(c[1]), [c2] "+v"(c[2]), [c3] "+v"(c[3]), [c4] "+v"(c[4]), [c5] "+v"(c[5]),
+        [c6] "+v"(c[6]), [c7] "+v"(c[7]), [a0] "=&v"(a0), [a1] "=&v"(a1), [a2] "=&v"(a2), [a3] "=&v"(a3),
+        [a4] "=&v"(a4), [a5] "=&v"(a5), [a6] "=&v"(a6), [a7] "=&v"(a7), [r0] "=&v"(r0), [r1] "=&v"(r1),
+        [r2] "=&v"(r2), [r3] "=&v"(r3), [r4] "=&v"(r4), [r5] "=&v"(r5), [r6] "=&v"(r6), [r7] "=&v"(r7),
+        [sv] "=&s"(sv), [sm] "=&s"(sm), [sx] "=&s"(sx), [sy] "=&s"(sy), [sc] "=&s"(sc)
+      : [pend] "v"(pend), [pb] "s"(pb), [off] "s"(off), [waddr] "v"(waddr), [sel] "s"(sel)
+      : "vcc", "scc", "memory");
+#undef SBH_CH_ADDR
+#undef SBH_CH_STEP
+}
+
 // LZ77 resolution of one block per workgroup, LZ_CHUNK tokens per chunk (LZ_TPT consecutive
 // tokens per thread); bytes before the chunk are final.  A chunk whose output fits PTR_CAP
 // bytes (the common case) is resolved by pointer chasing: every byte gets the position it
@@ -2504,6 +2561,10 @@ __global__ __launch_bounds__(LZ_THREADS, 4) void k_lz(const uint8_t *__restrict_
         // Each round replaces every in-pass pointer by the one stored at its target (a
         // final slot -- a literal -- stores itself, so it stays); a lane stops once no
         // pointer of its own moved to another in-pass position.
+#if SBH_ASM_CHASE && !defined(SBH_LZ_DEBUG) && !defined(SBH_LZ_PROBE)
+        chase8_asm(c[hh], pend[hh], pb, uni((uint32_t)reinterpret_cast<uintptr_t>(p16)) - 2u * abase,
+                   (uint32_t)reinterpret_cast<uintptr_t>(p16) + 16u * h);
+#else
         bool more = pend[hh] != 0;
         while (__builtin_expect(more, 0)) {
 #ifdef SBH_LZ_DEBUG
@@ -2531,6 +2592,7 @@ __global__ __launch_bounds__(LZ_THREADS, 4) void k_lz(const uint8_t *__restrict_
           // slots keep pointing at themselves)
           reinterpret_cast<uint4 *>(p16)[h] = pack8_u16(c[hh]);
         }
+#endif
         uint32_t w[2];
 #pragma unroll
         for (uint32_t q = 0; q < 2; ++q) {
