@@ -974,6 +974,12 @@ constexpr uint32_t FCCAP = 256;               // close calls buffered per workgr
 #ifndef SBH_FULL_CTG_LDS
 #define SBH_FULL_CTG_LDS 1
 #endif
+#ifndef SBH_FULL_ACCF
+#define SBH_FULL_ACCF 1  // fast tiles: failures accounted without the success / unknown / rbe cases
+#endif
+#ifndef SBH_FULL_FAST
+#define SBH_FULL_FAST 1  // tiles far from a segment end: full_first_win (no end-of-stream cases)
+#endif
 constexpr uint32_t FCTG = 1024;               // contig lengths staged in LDS (more: read from global)
 constexpr uint32_t FULL_SLOW = 0xFFFFFFFFu;   // "take the exact path" (no valid word has all bits)
 constexpr uint32_t FULL_PASS = 0xFFFFFFFEu;   // the first record passes: the chain decides
@@ -1072,6 +1078,56 @@ __device__ __forceinline__ uint32_t full_first(const Src &s, const uint32_t *bna
   return f ? f : FULL_PASS;  // a passing first record: the chain decides
 }
 
+// getRefPosError without branches (PosChecker.scala:43-63): the four error bits are
+// independent tests -- idx < -1, idx >= n, pos < -1, and pos past the contig of a valid idx --
+// which is exactly the reference's if/else chain (each earlier case rules the later bits out).
+__device__ __forceinline__ uint32_t ref_pos_error_bf(int32_t idx, int32_t pos, const Ctg &c) {
+  const bool inr = (uint32_t)idx < (uint32_t)c.n;
+  const int32_t L = c.len[inr ? idx : 0];
+  return (idx < -1 ? 1u : 0u) | (idx >= c.n ? 2u : 0u) | (pos < -1 ? 4u : 0u) | (inr && pos > L ? 8u : 0u);
+}
+
+// Bytes past a position that full_first may read or judge against the stream end: fixed
+// fields, the longest name, the longest CIGAR.  A tile all of whose positions lie at least
+// this far before their segment's end (and inside [begin, end)) never meets an end-of-stream
+// rule, so full_first reduces to full_first_win there.
+constexpr uint64_t FULL_FAST_REACH = 36 + 255 + 4ull * 65535 + 4;
+
+// full_first for a position of a fast tile (see FULL_FAST_REACH): the same word, from 32-bit
+// window offsets and no end-of-stream cases (every read of the name is inside the staged
+// window: q < FTILE, q + 36 + 255 < FSN).
+__device__ __forceinline__ uint32_t full_first_win(const Src &s, const uint32_t *bname, const uint32_t *bop,
+                                                   uint32_t q, const Fixed &x, const Ctg &c, const OpIdx &oi) {
+  const int32_t rnl = (int32_t)(x.bmn & 0xff), nc = (int32_t)(x.fnc & 0xffff);
+  uint32_t f = ref_pos_error_bf(x.idx, x.pos, c) << 1;
+  f |= x.rem < implied_min_remaining(rnl, nc, x.seq_len) ? 1u << 18 : 0u;
+  f |= ref_pos_error_bf(x.nidx, x.npos, c) << 5;
+  uint32_t a = q + 36;  // window offset of the name / CIGAR
+  if (rnl < 2) {
+    f |= rnl == 0 ? 1u << 12 : 1u << 13;
+  } else {
+    const uint32_t z = a + (uint32_t)rnl - 1;  // name bytes [a, z), its NUL at z
+    if ((uint8_t)(s.lds32[z >> 2] >> (8 * (z & 3))) != 0) f |= 1u << 10;
+    else if (next_set(bname, a, z, ~0u) < z) f |= 1u << 11;
+    a = z + 1;
+  }
+  const uint32_t stop = a + 4u * (uint32_t)nc;  // (no stream end within reach: lim = nc)
+  const uint32_t hi = stop < FSN ? stop : FSN;
+  const uint32_t y = next_set(bop, a, hi, 0x11111111u << (a & 3));
+  bool cig_err = y < hi;
+  if (!cig_err && stop > hi) {  // ops past the window: the op index, else the exact path
+    if (!(oi.ob && s.s0 + a >= oi.base && s.s0 + stop <= oi.end)) return FULL_SLOW;
+    cig_err = op_scan(oi, s.s0 + a, s.s0 + stop) < s.s0 + stop;
+  }
+  if (cig_err) {
+    f |= 1u << 15;
+  } else if ((x.fnc & (4u << 16)) == 0 && (x.seq_len == 0 || nc == 0)) {
+    if (x.seq_len == 0) f |= 1u << 16;  // EmptyMapped(emptySeq, emptyCigar) field swap
+    if (nc == 0) f |= 1u << 17;
+  }
+  return f ? f : FULL_PASS;
+}
+
 __device__ __forceinline__ Fixed fixed_at(const uint32_t *lds32, uint32_t q) {
   const uint32_t *d = lds32 + (q >> 2);
   const uint32_t k = q & 3;
@@ -1118,10 +1174,19 @@ __device__ uint32_t chain_full(const Src &s, const uint32_t *bname, const uint32
 
 __global__ __launch_bounds__(T, 5) void k_full(const uint8_t *__restrict__ U, uint64_t u_pad, uint64_t begin,
                                             uint64_t end, Segs sg, Ctg c, int32_t rtc, FullOut o, OpIdx oi) {
-#ifndef SBH_FULL_NREP
-#define SBH_FULL_NREP 4
+#ifndef SBH_FULL_PACKED
+#define SBH_FULL_PACKED 0  // 1: Counts replicas as 16-bit counter pairs (A/B: 7.53 -> 7.72 ms, not kept)
 #endif
-  constexpr uint32_t NREP = SBH_FULL_NREP, REP = 21 * 19 + 2;  // histogram replicas (odd stride: replica
+#ifndef SBH_FULL_NREP
+#define SBH_FULL_NREP (SBH_FULL_PACKED ? 8 : 4)
+#endif
+  // Counts histogram replicas, one per lane residue.  Packed: a row of 10 words per nnz, flags 2w
+  // and 2w + 1 as the low / high 16 bits of word w (a replica counts at most FTILE positions, so
+  // 16 bits hold it): the same LDS as 4 unpacked replicas gives 8, halving the lanes that add to
+  // one address in one instruction, and a failing position adds once per flag pair, not per flag.
+  constexpr uint32_t RW = SBH_FULL_PACKED ? 10 : 19;  // words per nnz row
+  static_assert(!SBH_FULL_PACKED || FTILE < 65536, "16-bit replica counters");
+  constexpr uint32_t NREP = SBH_FULL_NREP, REP = 21 * RW + (SBH_FULL_PACKED ? 1 : 2);  // (odd stride: replica
                                                                  // bases on distinct banks)
   constexpr uint32_t SLOWCAP = 512;
   __shared__ uint4 ldsv[FNV];
@@ -1187,12 +1252,46 @@ __global__ __launch_bounds__(T, 5) void k_full(const uint8_t *__restrict__ U, ui
 #ifdef SBH_FULL_NOHIST  // A/B: the check without its aggregation (tools/full_ab.py)
     if (nnz != 77) return;
 #endif
-    uint32_t *row = myhist + nnz * 19;
+    uint32_t *row = myhist + nnz * RW;
+#if SBH_FULL_PACKED
+    while (f) {
+      const uint32_t w = __builtin_ctz(f) >> 1;
+      const uint32_t pr = (f >> (2 * w)) & 3u;
+      atomicAdd(&row[w], (pr & 1u) | (pr >> 1) << 16);
+      f &= ~(3u << (2 * w));
+    }
+#else
     while (f) {
       atomicAdd(&row[__builtin_ctz(f)], 1u);
       f &= f - 1;
     }
+#endif
     if (rbe > 0 && rbe < 64) atomicAdd(&o.rbe[nnz * 64 + rbe], 1ull);  // rare: positions past a record
+    if (nnz <= 2) {
+      const uint32_t slot = atomicAdd(&ncl, 1u);
+      if (slot < FCCAP) {
+        cpos[slot] = p;
+        cword[slot] = r;
+      } else {
+        const unsigned long long gs = atomicAdd(o.close_n, 1ull);
+        if (gs < o.close_cap) { o.close_pos[gs] = p; o.close_word[gs] = r; }
+      }
+    }
+  };
+  // account() for a first-record failure of a fast tile: never success, unknown, TooFewFixed-
+  // BlockBytes alone or a readsBeforeError count, so only the Counts row and close calls
+  auto account_fail = [&](uint64_t p, uint32_t r) {
+    if (o.words) o.words[p - begin] = r;
+    uint32_t f = r;  // (a fast tile's failure word has no high bits)
+    const uint32_t nnz = __popc(f);
+#ifdef SBH_FULL_NOHIST
+    if (nnz != 77) return;
+#endif
+    uint32_t *row = myhist + nnz * RW;
+    while (f) {
+      atomicAdd(&row[__builtin_ctz(f)], 1u);
+      f &= f - 1;
+    }
     if (nnz <= 2) {
       const uint32_t slot = atomicAdd(&ncl, 1u);
       if (slot < FCCAP) {
@@ -1209,7 +1308,61 @@ __global__ __launch_bounds__(T, 5) void k_full(const uint8_t *__restrict__ U, ui
     *total = p < e0 ? e0 : sg.end[kseg];
     *open = sg.open_last && kseg == sg.n - 1;
   };
-  for (uint32_t step = 0; step < FTILE / (FPL * T); ++step) {
+  // a tile inside [begin, end) whose every position is FULL_FAST_REACH before its segment's
+  // end meets no end-of-stream rule: its positions take full_first_win
+  const bool fast = SBH_FULL_FAST && rtc > 0 && s0 >= begin && s0 + FTILE <= end &&
+                    s0 + FTILE + FULL_FAST_REACH <= e0;
+  if (fast) {
+    // queue overflows (more record starts in the tile than slowq holds) are kept as bits and
+    // decided after the sweep, so the exact path is not inlined into every unrolled position
+    uint32_t ovf = 0;
+    for (uint32_t step = 0; step < FTILE / (FPL * T); ++step) {
+      const uint32_t j = threadIdx.x + step * T;
+      const uint4 v0 = ldsv[j], v1 = ldsv[j + 1], v2 = ldsv[j + 2];
+      const uint32_t D[12] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w};
+#pragma unroll
+      for (uint32_t b = 0; b < 4; ++b) {  // dword b of the lane's 16 bytes (register-indexed: unrolled)
+#pragma unroll 1
+        for (uint32_t sh = 0; sh < 4; ++sh) {  // byte in the dword (a shift: rolled)
+          const uint32_t q = 16 * j + 4 * b + sh;
+          Fixed x;
+          x.rem = (int32_t)__builtin_amdgcn_alignbyte(D[b + 1], D[b], sh);
+          x.idx = (int32_t)__builtin_amdgcn_alignbyte(D[b + 2], D[b + 1], sh);
+          x.pos = (int32_t)__builtin_amdgcn_alignbyte(D[b + 3], D[b + 2], sh);
+          x.bmn = __builtin_amdgcn_alignbyte(D[b + 4], D[b + 3], sh);
+          x.fnc = __builtin_amdgcn_alignbyte(D[b + 5], D[b + 4], sh);
+          x.seq_len = (int32_t)__builtin_amdgcn_alignbyte(D[b + 6], D[b + 5], sh);
+          x.nidx = (int32_t)__builtin_amdgcn_alignbyte(D[b + 7], D[b + 6], sh);
+          x.npos = (int32_t)__builtin_amdgcn_alignbyte(D[b + 8], D[b + 7], sh);
+          const uint32_t r = full_first_win(s, bname, bop, q, x, c, oi);
+          if (r == FULL_SLOW || r == FULL_PASS) {  // record starts, long CIGARs: the balanced pass below
+            const uint32_t qi = atomicAdd(&nslow, 1u);
+            if (qi < SLOWCAP) slowq[qi] = q;
+            else ovf |= 1u << (16 * step + 4 * b + sh);
+            continue;
+          }
+#if SBH_FULL_ACCF
+          account_fail(s0 + q, r);
+#else
+          account(s0 + q, r);
+#endif
+        }
+      }
+    }
+    static_assert(FTILE / (FPL * T) * FPL <= 32, "overflow bits fit a word");
+    while (ovf) {
+      const uint32_t i = __builtin_ctz(ovf);
+      ovf &= ovf - 1;
+      const uint32_t q = 16 * (threadIdx.x + (i / 16) * T) + (i & 15);
+      const uint64_t p = s0 + q;
+      uint64_t total;
+      bool open;
+      where(p, &total, &open);
+      const uint32_t rc = chain_full(s, bname, bop, p, total, open, c, rtc, oi);
+      account(p, rc == FULL_SLOW ? full_at(s, p, total, open, c, rtc, oi) : rc);
+    }
+  }
+  for (uint32_t step = 0; step < (fast ? 0u : FTILE / (FPL * T)); ++step) {
     const uint32_t j = threadIdx.x + step * T;  // this lane's 16 positions: window bytes 16j..16j+15
     const uint4 v0 = ldsv[j], v1 = ldsv[j + 1], v2 = ldsv[j + 2];
     const uint32_t D[12] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w};
@@ -1266,7 +1419,12 @@ __global__ __launch_bounds__(T, 5) void k_full(const uint8_t *__restrict__ U, ui
   for (uint32_t i = threadIdx.x; i < 21 * 19; i += T) {
     uint32_t t = 0;
 #pragma unroll
-    for (uint32_t r = 0; r < NREP; ++r) t += hist[r * REP + i];
+    for (uint32_t r = 0; r < NREP; ++r)
+#if SBH_FULL_PACKED
+      t += (hist[r * REP + (i / 19) * RW + (i % 19) / 2] >> (16 * ((i % 19) & 1))) & 0xffffu;
+#else
+      t += hist[r * REP + i];
+#endif
     if (t) atomicAdd(&o.counts[i], (unsigned long long)t);
   }
   if (threadIdx.x == 0 && nsucc) atomicAdd(o.n_success, (unsigned long long)nsucc);
