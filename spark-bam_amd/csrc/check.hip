@@ -974,6 +974,9 @@ constexpr uint32_t FCCAP = 256;               // close calls buffered per workgr
 #ifndef SBH_FULL_CTG_LDS
 #define SBH_FULL_CTG_LDS 1
 #endif
+#ifndef SBH_FULL_RUN
+#define SBH_FULL_RUN 0  // 1: Counts rows of equal consecutive failure words added once per run (A/B: 7.44 -> 7.50 ms, off)
+#endif
 #ifndef SBH_FULL_ACCF
 #define SBH_FULL_ACCF 1  // fast tiles: failures accounted without the success / unknown / rbe cases
 #endif
@@ -1280,18 +1283,43 @@ __global__ __launch_bounds__(T, 5) void k_full(const uint8_t *__restrict__ U, ui
   };
   // account() for a first-record failure of a fast tile: never success, unknown, TooFewFixed-
   // BlockBytes alone or a readsBeforeError count, so only the Counts row and close calls
+  // Counts rows of a run of equal failure words are added once with the run's length: inside
+  // quality strings consecutive positions mostly fail the same checks (every field is ASCII)
+#if SBH_FULL_RUN
+  uint32_t run_f = 0, run_n = 0;
+  auto run_flush = [&]() {
+    if (run_n) {
+      uint32_t f = run_f;
+      uint32_t *row = myhist + __popc(f) * RW;
+      while (f) {
+        atomicAdd(&row[__builtin_ctz(f)], run_n);
+        f &= f - 1;
+      }
+    }
+  };
+#endif
   auto account_fail = [&](uint64_t p, uint32_t r) {
     if (o.words) o.words[p - begin] = r;
-    uint32_t f = r;  // (a fast tile's failure word has no high bits)
-    const uint32_t nnz = __popc(f);
+    const uint32_t nnz = __popc(r);  // (a fast tile's failure word has no high bits)
 #ifdef SBH_FULL_NOHIST
     if (nnz != 77) return;
 #endif
+#if SBH_FULL_RUN
+    if (r == run_f) {
+      ++run_n;
+    } else {
+      run_flush();
+      run_f = r;
+      run_n = 1;
+    }
+#else
+    uint32_t f = r;
     uint32_t *row = myhist + nnz * RW;
     while (f) {
       atomicAdd(&row[__builtin_ctz(f)], 1u);
       f &= f - 1;
     }
+#endif
     if (nnz <= 2) {
       const uint32_t slot = atomicAdd(&ncl, 1u);
       if (slot < FCCAP) {
@@ -1349,6 +1377,9 @@ __global__ __launch_bounds__(T, 5) void k_full(const uint8_t *__restrict__ U, ui
         }
       }
     }
+#if SBH_FULL_RUN
+    run_flush();
+#endif
     static_assert(FTILE / (FPL * T) * FPL <= 32, "overflow bits fit a word");
     while (ovf) {
       const uint32_t i = __builtin_ctz(ovf);

@@ -2207,10 +2207,13 @@ __global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__rest
 
 // The rest of a block k_huff deferred (INF_TAIL: a short final deflate block, typically),
 // by one wave per block: that block's header and the lane-parallel passes over 64 lanes,
-// with the remaining compressed bytes staged from the tail's first dword (4 KiB; longer
+// with the remaining compressed bytes staged from the tail's first dword (1 KiB; longer
 // tails read global memory).  The tokens continue at tok[ntok]; anything the fast path
 // does not prove leaves INF_SERIAL, and the serial decoder redoes the whole block.
-constexpr uint32_t TAIL_DW = 1024;
+#ifndef SBH_TAIL_DW
+#define SBH_TAIL_DW 256  // (A/B: 1024 -> 256 dwords: k_huff incl. tail 2.324 -> 2.214 ms at 4 M records; more tails per CU)
+#endif
+constexpr uint32_t TAIL_DW = SBH_TAIL_DW;
 using TailSmem = HuffSmemT<WAVE, TAIL_DW>;
 __global__ __launch_bounds__(WAVE) void k_huff_tail(const uint8_t *__restrict__ comp, DevBlocks bl, uint64_t nblocks,
                                                     uint32_t *__restrict__ tok) {
