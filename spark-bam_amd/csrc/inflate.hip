@@ -1673,15 +1673,31 @@ __device__ __forceinline__ bool hdr_walk(SM &t, const S &src, uint32_t p, uint32
     const uint32_t xv = __builtin_amdgcn_ubfe(b, L, xb);
     const uint32_t rep = sym < 16 ? 1 : sym == 16 ? 3 + xv : sym == 17 ? 3 + xv : 11 + xv;
     const uint32_t pack = (L + xb) | (rep << 8);
-    // serial part: the chain of symbol starts through this window
+    // serial part: the chain of symbol starts through this window.  (symbol index << 8 | bit
+    // offset) advances by one scalar add per symbol (pack = bits | rep << 8; the offset stays
+    // below 256), and both exit tests read that one word -- the walk is k_hdr's scalar hot loop
     uint64_t M = 0;
-    uint32_t o = 0, i0 = i;
-    while (o < WAVE && i < total) {
-      const uint32_t inf = __builtin_amdgcn_readlane(pack, o);
-      M |= 1ull << o;
-      o += inf & 255;
-      i += inf >> 8;
-    }
+    const uint32_t i0 = i, tot8 = uni(total << 8);
+    uint32_t oi = uni(i0 << 8), inf, tw;
+    // (v_readlane and s_bitset1_b64 take the offset's low 6 bits; the loop leaves once the
+    // offset reaches 64 or the symbols reach `total`; 7 scalar-unit instructions per symbol
+    // against the compiler's 12)
+    asm volatile(
+        "s_nop 3\n"  // (a lane select written by a VALU just before needs 4 wait states)
+        "L_walk%=:\n\t"
+        "v_readlane_b32 %[inf], %[pack], %[oi]\n\t"
+        "s_bitset1_b64 %[M], %[oi]\n\t"
+        "s_add_u32 %[oi], %[oi], %[inf]\n\t"
+        "s_and_b32 %[tw], %[oi], 0xc0\n\t"
+        "s_cbranch_scc1 L_wend%=\n\t"
+        "s_cmp_lt_u32 %[oi], %[tot8]\n\t"
+        "s_cbranch_scc1 L_walk%=\n"
+        "L_wend%=:"
+        : [M] "+s"(M), [oi] "+s"(oi), [inf] "=&s"(inf), [tw] "=&s"(tw)
+        : [pack] "v"(pack), [tot8] "s"(tot8)
+        : "scc");
+    const uint32_t o = oi & 0xffu;
+    i = oi >> 8;
     // parallel part: output index and value of each symbol, then its run of lengths
     const bool mine = (M >> lane) & 1;
     uint32_t ex;  // exclusive prefix of rep over the window's symbols
@@ -2288,6 +2304,9 @@ __device__ __forceinline__ uint4 pack8_u16(const uint32_t *c) {
                     __builtin_amdgcn_perm(c[5], c[4], 0x05040100u), __builtin_amdgcn_perm(c[7], c[6], 0x05040100u));
 }
 
+#ifndef SBH_LZ_NO_END_BAR
+#define SBH_LZ_NO_END_BAR 0  // k_lz: 1 = no barrier at a chunk's end (the next chunk's scan barrier orders it)
+#endif
 #ifndef SBH_ASM_CHASE
 #define SBH_ASM_CHASE 1  // k_lz's pointer chase as the hand-written loop below
 #endif
@@ -2614,11 +2633,20 @@ __global__ __launch_bounds__(LZ_THREADS, 4) void k_lz(const uint8_t *__restrict_
       __syncthreads();
     }
     base += chunk_len;
+#if !SBH_LZ_NO_END_BAR
     __syncthreads();  // slots / wsum are reused by the next chunk
+#endif
+    // (without it: the next chunk's slot writes all come after its scan's barrier, which every
+    // wave reaches only once done with this chunk; its wsum / sbits writes before that barrier
+    // touch nothing this chunk still reads -- wsum was read before this chunk's marks, sbits
+    // before its chase)
 #ifdef SBH_LZ_PROBE
     t_rounds += __builtin_readcyclecounter() - tb;
 #endif
   }
+#if SBH_LZ_NO_END_BAR
+  __syncthreads();  // the image is complete
+#endif
 #ifdef SBH_LZ_PROBE
   {
     uint32_t tot = 0;
