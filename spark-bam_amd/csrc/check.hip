@@ -1105,6 +1105,9 @@ __device__ __forceinline__ uint32_t full_first_win(const Src &s, const uint32_t 
   uint32_t f = ref_pos_error_bf(x.idx, x.pos, c) << 1;
   f |= x.rem < implied_min_remaining(rnl, nc, x.seq_len) ? 1u << 18 : 0u;
   f |= ref_pos_error_bf(x.nidx, x.npos, c) << 5;
+#ifdef SBH_FULL_FIXEDONLY  // A/B probe (timing only, results wrong): no read-name / CIGAR tests
+  if (f) return f;
+#endif
   uint32_t a = q + 36;  // window offset of the name / CIGAR
   if (rnl < 2) {
     f |= rnl == 0 ? 1u << 12 : 1u << 13;

@@ -984,7 +984,10 @@ struct HuffSmemT {
   WaveSmem t;               // tables (built by wave 0; the serial fallback's too)
   uint32_t stage[SDW + 8];  // the block's deflate dwords, from dword a0
   uint32_t exitv[NT];       // lane exits (NOPOS: the chain ended in the lane)
+  uint32_t exitv2[NT];      // (the repair rounds alternate between the two)
   uint32_t wsum[NT / WAVE];
+  uint32_t wsum2[NT / WAVE];
+  uint32_t wk[NT / WAVE], wkt[NT / WAVE], wko[NT / WAVE], wke[NT / WAVE];  // per wave: first ended lane
   uint32_t ctl[8];
 };
 using HuffSmem = HuffSmemT<HT, STAGE_DW>;
@@ -1863,7 +1866,6 @@ __device__ __forceinline__ uint32_t inflate_par(SM &sm, const uint8_t *__restric
     } else if (!par_header(sm, src, p, limit, fixed_built, wid, lane, p0, last)) {
       return PAR_FAIL;
     }
-    if (tid == 0) sm.ctl[3] = NT;
 
 #ifdef SBH_HUFF_PROBE
     const uint64_t tph = __builtin_readcyclecounter();
@@ -1894,7 +1896,11 @@ __device__ __forceinline__ uint32_t inflate_par(SM &sm, const uint8_t *__restric
     LaneRun r = lane_run<RUN_SPEC>(sm.t, src, A, stop, limit, ck, none, nullptr, 0, nobad);
 #endif
     const LaneRun r1 = r;  // the pass-1 chain's result: a redo that joins it at a checkpoint takes its rest
-    sm.exitv[tid] = r.st == LR_RUN ? r.exit : NOPOS;
+    // exits alternate between two arrays: a round reads one and writes the other, so the
+    // round's closing barrier (__syncthreads_or) is its only one
+    uint32_t *xa = sm.exitv, *xb = sm.exitv2;
+    xa[tid] = r.st == LR_RUN ? r.exit : NOPOS;
+    __syncthreads();
     // pass 2: repair rounds until every lane starts where its left neighbour exits.
     // A repair run stops as soon as it joins the lane's pass-1 chain (in any round: the
     // pass-1 result from a checkpoint on holds for every chain that reaches it).
@@ -1910,12 +1916,10 @@ __device__ __forceinline__ uint32_t inflate_par(SM &sm, const uint8_t *__restric
 #ifdef SBH_HUFF_PROBE
       ++nrounds;
 #endif
-      __syncthreads();
       // a lane keeps its speculation while its left neighbour's chain has ended (that
       // neighbour is then past the true end, or itself speculating and not yet repaired)
-      const uint32_t nA = tid == 0 ? p0 : sm.exitv[tid - 1];
+      const uint32_t nA = tid == 0 ? p0 : xa[tid - 1];
       const bool changed = nA != NOPOS && nA != A;
-      __syncthreads();
       if (changed) {
         A = nA;
 #if SBH_ASM_REDO
@@ -1924,27 +1928,69 @@ __device__ __forceinline__ uint32_t inflate_par(SM &sm, const uint8_t *__restric
 #else
         r = lane_run<RUN_REDO>(sm.t, src, A, stop, limit, ck, r1, nullptr, 0, nobad);
 #endif
-        sm.exitv[tid] = r.st == LR_RUN ? r.exit : NOPOS;
       }
+      xb[tid] = r.st == LR_RUN ? r.exit : NOPOS;
       const bool again = __syncthreads_or(changed);
+      uint32_t *const xt = xa;
+      xa = xb;
+      xb = xt;
 #ifdef SBH_HUFF_PROBE
       if (tid == 0 && nrounds == 1) atomicAdd(&hp_acc[12], __builtin_readcyclecounter() - tp1);
       if (tid == 0 && nrounds == 2) atomicAdd(&hp_acc[13], __builtin_readcyclecounter() - tp1);
 #endif
       if (!again) break;
     }
-    // the first lane whose chain ends decides the deflate block
-    if (r.st != LR_RUN) atomicMin(&sm.ctl[3], tid);
-    __syncthreads();
-    const uint32_t k = uni(sm.ctl[3]);
-    if (tid == k) sm.ctl[4] = (r.st == LR_EOB && r.exit <= limit) ? r.exit : NOPOS;
-    uint32_t ttot, otot;
-    const uint32_t tpre = block_scan<NT>(tid <= k ? r.ntok : 0, sm.wsum, &ttot);  // (syncs: ctl[4] visible)
-    __syncthreads();
-    const uint32_t opre = block_scan<NT>(tid <= k ? r.nout : 0, sm.wsum, &otot);
-    const uint32_t eob_end = uni(sm.ctl[4]);
-    ttot = uni(ttot);
-    otot = uni(otot);
+    // The first lane whose chain ends (k) decides the deflate block: the lanes up to it hold its
+    // tokens and bytes.  One barrier gives k, every lane's exclusive token / byte prefix (for
+    // tid <= k the same as a prefix over those lanes alone) and the block's totals (lane k's
+    // inclusive prefix): each wave posts its sums and its first ended lane with that lane's
+    // inclusive prefixes and end.
+    uint32_t k, tpre, opre, ttot, otot, eob_end;
+    {
+      const uint64_t em = __ballot(r.st != LR_RUN);
+      const uint32_t wf = em ? uni((uint32_t)__builtin_ctzll(em)) : (uint32_t)WAVE;
+      const uint32_t it = wave_incl_scan(r.ntok), io = wave_incl_scan(r.nout);
+      if (lane == WAVE - 1) {
+        sm.wsum[wid] = it;
+        sm.wsum2[wid] = io;
+      }
+      if (lane == (wf < WAVE ? wf : 0u)) {
+        sm.wk[wid] = wf < WAVE ? tid : NT;
+        sm.wkt[wid] = it;
+        sm.wko[wid] = io;
+        sm.wke[wid] = (r.st == LR_EOB && r.exit <= limit) ? r.exit : NOPOS;
+      }
+      __syncthreads();
+      uint32_t bt = 0, bo = 0, at = 0, ao = 0;
+      k = NT;
+      ttot = otot = 0;
+      eob_end = NOPOS;
+#pragma unroll
+      for (uint32_t w = 0; w < NT / WAVE; ++w) {
+        const uint32_t st = sm.wsum[w], so = sm.wsum2[w], wkw = sm.wk[w];
+        if (k == NT) {
+          if (wkw < NT) {
+            k = wkw;
+            ttot = at + sm.wkt[w];
+            otot = ao + sm.wko[w];
+            eob_end = sm.wke[w];
+          } else {
+            at += st;
+            ao += so;
+          }
+        }
+        if (w < wid) {
+          bt += st;
+          bo += so;
+        }
+      }
+      k = uni(k);
+      ttot = uni(ttot);
+      otot = uni(otot);
+      eob_end = uni(eob_end);
+      tpre = bt + it - r.ntok;
+      opre = bo + io - r.nout;
+    }
 #ifdef SBH_HUFF_PROBE
     const uint64_t tp3 = __builtin_readcyclecounter();
     if (tid == 0) {
@@ -2305,7 +2351,7 @@ __device__ __forceinline__ uint4 pack8_u16(const uint32_t *c) {
 }
 
 #ifndef SBH_LZ_NO_END_BAR
-#define SBH_LZ_NO_END_BAR 0  // k_lz: 1 = no barrier at a chunk's end (the next chunk's scan barrier orders it)
+#define SBH_LZ_NO_END_BAR 1  // k_lz: no barrier at a chunk's end (the next chunk's scan barrier orders it; A/B: k_lz -3% B, -2% D, -3% E)
 #endif
 #ifndef SBH_ASM_CHASE
 #define SBH_ASM_CHASE 1  // k_lz's pointer chase as the hand-written loop below
