@@ -12,6 +12,21 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 
+def counts_digest(r):
+    """sha1 prefix of Counts, rbe, success / close-call counts and the sorted close calls
+    (their order is atomic-slot order): variants must agree."""
+    import hashlib
+    import numpy as np
+    h = hashlib.sha1()
+    for k in ("counts", "rbe"):
+        h.update(np.ascontiguousarray(r[k]).tobytes())
+    h.update(f"{r['n_success']},{r['n_close']}".encode())
+    if r["n_close"] <= len(r["close_flat"]):  # (past close_cap, which calls are kept varies)
+        order = np.lexsort((r["close_word"], r["close_flat"]))
+        h.update(r["close_flat"][order].tobytes() + r["close_word"][order].tobytes())
+    return h.hexdigest()[:12]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--records", type=int, default=2_000_000)
@@ -34,11 +49,12 @@ def main():
             best = None
             for _ in range(3):
                 t0 = time.perf_counter()
-                r = sh.check_full(0, sh.flat_size, reads_to_check=rtc, close_cap=1 << 10)
+                r = sh.check_full(0, sh.flat_size, reads_to_check=rtc, close_cap=1 << 22)
                 dt = time.perf_counter() - t0
                 best = dt if best is None else min(best, dt)
             print(f"{os.path.basename(os.environ.get('SBH_LIB_PATH', '') or 'in-tree')} config {a.config} rtc {rtc}: {best * 1e3:.2f} ms for "
-                  f"{sh.flat_size} positions ({sh.flat_size / best / 1e9:.1f} GB/s), success {r['n_success']}",
+                  f"{sh.flat_size} positions ({sh.flat_size / best / 1e9:.1f} GB/s), success {r['n_success']}, "
+                  f"counts {counts_digest(r)}",
                   flush=True)
 
 
