@@ -243,11 +243,20 @@ __global__ void k_jump_mark(const int64_t *J, uint8_t *on, uint64_t nc) {
   if (i >= nc) return;
   if (on[i] && J[i] >= 0) on[J[i]] = 1;
 }
-__global__ void k_jump_double(const int64_t *J, int64_t *J2, uint64_t nc) {
+// One round of both: the mark and the doubling read only J, so they share a launch (a mark
+// that another thread of the same round sets early only spreads marks sooner -- still chain
+// nodes).  Half the launches of the two-kernel loop (each ~3 us of work behind ~7 us of
+// dispatch gap in the bench step's trace).
+__global__ void k_jump_round(const int64_t *J, int64_t *J2, uint8_t *on, uint64_t nc) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nc) return;
   const int64_t j = J[i];
-  J2[i] = j >= 0 ? J[j] : j;
+  if (j >= 0) {
+    if (on[i]) on[j] = 1;
+    J2[i] = J[j];
+  } else {
+    J2[i] = j;
+  }
 }
 
 // The chain starts at the candidate equal to start_rel (the scan may begin before it, so that
@@ -298,6 +307,20 @@ __global__ void k_chain_emit(const uint8_t *comp, uint64_t n, const uint64_t *ca
   usz[r] = (flags & (BLK_EMPTY | BLK_TRUNCATED)) || us > 65536u ? 0 : us;
   if (r + 1 == nchain)  // the bytes after the last block: the host checks the next header
     for (uint32_t j = 0; j < 18; ++j) next18[j] = p + cs + j < n ? comp[p + cs + j] : 0;
+}
+
+// The block table as one host-bound record (cstart, ustart as u64; csize, hsize, usize, flags
+// as u32; each a run of n): one device-to-host copy instead of six.
+__global__ void k_pack_blocks(DevBlocks bl, uint64_t n, uint64_t *out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[i] = bl.cstart[i];
+  out[n + i] = bl.ustart[i];
+  uint32_t *w = reinterpret_cast<uint32_t *>(out + 2 * n);
+  w[i] = bl.csize[i];
+  w[n + i] = bl.hsize[i];
+  w[2 * n + i] = bl.usize[i];
+  w[3 * n + i] = bl.flags[i];
 }
 
 __global__ void k_copy_u64(const uint64_t *a, uint64_t *b, uint64_t n) {
@@ -361,6 +384,11 @@ hipError_t launch_cand_write(const uint8_t *comp, uint64_t n, uint64_t from, con
 // Build the chain from cand[0] over nc candidates.  Scratch: J0, J1 (int64 x nc),
 // on (u8 x nc), v/rank (u64 x nc each), tmp (scan).  Writes the block table and
 // usz (u64 per block); returns the block count via *nchain (host).
+hipError_t launch_pack_blocks(DevBlocks bl, uint64_t n, uint64_t *out, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_pack_blocks, dim3(nblk(n, 256)), dim3(256), 0, st, bl, n, out);
+  return hipGetLastError();
+}
+
 hipError_t build_chain(const uint8_t *comp, uint64_t n, const uint64_t *cand, uint64_t nc, uint64_t start_rel,
                        int64_t *J0, int64_t *J1, uint8_t *on, uint64_t *v, uint64_t *rank, uint64_t *tmp,
                        DevBlocks bl, uint64_t *usz, uint64_t *nchain, uint8_t *next18, hipStream_t st) {
@@ -373,8 +401,7 @@ hipError_t build_chain(const uint8_t *comp, uint64_t n, const uint64_t *cand, ui
   hipLaunchKernelGGL(k_mark_start, dim3(1), dim3(64), 0, st, cand, nc, start_rel, on);
   int64_t *a = J0, *b = J1;
   for (uint64_t span = 1; span < nc; span <<= 1) {
-    hipLaunchKernelGGL(k_jump_mark, dim3(nblk(nc, T)), dim3(T), 0, st, a, on, nc);
-    hipLaunchKernelGGL(k_jump_double, dim3(nblk(nc, T)), dim3(T), 0, st, a, b, nc);
+    hipLaunchKernelGGL(k_jump_round, dim3(nblk(nc, T)), dim3(T), 0, st, a, b, on, nc);
     int64_t *t = a;
     a = b;
     b = t;

@@ -27,6 +27,7 @@ hipError_t launch_cand_count(const uint8_t *comp, uint64_t n, uint64_t from, uin
 hipError_t launch_cand_write(const uint8_t *comp, uint64_t n, uint64_t from, const uint64_t *counts,
                              const uint32_t *first, const uint64_t *offs, uint64_t *cand, uint64_t nchunks,
                              hipStream_t st);
+hipError_t launch_pack_blocks(DevBlocks bl, uint64_t n, uint64_t *out, hipStream_t st);
 hipError_t build_chain(const uint8_t *comp, uint64_t n, const uint64_t *cand, uint64_t nc, uint64_t start_rel,
                        int64_t *J0, int64_t *J1, uint8_t *on, uint64_t *v, uint64_t *rank, uint64_t *tmp, DevBlocks bl,
                        uint64_t *usz, uint64_t *nchain, uint8_t *next18, hipStream_t st);
@@ -102,7 +103,7 @@ struct sbh_shard {
   uint64_t index_start = 0, nblocks = 0, utotal = 0;
   DBuf<uint64_t> b_cstart, b_ustart, usz;
   DBuf<uint32_t> b_csize, b_hsize, b_usize, b_flags, b_status, b_ntok;
-  DBuf<uint64_t> counts, offs, cand, v, rank, tmp;
+  DBuf<uint64_t> counts, offs, cand, v, rank, tmp, blkpack;
   DBuf<uint32_t> cfirst;  // per scan chunk: offset of its first candidate
   uint64_t ncand = 0, cand_from = 0;  // header candidates in cand[] (shard-relative, >= cand_from)
   // sbh_index scans for header candidates from this file offset when it lies in
@@ -352,7 +353,7 @@ int sbh_shard_destroy(sbh_shard *sh) {
   (void)hipSetDevice(sh->ctx->device);
   (void)hipStreamSynchronize(sh->ctx->stream);
   sh->comp.release();
-  sh->b_cstart.release(); sh->b_ustart.release(); sh->usz.release();
+  sh->b_cstart.release(); sh->b_ustart.release(); sh->usz.release(); sh->blkpack.release();
   sh->b_csize.release(); sh->b_hsize.release(); sh->b_usize.release(); sh->b_flags.release();
   sh->b_status.release();
   sh->b_ntok.release();
@@ -492,12 +493,9 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
     uint64_t *cs = reinterpret_cast<uint64_t *>(sh->h_blk), *us = cs + nchain;
     uint32_t *csz = reinterpret_cast<uint32_t *>(us + nchain), *hsz = csz + nchain, *usz = hsz + nchain,
              *fl = usz + nchain;
-    HIPCHK(ctx, hipMemcpyAsync(cs, sh->b_cstart.p, nchain * 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipMemcpyAsync(us, sh->b_ustart.p, nchain * 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipMemcpyAsync(csz, sh->b_csize.p, nchain * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipMemcpyAsync(hsz, sh->b_hsize.p, nchain * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipMemcpyAsync(usz, sh->b_usize.p, nchain * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipMemcpyAsync(fl, sh->b_flags.p, nchain * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, sh->blkpack.ensure(4 * nchain));
+    HIPCHK(ctx, launch_pack_blocks(sh->dev_blocks(), nchain, sh->blkpack.p, st));
+    HIPCHK(ctx, hipMemcpyAsync(cs, sh->blkpack.p, nchain * 32, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipMemcpyAsync(nx, next18_dev, 18, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipStreamSynchronize(st));
     for (uint64_t i = 0; i < nchain; ++i)
