@@ -1478,10 +1478,14 @@ constexpr uint32_t FS_SPAN = 1024;  // words per chunk (4 per thread)
 __global__ __launch_bounds__(256) void k_first_set(const uint32_t *bits, uint64_t begin, uint64_t from,
                                                    uint64_t to, unsigned long long *best) {
   const uint64_t w0 = (from - begin) / 32, w_end = (to - begin + 31) / 32;
+  __shared__ unsigned long long wbest[256 / WAVE];
+  __shared__ uint32_t stop;
   for (uint64_t c = blockIdx.x;; c += gridDim.x) {
     const uint64_t cw = w0 + c * FS_SPAN;
-    if (cw >= w_end) return;
-    if (__hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < begin + 32 * cw) return;
+    if (cw >= w_end) return;  // (uniform)
+    if (threadIdx.x == 0) stop = __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < begin + 32 * cw;
+    __syncthreads();
+    if (stop) return;  // (uniform: read before the loop's closing barrier)
     const uint64_t w = cw + 4 * threadIdx.x;
     uint32_t v[4];
     if (w + 4 <= w_end && (w & 3) == 0) {
@@ -1501,10 +1505,19 @@ __global__ __launch_bounds__(256) void k_first_set(const uint32_t *bits, uint64_
         break;
       }
     }
-    // positions grow with the lane, so the wave's lowest hitting lane holds its minimum:
-    // one atomic per wave (a lane each made ~250 k atomics queue on one address)
+    // positions grow with the lane and the wave, so the workgroup's lowest hitting lane holds
+    // its minimum: one atomic per workgroup, and none when an earlier chunk already hit (the
+    // atomics of all workgroups on one address serialise: one per wave cost ~60 us per call)
     const uint64_t m = __ballot(hit != ~0ull);
-    if (m && (threadIdx.x & (WAVE - 1)) == (uint32_t)__builtin_ctzll(m)) atomicMin(best, hit);
+    if ((threadIdx.x & (WAVE - 1)) == 0) wbest[threadIdx.x / WAVE] = ~0ull;
+    if (m && (threadIdx.x & (WAVE - 1)) == (uint32_t)__builtin_ctzll(m)) wbest[threadIdx.x / WAVE] = hit;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long h = ~0ull;
+      for (uint32_t k = 0; k < 256 / WAVE && h == ~0ull; ++k) h = wbest[k];
+      if (h != ~0ull && h < __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(best, h);
+    }
+    __syncthreads();
   }
 }
 
@@ -1984,7 +1997,7 @@ hipError_t launch_first_set(const uint32_t *bits, uint64_t begin, uint64_t from,
                             unsigned long long *best, hipStream_t st) {
   if (to <= from) return hipSuccess;
   const uint64_t nw = (to - begin + 31) / 32 - (from - begin) / 32;
-  const uint32_t grid = (uint32_t)std::min<uint64_t>(ngrid(nw, FS_SPAN), 1024);
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(ngrid(nw, FS_SPAN), 256);
   hipLaunchKernelGGL(k_first_set, dim3(grid), dim3(256), 0, st, bits, begin, from, to, best);
   return hipGetLastError();
 }

@@ -1051,6 +1051,15 @@ struct Ckpt {
 };
 constexpr int RUN_SPEC = 0, RUN_REDO = 1, RUN_EMIT = 2;
 
+// The bytes up to the checkpoint a redo joined, as register selects: written as
+// `one ? ck.o1 : two ? ck.o2 : ck.o3` the compiler turned the select of fields into a select
+// of addresses, kept the checkpoints in scratch and read them back with a scratch load.
+__device__ __forceinline__ uint32_t ck_out(const Ckpt &ck, bool one, bool two) {
+  uint32_t o1 = ck.o1, o2 = ck.o2, o3 = ck.o3;
+  asm volatile("" : "+v"(o1), "+v"(o2), "+v"(o3));
+  return one ? o1 : two ? o2 : o3;
+}
+
 // Decode tokens from bit A while the position is below `stop`, as a two-state machine
 // (literal/length code, then distance code) so every lane runs the same instructions:
 // one table lookup per code, the extra bits taken straight from the entry.
@@ -1148,7 +1157,7 @@ __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, S src, uint32_t A
       const bool one = pos == ck.p1;
       const bool two = pos == ck.p2;
       r.ntok += sp.ntok - (one ? CK1 : two ? CK2 : CK3);
-      r.nout += sp.nout - (one ? ck.o1 : two ? ck.o2 : ck.o3);
+      r.nout += sp.nout - ck_out(ck, one, two);
       r.st = sp.st;
       r.exit = sp.exit;
     } else if (pos >= limit) {
@@ -1474,7 +1483,7 @@ __device__ __forceinline__ LaneRun redo_asm(const WaveSmem &t, const uint32_t *s
       const bool one = pos == k1;
       const bool two = pos == k2;
       r.ntok += sp.ntok - (one ? CK1 : two ? CK2 : CK3);
-      r.nout += sp.nout - (one ? ck.o1 : two ? ck.o2 : ck.o3);
+      r.nout += sp.nout - ck_out(ck, one, two);
       r.st = sp.st;
       r.exit = sp.exit;
     } else if (pos >= limit) {

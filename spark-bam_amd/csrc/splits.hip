@@ -183,12 +183,26 @@ __global__ __launch_bounds__(256) void k_split_popcount(const uint32_t *bits, ui
   if (c0 >= w_end) return;
   const uint64_t c1 = min(c0 + PC_WORDS, w_end);
   uint32_t c = 0;
-  for (uint64_t w = c0 + threadIdx.x; w < c1; w += 256) {
-    uint32_t v = bits[w];
+  auto count = [&](uint64_t w, uint32_t v) {
     const uint64_t p0 = begin + 32 * w;
     if (p0 < from) v &= ~0u << (uint32_t)(from - p0);
     if (p0 + 32 > to) v &= (to - p0) >= 32 ? ~0u : ((1u << (uint32_t)(to - p0)) - 1u);
     c += __popc(v);
+  };
+  const uint64_t a0 = (c0 + 3) & ~3ull, a1 = c1 & ~3ull;  // 16-byte loads over the aligned middle
+  if (a0 < a1) {
+    for (uint64_t w = c0 + threadIdx.x; w < a0; w += 256) count(w, bits[w]);
+#pragma unroll 4
+    for (uint64_t w = a0 + 4 * threadIdx.x; w < a1; w += 4 * 256) {
+      const uint4 q = *reinterpret_cast<const uint4 *>(bits + w);
+      count(w, q.x);
+      count(w + 1, q.y);
+      count(w + 2, q.z);
+      count(w + 3, q.w);
+    }
+    for (uint64_t w = a1 + threadIdx.x; w < c1; w += 256) count(w, bits[w]);
+  } else {
+    for (uint64_t w = c0 + threadIdx.x; w < c1; w += 256) count(w, bits[w]);
   }
   for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off);
   __shared__ uint32_t part[4];
