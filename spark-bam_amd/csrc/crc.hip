@@ -43,8 +43,12 @@ __global__ __launch_bounds__(256) void k_block_crc(const uint8_t *__restrict__ c
       const uint8_t *q = src + (uint64_t)lane * CRC_SEG;
       const uint32_t *g = reinterpret_cast<const uint32_t *>((uintptr_t)q & ~(uintptr_t)3);
       const uint32_t sh = (uint32_t)((uintptr_t)q & 3);
+      uint32_t lo = g[0];  // (each dword loaded once: the high one of a step is the next step's low one)
+#pragma unroll 8
       for (uint32_t k = 0; k < CRC_SEG; k += 4) {
-        const uint32_t w = __builtin_amdgcn_alignbyte(g[k / 4 + 1], g[k / 4], sh);  // bytes q[k .. k+3]
+        const uint32_t hi = g[k / 4 + 1];
+        const uint32_t w = __builtin_amdgcn_alignbyte(hi, lo, sh);  // bytes q[k .. k+3]
+        lo = hi;
         c = tab[(c ^ w) & 0xff] ^ (c >> 8);
         c = tab[(c ^ (w >> 8)) & 0xff] ^ (c >> 8);
         c = tab[(c ^ (w >> 16)) & 0xff] ^ (c >> 8);
