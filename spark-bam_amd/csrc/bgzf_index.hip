@@ -309,18 +309,16 @@ __global__ void k_chain_emit(const uint8_t *comp, uint64_t n, const uint64_t *ca
     for (uint32_t j = 0; j < 18; ++j) next18[j] = p + cs + j < n ? comp[p + cs + j] : 0;
 }
 
-// The block table as one host-bound record (cstart, ustart as u64; csize, hsize, usize, flags
-// as u32; each a run of n): one device-to-host copy instead of six.
-__global__ void k_pack_blocks(DevBlocks bl, uint64_t n, uint64_t *out) {
+// The block table as the host's sbh_block records (start = file offset, ustart, csize | hsize
+// << 32, usize | flags << 32): one device-to-host copy lands it in place.
+__global__ void k_pack_blocks(DevBlocks bl, uint64_t n, uint64_t file_off, uint64_t *out) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  out[i] = bl.cstart[i];
-  out[n + i] = bl.ustart[i];
-  uint32_t *w = reinterpret_cast<uint32_t *>(out + 2 * n);
-  w[i] = bl.csize[i];
-  w[n + i] = bl.hsize[i];
-  w[2 * n + i] = bl.usize[i];
-  w[3 * n + i] = bl.flags[i];
+  uint64_t *r = out + 4 * i;
+  r[0] = bl.cstart[i] + file_off;
+  r[1] = bl.ustart[i];
+  r[2] = (uint64_t)bl.csize[i] | (uint64_t)bl.hsize[i] << 32;
+  r[3] = (uint64_t)bl.usize[i] | (uint64_t)bl.flags[i] << 32;
 }
 
 __global__ void k_copy_u64(const uint64_t *a, uint64_t *b, uint64_t n) {
@@ -384,8 +382,8 @@ hipError_t launch_cand_write(const uint8_t *comp, uint64_t n, uint64_t from, con
 // Build the chain from cand[0] over nc candidates.  Scratch: J0, J1 (int64 x nc),
 // on (u8 x nc), v/rank (u64 x nc each), tmp (scan).  Writes the block table and
 // usz (u64 per block); returns the block count via *nchain (host).
-hipError_t launch_pack_blocks(DevBlocks bl, uint64_t n, uint64_t *out, hipStream_t st) {
-  if (n) hipLaunchKernelGGL(k_pack_blocks, dim3(nblk(n, 256)), dim3(256), 0, st, bl, n, out);
+hipError_t launch_pack_blocks(DevBlocks bl, uint64_t n, uint64_t file_off, uint64_t *out, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_pack_blocks, dim3(nblk(n, 256)), dim3(256), 0, st, bl, n, file_off, out);
   return hipGetLastError();
 }
 

@@ -13,6 +13,31 @@
 #include "sbh_internal.h"
 
 namespace sbh {
+// Pinned host storage for the host copy of the block table: the device writes it in the
+// sbh_block layout and one DMA lands it in place (no staging copy, no per-block host loop);
+// elements are default-initialised (resize() does not zero what the copy overwrites).
+template <class T>
+struct PinnedAlloc {
+  using value_type = T;
+  PinnedAlloc() = default;
+  template <class U>
+  PinnedAlloc(const PinnedAlloc<U> &) {}
+  T *allocate(size_t n) {
+    void *p = nullptr;
+    if (hipHostMalloc(&p, n * sizeof(T), hipHostMallocDefault) != hipSuccess) {
+      std::fprintf(stderr, "sparkbam: pinned host allocation of %zu bytes failed\n", n * sizeof(T));
+      std::abort();
+    }
+    return static_cast<T *>(p);
+  }
+  void deallocate(T *p, size_t) { (void)hipHostFree(p); }
+  template <class U>
+  void construct(U *p) { ::new (static_cast<void *>(p)) U; }
+  template <class U, class... A>
+  void construct(U *p, A &&...a) { ::new (static_cast<void *>(p)) U(static_cast<A &&>(a)...); }
+  bool operator==(const PinnedAlloc &) const { return true; }
+  bool operator!=(const PinnedAlloc &) const { return false; }
+};
 uint64_t scan_tmp_words(uint64_t n);
 hipError_t scan_exclusive_u64(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *tmp, hipStream_t st);
 hipError_t launch_chain_mark(const uint8_t *U, const uint32_t *bits, uint64_t begin, uint64_t from, uint64_t E,
@@ -27,7 +52,7 @@ hipError_t launch_cand_count(const uint8_t *comp, uint64_t n, uint64_t from, uin
 hipError_t launch_cand_write(const uint8_t *comp, uint64_t n, uint64_t from, const uint64_t *counts,
                              const uint32_t *first, const uint64_t *offs, uint64_t *cand, uint64_t nchunks,
                              hipStream_t st);
-hipError_t launch_pack_blocks(DevBlocks bl, uint64_t n, uint64_t *out, hipStream_t st);
+hipError_t launch_pack_blocks(DevBlocks bl, uint64_t n, uint64_t file_off, uint64_t *out, hipStream_t st);
 hipError_t build_chain(const uint8_t *comp, uint64_t n, const uint64_t *cand, uint64_t nc, uint64_t start_rel,
                        int64_t *J0, int64_t *J1, uint8_t *on, uint64_t *v, uint64_t *rank, uint64_t *tmp, DevBlocks bl,
                        uint64_t *usz, uint64_t *nchain, uint8_t *next18, hipStream_t st);
@@ -113,7 +138,7 @@ struct sbh_shard {
   uint64_t scan_from = ~0ull;
   DBuf<int64_t> J0, J1;
   DBuf<uint8_t> on;
-  std::vector<sbh_block> hb;
+  std::vector<sbh_block, PinnedAlloc<sbh_block>> hb;
   std::vector<uint64_t> seg_end;
   bool open_last = false, broken_end = false;
   DBuf<uint64_t> d_seg;
@@ -143,8 +168,6 @@ struct sbh_shard {
   DBuf<uint32_t> close_word;
   DBuf<unsigned long long> ctr;  // scratch counters
   unsigned long long *h_ctr = nullptr;  // pinned mirror
-  uint8_t *h_blk = nullptr;  // pinned staging of the block table (sbh_index), 32 B per block
-  uint64_t h_blk_cap = 0;
   uint64_t pad = 4096;
   // pipelined run (run_pipelined): extra streams, per-batch events, deferred positions
   hipStream_t s_lz = nullptr, s_eg = nullptr;
@@ -380,7 +403,6 @@ int sbh_shard_destroy(sbh_shard *sh) {
   sh->cm_pos.release(); sh->cm_wcnt.release(); sh->cm_wpre.release(); sh->cm_mark.release(); sh->cm_mpre.release();
   sh->cm_j.release(); sh->cm_j2.release(); sh->cm_j0.release();
   if (sh->h_ctr) (void)hipHostFree(sh->h_ctr);
-  if (sh->h_blk) (void)hipHostFree(sh->h_blk);
   delete sh;
   return SBH_OK;
 }
@@ -479,27 +501,14 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
   sh->ncand = nc;
   sh->cand_from = srel;
   // host copy of the block table (Pos mapping, segments)
-  sh->hb.assign(nchain, sbh_block{});
+  static_assert(sizeof(sbh_block) == 32, "k_pack_blocks writes 32-byte sbh_block records");
+  sh->hb.resize(nchain);
   if (nchain) {
-    // through pinned staging (pageable copies of ~32 B per block cost ~0.2 ms per GiB)
-    if (sh->h_blk_cap < nchain) {
-      if (sh->h_blk) (void)hipHostFree(sh->h_blk);
-      sh->h_blk = nullptr;
-      sh->h_blk_cap = 0;
-      const uint64_t cap = nchain + nchain / 4 + 1024;
-      HIPCHK(ctx, hipHostMalloc(reinterpret_cast<void **>(&sh->h_blk), cap * 32, hipHostMallocDefault));
-      sh->h_blk_cap = cap;
-    }
-    uint64_t *cs = reinterpret_cast<uint64_t *>(sh->h_blk), *us = cs + nchain;
-    uint32_t *csz = reinterpret_cast<uint32_t *>(us + nchain), *hsz = csz + nchain, *usz = hsz + nchain,
-             *fl = usz + nchain;
     HIPCHK(ctx, sh->blkpack.ensure(4 * nchain));
-    HIPCHK(ctx, launch_pack_blocks(sh->dev_blocks(), nchain, sh->blkpack.p, st));
-    HIPCHK(ctx, hipMemcpyAsync(cs, sh->blkpack.p, nchain * 32, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, launch_pack_blocks(sh->dev_blocks(), nchain, sh->file_off, sh->blkpack.p, st));
+    HIPCHK(ctx, hipMemcpyAsync(sh->hb.data(), sh->blkpack.p, nchain * 32, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipMemcpyAsync(nx, next18_dev, 18, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipStreamSynchronize(st));
-    for (uint64_t i = 0; i < nchain; ++i)
-      sh->hb[i] = sbh_block{cs[i] + sh->file_off, us[i], csz[i], hsz[i], usz[i], fl[i]};
   }
   // stream end: a truncated last block is not part of the resident stream
   sh->open_last = !sh->at_eof;
