@@ -566,11 +566,22 @@ def kernel_src_hash():
 
 
 def latest_pmc(name):
-    """The newest committed counter summary `profiles/r*_pmc/<name>` (tools/pmc_collect.sh)."""
+    """The committed counter summary `profiles/r*_pmc/<name>` (tools/pmc_collect.sh) collected
+    from the kernel sources this run uses (its `src_hash`), else the last by name."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc", name)))
     if not files:
         return None, None
+    cur = kernel_src_hash()
+    fresh = []
+    for f in files:
+        try:
+            with open(os.path.join(os.path.dirname(f), "src_hash")) as fh:
+                if fh.read().strip() == cur:
+                    fresh.append(f)
+        except OSError:
+            pass
+    files = fresh or files
     with open(files[-1]) as fh:
         return json.load(fh), os.path.relpath(files[-1], ROOT)
 
