@@ -238,6 +238,31 @@ def test_synthetic_inflate_and_eager(ctx, synth_files, name):
         sh.close()
 
 
+@pytest.mark.parametrize("name", ["long", "adversarial", "short_l6"])
+def test_synthetic_find_record_start(ctx, synth_files, name):
+    # FindRecordStart from random offsets through the eager bitmap (k_first_set's chunked
+    # grid walk: long reads put the next record start tens of KiB, i.e. chunks, ahead) and
+    # through fresh eager windows (a shard with no bitmap yet), against the oracle
+    data = synth_files[name]
+    of = OracleFile(data)
+    rng = np.random.default_rng(len(name))
+    offs = rng.integers(0, of.flat_size - 1, 16).tolist() + [0, of.flat_size - 40]
+    for covered in (False, True):
+        sh = load(ctx, data, of.contig_len)
+        try:
+            if covered:
+                sh.check_eager(0, of.flat_size)
+            for f in offs:
+                rc, want, d = of.find_record_start(int(f))
+                if rc == OR_OK:
+                    assert sh.find_record_start(int(f)) == (want, d), (name, covered, f)
+                else:
+                    with pytest.raises(sb.SparkBamError):
+                        sh.find_record_start(int(f))
+        finally:
+            sh.close()
+
+
 def test_synthetic_empty_block_segments(ctx, synth_files):
     # empty BGZF blocks end the stream (Stream.scala:56-58): a stream opened after the
     # k-th empty block sees only that segment
