@@ -1636,7 +1636,7 @@ __global__ __launch_bounds__(256) void k_verify_chain_w(const uint8_t *U, const 
 
 // ---- chain marking by pointer doubling (the parallel replacement of k_chain_walk when
 // the eager bitmap holds false positives or misses chain records) ----
-// Nodes are the n set bits of [from, E) in order (pos[], word prefix counts wpre from word
+// Nodes are the n set bits of [from, E) in order (pos[], group prefix counts wpre from word
 // (from - begin) / 32).  J[i] = index of the node the chain steps to from node i
 // (next = s + 4 + block_size), or CM_TERM when the step leaves [from, E) / reaches the
 // stream end (a valid end of the counted range), or CM_BROKEN when it lands on a
@@ -1667,9 +1667,14 @@ __global__ void k_cm_succ(const uint8_t *U, const uint32_t *bits, uint64_t begin
         j = broken;
       } else {
         const uint64_t w0 = (from - begin) >> 5;
+        const uint32_t lo = ~0u << (uint32_t)((from - begin) & 31);  // bits before `from` are not nodes
         uint32_t below = v & ((1u << b) - 1u);
-        if (w == w0) below &= ~0u << (uint32_t)((from - begin) & 31);  // bits before `from` are not nodes
-        j = (uint32_t)(wpre[w - w0] + __popc(below));
+        if (w == w0) below &= lo;
+        // the group's prefix plus the set bits of its words before w
+        const uint64_t r = w - w0, g0 = r - r % WPRE_GROUP;
+        uint64_t c = wpre[r / WPRE_GROUP];
+        for (uint64_t k = g0; k < r; ++k) c += __popc(k == 0 ? bits[w0] & lo : bits[w0 + k]);
+        j = (uint32_t)(c + __popc(below));
       }
     }
   }

@@ -18,29 +18,11 @@ __device__ __forceinline__ uint32_t rd_u32(const uint8_t *U, uint64_t p) {
   return (uint32_t)U[p] | (uint32_t)U[p + 1] << 8 | (uint32_t)U[p + 2] << 16 | (uint32_t)U[p + 3] << 24;
 }
 
-// Record starts = set bits of [first, E): a thread per bitmap word, positions written at
-// the word's exclusive popcount prefix (wpre).
-__global__ void k_bits_positions(const uint32_t *bits, uint64_t begin, uint64_t first, uint64_t E,
-                                 const uint64_t *wpre, uint64_t *pos) {
-  const uint64_t w0 = (first - begin) / 32;
-  const uint64_t w = w0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= (E - begin + 31) / 32) return;
-  uint32_t v = bits[w];
-  const uint64_t p0 = begin + 32 * w;
-  if (p0 < first) v &= ~0u << (uint32_t)(first - p0);
-  if (p0 + 32 > E) v &= (E - p0) >= 32 ? ~0u : ((1u << (uint32_t)(E - p0)) - 1u);
-  uint64_t o = wpre[w - w0];
-  while (v) {
-    pos[o++] = p0 + __builtin_ctz(v);
-    v &= v - 1;
-  }
-}
-
 // Per-word prefix counts in two levels: a workgroup covers WP_CHUNK words (WP_WPT per
 // thread); k_chunk_popcounts sums each chunk, the chunk sums are scanned (a few thousand
 // values), and k_word_prefix re-counts its words, scans them inside the workgroup and
 // writes wpre -- one write pass over the words instead of a multi-pass global scan.
-constexpr uint32_t WP_T = 256, WP_WPT = 16, WP_CHUNK = WP_T * WP_WPT;
+constexpr uint32_t WP_T = 256, WP_WPT = WPRE_GROUP, WP_CHUNK = WP_T * WP_WPT;
 
 __device__ __forceinline__ uint32_t masked_word(const uint32_t *bits, uint64_t begin, uint64_t first, uint64_t E,
                                                 uint64_t w) {
@@ -50,6 +32,25 @@ __device__ __forceinline__ uint32_t masked_word(const uint32_t *bits, uint64_t b
   if (p0 < first) v &= ~0u << (uint32_t)(first - p0);
   if (p0 + 32 > E) v &= (E - p0) >= 32 ? ~0u : ((1u << (uint32_t)(E - p0)) - 1u);
   return v;
+}
+
+// Record starts = set bits of [first, E): a thread per group of WPRE_GROUP bitmap words,
+// positions written from the group's prefix (wpre) on.
+__global__ void k_bits_positions(const uint32_t *bits, uint64_t begin, uint64_t first, uint64_t E,
+                                 const uint64_t *wpre, uint64_t *pos) {
+  const uint64_t w0 = (first - begin) / 32, wend = (E - begin + 31) / 32;
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t wg = w0 + g * WPRE_GROUP;
+  if (wg >= wend) return;
+  uint64_t o = wpre[g];
+  for (uint32_t k = 0; k < WPRE_GROUP; ++k) {
+    uint32_t v = masked_word(bits, begin, first, E, wg + k);
+    const uint64_t p0 = begin + 32 * (wg + k);
+    while (v) {
+      pos[o++] = p0 + __builtin_ctz(v);
+      v &= v - 1;
+    }
+  }
 }
 
 __global__ __launch_bounds__(WP_T) void k_chunk_popcounts(const uint32_t *bits, uint64_t begin, uint64_t first,
@@ -75,24 +76,16 @@ __global__ __launch_bounds__(WP_T) void k_word_prefix(const uint32_t *bits, uint
   const uint64_t wb = (first - begin) / 32;
   const uint64_t nw = (E - begin + 31) / 32 - wb;
   const uint64_t r0 = (uint64_t)blockIdx.x * WP_CHUNK + (uint64_t)threadIdx.x * WP_WPT;  // relative word
-  uint32_t cnt[WP_WPT], mine = 0;
+  uint32_t mine = 0;
 #pragma unroll
-  for (uint32_t k = 0; k < WP_WPT; ++k) {
-    cnt[k] = __popc(masked_word(bits, begin, first, E, wb + r0 + k));
-    mine += cnt[k];
-  }
+  for (uint32_t k = 0; k < WP_WPT; ++k) mine += __popc(masked_word(bits, begin, first, E, wb + r0 + k));
   const uint32_t lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
   const uint32_t incl = wave_incl_scan(mine);
   if (lane == WAVE - 1) wsum[wv] = incl;
   __syncthreads();
   uint32_t before = 0;
   for (uint32_t k = 0; k < wv; ++k) before += wsum[k];
-  uint64_t o = cpre[blockIdx.x] + before + incl - mine;
-#pragma unroll
-  for (uint32_t k = 0; k < WP_WPT; ++k) {
-    if (r0 + k < nw) wpre[r0 + k] = o;
-    o += cnt[k];
-  }
+  if (r0 < nw) wpre[r0 / WP_WPT] = cpre[blockIdx.x] + before + incl - mine;  // (the group's prefix)
 }
 
 // Sequential chain from first while the start is < E (fallback when no verified bitmap).
@@ -234,13 +227,13 @@ __global__ __launch_bounds__(256) void k_rec_fields(const uint8_t *__restrict__ 
 
 hipError_t scan_exclusive_u64(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *tmp, hipStream_t st);
 
-// cnt, wpre: one u64 per bitmap word of [first, E) (cnt holds 2 per WP_CHUNK words: chunk
-// sums and their prefix); tmp: scan_tmp_words(words)
+// cnt: 2 u64 per WP_CHUNK words (chunk sums and their prefix); wpre: one u64 per WPRE_GROUP
+// words of [first, E); tmp: scan_tmp_words(words)
 hipError_t launch_rec_positions_bits(const uint32_t *bits, uint64_t begin, uint64_t first, uint64_t E, uint64_t *cnt,
                                      uint64_t *wpre, uint64_t *tmp, uint64_t *pos, hipStream_t st) {
   const uint64_t nw = (E - begin + 31) / 32 - (first - begin) / 32;
   if (!nw) return hipSuccess;
-  const uint32_t g = (uint32_t)((nw + 255) / 256);
+  const uint32_t g = (uint32_t)(((nw + WPRE_GROUP - 1) / WPRE_GROUP + 255) / 256);
   const uint64_t nch = (nw + WP_CHUNK - 1) / WP_CHUNK;  // cnt: chunk sums, then (cnt + nch) their prefix
   hipLaunchKernelGGL(k_chunk_popcounts, dim3((uint32_t)nch), dim3(WP_T), 0, st, bits, begin, first, E, cnt);
   hipError_t e = scan_exclusive_u64(cnt, cnt + nch, nch, tmp, st);

@@ -85,6 +85,10 @@ constexpr uint32_t INF_SERIAL = 0xffu; // (inside inflate only) left to the seri
 #endif
 constexpr uint64_t EAGER_TILE = SBH_ETILE;
 constexpr uint64_t EAGER_REACH = SBH_ETILE + 4096 + 512 + 64;
+// Bitmap set-bit prefix (launch_rec_positions_bits): one u64 per group of WPRE_GROUP
+// consecutive words of [first, E) -- the set bits before the group; a lookup adds the
+// popcounts of the group's earlier words (one 64-byte read).
+constexpr uint32_t WPRE_GROUP = 16;
 
 // Launchers (defined in the .hip files, called from sbh_api.hip).
 // Inflate = k_huff (Huffman decode -> LZ77 tokens, block status) then k_lz (tokens ->
