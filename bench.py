@@ -48,6 +48,21 @@ CONFIGS = {  # BASELINE.json configs; SURVEY 8d
 }
 
 
+def launch_ranks(n):
+    """torch.distributed.run --nproc-per-node n over this script with the same arguments, on
+    127.0.0.1 and a free port, as a child process; returns its exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"launching {n} ranks: {' '.join(cmd)}")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -80,11 +95,17 @@ def main():
                          "rocprofv3 --pmc summary, profiles/*_pmc_traffic.json)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N` outside a launcher: start the N ranks as a CHILD process
+        # group (torch.distributed.run), before anything here has touched the GPU, and hand back
+        # its exit code; rank 0's JSON line reaches stdout through the inherited descriptors.
+        sys.exit(launch_ranks(args.gpus))
+
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
+        log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; the line reports ranks_seen and exits non-zero")
 
     import torch
     import torch.distributed as dist
@@ -332,6 +353,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(seg.comp, seg.file_offset or 0, contig_len, args.cpu_seconds, args.cpu_threads)
 
+    ranks_seen = dist.get_world_size() if coll else 1
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
         value = total_flat * args.steps / elapsed / 1e9
@@ -361,6 +383,8 @@ def main():
             "records_per_s": round(total_records * args.steps / elapsed, 1),
             "compressed_GBps": round(sum(own_sizes) * args.steps / elapsed / 1e9, 3),
             "correct": bool(ok),
+            "ranks_seen": ranks_seen,
+            "backend": backend if coll else "none (one rank)",
             "stitch_ok": bool(stitch["ok"]),
             "splits_rank0": {"n": len(stream_splits), "split_bytes": 32 << 20,
                              "host_path": int(sl.get("splits_host", 0)),
@@ -414,6 +438,9 @@ def main():
         log(f"STITCH CHECK FAILED: records {total_records} true {total_true} expected {expect}; "
             f"stitch {stitch}")
         sys.exit(3)
+    if ranks_seen != args.gpus:
+        log(f"ranks_seen {ranks_seen} != --gpus {args.gpus}")
+        sys.exit(4)
 
 
 def main_strong(args, rank, world, local_rank, device, backend, xdev, coll, dist, torch, synth, sb, sharded):
@@ -500,6 +527,7 @@ def main_strong(args, rank, world, local_rank, device, backend, xdev, coll, dist
     total_flat = sum(x[3] for x in allr)
     ok = (total_records == F.records and sum(counts) == F.records and st["ok"] and sum(crc_bad) == 0
           and split_bad == 0 and len(counts) == nsplits)
+    ranks_seen = dist.get_world_size() if coll else 1
     if rank == 0:
         value = total_flat * args.steps / elapsed / 1e9
         out = {
@@ -528,6 +556,8 @@ def main_strong(args, rank, world, local_rank, device, backend, xdev, coll, dist
             "records_per_s": round(total_records * args.steps / elapsed, 1),
             "compressed_GBps": round(F.size * args.steps / elapsed / 1e9, 3),
             "correct": bool(ok),
+            "ranks_seen": ranks_seen,
+            "backend": backend if coll else "none (one rank)",
             "stitch_ok": bool(st["ok"]),
             "records": int(total_records),
             "splits_nonempty": len(splits),
@@ -549,6 +579,9 @@ def main_strong(args, rank, world, local_rank, device, backend, xdev, coll, dist
         log(f"CHECK FAILED: records {total_records}/{F.records}, counts {sum(counts)}, stitch {st['ok']}, "
             f"crc {crc_bad}, split errors {split_bad}, splits {len(counts)}/{nsplits}")
         sys.exit(3)
+    if ranks_seen != args.gpus:
+        log(f"ranks_seen {ranks_seen} != --gpus {args.gpus}")
+        sys.exit(4)
 
 
 def kernel_src_hash():

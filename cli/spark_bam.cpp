@@ -235,7 +235,7 @@ std::string bytes_fmt(uint64_t b) {
 }
 
 struct Args {
-  std::string cmd, path, out, records;
+  std::string cmd, path, out, records, blocks_path;
   uint64_t split = 0;
   bool has_split = false, s = false, u = false;
   long limit = 1000000;
@@ -268,6 +268,7 @@ Args parse(int argc, char **argv) {
     else if (t == "-l" || t == "--print-limit") a.limit = std::stol(next());
     else if (t == "-i" || t == "--intervals") { a.ranges = parse_ranges(next()); a.has_ranges = true; }
     else if (t == "-r" || t == "--records-path") a.records = next();
+    else if (t == "-b" || t == "--blocks-path") a.blocks_path = next();
     else if (t == "--reads-to-check") a.reads_to_check = std::stoi(next());
     else if (t == "--max-read-size") a.max_read_size = std::stoi(next());
     else if (t == "-z" || t == "--bgzf-blocks-to-check") a.blocks_to_check = std::stoi(next());
@@ -433,24 +434,6 @@ int count_reads(const Args &a) {
   return 0;
 }
 
-// Blocks.apply `-i` filter: blocks whose start is in the ranges (Blocks.scala:89-96)
-std::vector<std::pair<uint64_t, uint64_t>> selected(const Loaded &L, const Args &a, uint64_t *comp) {
-  std::vector<std::pair<uint64_t, uint64_t>> fr;
-  *comp = 0;
-  for (const sbh_block &b : L.blocks) {
-    if (b.flags & SBH_BLOCK_EMPTY || b.usize == 0) continue;
-    if (a.has_ranges) {
-      bool in = false;
-      for (auto &r : a.ranges) in |= r.first <= b.start && b.start < r.second;
-      if (!in) continue;
-    }
-    *comp += b.csize;
-    if (!fr.empty() && fr.back().second == b.ustart) fr.back().second = b.ustart + b.usize;
-    else fr.push_back({b.ustart, b.ustart + b.usize});
-  }
-  return fr;
-}
-
 std::vector<Pos> read_records_file(const std::string &p) {
   std::ifstream f(p);
   if (!f) throw Error(SBH_E_ARG, "no records file " + p + " (run index-records first)");
@@ -476,42 +459,218 @@ std::vector<uint64_t> bits_to_positions(const std::vector<uint8_t> &bits, uint64
   return out;
 }
 
-int check_bam(const Args &a) {
-  if (!a.s) no_hadoop_bam();
-  Loaded L(a.path);
-  std::vector<Pos> recs = read_records_file(a.records.empty() ? a.path + ".records" : a.records);
-  std::vector<uint64_t> truth(recs.size());
-  for (size_t i = 0; i < recs.size(); ++i) truth[i] = recs[i].block << 16 | recs[i].off;
-  uint64_t comp = 0;
-  auto fr = selected(L, a, &comp);
-  std::vector<uint64_t> rb(fr.size()), re(fr.size());
-  uint64_t positions = 0;
-  for (size_t i = 0; i < fr.size(); ++i) rb[i] = fr[i].first, re[i] = fr[i].second, positions += re[i] - rb[i];
-  // TP / FP / FN on the device: eager bitmap vs the truth bitmap, mismatches compacted
-  const uint64_t cap = (uint64_t)std::max(a.limit, 0L);
-  std::vector<uint64_t> fps(cap + 1), fns(cap + 1);
-  uint64_t out[4] = {0, 0, 0, 0};
-  chk(sbh_check_records(L.sh, rb.data(), re.data(), fr.size(), a.reads_to_check, truth.data(), truth.size(), out,
-                        fps.data(), cap, fns.data(), cap),
-      "check-bam");
-  if (out[3]) throw Error(SBH_E_NOT_FOUND, std::to_string(out[3]) + " records-file positions are not block starts");
-  const uint64_t tp = out[0], fp = out[1], fn = out[2];
+// Blocks.apply (check/src/main/scala/org/hammerlab/bam/check/Blocks.scala:47-208): the blocks the
+// all-positions modes examine, per partition.  With a `.blocks` file (-b, default BAM.blocks): its
+// blocks whose start is in -i, partitioned by cumulative compressed size / split size (:86-139);
+// without one: the file cut every split size, the splits meeting -i, each one's blocks found on
+// the device (FindBlockStart, then MetadataStream while start < split end: sbh_find_blocks,
+// :141-206).  The split size is -m, default 2 MB (:74-78).
+struct BlockMeta {
+  uint64_t start;
+  uint32_t csize, usize;
+};
+struct BlocksPartitions {
+  std::vector<std::vector<BlockMeta>> parts;
+  std::vector<std::pair<uint64_t, uint64_t>> bounds;
+  std::vector<uint64_t> starts() const {
+    std::vector<uint64_t> v;
+    for (auto &p : parts)
+      for (auto &m : p) v.push_back(m.start);
+    return v;
+  }
+};
+
+bool in_ranges(const Args &a, uint64_t x) {
+  if (!a.has_ranges) return true;
+  for (auto &r : a.ranges)
+    if (r.first <= x && x < r.second) return true;
+  return false;
+}
+
+BlocksPartitions blocks_apply(const Args &a, const uint8_t *data, uint64_t size) {
+  const uint64_t split = a.has_split ? a.split : 2ull << 20;
+  const std::string bp = a.blocks_path.empty() ? a.path + ".blocks" : a.blocks_path;
+  BlocksPartitions R;
+  std::ifstream f(bp);
+  if (f) {
+    std::vector<BlockMeta> metas;
+    std::string line;
+    while (std::getline(f, line)) {
+      if (line.empty()) continue;
+      const size_t c1 = line.find(','), c2 = c1 == std::string::npos ? c1 : line.find(',', c1 + 1);
+      if (c2 == std::string::npos) throw Error(SBH_E_ARG, "Bad blocks-index line: " + line);
+      BlockMeta m{std::stoull(line.substr(0, c1)), (uint32_t)std::stoul(line.substr(c1 + 1, c2 - c1 - 1)),
+                  (uint32_t)std::stoul(line.substr(c2 + 1))};
+      if (in_ranges(a, m.start)) metas.push_back(m);
+    }
+    // partition = (compressed bytes of the blocks before it) / split; the partition count is the last
+    // block's partition + 1 (as BlocksTest's "block boundaries" case pins it)
+    uint64_t off = 0;
+    for (auto &m : metas) {
+      const uint64_t k = off / split;
+      if (R.parts.size() <= k) R.parts.resize(k + 1);
+      R.parts[k].push_back(m);
+      off += m.csize;
+    }
+    for (uint64_t i = 0; i < R.parts.size(); ++i) R.bounds.push_back({i * split, (i + 1) * split});
+    return R;
+  }
+  std::vector<uint64_t> idx, st, en;
+  for (uint64_t i = 0; i * split < size; ++i) {
+    bool meets = !a.has_ranges;
+    for (auto &r : a.ranges) meets |= r.first < r.second && r.first < (i + 1) * split && r.second > i * split;
+    if (!meets) continue;
+    idx.push_back(i);
+    st.push_back(i * split);
+    en.push_back(std::min(size, (i + 1) * split));
+    R.bounds.push_back({i * split, (i + 1) * split});
+  }
+  R.parts.resize(idx.size());
+  std::vector<sbh_block> out(size / 4096 + 16);
+  uint64_t n = 0;
+  for (;;) {
+    chk(sbh_find_blocks(g_ctx, data, size, st.data(), en.data(), st.size(), a.blocks_to_check, 1ull << 30, out.data(),
+                        out.size(), &n),
+        "find blocks");
+    if (n <= out.size()) break;
+    out.resize(n);
+  }
+  for (uint64_t i = 0; i < n; ++i)
+    if (in_ranges(a, out[i].start)) R.parts[out[i].ustart].push_back(BlockMeta{out[i].start, out[i].csize, out[i].usize});
+  return R;
+}
+
+uint64_t stream_window() {
+  const char *e = std::getenv("SBH_STREAM_WINDOW");
+  return e && *e ? std::strtoull(e, nullptr, 10) : 1ull << 30;
+}
+
+// The file's record at/after a vpos, for PosMetadata (a few KB of the file around it inflated on
+// the device; grown x4 while the search needs more bytes).
+struct NextRecord {
+  bool found = false;
+  int32_t delta = 0, ref = 0, pos = 0, lseq = 0;
+  uint32_t flag = 0;
+  std::string name;
+};
+NextRecord next_record(const uint8_t *data, uint64_t size, const BamHeader &h, const Args &a, uint64_t vpos) {
+  NextRecord r;
+  const uint64_t blk = vpos >> 16;
+  for (uint64_t span = 4ull << 20;; span *= 4) {
+    const uint64_t n = std::min(size - blk, span);
+    sbh_shard *sh = nullptr;
+    chk(sbh_shard_create(g_ctx, data + blk, n, blk, size, 0, &sh), "shard");
+    uint64_t nb = 0, flat = 0, nxt = 0;
+    int rc = sbh_index(sh, blk, &nb, &flat);
+    if (!rc) rc = sbh_inflate(sh, nullptr);
+    if (!rc) rc = sbh_set_contigs(sh, h.lens.data(), (int32_t)h.lens.size());
+    if (!rc) rc = sbh_find_record_start(sh, vpos & 0xffff, a.reads_to_check, a.max_read_size, &nxt, &r.delta);
+    if (rc == SBH_E_NEED_HALO && blk + n < size) {
+      sbh_shard_destroy(sh);
+      continue;
+    }
+    if (!rc && nxt + 36 <= flat) {
+      uint8_t f[36];
+      chk(sbh_read_flat(sh, nxt, 36, f), "read record");
+      r.ref = rd32(f + 4), r.pos = rd32(f + 8), r.lseq = rd32(f + 20);
+      const uint32_t rnl = (uint32_t)rd32(f + 12) & 0xff;
+      r.flag = (uint32_t)rd32(f + 16) >> 16;
+      std::vector<uint8_t> name(rnl ? rnl : 1, 0);
+      if (rnl && nxt + 36 + rnl <= flat) chk(sbh_read_flat(sh, nxt + 36, rnl, name.data()), "read name");
+      r.name.assign((const char *)name.data(), strnlen((const char *)name.data(), rnl));
+      r.found = true;
+    }
+    sbh_shard_destroy(sh);
+    return r;
+  }
+}
+
+// check-bam -s and full-check's pass over Blocks.apply's blocks: sbh_check_stream moves the file
+// through HBM in windows, so any file size runs in bounded HBM.
+struct AllPositions {
+  sbh_check_result res{};
+  std::vector<uint64_t> fp, fn, close_v, counts, rbe;
+  std::vector<uint32_t> close_w;
+};
+AllPositions all_positions(const Args &a, const Mapped &f, const BamHeader &h, const std::vector<uint64_t> *truth,
+                           bool full, uint64_t cap) {
+  const BlocksPartitions B = blocks_apply(a, f.p, f.n);
+  const std::vector<uint64_t> starts = B.starts();
+  AllPositions R;
+  sbh_check_opts o{};
+  o.window = stream_window();
+  o.halo = 4ull << 20;
+  o.reads_to_check = a.reads_to_check;
+  o.blocks = starts.data();
+  o.n_blocks = starts.size();
+  if (truth) {
+    R.fp.resize(cap + 1);
+    R.fn.resize(cap + 1);
+    o.truth_vpos = truth->data();
+    o.n_truth = truth->size();
+    o.fp_vpos = R.fp.data(), o.fn_vpos = R.fn.data();
+    o.fp_cap = o.fn_cap = cap;
+  }
+  if (full) {
+    const uint64_t ccap = 1 << 22;
+    R.counts.resize(21 * 19);
+    R.rbe.resize(21 * 64);
+    R.close_v.resize(ccap);
+    R.close_w.resize(ccap);
+    o.full = 1;
+    o.counts = R.counts.data(), o.rbe_hist = R.rbe.data();
+    o.close_vpos = R.close_v.data(), o.close_word = R.close_w.data(), o.close_cap = ccap;
+  }
+  chk(sbh_check_stream(g_ctx, f.p, f.n, h.lens.data(), (int32_t)h.lens.size(), &o, &R.res), "check");
+  R.fp.resize(std::min<uint64_t>(R.res.fp, cap));
+  R.fn.resize(std::min<uint64_t>(R.res.fn, cap));
+  if (full) {
+    R.close_v.resize(std::min<uint64_t>(R.res.n_close, R.close_v.size()));
+    R.close_w.resize(R.close_v.size());
+  }
+  return R;
+}
+
+Pos pos_of_vpos(uint64_t v) { return Pos{v >> 16, (uint32_t)(v & 0xffff)}; }
+
+// CheckerApp's summary (CheckerApp.scala:150-227) of the eager calls vs the `.records` truth
+void print_check_summary(const Args &a, const AllPositions &R) {
+  const uint64_t tp = R.res.tp, fp = R.res.fp, fn = R.res.fn, positions = R.res.positions, comp = R.res.comp_bytes;
+  if (R.res.unknown)
+    throw Error(SBH_E_NOT_FOUND, std::to_string(R.res.unknown) + " records-file positions are not block starts");
   printf("%llu uncompressed positions\n%s compressed\nCompression ratio: %.2f\n%llu reads\n",
          (unsigned long long)positions, bytes_fmt(comp).c_str(), (double)positions / (double)comp,
          (unsigned long long)(tp + fn));
   if (!fp && !fn) {
     printf("All calls matched!\n");
-    return 0;
+    return;
   }
   printf("%llu false positives, %llu false negatives\n\n", (unsigned long long)fp, (unsigned long long)fn);
   if (fp) {
     printf("False positives:\n");
-    for (uint64_t i = 0; i < std::min(fp, cap); ++i) printf("\t%s\n", L.pos(fps[i]).str().c_str());
+    for (uint64_t v : R.fp) printf("\t%s\n", pos_of_vpos(v).str().c_str());
   }
   if (fn) {
     printf("%llu false negatives:\n", (unsigned long long)fn);
-    for (uint64_t i = 0; i < std::min(fn, cap); ++i) printf("\t%s\n", L.pos(fns[i]).str().c_str());
+    for (uint64_t v : R.fn) printf("\t%s\n", pos_of_vpos(v).str().c_str());
   }
+}
+
+std::vector<uint64_t> truth_of(const Args &a) {
+  std::vector<Pos> recs = read_records_file(a.records.empty() ? a.path + ".records" : a.records);
+  std::vector<uint64_t> truth(recs.size());
+  for (size_t i = 0; i < recs.size(); ++i) truth[i] = recs[i].block << 16 | recs[i].off;
+  std::sort(truth.begin(), truth.end());
+  return truth;
+}
+
+int check_bam(const Args &a) {
+  if (!a.s) no_hadoop_bam();
+  Mapped f(a.path);
+  const BamHeader h = header_of(f.p, f.n);
+  const std::vector<uint64_t> truth = truth_of(a);
+  const AllPositions R = all_positions(a, f, h, &truth, false, (uint64_t)std::max(a.limit, 0L));
+  print_check_summary(a, R);
   return 0;
 }
 
@@ -530,31 +689,21 @@ std::string flags_str(uint32_t w) {
 }
 
 // PosMetadata show (check/.../PosMetadata.scala:20-53) with htsjdk SAMRecord.toString
-std::string pos_metadata(Loaded &L, const Args &a, uint64_t flat, uint32_t word) {
+std::string pos_metadata(const Mapped &f, const BamHeader &h, const Args &a, uint64_t vpos, uint32_t word) {
   std::string rec = "no next record";
-  uint64_t nxt = 0;
-  int32_t delta = 0;
-  if (sbh_find_record_start(L.sh, flat, a.reads_to_check, a.max_read_size, &nxt, &delta) == SBH_OK &&
-      nxt + 36 <= L.flat) {
-    uint8_t f[36];
-    chk(sbh_read_flat(L.sh, nxt, 36, f), "read record");
-    int32_t ref = rd32(f + 4), pos = rd32(f + 8);
-    uint32_t rnl = (uint32_t)rd32(f + 12) & 0xff;
-    uint32_t flag = (uint32_t)rd32(f + 16) >> 16;
-    int32_t lseq = rd32(f + 20);
-    std::vector<uint8_t> name(rnl ? rnl : 1, 0);
-    if (rnl) chk(sbh_read_flat(L.sh, nxt + 36, rnl, name.data()), "read name");
-    std::string s = std::to_string(delta) + " before " + std::string((const char *)name.data(), strnlen((const char *)name.data(), rnl));
-    if (flag & 1) s += (flag & 0x40) ? " 1/2" : " 2/2";
-    s += " " + std::to_string(lseq) + "b";
-    const bool unmapped = flag & 4;
+  const NextRecord r = next_record(f.p, f.n, h, a, vpos);
+  if (r.found) {
+    std::string s = std::to_string(r.delta) + " before " + r.name;
+    if (r.flag & 1) s += (r.flag & 0x40) ? " 1/2" : " 2/2";
+    s += " " + std::to_string(r.lseq) + "b";
+    const bool unmapped = r.flag & 4;
     s += unmapped ? " unmapped read" : " aligned read";
-    auto where = [&]() { return L.hdr.names[ref] + ":" + std::to_string(pos + 1); };
-    if (unmapped && pos + 1 >= 0 && ref >= 0 && ref < (int32_t)L.hdr.names.size()) s += " (placed at " + where() + ")";
-    else if (!unmapped && ref >= 0 && ref < (int32_t)L.hdr.names.size()) s += " @ " + where();
+    auto where = [&]() { return h.names[r.ref] + ":" + std::to_string(r.pos + 1); };
+    if (unmapped && r.pos + 1 >= 0 && r.ref >= 0 && r.ref < (int32_t)h.names.size()) s += " (placed at " + where() + ")";
+    else if (!unmapped && r.ref >= 0 && r.ref < (int32_t)h.names.size()) s += " @ " + where();
     rec = s;
   }
-  return L.pos(flat).str() + ":\t" + rec + ". Failing checks: " + flags_str(word & SBH_FULL_FLAGS_MASK);
+  return pos_of_vpos(vpos).str() + ":\t" + rec + ". Failing checks: " + flags_str(word & SBH_FULL_FLAGS_MASK);
 }
 
 std::vector<std::string> counts_lines(const std::vector<uint64_t> &c, const std::map<uint32_t, uint64_t> &rbe,
@@ -581,35 +730,26 @@ std::vector<std::string> counts_lines(const std::vector<uint64_t> &c, const std:
 }
 
 int full_check(const Args &a) {
-  Loaded L(a.path);
-  uint64_t comp = 0;
-  auto fr = selected(L, a, &comp);
-  std::vector<uint64_t> counts(21 * 19, 0), rbe(21 * 64, 0);
-  std::vector<std::pair<uint64_t, uint32_t>> close;
-  uint64_t positions = 0;
-  const uint64_t cap = 1 << 22;
-  std::vector<uint64_t> cf(cap);
-  std::vector<uint32_t> cw(cap);
-  for (auto &r : fr) {
-    std::vector<uint64_t> c(21 * 19), rb(21 * 64);
-    uint64_t ns = 0, nclose = 0;
-    chk(sbh_check_full(L.sh, r.first, r.second, a.reads_to_check, nullptr, c.data(), rb.data(), &ns, cf.data(),
-                       cw.data(), cap, &nclose),
-        "full");
-    for (int i = 0; i < 21 * 19; ++i) counts[i] += c[i];
-    for (int i = 0; i < 21 * 64; ++i) rbe[i] += rb[i];
-    for (uint64_t i = 0; i < std::min(nclose, cap); ++i) close.push_back({cf[i], cw[i]});
-    positions += r.second - r.first;
-  }
-  // records file, if present: the indexed comparison summary first (FullCheck.scala:94-106)
-  std::string rp = a.records.empty() ? a.path + ".records" : a.records;
-  if (std::ifstream(rp)) {
+  Mapped f(a.path);
+  const BamHeader h = header_of(f.p, f.n);
+  // records file, if present: the indexed comparison summary first (FullCheck.scala:94-106), from
+  // the same pass over the blocks
+  const std::string rp = a.records.empty() ? a.path + ".records" : a.records;
+  const bool have_records = (bool)std::ifstream(rp);
+  std::vector<uint64_t> truth;
+  if (have_records) {
     Args e = a;
-    e.s = true;
     e.records = rp;
-    check_bam(e);
+    truth = truth_of(e);
+  }
+  const AllPositions R = all_positions(a, f, h, have_records ? &truth : nullptr, true, (uint64_t)std::max(a.limit, 0L));
+  if (have_records) {
+    print_check_summary(a, R);
     printf("\n");
   }
+  const std::vector<uint64_t> &counts = R.counts, &rbe = R.rbe;
+  std::vector<std::pair<uint64_t, uint32_t>> close;
+  for (size_t i = 0; i < R.close_v.size(); ++i) close.push_back({R.close_v[i], R.close_w[i]});
   auto nnz_of = [](uint32_t w) { return __builtin_popcount(w & SBH_FULL_FLAGS_MASK) + (((w >> SBH_FULL_N_SHIFT) & 0x3FF) > 0); };
   auto per = [&](int k) {
     std::vector<uint64_t> c(19);
@@ -631,7 +771,7 @@ int full_check(const Args &a) {
     if ((long)ones.size() <= a.limit) printf("%zu critical positions:\n", ones.size());
     else printf("%ld of %zu critical positions:\n", a.limit, ones.size());
     for (size_t i = 0; i < ones.size() && (long)i < a.limit; ++i)
-      printf("\t%s\n", pos_metadata(L, a, ones[i].first, ones[i].second).c_str());
+      printf("\t%s\n", pos_metadata(f, h, a, ones[i].first, ones[i].second).c_str());
     if ((long)ones.size() > a.limit) printf("\t…\n");
   }
   printf("\n");
@@ -641,7 +781,7 @@ int full_check(const Args &a) {
     if ((long)twos.size() <= a.limit) printf("%zu positions where exactly two checks failed:\n", twos.size());
     else printf("%ld of %zu positions where exactly two checks failed:\n", a.limit, twos.size());
     for (size_t i = 0; i < twos.size() && (long)i < a.limit; ++i)
-      printf("\t%s\n", pos_metadata(L, a, twos[i].first, twos[i].second).c_str());
+      printf("\t%s\n", pos_metadata(f, h, a, twos[i].first, twos[i].second).c_str());
     if ((long)twos.size() > a.limit) printf("\t…\n");
     printf("\n");
     std::map<uint32_t, uint64_t> hist;

@@ -110,6 +110,11 @@ int sbh_header_make(const uint8_t *bytes, uint64_t avail, int32_t *hsize, int32_
 int sbh_shard_create(sbh_ctx *ctx, const void *comp, uint64_t n, uint64_t file_offset,
                      uint64_t file_size, int comp_on_device, sbh_shard **out);
 int sbh_shard_destroy(sbh_shard *sh);
+/* Replace a shard's resident bytes with [file_offset, file_offset + n) of the same file (same
+ * file_size), keeping its device allocations (grow-only): a window sliding along a file
+ * (jni/Native.scala GpuWindow, sbh_check_stream) reuses one shard instead of allocating per
+ * window.  Index, inflate and checker state are reset; the contig lengths are kept. */
+int sbh_shard_load(sbh_shard *sh, const void *comp, uint64_t n, uint64_t file_offset, int comp_on_device);
 /* Device pointer of the resident compressed bytes (padded). */
 const void *sbh_shard_comp_device_ptr(sbh_shard *sh);
 
@@ -310,6 +315,61 @@ int sbh_run_stream2(sbh_ctx *ctx, const void *host_comp, uint64_t n, uint64_t fi
                     const int32_t *contig_len, int32_t n_contigs, const sbh_stream_opts *opts,
                     sbh_stream_result *res);
 
+/* ---- the all-positions modes over a file of any size ----
+ * Blocks.apply (check/src/main/scala/org/hammerlab/bam/check/Blocks.scala:47-208) picks the
+ * BGZF blocks whose every position check-bam / full-check examine; CallPartition
+ * (cli/.../CallPartition.scala:23-54) and FullCheck.checkPartition (cli/.../full/FullCheck.scala:
+ * 65-86) then call the checkers at every offset of those blocks, reading the chain past them
+ * freely.  Both calls below take the whole file in host memory (mapped or pinned) and move it
+ * through HBM in windows of about `window` compressed bytes, so HBM use is bounded whatever
+ * the file size; a window whose answers need bytes past its halo grows the halo x4 and runs
+ * again. */
+
+/* Blocks.apply's branch without a `.blocks` file (Blocks.scala:141-206): for split i =
+ * [split_start[i], split_end[i]) (file offsets, ascending), FindBlockStart(split_start[i],
+ * bgzf_blocks_to_check) then MetadataStream from there while the block start is < split_end[i]
+ * (an empty block ends the stream, MetadataStream.scala:43-45).  Writes (start, csize, usize)
+ * of each block into out[] (ustart / hsize / flags zero; ustart = the split index) up to cap
+ * entries, in split order; *n_out = how many there are.  A split whose search fails answers
+ * SBH_E_HEADER_SEARCH_FAILED (HeaderSearchFailedException) for the whole call. */
+int sbh_find_blocks(sbh_ctx *ctx, const void *host_file, uint64_t file_size, const uint64_t *split_start,
+                    const uint64_t *split_end, uint64_t n_splits, int32_t bgzf_blocks_to_check, uint64_t window,
+                    sbh_block *out, uint64_t cap, uint64_t *n_out);
+
+/* check-bam -s and full-check over the given blocks (file offsets of block starts, ascending --
+ * Blocks.apply's partitions concatenated): every uncompressed offset of every listed block is
+ * checked.  truth_vpos (optional, ascending htsjdk virtual positions: the `.records` file,
+ * CheckerApp.scala:65-227) turns the eager calls into TP / FP / FN with the mismatching
+ * positions (first fp_cap / fn_cap of them, as vpos); full != 0 adds full.Checker's FullCheck
+ * aggregation (FullCheck.scala:142-192): Counts and readsBeforeError histograms by
+ * numNonZeroFields (include/sparkbam.h layout above) and the close calls (<= 2 non-zero
+ * fields) as (vpos, word) up to close_cap, ascending. */
+typedef struct {
+  uint64_t window, halo;
+  int32_t reads_to_check, full;
+  const uint64_t *blocks;
+  uint64_t n_blocks;
+  const uint64_t *truth_vpos; /* NULL: no comparison (n_true only) */
+  uint64_t n_truth;
+  uint64_t *fp_vpos, *fn_vpos;
+  uint64_t fp_cap, fn_cap;
+  uint64_t *counts;   /* full: 21 * 19 */
+  uint64_t *rbe_hist; /* full: 21 * 64 */
+  uint64_t *close_vpos;
+  uint32_t *close_word;
+  uint64_t close_cap;
+} sbh_check_opts;
+typedef struct {
+  uint64_t n_windows, positions, comp_bytes; /* checked positions and their blocks' compressed bytes */
+  uint64_t n_true;                           /* eager-true checked positions                      */
+  uint64_t tp, fp, fn, unknown;              /* vs truth_vpos (unknown: truth records off the chain) */
+  uint64_t n_success, n_close;               /* full                                             */
+  uint64_t halo_final;
+  double ms_wall, ms_h2d;
+} sbh_check_result;
+int sbh_check_stream(sbh_ctx *ctx, const void *host_file, uint64_t file_size, const int32_t *contig_len,
+                     int32_t n_contigs, const sbh_check_opts *opts, sbh_check_result *res);
+
 /* ---- record field extraction ----
  * RecordStream from first_flat while the record start is < end_flat, decoded like
  * htsjdk BAMRecordCodec.decode (check/.../iterator/RecordStream.scala:16-41,
@@ -363,9 +423,13 @@ int sbh_records_scan_regions(sbh_shard *sh, const uint64_t *chunk_begin, const u
  * that level (6 is samtools' default); 0 stored members; SBH_LEVEL_FAST this library's own
  * faster coder (hash-chain LZ77 with lazy matching, one dynamic-Huffman block per member, not
  * zlib's bytes).  src is a host or device pointer (src_on_device); out is host memory of at
- * least sbh_bgzf_compress_bound(n) bytes.  Device scratch is bounded by a batch of 2048 members
- * (~2 GB), whatever n.  *deflate_ms (optional): the compress kernels' device time, summed over
- * the batches (HIP events on the context's stream). */
+ * least sbh_bgzf_compress_bound(n) bytes.  Device scratch is bounded by a batch of members,
+ * whatever n: about 1.04 MB per member at levels 4..9 (prev 128 KiB, match records 512 KiB,
+ * tokens 256 KiB, block record 16 KiB, two 65.6 KB slots), batches of up to 8192 members
+ * (~8.5 GB; SBH_ZDEFLATE_BATCH overrides) and never more than half of the free HBM at the call
+ * (at least 256 members); SBH_LEVEL_FAST batches up to 2048 members of ~0.4 MB.  The uncompressed
+ * input (n bytes, when src is host memory) is staged in HBM as well.  *deflate_ms (optional): the
+ * compress kernels' device time, summed over the batches (HIP events on the context's stream). */
 #define SBH_LEVEL_HTSJDK 5
 #define SBH_LEVEL_FAST (-1)
 uint64_t sbh_bgzf_compress_bound(uint64_t n);

@@ -24,6 +24,7 @@ import org.hammerlab.bam.header.ContigLengths
 import org.hammerlab.bgzf.Pos
 import org.hammerlab.bgzf.block.{ Block, StreamI }
 import org.hammerlab.channel.{ ByteChannel, CachingChannel, SeekableByteChannel }
+import hammerlab.path._
 
 class NeedHaloException(msg: String) extends RuntimeException(msg)
 
@@ -42,6 +43,7 @@ object Native {
   @native def blocks(ctx: Long, sh: Long, first: Long, count: Long, out: Array[Long]): Unit
   @native def readFlat(ctx: Long, sh: Long, flat: Long, n: Long, out: ByteBuffer): Unit
   @native def flatOf(ctx: Long, sh: Long, vpos: Long): Long
+  @native def flatBound(ctx: Long, sh: Long, fileOff: Long): Long
   @native def posOf(ctx: Long, sh: Long, flat: Long): Long
   @native def setContigs(ctx: Long, sh: Long, lengths: Array[Int]): Unit
 
@@ -85,19 +87,21 @@ object Device {
   lazy val ctx: Long = Native.ctxCreate(sys.env.getOrElse("LOCAL_RANK", "0").toInt)
 }
 
-/** Compressed bytes [fileOffset, fileOffset + n) of a BGZF file, resident in HBM, indexed and
-  * inflated from block `start`, with the eager bitmap of every position once asked for. */
+/** Compressed bytes [fileOffset, fileOffset + n) of a BGZF file, resident in HBM. */
 class GpuShard(comp: ByteBuffer, n: Long, val fileOffset: Long, fileSize: Long, contigs: Array[Int])
   extends AutoCloseable {
   private val ctx = Device.ctx
   val sh: Long = Native.shardCreate(ctx, comp, n, fileOffset, fileSize)
   Native.setContigs(ctx, sh, contigs)
+  val atEof: Boolean = fileOffset + n == fileSize
   private val nf = new Array[Long](2)
   def load(start: Long): Unit = Native.indexAndInflate(ctx, sh, start, nf)
   def numBlocks: Long = nf(0)
   def flatSize: Long = nf(1)
   def flatOf(pos: Pos): Long = Native.flatOf(ctx, sh, pos.toHTSJDK)
   def posOf(flat: Long): Pos = Pos(Native.posOf(ctx, sh, flat))
+  /** flat image of Pos(fileOff, 0) as an exclusive bound (sbh_flat_bound) */
+  def flatBound(fileOff: Long): Long = Native.flatBound(ctx, sh, fileOff)
   /** (start, ustart, csize, hsize, usize, flags) of blocks [first, first + count) */
   def blocks(first: Long, count: Long): Array[Long] = {
     val out = new Array[Long](6 * count.toInt)
@@ -111,21 +115,19 @@ class GpuShard(comp: ByteBuffer, n: Long, val fileOffset: Long, fileSize: Long, 
     b.get(a)
     a
   }
-
-  private var bits: ByteBuffer = _
-  def eagerBits(readsToCheck: Int): ByteBuffer = {
-    if (bits == null) {
-      bits = ByteBuffer.allocateDirect(((flatSize + 7) / 8).toInt)
-      Native.checkEager(ctx, sh, 0, flatSize, readsToCheck, bits)
-    }
+  /** the eager bit of every flat position of [begin, end), in one batch */
+  def eagerBits(begin: Long, end: Long, readsToCheck: Int): ByteBuffer = {
+    val bits = ByteBuffer.allocateDirect(math.max(1L, (end - begin + 7) / 8).toInt)
+    Native.checkEager(ctx, sh, begin, end, readsToCheck, bits)
     bits
   }
-  def fullWord(flat: Long, readsToCheck: Int): Int = {
-    val w = ByteBuffer.allocateDirect(4).order(ByteOrder.LITTLE_ENDIAN)
-    val out = new Array[Long](2)
-    Native.checkFull(ctx, sh, flat, flat + 1, readsToCheck, w, null, null, null, null, 0, out)
-    w.getInt(0)
+  /** the full-checker word of every flat position of [begin, end), in one batch */
+  def fullWords(begin: Long, end: Long, readsToCheck: Int): ByteBuffer = {
+    val words = ByteBuffer.allocateDirect(math.max(4L, 4 * (end - begin)).toInt).order(ByteOrder.LITTLE_ENDIAN)
+    Native.checkFull(ctx, sh, begin, end, readsToCheck, words, null, null, null, null, 0, new Array[Long](2))
+    words
   }
+  /** FindRecordStart.withDelta from a flat position: Some((flat, delta)) or None */
   def findRecordStart(from: Long, readsToCheck: Int, maxReadSize: Int): Option[(Long, Int)] = {
     val out = new Array[Long](2)
     try {
@@ -146,62 +148,139 @@ class GpuShard(comp: ByteBuffer, n: Long, val fileOffset: Long, fileSize: Long, 
 }
 
 object GpuShard {
-  val Halo: Long = 4L << 20
-
-  /** The window [lo, lo + window) of the channel's file plus a halo, indexed from the first
-    * block at/after lo (FindBlockStart, bgzf/.../block/FindBlockStart.scala:8-36) and inflated. */
-  def load(ch: CachingChannel[SeekableByteChannel], lo: Long, window: Long, contigs: Array[Int],
-           blocksToCheck: Int = 5): GpuShard = {
+  /** [lo, min(size, lo + n)) of the channel's file as a resident shard */
+  def read(ch: SeekableByteChannel, lo: Long, n: Long, contigs: Array[Int]): GpuShard = {
     val size = ch.size
-    val n = math.min(size - lo, window + Halo)
-    val buf = Native.hostAlloc(n)
-    ch.seek(lo)
-    ch.readFully(buf)
-    buf.flip()
-    val s = new GpuShard(buf, n, lo, size, contigs)
-    s.load(Native.findBlockStart(Device.ctx, s.sh, lo, blocksToCheck))
-    Native.hostFree(buf)
-    s
+    val m = math.min(size - lo, n)
+    val buf = Native.hostAlloc(m)
+    try {
+      ch.seek(lo)
+      ch.readFully(buf)
+      buf.flip()
+      new GpuShard(buf, m, lo, size, contigs)
+    } finally Native.hostFree(buf)
   }
 
   def contigArray(contigLengths: ContigLengths): Array[Int] =
     contigLengths.map.values.map(_._2.toInt).toArray
 }
 
-/** Drop-in for check/.../eager/Checker.scala: Checker[Boolean] with ReadStartFinder, answered
-  * from the eager bitmap of a GPU window that holds the asked position (the window slides
-  * when a position past it is asked; a partition's positions come in order,
-  * CallPartition.scala:35-52). */
-class GpuEagerChecker(ch: CachingChannel[SeekableByteChannel],
-                      contigLengths: ContigLengths,
-                      readsToCheck: ReadsToCheck,
-                      window: Long = 256L << 20)
-  extends Checker[Boolean]
-    with ReadStartFinder {
+/** A window of the file on the GPU: compressed bytes [lo, lo + window + halo) indexed from
+  * FindBlockStart(lo) (bgzf/.../block/FindBlockStart.scala:8-36) and inflated.  It owns the blocks
+  * starting in [lo, hi = lo + window), i.e. flat positions [0, owned = flatBound(hi)); the halo
+  * only feeds the chains of the owned positions.  A halo with no block past hi throws
+  * NeedHaloException (the last owned block, or what follows it, is cut off).  Mirrored by
+  * spark_bam_amd.checkers.GpuWindow. */
+class GpuWindow(val shard: GpuShard, val lo: Long, val hi: Long) extends AutoCloseable {
+  val atEof: Boolean = shard.atEof
+  val owned: Long = shard.flatBound(hi)
+  if (!atEof && owned == shard.flatSize) {
+    shard.close()
+    throw new NeedHaloException(s"no block past $hi in the halo")
+  }
+  // the host block table: flatOf(pos) without a JNI call per position
+  private val table = shard.blocks(0, shard.numBlocks)
+  private val starts = Array.tabulate(shard.numBlocks.toInt)(i ⇒ table(6 * i))
+  def owns(blockPos: Long): Boolean = lo <= blockPos && blockPos < hi
+  def flatOf(pos: Pos): Long = {
+    val i = java.util.Arrays.binarySearch(starts, pos.blockPos)
+    if (i < 0) throw new IllegalArgumentException(s"${pos.blockPos} is not a block start of this window")
+    table(6 * i + 1) + pos.offset
+  }
+  def posOf(flat: Long): Pos = shard.posOf(flat)
+  override def close(): Unit = shard.close()
+}
 
-  private val contigs = GpuShard.contigArray(contigLengths)
-  private var shard: GpuShard = _
-  private var hi = -1L  // first file offset past the window's owned blocks
-
-  private def shardFor(blockPos: Long): GpuShard = {
-    if (shard == null || blockPos < shard.fileOffset || blockPos >= hi) {
-      if (shard != null) shard.close()
-      shard = GpuShard.load(ch, blockPos, window, contigs)
-      hi = blockPos + window
+object GpuWindow {
+  def load(ch: SeekableByteChannel, lo: Long, window: Long, halo: Long, contigs: Array[Int],
+           blocksToCheck: Int): GpuWindow = {
+    val s = GpuShard.read(ch, lo, window + halo, contigs)
+    try {
+      s.load(Native.findBlockStart(Device.ctx, s.sh, lo, blocksToCheck))
+    } catch {
+      case e: Throwable ⇒ s.close(); throw e
     }
-    shard
+    new GpuWindow(s, lo, lo + window)
+  }
+}
+
+/** The window cache both checkers share: the window holding the asked block (a partition's
+  * positions come in order, CallPartition.scala:35-52, so a window serves a run of calls) plus
+  * its batch (`fill`), reloaded with 4x the halo whenever either needs bytes past it. */
+abstract class WindowedChecker[B](ch: SeekableByteChannel, contigs: Array[Int], val readsToCheck: Int,
+                                  window: Long, var halo: Long, blocksToCheck: Int) {
+  protected def fill(w: GpuWindow): B
+
+  protected var w: GpuWindow = _
+  protected var batch: B = _
+
+  private def load(lo: Long): Unit = {
+    while (true) {
+      var nw: GpuWindow = null
+      try {
+        nw = GpuWindow.load(ch, lo, window, halo, contigs, blocksToCheck)
+        batch = fill(nw)
+        w = nw
+        return
+      } catch {
+        case e: NeedHaloException ⇒
+          if (nw != null) nw.close()
+          if (lo + window + halo >= ch.size) throw e
+          halo *= 4
+      }
+    }
   }
 
+  protected def windowFor(blockPos: Long, reload: Boolean = false): GpuWindow = {
+    if (reload || w == null || !w.owns(blockPos)) {
+      if (w != null) { w.close(); w = null }
+      load(blockPos)
+    }
+    w
+  }
+
+  def close(): Unit = if (w != null) { w.close(); w = null }
+}
+
+/** Drop-in for check/.../eager/Checker.scala: Checker[Boolean] with ReadStartFinder.  apply(pos)
+  * is a lookup in the window's eager bitmap, computed over the OWNED positions only
+  * ([0, flatBound(hi)): no position whose answer needs bytes past the halo); nextReadStart is
+  * FindRecordStart on the device, the halo grown on NeedHaloException.  Mirrored call for call by
+  * spark_bam_amd.checkers.WindowedEagerChecker (tests/test_checkers_gpu.py). */
+class GpuEagerChecker(ch: SeekableByteChannel,
+                      contigLengths: ContigLengths,
+                      readsToCheck: ReadsToCheck,
+                      window: Long = 256L << 20,
+                      halo: Long = 4L << 20,
+                      blocksToCheck: Int = 5)
+  extends WindowedChecker[ByteBuffer](ch, GpuShard.contigArray(contigLengths), readsToCheck.n, window, halo,
+                                      blocksToCheck)
+    with Checker[Boolean]
+    with ReadStartFinder {
+
+  override protected def fill(w: GpuWindow): ByteBuffer = w.shard.eagerBits(0, w.owned, readsToCheck.n)
+
   override def apply(pos: Pos): Boolean = {
-    val s = shardFor(pos.blockPos)
-    val f = s.flatOf(pos)
-    val bits = s.eagerBits(readsToCheck.n)
-    (bits.get((f >> 3).toInt) & (1 << (f & 7).toInt)) != 0
+    val f = windowFor(pos.blockPos).flatOf(pos)
+    (batch.get((f >> 3).toInt) & (1 << (f & 7).toInt)) != 0
   }
 
   override def nextReadStart(start: Pos)(implicit maxReadSize: MaxReadSize): Option[Pos] = {
-    val s = shardFor(start.blockPos)
-    s.findRecordStart(s.flatOf(start), readsToCheck.n, maxReadSize.n).map { case (f, _) ⇒ s.posOf(f) }
+    var reload = false
+    while (true) {
+      val cur = windowFor(start.blockPos, reload)
+      try {
+        return cur.shard.findRecordStart(cur.flatOf(start), readsToCheck.n, maxReadSize.n).map {
+          case (f, _) ⇒ cur.posOf(f)
+        }
+      } catch {
+        case e: NeedHaloException ⇒
+          if (cur.atEof) throw e
+          halo *= 4
+          reload = true
+      }
+    }
+    None
   }
 }
 
@@ -216,26 +295,26 @@ object GpuEagerChecker {
     }
 }
 
-/** Drop-in for check/.../full/Checker.scala: Checker[Result] -- the GPU's full-checker word
-  * (include/sparkbam.h: bit 31 Success, bits 20-29 readsParsed / readsBeforeError, bits 0-18
-  * the Flags in Flags.scala's serde order) turned back into Success(n) or Flags(...). */
-class GpuFullChecker(ch: CachingChannel[SeekableByteChannel],
+/** Drop-in for check/.../full/Checker.scala: Checker[Result].  The window's full-checker words
+  * (include/sparkbam.h: bit 31 Success, bits 20-29 readsParsed / readsBeforeError, bits 0-18 the
+  * Flags in Flags.scala's serde order) are computed once per window over its owned positions;
+  * apply(pos) turns one back into Success(n) or Flags(...).  32 MiB windows keep the word buffer
+  * (4 B per position) near 400 MB.  Mirrored by spark_bam_amd.checkers.WindowedFullChecker. */
+class GpuFullChecker(ch: SeekableByteChannel,
                      contigLengths: ContigLengths,
                      readsToCheck: ReadsToCheck,
-                     window: Long = 256L << 20)
-  extends Checker[Result] {
+                     window: Long = 32L << 20,
+                     halo: Long = 4L << 20,
+                     blocksToCheck: Int = 5)
+  extends WindowedChecker[ByteBuffer](ch, GpuShard.contigArray(contigLengths), readsToCheck.n, window, halo,
+                                      blocksToCheck)
+    with Checker[Result] {
 
-  private val contigs = GpuShard.contigArray(contigLengths)
-  private var shard: GpuShard = _
-  private var hi = -1L
+  override protected def fill(w: GpuWindow): ByteBuffer = w.shard.fullWords(0, w.owned, readsToCheck.n)
 
   override def apply(pos: Pos): Result = {
-    if (shard == null || pos.blockPos < shard.fileOffset || pos.blockPos >= hi) {
-      if (shard != null) shard.close()
-      shard = GpuShard.load(ch, pos.blockPos, window, contigs)
-      hi = pos.blockPos + window
-    }
-    GpuFullChecker.result(shard.fullWord(shard.flatOf(pos), readsToCheck.n))
+    val f = windowFor(pos.blockPos).flatOf(pos)
+    GpuFullChecker.result(batch.getInt((4 * f).toInt))
   }
 }
 
@@ -260,6 +339,153 @@ object GpuFullChecker {
     }
 }
 
+/** Drop-in for load/.../CanLoadBam.scala:268-302,316-356 (loadSplitsAndReads / loadBam's splits
+  * and per-partition counts) on the executors' GPUs.  The Hadoop FileSplits (SPLIT_SLOP 1.1,
+  * FileSplits.asJava) are dealt to `numTasks` Spark tasks as contiguous runs; each task loads its
+  * byte range plus a halo into one shard and runs FindBlockStart + index + inflate + the eager
+  * check at every owned position + every split's FindRecordStart and record count in a few
+  * launches (runTask); the driver collects the TaskParts, forms the splits by sliding2 over the
+  * non-empty splits' first records with Pos(fileSize, 0), and checks that the record chain leaving
+  * each task enters the next non-empty task at its first record, re-walking that task from the
+  * upstream exit (rewalk, a task of its own) where it does not.  Record decoding stays htsjdk's
+  * (loadBam: RecordStream from each split's first record while pos < the split's end).
+  * Mirrored call for call by spark_bam_amd.sharded.load_splits_and_reads_tasks / RankRun
+  * (tests/test_sharded.py test_gpu_tasks_*). */
+object GpuLoadBam {
+  /** One task's answer: per split (first record vpos or -1, count), and the task's record chain
+    * (first vpos or -1, count, exit vpos or -1: the first chain record at/after the task's end). */
+  case class TaskPart(task: Int, splitIndex: Int, firsts: Array[Long], counts: Array[Long], first: Long, count: Long,
+                      exit: Long)
+
+  /** Hadoop FileInputFormat.getSplits' arithmetic (SPLIT_SLOP 1.1) */
+  def fileSplits(size: Long, splitSize: Long): Array[(Long, Long)] = {
+    val out = scala.collection.mutable.ArrayBuffer[(Long, Long)]()
+    var rem = size
+    while (rem.toDouble / splitSize > 1.1) { out += ((size - rem, size - rem + splitSize)); rem -= splitSize }
+    if (rem != 0) out += ((size - rem, size))
+    out.toArray
+  }
+
+  /** task t's contiguous run of splits: (index of its first split, its splits) */
+  def taskSplits(size: Long, splitSize: Long, tasks: Int, t: Int): (Int, Array[(Long, Long)]) = {
+    val all = fileSplits(size, splitSize)
+    val a = t * all.length / tasks
+    (a, all.slice(a, (t + 1) * all.length / tasks))
+  }
+
+  private def exitVpos(s: GpuShard, flat: Long): Long = try s.posOf(flat).toHTSJDK catch { case _: Exception ⇒ -1L }
+
+  def runTask(path: Path, t: Int, splitIndex: Int, splits: Array[(Long, Long)], contigs: Array[Int],
+              halo0: Long = 1L << 20, blocksToCheck: Int = 5, readsToCheck: Int = 10,
+              maxReadSize: Int = 100000000): TaskPart = {
+    if (splits.isEmpty) return TaskPart(t, splitIndex, Array.empty, Array.empty, -1L, 0L, -1L)
+    val ch = SeekableByteChannel(path)
+    try {
+      val (lo, hi) = (splits.head._1, splits.last._2)
+      var halo = halo0
+      while (true) {
+        val s = GpuShard.read(ch, lo, hi - lo + halo, contigs)
+        try {
+          val start = Native.findBlockStart(Device.ctx, s.sh, lo, blocksToCheck)
+          val r = new Array[Long](7)  // nBlocks, compBytes, flatBytes, nTrue, firstVpos, count, exitFlat
+          Native.runShard(Device.ctx, s.sh, start, hi, readsToCheck, maxReadSize, r)
+          val per = s.splits(splits.map(_._1), splits.map(_._2), blocksToCheck, readsToCheck, maxReadSize)
+          per.zip(splits).find(_._1._1 != 0).foreach {
+            case ((st, _, _), (a, e)) ⇒ throw new IllegalStateException(s"split $a-$e: status $st")
+          }
+          val exit = if (r(5) > 0) exitVpos(s, r(6)) else -1L
+          return TaskPart(t, splitIndex, per.map { case (_, v, n) ⇒ if (n > 0) v else -1L }, per.map(_._3),
+                          if (r(5) > 0) r(4) else -1L, r(5), exit)
+        } catch {
+          case e: NeedHaloException ⇒
+            if (hi + halo >= ch.size) throw e
+            halo *= 4
+        } finally s.close()
+      }
+      throw new IllegalStateException("unreachable")
+    } finally ch.close()
+  }
+
+  /** The chain from fromVpos through the task's range [.., hi), window by window (each window's
+    * eager bitmap first, then the chain): (records, exit vpos or -1). */
+  def rewalk(path: Path, hi: Long, halo0: Long, contigs: Array[Int], fromVpos: Long, readsToCheck: Int = 10,
+             window: Long = 1L << 30): (Long, Long) = {
+    val ch = SeekableByteChannel(path)
+    try {
+      var total = 0L
+      var v = fromVpos
+      while (true) {
+        val blo = v >>> 16
+        if (blo >= hi) return (total, v)
+        val whi = math.min(hi, blo + window)
+        var halo = math.max(halo0, 1L << 20)
+        var (n, ex, nxt) = (0L, -1L, -1L)
+        var done = false
+        while (!done) {
+          val s = GpuShard.read(ch, blo, whi - blo + halo, contigs)
+          try {
+            s.load(blo)
+            val f = s.flatOf(Pos(v))
+            val e = s.flatBound(whi)
+            Native.checkEager(Device.ctx, s.sh, f, e, readsToCheck, null)
+            val out = new Array[Long](2)
+            Native.chainFrom(Device.ctx, s.sh, f, e, out)
+            n = out(0)
+            ex = if (n > 0) exitVpos(s, out(1)) else v
+            val t = s.blocks(0, s.numBlocks)
+            nxt = (0 until s.numBlocks.toInt).map(i ⇒ t(6 * i)).find(_ >= whi).getOrElse(-1L)
+            done = true
+          } catch {
+            case e: NeedHaloException ⇒
+              if (whi + halo >= ch.size) throw e
+              halo *= 4
+          } finally s.close()
+        }
+        total += n
+        if (ex < 0 || whi >= hi) return (total, ex)
+        v = if (ex == v) { if (nxt < 0) throw new NeedHaloException(s"no block past $whi"); nxt << 16 } else ex
+      }
+      (total, v)
+    } finally ch.close()
+  }
+
+  /** Chain mismatches of the non-empty tasks in order: (next task, upstream exit vpos) where the
+    * chain leaving a task does not enter the next one at its first record (after re-walks). */
+  def mismatches(parts: Seq[TaskPart], rewalks: Map[Int, (Long, Long, Long)]): Seq[(Int, Long)] = {
+    val eff = parts.map(p ⇒ rewalks.get(p.task).map { case (f, n, x) ⇒ (p.task, f, n, x) }
+                                  .getOrElse((p.task, p.first, p.count, p.exit))).filter(_._3 > 0)
+    eff.zip(eff.drop(1)).collect { case (a, b) if a._4 != b._2 && a._4 >= 0 ⇒ (b._1, a._4) }
+  }
+
+  /** loadSplitsAndReads' splits and per-split record counts (CanLoadBam.scala:268-302). */
+  def loadSplitsAndCounts(sc: org.apache.spark.SparkContext, path: Path, splitSize: Long, numTasks: Int,
+                          contigLengths: ContigLengths): (Vector[org.hammerlab.bam.spark.Split], Vector[Long]) = {
+    val size = path.size
+    val contigs = GpuShard.contigArray(contigLengths)
+    val tasks = (0 until numTasks).map(t ⇒ (t, taskSplits(size, splitSize, numTasks, t)))
+    val parts = sc.parallelize(tasks, numTasks)
+      .map { case (t, (a, sp)) ⇒ runTask(path, t, a, sp, contigs) }
+      .collect()
+      .sortBy(_.splitIndex)
+      .toSeq
+    var rewalks = Map.empty[Int, (Long, Long, Long)]
+    var round = 0
+    var todo = mismatches(parts, rewalks)
+    while (todo.nonEmpty && round < numTasks) {
+      val his = parts.map(p ⇒ p.task → (if (p.counts.isEmpty) 0L else taskSplits(size, splitSize, numTasks, p.task)._2.last._2)).toMap
+      val redone = sc.parallelize(todo.distinct, todo.size)
+        .map { case (t, v) ⇒ t → { val (n, x) = rewalk(path, his(t), 1L << 20, contigs, v); (v, n, x) } }
+        .collect()
+      rewalks ++= redone
+      todo = mismatches(parts, rewalks)
+      round += 1
+    }
+    val firsts = parts.flatMap(p ⇒ p.firsts.zip(p.counts).collect { case (v, n) if n > 0 ⇒ Pos(v) })
+    val splits = firsts.zip(firsts.drop(1) :+ Pos(size, 0)).map { case (a, b) ⇒ org.hammerlab.bam.spark.Split(a, b) }
+    (splits.toVector, parts.flatMap(_.counts).toVector)
+  }
+}
+
 /** Drop-in for bgzf/.../block/Stream.scala's StreamI: the Block iterator over a channel, blocks
   * inflated on the GPU a window at a time; Block.bytes is copied out only for the block handed
   * out (Block.scala:12-46).  An empty block ends the stream (Stream.scala:56-58). */
@@ -274,14 +500,8 @@ case class GpuStream(compressedBytes: ByteChannel with SeekableByteChannel, wind
   private def refill(): Boolean = {
     if (shard != null) shard.close()
     if (lo >= compressedBytes.size) return false
-    val n = math.min(compressedBytes.size - lo, window + GpuShard.Halo)
-    val buf = Native.hostAlloc(n)
-    compressedBytes.seek(lo)
-    compressedBytes.readFully(buf)
-    buf.flip()
-    shard = new GpuShard(buf, n, lo, compressedBytes.size, Array.empty[Int])
+    shard = GpuShard.read(compressedBytes, lo, window + (4L << 20), Array.empty[Int])
     shard.load(lo)
-    Native.hostFree(buf)
     table = shard.blocks(0, shard.numBlocks)
     next = 0
     true

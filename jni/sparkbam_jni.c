@@ -197,6 +197,14 @@ JNIEXPORT jlong JNICALL Java_org_hammerlab_bam_gpu_Native_00024_posOf(JNIEnv *en
   return (jlong)((bp << 16) | off);
 }
 
+/* flat image of Pos(fileOff, 0) as an exclusive bound: the first block at/after fileOff */
+JNIEXPORT jlong JNICALL Java_org_hammerlab_bam_gpu_Native_00024_flatBound(JNIEnv *env, jobject self, jlong ctx,
+                                                                          jlong sh, jlong fileOff) {
+  uint64_t f = 0;
+  if (failed(env, ctx, sbh_flat_bound(SH(sh), (uint64_t)fileOff, &f))) return -1;
+  return (jlong)f;
+}
+
 /* ContigLengths (check/.../header/ContigLengths.scala) */
 JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_setContigs(JNIEnv *env, jobject self, jlong ctx,
                                                                           jlong sh, jintArray lens) {

@@ -5,7 +5,8 @@ Import name: ``spark_bam_amd`` (the directory name contains a hyphen, so load it
 ``__graft_entry__.load_package()`` or importlib).  Names follow the reference:
 
   bgzf:   Pos, Header.make, Metadata, FindBlockStart, Stream (blocks / inflated bytes)
-  check:  eager.Checker / full.Checker (batched over positions), FindRecordStart
+  check:  eager.Checker / full.Checker (batched over positions; per-position windowed
+          WindowedEagerChecker / WindowedFullChecker), FindRecordStart
   load:   load_splits_and_reads / load_bam_count / load_reads / load_bam_intervals
           (CanLoadBam), FileSplits, read_bai (bam.index.Index)
 """
@@ -16,6 +17,7 @@ from .api import (FLAG_NAMES, htsjdk_rewrite, Header, Metadata, Pos, Split, bam_
                   file_splits, full_check, load_bam_count, load_reads, load_splits_and_reads,
                   parse_bam_header)
 from .records import Reads  # noqa: F401
+from .checkers import GpuWindow, WindowedEagerChecker, WindowedFullChecker  # noqa: F401
 from .intervals import (Chunk, Index, get_interval_chunks, load_bam_intervals,  # noqa: F401
                         parse_loci, read_bai)
 
@@ -25,4 +27,5 @@ __all__ = [
     "file_splits", "load_splits_and_reads", "load_bam_count", "check_bam", "full_check",
     "bam_header", "parse_bam_header", "lib", "load_reads", "Reads", "Chunk", "Index",
     "read_bai", "parse_loci", "get_interval_chunks", "load_bam_intervals",
+    "GpuWindow", "WindowedEagerChecker", "WindowedFullChecker",
 ]

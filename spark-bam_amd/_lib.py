@@ -39,6 +39,7 @@ EXPORTS = [
     "sbh_check_records", "sbh_run_shard",
     "sbh_stage_times", "sbh_run_stream", "sbh_run_stream2", "sbh_records_scan", "sbh_records_fetch", "sbh_records_scan_regions", "sbh_verify_crc",
     "sbh_bgzf_compress_bound", "sbh_bgzf_compress", "sbh_bgzf_compress_level",
+    "sbh_shard_load", "sbh_find_blocks", "sbh_check_stream",
 ]
 LEVEL_HTSJDK, LEVEL_FAST = 5, -1  # sbh_bgzf_compress_level: htsjdk's zlib level 5 / this library's own coder
 
@@ -70,6 +71,21 @@ class SbhStreamOpts(C.Structure):
                 ("split_start", C.c_void_p), ("split_end", C.c_void_p), ("n_splits", C.c_uint64),
                 ("split_first_vpos", C.c_void_p), ("split_count", C.c_void_p), ("split_status", C.c_void_p),
                 ("out_bits", C.c_void_p), ("out_bits_cap", C.c_uint64)]
+
+
+class SbhCheckOpts(C.Structure):
+    _fields_ = [("window", C.c_uint64), ("halo", C.c_uint64), ("reads_to_check", C.c_int32), ("full", C.c_int32),
+                ("blocks", C.c_void_p), ("n_blocks", C.c_uint64), ("truth_vpos", C.c_void_p),
+                ("n_truth", C.c_uint64), ("fp_vpos", C.c_void_p), ("fn_vpos", C.c_void_p), ("fp_cap", C.c_uint64),
+                ("fn_cap", C.c_uint64), ("counts", C.c_void_p), ("rbe_hist", C.c_void_p),
+                ("close_vpos", C.c_void_p), ("close_word", C.c_void_p), ("close_cap", C.c_uint64)]
+
+
+class SbhCheckResult(C.Structure):
+    _fields_ = [("n_windows", C.c_uint64), ("positions", C.c_uint64), ("comp_bytes", C.c_uint64),
+                ("n_true", C.c_uint64), ("tp", C.c_uint64), ("fp", C.c_uint64), ("fn", C.c_uint64),
+                ("unknown", C.c_uint64), ("n_success", C.c_uint64), ("n_close", C.c_uint64),
+                ("halo_final", C.c_uint64), ("ms_wall", C.c_double), ("ms_h2d", C.c_double)]
 
 
 class SbhRecordsSizes(C.Structure):
@@ -141,6 +157,9 @@ def lib():
         "sbh_records_fetch": [P, C.POINTER(SbhRecordsOut)],
         "sbh_records_scan_regions": [P, P, P, U64, P, P, P, C.c_uint32, C.POINTER(SbhRecordsSizes)],
         "sbh_verify_crc": [P, PU64, PU64],
+        "sbh_shard_load": [P, P, U64, U64, C.c_int],
+        "sbh_find_blocks": [P, P, U64, P, P, U64, I32, U64, P, U64, PU64],
+        "sbh_check_stream": [P, P, U64, P, I32, C.POINTER(SbhCheckOpts), C.POINTER(SbhCheckResult)],
         "sbh_bgzf_compress": [P, P, U64, I32, P, U64, PU64, PU64, C.POINTER(C.c_float)],
         "sbh_bgzf_compress_level": [P, P, U64, I32, I32, P, U64, PU64, PU64, C.POINTER(C.c_float)],
     }

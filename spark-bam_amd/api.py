@@ -191,74 +191,149 @@ def load_bam_count(path_or_bytes, split_size=DEFAULT_SPLIT_SIZE, ctx=None, **kw)
     return sum(counts)
 
 
-def _selected_flat_ranges(shard, ranges):
-    """Blocks.apply's `-i` filter: blocks whose START lies in one of the byte ranges
-    (check/.../check/Blocks.scala:89-96) -> merged flat ranges."""
-    blocks = shard.blocks()
-    out = []
-    for start, csize, usize, ustart, _h, flags in blocks:
-        if usize == 0:
-            continue
-        if ranges is not None and not any(a <= start < b for a, b in ranges):
-            continue
-        if out and out[-1][1] == ustart:
-            out[-1][1] = ustart + usize
-        else:
-            out.append([ustart, ustart + usize])
-    comp = sum(c for s, c, u, *_ in blocks if u and (ranges is None or any(a <= s < b for a, b in ranges)))
-    return [(a, b) for a, b in out], comp
+DEFAULT_BLOCKS_SPLIT_SIZE = 2 << 20  # Blocks.apply's maxSplitSize(2 MB) (check/.../check/Blocks.scala:74-78)
+STREAM_WINDOW = int(os.environ.get("SBH_STREAM_WINDOW", str(1 << 30)))  # compressed bytes per HBM window
 
 
-def check_bam(path_or_bytes, records=None, ranges=None, ctx=None,
-              reads_to_check=DEFAULT_READS_TO_CHECK):
-    """CheckBam -s (cli/.../check/eager/CheckBam.scala + CheckerApp.scala:65-227): the
-    eager checker at every position of the selected blocks vs the `.records` truth.
-    `records` is a list of (blockPos, offset); returns the summary numbers."""
-    L = _Loaded(path_or_bytes, ctx, reads_to_check)
+def _file_array(path_or_bytes):
+    """The whole file as numpy uint8: memory-mapped for a path (pages are read as windows
+    move through HBM, never all at once)."""
+    if isinstance(path_or_bytes, np.ndarray):
+        return path_or_bytes
+    if isinstance(path_or_bytes, (bytes, bytearray, memoryview)):
+        return np.frombuffer(bytes(path_or_bytes), dtype=np.uint8)
+    return np.memmap(path_or_bytes, dtype=np.uint8, mode="r")
+
+
+def file_header(ctx, data):
+    """Header(path) (check/.../header/Header.scala:26-60) from the file's leading blocks inflated
+    on the device: (contig names, contig lengths, flat end of the header)."""
+    size = int(data.size)
+    n = min(size, 1 << 20)
+    while True:
+        sh = ctx.shard(np.ascontiguousarray(data[:n]), file_offset=0, file_size=size)
+        try:
+            sh.index(0)
+            sh.inflate()
+            try:
+                return parse_bam_header(sh.read_flat(0, sh.flat_size))
+            except (IndexError, ValueError):
+                if n >= size:
+                    raise
+        finally:
+            sh.close()
+        n = min(size, n * 4)
+
+
+def _in_ranges(ranges, x):
+    return ranges is None or any(a <= x < b for a, b in ranges)
+
+
+def blocks(path_or_bytes, split_size=None, ranges=None, blocks_path=None, ctx=None,
+           bgzf_blocks_to_check=DEFAULT_BGZF_BLOCKS_TO_CHECK):
+    """Blocks.apply (check/src/main/scala/org/hammerlab/bam/check/Blocks.scala:47-208): the BGZF
+    blocks the all-positions modes examine, as (partitions, bounds) -- partitions a list of
+    [Metadata, ...] per partition, bounds the [(start, end)] byte range of each.
+
+    With a `.blocks` file (`blocks_path`, default the BAM path + ".blocks"): its blocks whose start
+    lies in `ranges`, partitioned by their cumulative compressed size / split_size (:86-139).
+    Without one: the file is cut every split_size bytes, the splits that meet `ranges` are kept,
+    and each one's blocks are FindBlockStart(split start) then MetadataStream while the block
+    start is < the split end (:141-206), found on the device (sbh_find_blocks)."""
+    split = int(split_size or DEFAULT_BLOCKS_SPLIT_SIZE)
+    if blocks_path is None and isinstance(path_or_bytes, (str, os.PathLike)):
+        blocks_path = str(path_or_bytes) + ".blocks"
+    if blocks_path is not None and os.path.exists(blocks_path):
+        metas = []
+        with open(blocks_path) as f:
+            for line in f:
+                if not line.strip():
+                    continue
+                parts = line.strip().split(",")
+                if len(parts) != 3:
+                    raise ValueError(f"Bad blocks-index line: {line.strip()}")
+                m = Metadata(int(parts[0]), int(parts[1]), int(parts[2]))
+                if _in_ranges(ranges, m.start):
+                    metas.append(m)
+        # partition = (compressed bytes of the blocks before it) / split_size; the partition count is
+        # the last block's partition + 1 (as BlocksTest pins it: "block boundaries" has 5 partitions
+        # for blocks at offsets 0, 25228, 50313 of 74344 bytes at a 10 KiB split size)
+        out, off = [], 0
+        for m in metas:
+            k = off // split
+            out += [[] for _ in range(k + 1 - len(out))]
+            out[k].append(m)
+            off += m.compressed_size
+        return out, [(i * split, (i + 1) * split) for i in range(len(out))]
+    data = _file_array(path_or_bytes)
+    size = int(data.size)
+    idxs = [i for i in range(-(-size // split))
+            if ranges is None or any(a < (i + 1) * split and b > i * split and a < b for a, b in ranges)]
+    own_ctx = ctx is None
+    ctx = ctx or Context(0)
     try:
-        sh = L.shard
-        fr, comp = _selected_flat_ranges(sh, ranges)
-        positions = sum(b - a for a, b in fr)
-        if records is None:
-            tp = sum(sh.check_eager(a, b, reads_to_check, want_bits=False)[0] for a, b in fr)
-            return {"positions": positions, "compressed": comp, "reads": tp, "true_positives": tp,
-                    "false_positives": 0, "false_negatives": 0, "fp_positions": [], "fn_positions": []}
-        vpos = np.asarray([(b << 16) | o for b, o in records], dtype=np.uint64)
-        tp, fp, fn, unknown, fpl, fnl = sh.check_records(fr, vpos, reads_to_check)
-        if unknown:
-            raise SparkBamError(19, f"{unknown} .records positions are not block starts of this file")
-        return {"positions": positions, "compressed": comp, "reads": tp + fn,
-                "true_positives": tp, "false_positives": fp, "false_negatives": fn,
-                "fp_positions": [Pos(*sh.pos_of(int(x))) for x in fpl],
-                "fn_positions": [Pos(*sh.pos_of(int(x))) for x in fnl]}
+        found = ctx.find_blocks(data, [(i * split, min(size, (i + 1) * split)) for i in idxs], bgzf_blocks_to_check)
     finally:
-        L.close()
+        if own_ctx:
+            ctx.close()
+    out = [[] for _ in idxs]
+    for k, start, cs, us in found:
+        if _in_ranges(ranges, start):
+            out[k].append(Metadata(start, cs, us))
+    return out, [(i * split, (i + 1) * split) for i in idxs]
 
 
-def full_check(path_or_bytes, ranges=None, ctx=None, reads_to_check=DEFAULT_READS_TO_CHECK):
-    """FullCheck (cli/.../check/full/FullCheck.scala:88-329) aggregation: Counts per
-    numNonZeroFields, totals, and the critical (1-flag) / close (2-flag) positions."""
-    L = _Loaded(path_or_bytes, ctx, reads_to_check)
+def _all_positions(path_or_bytes, ranges, ctx, reads_to_check, split_size, blocks_path, window, **kw):
+    """Blocks.apply, then every position of those blocks through sbh_check_stream (HBM windows
+    of `window` compressed bytes, whatever the file size)."""
+    data = _file_array(path_or_bytes)
+    own_ctx = ctx is None
+    ctx = ctx or Context(0)
     try:
-        sh = L.shard
-        fr, comp = _selected_flat_ranges(sh, ranges)
-        counts = np.zeros((21, 19), dtype=np.uint64)
-        rbe = np.zeros((21, 64), dtype=np.uint64)
-        n_success = positions = 0
-        close = []
-        for a, b in fr:
-            r = sh.check_full(a, b, reads_to_check)
-            counts += r["counts"]
-            rbe += r["rbe"]
-            n_success += r["n_success"]
-            positions += b - a
-            for f, w in zip(r["close_flat"].tolist(), r["close_word"].tolist()):
-                close.append((Pos(*sh.pos_of(int(f))), int(w)))
-        totals = dict(zip(FLAG_NAMES, counts.sum(axis=0).astype(np.int64).tolist()))
-        return {"positions": positions, "compressed": comp, "n_success": n_success,
-                "counts_by_nnz": counts, "rbe_by_nnz": rbe, "totals": totals, "close": close}
+        parts, _ = blocks(path_or_bytes if not isinstance(path_or_bytes, (bytes, bytearray, memoryview))
+                          else data, split_size, ranges, blocks_path, ctx)
+        starts = [m.start for p in parts for m in p]
+        _, contig_len, _ = file_header(ctx, data)
+        return ctx.check_stream(data, contig_len, starts, window=window or STREAM_WINDOW,
+                                reads_to_check=reads_to_check, **kw)
     finally:
-        L.close()
+        if own_ctx:
+            ctx.close()
+
+
+def check_bam(path_or_bytes, records=None, ranges=None, ctx=None, reads_to_check=DEFAULT_READS_TO_CHECK,
+              split_size=None, blocks_path=None, window=None):
+    """CheckBam -s (cli/.../check/eager/CheckBam.scala + CheckerApp.scala:65-227): the eager
+    checker at every position of Blocks.apply's blocks vs the `.records` truth.  `records` is a
+    list of (blockPos, offset); returns the summary numbers.  Any file size: the blocks move
+    through HBM in windows (sbh_check_stream)."""
+    truth = None
+    if records is not None:
+        truth = np.sort(np.asarray([(b << 16) | o for b, o in records], dtype=np.uint64))
+    r = _all_positions(path_or_bytes, ranges, ctx, reads_to_check, split_size, blocks_path, window,
+                       truth_vpos=truth)
+    out = {"positions": r["positions"], "compressed": r["comp_bytes"], "n_windows": r["n_windows"]}
+    if truth is None:
+        return dict(out, reads=r["n_true"], true_positives=r["n_true"], false_positives=0, false_negatives=0,
+                    fp_positions=[], fn_positions=[])
+    if r["unknown"]:
+        raise SparkBamError(19, f"{r['unknown']} .records positions are not block starts of this file")
+    return dict(out, reads=r["tp"] + r["fn"], true_positives=r["tp"], false_positives=r["fp"],
+                false_negatives=r["fn"], fp_positions=[Pos.from_htsjdk(int(v)) for v in r["fp_vpos"]],
+                fn_positions=[Pos.from_htsjdk(int(v)) for v in r["fn_vpos"]])
+
+
+def full_check(path_or_bytes, ranges=None, ctx=None, reads_to_check=DEFAULT_READS_TO_CHECK, split_size=None,
+               blocks_path=None, window=None):
+    """FullCheck (cli/.../check/full/FullCheck.scala:88-329) aggregation over Blocks.apply's
+    blocks: Counts per numNonZeroFields, totals, and the critical (1-flag) / close (2-flag)
+    positions.  Any file size (sbh_check_stream)."""
+    r = _all_positions(path_or_bytes, ranges, ctx, reads_to_check, split_size, blocks_path, window, full=True)
+    counts = r["counts"]
+    totals = dict(zip(FLAG_NAMES, counts.sum(axis=0).astype(np.int64).tolist()))
+    return {"positions": r["positions"], "compressed": r["comp_bytes"], "n_success": r["n_success"],
+            "counts_by_nnz": counts, "rbe_by_nnz": r["rbe"], "totals": totals, "n_windows": r["n_windows"],
+            "close": [(Pos.from_htsjdk(int(v)), int(w)) for v, w in zip(r["close_vpos"], r["close_word"])]}
 
 
 def flags_of(word):

@@ -407,6 +407,30 @@ int sbh_shard_destroy(sbh_shard *sh) {
   return SBH_OK;
 }
 
+int sbh_shard_load(sbh_shard *sh, const void *src, uint64_t n, uint64_t file_offset, int comp_on_device) {
+  if (!sh || (!src && n) || file_offset + n > sh->file_size) return SBH_E_ARG;
+  sbh_ctx *ctx = sh->ctx;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));  // (no kernel may still read the old bytes)
+  HIPCHK(ctx, sh->comp.ensure(n + sh->pad));
+  if (n)
+    HIPCHK(ctx, hipMemcpyAsync(sh->comp.p, src, n, comp_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                               ctx->stream));
+  HIPCHK(ctx, hipMemsetAsync(sh->comp.p + n, 0, sh->pad, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  sh->file_off = file_offset;
+  sh->n = n;
+  sh->at_eof = file_offset + n == sh->file_size;
+  sh->indexed = sh->inflated = sh->bits_valid = sh->chain_ok = sh->cm_valid = false;
+  sh->rec.valid = false;
+  sh->ncand = 0;
+  sh->scan_from = ~0ull;
+  sh->hb.clear();
+  sh->nblocks = sh->utotal = 0;
+  return SBH_OK;
+}
+
 const void *sbh_shard_comp_device_ptr(sbh_shard *sh) { return sh ? sh->comp.p : nullptr; }
 
 // FindBlockStart.apply (bgzf/.../block/FindBlockStart.scala:8-36)
@@ -1618,21 +1642,25 @@ int sbh_run_stream2(sbh_ctx *ctx, const void *host, uint64_t n, uint64_t file_of
   const uint64_t data_end = file_offset + n, pad = sh->pad;
   // the first window is short: its copy is the only one no kernel overlaps
   const uint64_t first_window = std::max<uint64_t>(std::min<uint64_t>(window, 64ull << 20), window / 8);
-  // window ends: split starts when splits are given (a split never straddles two windows)
+  // window ends: the last split start in (lo, lo + window] when splits are given, so a split
+  // lies in one window unless it is longer than a window; such a split is cut at lo + window and
+  // its chain followed window by window (the straddling split below), so HBM stays bounded
+  // whatever the split size (one split per rank included)
   auto win_end = [&](uint64_t lo) {
     const uint64_t want = lo + (lo == file_offset ? first_window : window);
     uint64_t hi = std::min(want, own_end_file);
     if (own_end_file - hi < window / 4) hi = own_end_file;  // no sliver of a last window
     if (ns && hi < own_end_file) {
-      // the last split start in (lo, hi], else the first one after lo
       const uint64_t *S = O.split_start;
       const uint64_t k = (uint64_t)(std::upper_bound(S, S + ns, hi) - S);  // starts <= hi: [0, k)
       if (k > 0 && S[k - 1] > lo) hi = S[k - 1];
-      else if (k < ns) hi = S[k];
-      else hi = own_end_file;
     }
     return hi;
   };
+  // the split that runs past its first window: its index, and the htsjdk vpos of the next record
+  // of its own chain (from its first record, CanLoadBam.scala:338-355) not yet counted
+  int64_t strad = -1;
+  uint64_t strad_cur = 0;
   auto load_end = [&](uint64_t hi) { return std::min(hi + halo, data_end); };
   auto size_bufs = [&]() -> hipError_t {  // (enqueue grows a buffer for a longer split-aligned window)
     const uint64_t cap = window + window / 4 + halo + pad;
@@ -1694,21 +1722,69 @@ int sbh_run_stream2(sbh_ctx *ctx, const void *host, uint64_t n, uint64_t file_of
     sbh_shard_result r{};
     sh->scan_from = lo;  // header candidates from the window's first byte (its first split's FindBlockStart)
     rc = sbh_run_shard(sh, start, hi, rtc, mrs, &r);
-    // this window's splits (every one inside [lo, hi)): the batched per-split path
+    // this window's splits (every one starting in [lo, hi)): the batched per-split path for the
+    // ones that end by hi; the last one may run past hi (a split longer than the window)
     uint64_t k0 = 0, k1 = 0, nh = 0;
     double split_ms = 0;
+    // the straddling split's progress in this window, committed once the window holds
+    int64_t s_idx = strad;
+    uint64_t s_cur = strad_cur, s_add = 0, s_first = 0;
+    int32_t s_status = SBH_OK;
+    bool s_new = false, s_done = false;
     if (!rc && ns) {
+      const auto ts0 = std::chrono::steady_clock::now();
       k0 = (uint64_t)(std::lower_bound(O.split_start, O.split_start + ns, lo) - O.split_start);
       k1 = (uint64_t)(std::lower_bound(O.split_start, O.split_start + ns, hi) - O.split_start);
-      if (k1 > k0) {
-        const auto ts0 = std::chrono::steady_clock::now();
-        rc = sbh_split_starts(sh, O.split_start + k0, O.split_end + k0, k1 - k0, kcheck, rtc, mrs,
+      const bool straddles = k1 > k0 && O.split_end[k1 - 1] > hi;
+      const uint64_t kb = straddles ? k1 - 1 : k1;
+      if (kb > k0) {
+        rc = sbh_split_starts(sh, O.split_start + k0, O.split_end + k0, kb - k0, kcheck, rtc, mrs,
                               O.split_first_vpos + k0, O.split_count + k0, O.split_status + k0, &nh);
         if (!rc)
-          for (uint64_t i = k0; i < k1; ++i)
+          for (uint64_t i = k0; i < kb; ++i)
             if (O.split_status[i] == SBH_E_NEED_HALO) rc = SBH_E_NEED_HALO;
-        split_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
       }
+      uint64_t E_hi = 0;
+      if (!rc) rc = sbh_flat_bound(sh, hi, &E_hi);
+      // follow a chain from flat f while its records start before min(Pos(split end, 0), Pos(hi, 0))
+      auto follow = [&](uint64_t f, uint64_t split_end) -> int {
+        uint64_t E_end = 0, n = 0, x = 0, bp = 0;
+        uint32_t off = 0;
+        int r = sbh_flat_bound(sh, split_end, &E_end);
+        if (!r) r = sbh_chain_from(sh, f, std::min(E_end, E_hi), &n, &x);
+        if (!r && x >= sh->utotal && !sh->at_eof) r = SBH_E_NEED_HALO;  // its next record is past the halo
+        if (!r) r = sbh_pos_of(sh, x, &bp, &off);
+        if (r) return r;
+        s_add += n;
+        s_cur = bp << 16 | off;
+        s_done = E_end <= E_hi || s_cur >= (split_end << 16);
+        return SBH_OK;
+      };
+      if (!rc && s_idx >= 0 && (s_cur >> 16) < hi) {  // a split from an earlier window goes on here
+        uint64_t f = 0;
+        rc = sbh_flat_of(sh, s_cur >> 16, (uint32_t)(s_cur & 0xffff), &f);
+        if (!rc) rc = follow(f, O.split_end[s_idx]);
+      }
+      if (!rc && straddles) {  // FindBlockStart + FindRecordStart here, then its chain to hi
+        const uint64_t a = O.split_start[k1 - 1], e = O.split_end[k1 - 1];
+        uint64_t fbs = 0, f0 = 0, first = 0, bp = 0;
+        uint32_t off = 0;
+        int32_t delta = 0;
+        s_idx = (int64_t)(k1 - 1), s_new = true, s_add = 0;
+        rc = sbh_find_block_start(sh, a, kcheck, &fbs);
+        if (!rc) rc = sbh_flat_of(sh, fbs, 0, &f0);
+        if (!rc) rc = sbh_find_record_start(sh, f0, rtc, mrs, &first, &delta);
+        if (!rc) rc = sbh_pos_of(sh, first, &bp, &off);
+        if (rc == SBH_E_NO_READ_FOUND || rc == SBH_E_HEADER_SEARCH_FAILED) {
+          s_status = rc, s_done = true, rc = SBH_OK;
+        } else if (!rc) {
+          s_first = bp << 16 | off;
+          s_cur = s_first;
+          if (s_first >= (e << 16)) s_done = true;
+          else rc = follow(first, e);
+        }
+      }
+      split_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
     }
     if (rc == SBH_E_NEED_HALO && ld < data_end) {  // grow the halo and redo this window
       HIPCHK(ctx, hipStreamSynchronize(R.cs));
@@ -1725,6 +1801,16 @@ int sbh_run_stream2(sbh_ctx *ctx, const void *host, uint64_t n, uint64_t file_of
       continue;
     }
     if (rc) return res->status = rc;
+    if (s_idx >= 0) {  // commit the straddling split's progress
+      if (s_new) {
+        O.split_status[s_idx] = s_status;
+        O.split_first_vpos[s_idx] = s_first;
+        O.split_count[s_idx] = 0;
+      }
+      O.split_count[s_idx] += s_add;
+      strad = s_done ? -1 : s_idx;
+      strad_cur = s_cur;
+    }
     res->ms_splits += split_ms;
     res->splits_host += nh;  // (a window redone with a larger halo counts its final attempt only)
     account(cur);
@@ -2034,8 +2120,18 @@ int sbh_bgzf_compress_level(sbh_ctx *ctx, const void *src, uint64_t n, int src_o
     uint64_t bmax = fast ? DEFLATE_BATCH : ZDEFLATE_BATCH;
     if (const char *e = std::getenv("SBH_ZDEFLATE_BATCH"))
       if (!fast && std::strtoull(e, nullptr, 10) > 0) bmax = std::strtoull(e, nullptr, 10);
-    const uint64_t cap = nb < bmax ? nb : bmax;
     const uint64_t stride = fast ? 65536ull : ZDEFLATE_SLOT;
+    // scratch per member; the batch shrinks to half of the free HBM (a resident shard may hold
+    // the rest), never below 256 members
+    const uint64_t per_member =
+        2 * stride + (fast ? DEFLATE_PREV_BYTES + DEFLATE_TOK_BYTES + DEFLATE_REC_BYTES
+                           : level > 0 ? ZDEFLATE_PREV_ENTRIES * 2 + ZDEFLATE_INFO_ENTRIES * 8 +
+                                             ZDEFLATE_TOK_ENTRIES * 4 + ZDEFLATE_REC_BYTES
+                                       : 0) + 16;
+    size_t hbm_free = 0, hbm_total = 0;
+    if (hipMemGetInfo(&hbm_free, &hbm_total) == hipSuccess && hbm_free / 2 / per_member < bmax)
+      bmax = std::max<uint64_t>(256, hbm_free / 2 / per_member);
+    const uint64_t cap = nb < bmax ? nb : bmax;
     HIPCHK(ctx, B.slots.ensure(cap * stride));
     HIPCHK(ctx, B.packed.ensure(cap * stride));
     if (fast) {

@@ -4,8 +4,8 @@ import weakref
 
 import numpy as np
 
-from ._lib import (SBH_OK, SbhBlock, SbhRecordsOut, SbhRecordsSizes, SbhShardResult, SbhStreamOpts,
-                   SbhStreamResult, SparkBamError, lib)
+from ._lib import (SBH_OK, SbhBlock, SbhCheckOpts, SbhCheckResult, SbhRecordsOut, SbhRecordsSizes,
+                   SbhShardResult, SbhStreamOpts, SbhStreamResult, SparkBamError, lib)
 
 
 def _check(ctx_handle, rc):
@@ -145,6 +145,62 @@ class Context:
             bits = bits[:(out["flat_bytes"] + 7) // 8]
         return out, bits
 
+    def find_blocks(self, data, splits, bgzf_blocks_to_check=5, window=1 << 30):
+        """Blocks.apply's unindexed branch (Blocks.scala:141-206) on the device (sbh_find_blocks):
+        data = the whole file (numpy uint8, e.g. a memmap); splits = [(start, end), ...].  Returns
+        [(split index, start, compressed size, uncompressed size), ...] in split order."""
+        arr = data if isinstance(data, np.ndarray) else np.frombuffer(data, dtype=np.uint8)
+        st = np.ascontiguousarray([a for a, _ in splits], dtype=np.uint64)
+        en = np.ascontiguousarray([b for _, b in splits], dtype=np.uint64)
+        cap = max(16, int(arr.size) // 4096 + 16)  # (a BGZF block is >= 28 bytes; grown below if short)
+        while True:
+            out = (SbhBlock * cap)()
+            n = C.c_uint64()
+            _check(self.h, lib().sbh_find_blocks(self.h, _ptr(arr), int(arr.size), _ptr(st), _ptr(en), st.size,
+                                                 int(bgzf_blocks_to_check), int(window), out, cap, C.byref(n)))
+            if n.value <= cap:
+                return [(int(b.ustart), int(b.start), int(b.csize), int(b.usize)) for b in out[:n.value]]
+            cap = n.value
+
+    def check_stream(self, data, contig_len, blocks, truth_vpos=None, full=False, window=1 << 30, halo=4 << 20,
+                     reads_to_check=10, fp_cap=1 << 20, close_cap=1 << 22):
+        """check-bam -s / full-check over the listed blocks of a file of any size, streamed through
+        HBM in windows (sbh_check_stream): data = the whole file (numpy uint8, e.g. a memmap),
+        blocks = file offsets of the block starts to check (ascending), truth_vpos = the `.records`
+        positions as htsjdk vpos (ascending) or None.  Returns a dict of the result fields plus
+        fp_vpos / fn_vpos and, with full, counts (21 x 19), rbe (21 x 64), close_vpos / close_word."""
+        arr = data if isinstance(data, np.ndarray) else np.frombuffer(data, dtype=np.uint8)
+        cl = np.ascontiguousarray(np.asarray(contig_len, dtype=np.int32))
+        bl = np.ascontiguousarray(blocks, dtype=np.uint64)
+        o = SbhCheckOpts()
+        o.window, o.halo, o.reads_to_check, o.full = int(window), int(halo), int(reads_to_check), 1 if full else 0
+        o.blocks, o.n_blocks = _ptr(bl).value, bl.size
+        keep = [bl]
+        fp = fn = None
+        if truth_vpos is not None:
+            tv = np.ascontiguousarray(truth_vpos, dtype=np.uint64)
+            fp, fn = np.zeros(max(fp_cap, 1), np.uint64), np.zeros(max(fp_cap, 1), np.uint64)
+            keep += [tv, fp, fn]
+            o.truth_vpos, o.n_truth = _ptr(tv).value, tv.size
+            o.fp_vpos, o.fn_vpos, o.fp_cap, o.fn_cap = _ptr(fp).value, _ptr(fn).value, fp_cap, fp_cap
+        counts = rbe = cv = cw = None
+        if full:
+            counts, rbe = np.zeros(21 * 19, np.uint64), np.zeros(21 * 64, np.uint64)
+            cv, cw = np.zeros(max(close_cap, 1), np.uint64), np.zeros(max(close_cap, 1), np.uint32)
+            keep += [counts, rbe, cv, cw]
+            o.counts, o.rbe_hist = _ptr(counts).value, _ptr(rbe).value
+            o.close_vpos, o.close_word, o.close_cap = _ptr(cv).value, _ptr(cw).value, close_cap
+        r = SbhCheckResult()
+        _check(self.h, lib().sbh_check_stream(self.h, _ptr(arr), int(arr.size), _ptr(cl), int(cl.size), C.byref(o),
+                                              C.byref(r)))
+        out = {f: getattr(r, f) for f, _ in SbhCheckResult._fields_}
+        if fp is not None:
+            out["fp_vpos"], out["fn_vpos"] = fp[:min(r.fp, fp_cap)], fn[:min(r.fn, fp_cap)]
+        if full:
+            k = min(r.n_close, close_cap)
+            out.update(counts=counts.reshape(21, 19), rbe=rbe.reshape(21, 64), close_vpos=cv[:k], close_word=cw[:k])
+        return out
+
     def shard(self, comp, file_offset=0, file_size=None, on_device=False, nbytes=None):
         return Shard(self, comp, file_offset, file_size, on_device, nbytes)
 
@@ -189,6 +245,14 @@ class Shard:
             self.close()
         except Exception:
             pass
+
+    def load(self, comp, file_offset):
+        """Replace the resident bytes with file bytes [file_offset, file_offset + comp.size)
+        of the same file, keeping the device buffers (sbh_shard_load)."""
+        arr = np.ascontiguousarray(comp, dtype=np.uint8)
+        self._c(lib().sbh_shard_load(self.h, _ptr(arr), int(arr.size), int(file_offset), 0))
+        self.n, self.file_offset = int(arr.size), int(file_offset)
+        self.n_blocks = self.flat_size = 0
 
     # -- bgzf --------------------------------------------------------------
     def find_block_start(self, start, bgzf_blocks_to_check=5):

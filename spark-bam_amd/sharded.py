@@ -28,7 +28,7 @@ from collections import namedtuple
 
 import numpy as np
 
-from ._lib import SBH_E_NEED_HALO, SBH_E_NO_READ_FOUND, SparkBamError
+from ._lib import SBH_E_NEED_HALO, SparkBamError
 from .api import (DEFAULT_BGZF_BLOCKS_TO_CHECK, DEFAULT_MAX_READ_SIZE, DEFAULT_READS_TO_CHECK,
                   Pos, Split, file_splits, parse_bam_header)
 from .device import Context
@@ -117,6 +117,7 @@ class RankRun:
             return
         lo, hi = splits[0][0], splits[-1][1]
         self.lo, self.hi = lo, hi
+        self.halo = halo
         self.streamed = (hi - lo > RESIDENT_MAX) if stream is None else bool(stream)
         if self.streamed:
             self._run_streamed(split_index, splits, halo, window or STREAM_WINDOW, bgzf_blocks_to_check)
@@ -134,6 +135,7 @@ class RankRun:
                 self.part = self._part(split_index, splits, status, v, n, r["first_vpos"] if r["count"] else None,
                                        r["count"], sh.exit_vpos(r))
                 self.sh = sh
+                self.halo = halo
                 return
             except SparkBamError as err:
                 sh.close()
@@ -145,9 +147,11 @@ class RankRun:
                 raise
 
     def _part(self, split_index, splits, status, v, n, first, count, exit_vpos):
-        for k in np.flatnonzero((status != 0) & (status != SBH_E_NO_READ_FOUND)):
+        # one policy on every path (resident, streamed, CLI): a split's error is the job's error,
+        # NoReadFoundException included, as FindRecordStart throws it (FindRecordStart.scala:66-71)
+        for k in np.flatnonzero(status != 0):
             raise SparkBamError(int(status[k]), f"split {splits[k][0]}-{splits[k][1]}")
-        counts = [int(c) if st == 0 else 0 for st, c in zip(status, n)]
+        counts = [int(c) for c in n]
         firsts = [int(x) if c else None for x, c in zip(v, counts)]
         return RankPart(self.rank, split_index, firsts, counts, first, count, exit_vpos)
 
@@ -171,6 +175,11 @@ class RankRun:
             self.part = self._part(split_index, splits, r["split_status"], r["split_first_vpos"], r["split_count"],
                                    r["first_vpos"] if r["count"] else None, r["count"], r["exit_vpos"])
             return
+
+    def rewalk_reload(self, from_vpos):
+        """rewalk() from the file bytes again (the shard need not be kept): what a Spark task that
+        re-walks a finished task's range does (jni/Native.scala GpuLoadBam.rewalk)."""
+        return self._rewalk_streamed(from_vpos)
 
     def rewalk(self, from_vpos):
         """The chain from the upstream rank's exit (SURVEY 8e stitch fix-up): (records from
@@ -198,14 +207,16 @@ class RankRun:
                 end = min(self.file_size, whi + halo)
                 sh = self.ctx.shard(self.read(blo, end), file_offset=blo, file_size=self.file_size)
                 try:
+                    sh.set_contigs(self.contig_len)
                     sh.index(blo)
                     sh.inflate()
-                    sh.set_contigs(self.contig_len)
                     f = sh.flat_of(blo, v & 0xFFFF)
                     E = sh.flat_bound(whi)
                     sh.check_eager(f, E, self.rtc, want_bits=False)
                     n, x = sh.chain_from(f, E)
                     ex = sh.exit_vpos({"count": n, "exit_flat": x}) if n else v
+                    # (no record started in this window: the walk goes on from its next block)
+                    nxt = next((b[0] for b in sh.blocks() if b[0] >= whi), None)
                     break
                 except SparkBamError as err:
                     if err.code != SBH_E_NEED_HALO or end >= self.file_size:
@@ -216,8 +227,10 @@ class RankRun:
             total += n
             if ex is None or whi >= self.hi:
                 return total, ex
-            if ex == v:  # no record started in this window: continue after it
-                ex = whi << 16
+            if ex == v:  # no record started in this window: continue at the first block after it
+                if nxt is None:
+                    raise SparkBamError(SBH_E_NEED_HALO, f"re-walk: no block past {whi} in the halo")
+                ex = nxt << 16
             v = ex
 
     def close(self):
@@ -336,6 +349,50 @@ def reconcile(parts, file_size, rank, rewalk, group=None, max_rounds=None):
     return stitch(parts, file_size, rewalks)
 
 
+def reconcile_local(parts, file_size, rewalk_of, max_rounds=None):
+    """reconcile() with every rank's part in one process (a Spark driver after collect): the
+    re-walk of rank r is rewalk_of[r](vpos) -> (count, exit_vpos)."""
+    rewalks = {}
+    for _ in range(max_rounds or len(parts)):
+        _, _, st = stitch(parts, file_size, rewalks)
+        if st["chain_ok"]:
+            break
+        new = {}
+        for m in st["chain_mismatches"]:
+            if m["exit"] is not None and m["next_rank"] not in new:
+                n, ex = rewalk_of[m["next_rank"]](m["exit"])
+                new[m["next_rank"]] = (m["exit"], n, ex)
+        if not new:
+            break
+        rewalks.update(new)
+    return stitch(parts, file_size, rewalks)
+
+
+def load_splits_and_reads_tasks(path_or_bytes, split_size, tasks, ctx=None, halo=DEFAULT_HALO, **kw):
+    """loadSplitsAndReads the way jni/Native.scala's GpuLoadBam runs it on Spark, call for call:
+    the Hadoop splits dealt to `tasks` tasks as contiguous runs (rank_splits), each task a RankRun
+    on its own bytes (sbh_shard_create over [lo, hi + halo), sbh_find_block_start, sbh_run_shard,
+    sbh_split_starts, the exit's sbh_pos_of) whose shard is closed when the task ends; the
+    driver's collect, the sliding2 stitch (CanLoadBam.scala:283-297), and a chain re-walk from the
+    upstream exit, re-reading the task's bytes, wherever the chain does not enter a task at its
+    first record.  Returns (splits, counts, stitch report)."""
+    read = file_reader(path_or_bytes) if isinstance(path_or_bytes, (str, os.PathLike)) else bytes_reader(path_or_bytes)
+    own_ctx = ctx is None
+    ctx = ctx or Context(int(os.environ.get("LOCAL_RANK", "0")))
+    try:
+        _, contig_len, _ = read_header(ctx, read, read.size)
+        runs = []
+        for t in range(tasks):
+            a, mine = rank_splits(read.size, split_size, tasks, t)
+            run = RankRun(ctx, read, read.size, a, mine, contig_len, t, halo, stream=False, **kw)
+            run.close()  # (the task ends; a re-walk reads its bytes again)
+            runs.append(run)
+        return reconcile_local([r.part for r in runs], read.size, {r.rank: r.rewalk_reload for r in runs})
+    finally:
+        if own_ctx:
+            ctx.close()
+
+
 def load_splits_and_reads(path_or_bytes, split_size=None, ctx=None, rank=None, world=None,
                           group=None, halo=DEFAULT_HALO, **kw):
     """CanLoadBam.loadSplitsAndReads (load/.../CanLoadBam.scala:268-302) over the ranks of
@@ -363,7 +420,11 @@ def load_splits_and_reads(path_or_bytes, split_size=None, ctx=None, rank=None, w
             run = RankRun(ctx, read, file_size, a, mine, contig_len, rank, halo, **kw)
             part = run.part
         except Exception as err:  # exchanged: the peers must not block in the allgather
+            if world == 1:
+                raise
             part = err
+        if world == 1:  # one rank owns every split: nothing to exchange, whatever process group exists
+            return stitch([part], file_size)
         parts = exchange(part, group)
         return reconcile(parts, file_size, rank, run.rewalk, group)
     finally:

@@ -73,6 +73,54 @@ def test_full_check_outputs(golden, args):
     assert out.splitlines() == want.splitlines()
 
 
+@pytest.fixture(scope="module")
+def noblocks(tmp_path_factory):
+    """1.noblocks.bam: 1.bam's bytes with no `.blocks` / `.records` beside them (in the reference it
+    is a link to 1.bam, test_bams/src/main/resources)."""
+    import shutil
+    d = tmp_path_factory.mktemp("noblocks")
+    p = d / "1.noblocks.bam"
+    shutil.copyfile(os.path.join(BAMS, "1.bam"), p)
+    return str(p)
+
+
+def test_full_check_noblocks(noblocks):
+    # FullCheckTest "1.bam without indexed records": Blocks.apply without `.blocks` (FindBlockStart
+    # per 200k split on the device, Blocks.scala:141-206) and no records summary
+    out = run("full-check", "-l", "10", "-m", "200k", noblocks)
+    with open(os.path.join(GOLDEN, "output", "full-check", "1.noblocks.bam"), encoding="utf-8") as f:
+        assert out.splitlines() == f.read().splitlines()
+
+
+def test_check_bam_noblocks(noblocks):
+    # CheckBamTest's eager summary on the unindexed file (truth records given with -r)
+    out = run("check-bam", "-s", "-m", "200k", "-r", os.path.join(BAMS, "1.bam.records"), noblocks)
+    assert out == ("1608257 uncompressed positions\n583K compressed\nCompression ratio: 2.69\n"
+                   "4917 reads\nAll calls matched!\n")
+
+
+@pytest.mark.parametrize("window", ["100000", "30000"])
+def test_all_positions_streamed_windows(window, noblocks):
+    """check-bam -s and every full-check golden with the file moved through HBM in windows of
+    `window` compressed bytes (sbh_check_stream; SBH_STREAM_WINDOW): byte-identical outputs."""
+    env = dict(os.environ, SBH_STREAM_WINDOW=window)
+
+    def run_env(*args):
+        r = subprocess.run([CLI, *args], capture_output=True, text=True, timeout=300, env=env)
+        assert r.returncode == 0, r.stderr
+        return r.stdout
+    assert run_env("check-bam", "-s", "-m", "200k", os.path.join(BAMS, "1.bam")).endswith("All calls matched!\n")
+    cases = [("2.bam", ["2.bam"]), ("2.bam.first", ["-i", "0", "2.bam"]), ("2.bam.second", ["-i", "26169", "2.bam"]),
+             ("2.bam.200k", ["-i", "0-200k", "-m", "100k", "2.bam"]), ("1.bam", ["-m", "200k", "1.bam"])]
+    for golden, args in cases:
+        out = run_env("full-check", "-l", "10", *args[:-1], os.path.join(BAMS, args[-1]))
+        with open(os.path.join(GOLDEN, "output", "full-check", golden), encoding="utf-8") as f:
+            assert out.splitlines() == f.read().splitlines(), golden
+    out = run_env("full-check", "-l", "10", "-m", "200k", noblocks)
+    with open(os.path.join(GOLDEN, "output", "full-check", "1.noblocks.bam"), encoding="utf-8") as f:
+        assert out.splitlines() == f.read().splitlines()
+
+
 def test_count_reads_1bam():
     out = run("count-reads", "-m", "100k", os.path.join(BAMS, "1.bam"))
     assert "spark-bam found 4917 reads" in out

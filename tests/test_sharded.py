@@ -443,3 +443,55 @@ def test_gpu_stitch_rewalk_streamed(tmp_path):
     for r in res:
         assert not r["ok"] and r["chain_ok"] and r["chain_count"] == 20000
         assert r["rewalk"]["1"]["count"] == r["rank_counts"][1] + 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tasks", [1, 2, 3, 5])
+def test_gpu_tasks_mirror_of_scala_facade(tasks):
+    """jni/Native.scala GpuLoadBam's call sequence (sharded.load_splits_and_reads_tasks): the
+    Hadoop splits dealt to Spark tasks, each task's shard closed when it ends, the driver's
+    stitch: ComputeSplitsTest's 230k splits and LoadBAMTest's counts of 1.bam for every task
+    count."""
+    splits, counts, st = sharded.load_splits_and_reads_tasks(golden_bam("1.bam"), 230 * 1024, tasks)
+    assert [(str(a), str(b)) for a, b in splits] == [("0:45846", "239479:312"), ("239479:312", "484396:25"),
+                                                    ("484396:25", "597482:0")]
+    assert sum(counts) == 4917 and st["ok"] and st["chain_ok"]
+
+
+@pytest.mark.gpu
+def test_gpu_tasks_rewalk_reads_bytes_again(tmp_path):
+    """A task whose first record is a false positive (injected) is re-walked by the driver from
+    the upstream task's exit, re-reading that task's bytes (the task's shard is gone)."""
+    path, data = _synth_file(tmp_path, 0x5B4D0030, 0, 20000, "wgs_tasks.bam")
+    of = OracleFile(data)
+    ss = data.size // 7
+    ref_splits, ref_counts = oracle_splits(of, ss)
+    orig = sharded.RankRun._part
+
+    def fp_part(self, split_index, splits, status, v, n, first, count, exit_vpos):
+        if self.rank == 2:  # rank 2 reports its first record one byte later and one record fewer
+            first, count = first + 1, count - 1
+        return orig(self, split_index, splits, status, v, n, first, count, exit_vpos)
+
+    sharded.RankRun._part = fp_part
+    try:
+        splits, counts, st = sharded.load_splits_and_reads_tasks(path, ss, 4)
+    finally:
+        sharded.RankRun._part = orig
+    assert counts == ref_counts and [(a.to_htsjdk(), b.to_htsjdk()) for a, b in splits] == ref_splits
+    assert not st["ok"] and st["chain_ok"] and st["chain_count"] == 20000 and 2 in st["rewalk"]
+
+
+@pytest.mark.gpu
+def test_gpu_streamed_rank_with_one_split(tmp_path, monkeypatch):
+    """one split per rank (split_size = the whole file) streamed through 150 KB windows:
+    the split runs through every window (its chain followed window by window), HBM stays bounded,
+    and the answer equals the oracle."""
+    path, data = _synth_file(tmp_path, 0x5B4D0030, 0, 20000, "wgs_one.bam")
+    of = OracleFile(data)
+    monkeypatch.setattr(sharded, "RESIDENT_MAX", 1)
+    monkeypatch.setattr(sharded, "STREAM_WINDOW", 150_000)
+    splits, counts, st = sharded.load_splits_and_reads(path, None, world=1, rank=0)
+    ref_splits, ref_counts = oracle_splits(of, data.size)
+    assert counts == ref_counts == [20000]
+    assert [(a.to_htsjdk(), b.to_htsjdk()) for a, b in splits] == ref_splits

@@ -107,13 +107,16 @@ def test_stream_subrange_of_a_file(ctx, files):
 
 
 @pytest.mark.parametrize("name", list(CORPORA))
-@pytest.mark.parametrize("window,split", [(150_000, 40_000), (400_000, 97_000), (150_000, 400_000)])
+@pytest.mark.parametrize("window,split", [(150_000, 40_000), (400_000, 97_000), (150_000, 400_000),
+                                          (150_000, 1 << 40)])
 def test_stream_splits_equal_resident_and_oracle(ctx, files, name, window, split):
     """loadSplitsAndReads' per-split answer through bounded HBM (sbh_run_stream2): windows cut
     at split starts, each split decided by the batched split path in its window -- equal to
     the resident batch (sbh_split_starts on the whole file) and to the oracle
-    (CanLoadBam.scala:283-297,316-356).  A split larger than the window makes its window
-    larger than asked.  The in-run CRC32 check finds no bad block."""
+    (CanLoadBam.scala:283-297,316-356).  A split larger than a window runs through several (its
+    chain followed window by window; the last case is ONE split for the whole file, a rank with a
+    single split), so HBM stays bounded.
+    The in-run CRC32 check finds no bad block."""
     from oracle_lib import OR_OK, file_splits
     data, nrec = files[name]
     of = OracleFile(data)
@@ -121,6 +124,7 @@ def test_stream_splits_equal_resident_and_oracle(ctx, files, name, window, split
     s, _ = ctx.run_stream(data, of.contig_len, index_start=0, window=window, halo=1 << 16, splits=splits,
                           verify_crc=True)
     assert s["status"] == 0 and s["crc_bad_blocks"] == 0 and s["count"] == nrec
+    assert s["n_windows"] >= data.size // window - 1
     sh = ctx.shard(data)
     try:
         sh.index(0)
@@ -151,3 +155,36 @@ def test_stream_crc_detects_a_bad_footer(ctx, files):
     bad[start + csize - 8] ^= 0xFF
     s, _ = ctx.run_stream(bad, of.contig_len, index_start=0, window=150_000, halo=1 << 16, verify_crc=True)
     assert s["crc_bad_blocks"] == 1 and s["crc_first_bad"] == start
+
+
+@pytest.mark.parametrize("name", ["short_l6", "long", "adversarial"])
+def test_all_positions_streamed_equal_one_window_and_oracle(ctx, files, name):
+    """check-bam -s / full-check through bounded HBM (sbh_check_stream, 150 KB windows) equal the
+    same pass in one window and the oracle at every position (CallPartition.scala:35-52,
+    FullCheck.scala:65-86,142-192); truth = the oracle's record chain with two records dropped
+    and one false record added, so the FP / FN lists are exercised."""
+    data, _ = files[name]
+    of = OracleFile(data)
+    chain = [int(f) for f in of.record_chain(of.header_end)]
+    truth_flat = sorted(set(chain[:50] + chain[51:-7] + chain[-6:] + [chain[100] + 1]))
+    truth = [of.pos_of(f) for f in truth_flat]
+    one = sb.check_bam(data, records=truth, ctx=ctx, window=1 << 40)
+    many = sb.check_bam(data, records=truth, ctx=ctx, window=150_000)
+    assert one["n_windows"] == 1 and many["n_windows"] >= 3
+    for k in ("positions", "compressed", "reads", "true_positives", "false_positives", "false_negatives",
+              "fp_positions", "fn_positions"):
+        assert many[k] == one[k], k
+    _, bits = of.eager_range(0, of.flat_size)
+    calls = set(np.flatnonzero(np.unpackbits(bits, bitorder="little")[:of.flat_size]).tolist())
+    tset = set(truth_flat)
+    assert many["positions"] == of.flat_size
+    assert many["true_positives"] == len(calls & tset)
+    assert [of.flat_of(p.block_pos, p.offset) for p in many["fp_positions"]] == sorted(calls - tset)
+    assert [of.flat_of(p.block_pos, p.offset) for p in many["fn_positions"]] == sorted(tset - calls)
+    f1 = sb.full_check(data, ctx=ctx, window=1 << 40)
+    fm = sb.full_check(data, ctx=ctx, window=150_000)
+    ns, counts, rbe, _ = of.full_range(0, of.flat_size)
+    assert fm["n_success"] == f1["n_success"] == ns
+    assert np.array_equal(fm["counts_by_nnz"], f1["counts_by_nnz"]) and np.array_equal(fm["counts_by_nnz"], counts)
+    assert np.array_equal(fm["rbe_by_nnz"], rbe)
+    assert fm["close"] == f1["close"] and len(fm["close"]) > 0
