@@ -10,7 +10,7 @@ from collections import namedtuple
 
 import numpy as np
 
-from ._lib import FULL_FLAGS_MASK, FULL_N_SHIFT, SBH_OK, SparkBamError, lib
+from ._lib import FULL_FLAGS_MASK, FULL_N_SHIFT, SBH_E_NEED_HALO, SBH_OK, SparkBamError, lib
 from .device import Context
 from .records import Reads
 
@@ -164,13 +164,28 @@ def load_splits_and_reads(path_or_bytes, split_size=DEFAULT_SPLIT_SIZE, ctx=None
         L.close()
 
 
-def load_reads(path_or_bytes, ctx=None, reads_to_check=DEFAULT_READS_TO_CHECK):
+def load_reads(path_or_bytes, ctx=None, reads_to_check=DEFAULT_READS_TO_CHECK, window=None):
     """CanLoadBam.loadReads (load/.../CanLoadBam.scala:244-264) on one device: every
     record of the file's BAM stream, in file order, decoded on the GPU into a columnar
     `Reads` batch (RecordStream.scala:16-41 semantics: records from the first one after
     the header while they start before the stream's end).  The eager bitmap of the
     record range is computed first, so record starts come from it in parallel (verified
-    against the chain) rather than from a sequential chain walk."""
+    against the chain) rather than from a sequential chain walk.  A file larger than
+    sharded.RESIDENT_MAX (or with `window` given) is decoded a window at a time (iter_reads)
+    and the batches joined."""
+    from . import sharded
+    size = os.path.getsize(path_or_bytes) if isinstance(path_or_bytes, (str, os.PathLike)) else len(path_or_bytes)
+    if window is not None or size > sharded.RESIDENT_MAX:
+        own_ctx = ctx is None
+        ctx = ctx or Context(0)
+        try:
+            batches = list(iter_reads(path_or_bytes, window=window or sharded.STREAM_WINDOW, ctx=ctx,
+                                      reads_to_check=reads_to_check))
+            names = file_header(ctx, _file_array(path_or_bytes))[0]
+        finally:
+            if own_ctx:
+                ctx.close()
+        return Reads.concat(batches, names)
     L = _Loaded(path_or_bytes, ctx, reads_to_check)
     try:
         sh = L.shard
@@ -180,9 +195,79 @@ def load_reads(path_or_bytes, ctx=None, reads_to_check=DEFAULT_READS_TO_CHECK):
                 end = b[3]
                 break
         sh.check_eager(L.header_end, end, reads_to_check, want_bits=False)
-        return Reads(sh.records(L.header_end, end), L.names)
+        cols = sh.records(L.header_end, end)
+        cols["vpos"] = _vpos_of(cols["flat"], sh.blocks())
+        return Reads(cols, L.names)
     finally:
         L.close()
+
+
+def _vpos_of(flat, blocks):
+    """htsjdk vpos of flat positions (numpy) from a shard's block table (Pos.scala's canonical
+    form: a record at a block's end is Pos(next block, 0); empty blocks never hold one)."""
+    blk = np.asarray([(b[0], b[3], b[2]) for b in blocks if b[2] > 0], dtype=np.int64).reshape(-1, 3)
+    if flat.size == 0 or blk.size == 0:
+        return np.zeros(flat.size, dtype=np.uint64)
+    f = flat.astype(np.int64)
+    i = np.searchsorted(blk[:, 1], f, side="right") - 1
+    return (blk[i, 0].astype(np.uint64) << np.uint64(16)) | (f - blk[i, 1]).astype(np.uint64)
+
+
+def iter_reads(path_or_bytes, window=None, halo=4 << 20, ctx=None, reads_to_check=DEFAULT_READS_TO_CHECK):
+    """CanLoadBam.loadReads (load/.../CanLoadBam.scala:244-264) over a file of any size: the
+    records from the first one after the header while they start before the stream's end
+    (RecordStream.scala:16-41), decoded on the GPU a window of `window` compressed bytes at a
+    time; yields one columnar `Reads` batch per window, in file order, each with a `vpos` column
+    (htsjdk virtual offsets; `flat` is window-relative).  A window starts at the block of the
+    previous window's chain exit, so batches never overlap."""
+    window = int(window or STREAM_WINDOW)
+    data = _file_array(path_or_bytes)
+    size = int(data.size)
+    own_ctx = ctx is None
+    ctx = ctx or Context(0)
+    try:
+        names, contig_len, header_end = file_header(ctx, data)
+        lo, start = 0, None  # window start (a block) and the record to start from (vpos; None: after the header)
+        while lo < size:
+            hi = lo + window
+            while True:
+                end = min(size, hi + halo)
+                sh = ctx.shard(np.ascontiguousarray(data[lo:end]), file_offset=lo, file_size=size)
+                try:
+                    sh.set_contigs(contig_len)
+                    sh.index(lo)
+                    sh.inflate()
+                    blocks = sh.blocks()
+                    E = sh.flat_bound(hi)
+                    if end < size and E == sh.flat_size:
+                        raise SparkBamError(SBH_E_NEED_HALO, "no block past the window in the halo")
+                    f = header_end if start is None else sh.flat_of(start >> 16, start & 0xFFFF)
+                    seg = next((b[3] for b in blocks if b[5] & 1 and b[3] >= f), None)  # an empty block ends the stream
+                    last = seg is not None and seg <= E or end == size and E == sh.flat_size
+                    if seg is not None:
+                        E = min(E, seg)
+                    sh.check_eager(f, E, reads_to_check, want_bits=False)
+                    cols = sh.records(f, E) if E > f else None
+                    n, x = sh.chain_from(f, E) if E > f else (0, f)
+                    if not last and x >= sh.flat_size:
+                        raise SparkBamError(SBH_E_NEED_HALO, "the chain leaves the halo")
+                    nxt = None if last else int(Pos(*sh.pos_of(x)).to_htsjdk())
+                    break
+                except SparkBamError as err:
+                    if err.code != SBH_E_NEED_HALO or end >= size:
+                        raise
+                    halo *= 4
+                finally:
+                    sh.close()
+            if cols is not None and cols["flat"].size:
+                cols["vpos"] = _vpos_of(cols["flat"], blocks)  # (flat: window-relative)
+                yield Reads(cols, names)
+            if last:
+                return
+            start, lo = nxt, nxt >> 16
+    finally:
+        if own_ctx:
+            ctx.close()
 
 
 def load_bam_count(path_or_bytes, split_size=DEFAULT_SPLIT_SIZE, ctx=None, **kw):

@@ -78,6 +78,29 @@ class Reads:
     def __len__(self):
         return self.n
 
+    OFFSETS = {"name_off": "names", "cigar_off": "cigar", "seq_off": "seq", "aux_off": "aux"}
+
+    @classmethod
+    def concat(cls, batches, ref_names):
+        """One batch of the records of several, in order (windowed loadReads, api.iter_reads)."""
+        batches = [b for b in batches if b.n]
+        if not batches:
+            return cls({k: np.empty(1 if k in cls.OFFSETS else 0, np.uint64) for k in
+                        ("flat", "vpos", *cls.OFFSETS)}, ref_names)
+        cols = {}
+        for k in batches[0].cols:
+            if k in cls.OFFSETS:
+                parts, base = [], 0
+                for b in batches:
+                    o = b.cols[k]
+                    parts.append(o[:-1] + base)
+                    base += int(o[-1])
+                parts.append(np.asarray([base], dtype=batches[0].cols[k].dtype))
+                cols[k] = np.concatenate(parts)
+            else:
+                cols[k] = np.concatenate([b.cols[k] for b in batches])
+        return cls(cols, ref_names)
+
     def _slice(self, name, off, i):
         o = self.cols[off]
         return self.cols[name][int(o[i]):int(o[i + 1])]

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""A/B the inflate-kernel variants (spark-bam_amd/build/variants/lib_*.so) on one
+"""A/B the inflate-kernel variants (spark-bam_amd/build/ab/lib_*.so) on one
 synthetic shard: per-variant k_inflate time (HIP events) and output identity vs the
 in-tree library.  Each variant runs in its own process (the library path is bound at
 import).  Usage: python tools/ab_inflate.py [--records N] [--config B|D|E] [variant ...]"""
@@ -68,7 +68,7 @@ def main():
     a = ap.parse_args()
     if a.child is not None:
         return child(a.child, a.records, a.reps, a.config)
-    vdir = os.path.join(ROOT, "spark-bam_amd/build/variants")
+    vdir = os.path.join(ROOT, "spark-bam_amd/build/ab")
     named = [v if v.endswith(".so") else os.path.join(vdir, f"lib_{v}.so") for v in a.variants]
     libs = [""] + (named or sorted(glob.glob(os.path.join(vdir, "lib_*.so"))))
     for lib in libs:

@@ -3,7 +3,7 @@
 # status -- no box taken, nothing of the command ran.  Any other outcome is returned as is.
 # usage: tools/gpurun_retry.sh OUTFILE TIMEOUT 'command'
 OUT=$1; TMO=$2; CMD=$3
-for i in 1 2 3 4 5 6 7 8; do
+for i in $(seq 1 ${GPURUN_TRIES:-20}); do
   /usr/local/graft/bin/gpurun --timeout "$TMO" -- "$CMD" > "$OUT" 2>&1
   rc=$?
   if grep -q '"status": "transient"' gpurun_out/.last_call.json 2>/dev/null; then
