@@ -1301,54 +1301,13 @@ __global__ __launch_bounds__(T, 5) void k_full(const uint8_t *__restrict__ U, ui
     }
   };
 #endif
-#ifndef SBH_FULL_WCACHE
-#define SBH_FULL_WCACHE 0  // K: each lane counts its K most recent hot failure words in registers
-#endif
-#if SBH_FULL_WCACHE
-  // A few failure words make most of the Counts adds (short reads: one word is 43% of the
-  // failures, four are 65%), and lanes adding the same word's flags hit the same replica
-  // addresses.  Each lane keeps K (word, count) slots in registers; a word that misses evicts
-  // the slot with the smaller count, whose flags are added once with its count.
-  constexpr uint32_t WK = SBH_FULL_WCACHE;
-  uint32_t wc_w[WK], wc_n[WK];
-#pragma unroll
-  for (uint32_t k = 0; k < WK; ++k) wc_w[k] = 0, wc_n[k] = 0;
-  auto wc_flush = [&](uint32_t w, uint32_t n) {
-    uint32_t *row = myhist + __popc(w) * RW;
-    while (w) {
-      atomicAdd(&row[__builtin_ctz(w)], n);
-      w &= w - 1;
-    }
-  };
-#endif
   auto account_fail = [&](uint64_t p, uint32_t r) {
     if (o.words) o.words[p - begin] = r;
     const uint32_t nnz = __popc(r);  // (a fast tile's failure word has no high bits)
 #ifdef SBH_FULL_NOHIST
     if (nnz != 77) return;
 #endif
-#if SBH_FULL_WCACHE
-    {
-      bool hit = false;
-      uint32_t kmin = 0;
-#pragma unroll
-      for (uint32_t k = 0; k < WK; ++k) {
-        const bool h = wc_w[k] == r;
-        wc_n[k] += h ? 1u : 0u;
-        hit = hit || h;
-        kmin = wc_n[k] < wc_n[kmin] ? k : kmin;
-      }
-      if (!hit) {
-#pragma unroll
-        for (uint32_t k = 0; k < WK; ++k)
-          if (k == kmin) {
-            if (wc_n[k]) wc_flush(wc_w[k], wc_n[k]);
-            wc_w[k] = r;
-            wc_n[k] = 1;
-          }
-      }
-    }
-#elif SBH_FULL_RUN
+#if SBH_FULL_RUN
     if (r == run_f) {
       ++run_n;
     } else {
@@ -1421,11 +1380,7 @@ __global__ __launch_bounds__(T, 5) void k_full(const uint8_t *__restrict__ U, ui
         }
       }
     }
-#if SBH_FULL_WCACHE
-#pragma unroll
-    for (uint32_t k = 0; k < WK; ++k)
-      if (wc_n[k]) wc_flush(wc_w[k], wc_n[k]);
-#elif SBH_FULL_RUN
+#if SBH_FULL_RUN
     run_flush();
 #endif
     static_assert(FTILE / (FPL * T) * FPL <= 32, "overflow bits fit a word");

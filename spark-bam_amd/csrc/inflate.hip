@@ -2365,6 +2365,9 @@ __device__ __forceinline__ uint4 pack8_u16(const uint32_t *c) {
 #ifndef SBH_ASM_CHASE
 #define SBH_ASM_CHASE 1  // k_lz's pointer chase as the hand-written loop below
 #endif
+#ifndef SBH_LZ_OVL_WAVE
+#define SBH_LZ_OVL_WAVE 0  // 1: overlapping short matches (dist < len) marked byte by byte by the wave (A/B r04c: k_lz +5% B, +26% D, +10% E: kept off)
+#endif
 // k_lz's pointer chase for one half granule (8 slots) as hand-written code, the same rounds as
 // the C++ loop: every pointer at or past the pass start pb is replaced by its target's slot
 // value (u16 LDS reads at 2 * max(c, pb) + p16 - 2 * abase), the 8 slots written back as
@@ -2525,9 +2528,15 @@ __global__ __launch_bounds__(LZ_THREADS, 4) void k_lz(const uint8_t *__restrict_
       // Tokens mark their starts: one slot write (a literal points at itself, a short
       // match at its source) and one start bit each; the bytes inside a short match get
       // their pointers in the slot pass below, from the nearest start.
+      // a match the wave marks byte by byte: longer than LZ_SHORT, or overlapping itself
+      // (dist < len: its bytes repeat a period shorter than the match, a mod per byte)
+      bool wide[LZ_TPT];
+#pragma unroll
+      for (uint32_t k = 0; k < LZ_TPT; ++k)
+        wide[k] = match[k] && (len[k] > LZ_SHORT || (SBH_LZ_OVL_WAVE && dist[k] < len[k]));
 #pragma unroll
       for (uint32_t k = 0; k < LZ_TPT; ++k) {
-        if (i0 + k >= n || len[k] > LZ_SHORT || !(off[k] - pb < plen)) continue;
+        if (i0 + k >= n || wide[k] || !(off[k] - pb < plen)) continue;
         const uint32_t d = off[k] - abase;
         p16[d] = (uint16_t)(match[k] ? off[k] - dist[k] : off[k]);
         if (!match[k]) img[off[k]] = (uint8_t)(x[k] >> 8);
@@ -2535,7 +2544,7 @@ __global__ __launch_bounds__(LZ_THREADS, 4) void k_lz(const uint8_t *__restrict_
       }
 #pragma unroll
       for (uint32_t k = 0; k < LZ_TPT; ++k) {  // long matches: the wave writes every byte's pointer
-        uint64_t lm = __ballot(i0 + k < n && match[k] && len[k] > LZ_SHORT && off[k] - pb < plen);
+        uint64_t lm = __ballot(i0 + k < n && wide[k] && off[k] - pb < plen);
 #ifdef SBH_LZ_PROBE
         nlong += __builtin_popcountll(lm);
 #endif
@@ -2594,6 +2603,15 @@ __global__ __launch_bounds__(LZ_THREADS, 4) void k_lz(const uint8_t *__restrict_
         }
 #pragma unroll
         for (uint32_t k = 0; k < PTR_HALF; ++k) v[k] = p16[sidx[k]];
+#if SBH_LZ_OVL_WAVE
+        // (no byte of a short start-marked match reaches past its distance: overlapping matches
+        // had every byte marked with its final offset by the wave)
+#pragma unroll
+        for (uint32_t k = 0; k < PTR_HALF; ++k) {
+          const bool in = k - klo < khi - klo;
+          c[hh][k] = in ? v[k] + (s0 + k - sidx[k]) : g0 + k;
+        }
+#else
         uint32_t ovl = 0;  // slots of overlapping matches
 #pragma unroll
         for (uint32_t k = 0; k < PTR_HALF; ++k) {
@@ -2607,6 +2625,7 @@ __global__ __launch_bounds__(LZ_THREADS, 4) void k_lz(const uint8_t *__restrict_
           for (uint32_t k = 0; k < PTR_HALF; ++k)
             if ((ovl >> k) & 1u) c[hh][k] = v[k] + mod_small(s0 + k - sidx[k], abase + sidx[k] - v[k]);
         }
+#endif
 #pragma unroll
         for (uint32_t k = 0; k < PTR_HALF; ++k)  // in the pass, not a literal, not final yet
           pend[hh] |= (c[hh][k] != g0 + k && c[hh][k] >= pb) ? 1u << k : 0u;

@@ -9,6 +9,7 @@ from conftest import golden_bam
 from oracle_lib import OracleFile
 import oracle_records as orr
 from pkg import sb
+SBH_E_BAD_RECORD = sb._lib.SBH_E_BAD_RECORD
 from test_records_cpu import sam_golden
 
 pytestmark = pytest.mark.gpu
@@ -54,16 +55,29 @@ def test_load_reads_windowed(name, window):
 
 def test_load_reads_windowed_synthetic():
     """Long reads (records spanning blocks and windows, a 4 KiB halo grown on demand) and an
-    adversarial corpus with empty blocks (the stream ends at the first one), windowed vs resident."""
+    adversarial corpus, windowed vs resident; with an empty block mid-file (the stream ends at
+    its start, cutting the record that spans it) both paths raise the same malformed-record error."""
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tools"))
     import synth
-    for seed, shape, level, nrec, empty in ((0x5B4D004C, 1, 6, 150, 0), (0x5B4D00AE, 2, -1, 20000, 5)):
+    for seed, shape, level, nrec, empty in ((0x5B4D004C, 1, 6, 150, 0), (0x5B4D00AE, 2, -1, 20000, 0),
+                                            (0x5B4D00AE, 2, -1, 20000, 5)):
         data = synth.make_bam(synth.params(seed, shape=shape, level=level, empty_every=empty), nrec)[0]
+
+        def windowed():
+            with sb.Context(0) as ctx:
+                return sb.Reads.concat(list(sb.api.iter_reads(data, window=120_000, halo=4096, ctx=ctx)),
+                                       sb.api.file_header(ctx, data)[0])
+
+        if empty:
+            with pytest.raises(sb.SparkBamError) as e1:
+                sb.load_reads(data)
+            with pytest.raises(sb.SparkBamError) as e2:
+                windowed()
+            assert e1.value.code == e2.value.code == SBH_E_BAD_RECORD
+            continue
         one = sb.load_reads(data)
-        win = None
-        with sb.Context(0) as ctx:
-            win = sb.Reads.concat(list(sb.api.iter_reads(data, window=120_000, halo=4096, ctx=ctx)), one.ref_names)
+        win = windowed()
         assert win.n == one.n > 0
         for k in one.cols:
             if k != "flat":
