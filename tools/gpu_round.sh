@@ -10,6 +10,8 @@
 #   bash tools/gpu_round.sh fullab TAG RECORDS V...      full-checker A/B (tools/full_ab.py), same variants
 #   bash tools/gpu_round.sh pmc TAG ARGS...        counter passes (tools/pmc_collect.sh) over bench.py ARGS
 #   bash tools/gpu_round.sh trace TAG              kernel-trace timeline of 8 bench steps + idle gaps
+#   bash tools/gpu_round.sh allpos TAG GIB ARGS...  check-bam -s over configs[2]'s one GIB-GiB file
+#                                                  (tools/allpos_configC.py: a 2 GiB rehearsal first)
 set -o pipefail
 M=$1; T=$2; shift 2
 mkdir -p gpurun_out
@@ -63,6 +65,11 @@ trace)
     --no-cpu-baseline --no-full --no-e2e > gpurun_out/${T}_trbench.log 2>&1 || exit 9
   cp "$(find /tmp/${T}_tr -name '*.db' -print -quit)" gpurun_out/${T}_trace.db
   python3 tools/prof_gaps.py gpurun_out/${T}_trace.db --step-kernel k_lz --steps 6 --top 30 > gpurun_out/${T}_gaps.log 2>&1
+  ;;
+allpos)
+  G=$1; shift
+  timeout -k 10 300 python -u tools/allpos_configC.py --file-gib 2 "$@" > gpurun_out/${T}_allpos2.log 2>&1 || exit 10
+  timeout -k 10 1000 python -u tools/allpos_configC.py --file-gib $G "$@" > gpurun_out/${T}_allpos.log 2>&1 || exit 11
   ;;
 *)
   echo "unknown mode $M" >&2
