@@ -352,6 +352,7 @@ struct EagerOut {
   unsigned long long *xq_n;
   uint64_t xq_cap;                // 0: every exact check runs inline
   unsigned long long *true_spread;  // k_eager: per-wave true counts, folded into n_true by k_fold_true
+  TileSum *tsum;                  // per tile: the chain proof's summary (nullptr: none)
 };
 
 // k_eager's true count goes to TRUE_SLOTS counters TRUE_STRIDE u64 apart (one atomic per
@@ -506,6 +507,7 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
   __shared__ uint32_t lnk[EQ_CHUNK / 32], lfail[EQ_CHUNK / 32];  // per sorted candidate: LINK / FAIL step
   __shared__ uint32_t seg0, nq, wcnt[NWV];
   __shared__ uint64_t seg_end0;
+  __shared__ uint32_t ts_dirty;  // a result settled after this kernel (no chain summary)
   __shared__ uint16_t queue[EQ_CHUNK];
   const uint32_t *lds32 = reinterpret_cast<const uint32_t *>(ldsv);
   const uint64_t t0 = begin + (uint64_t)blockIdx.x * ETILE;
@@ -523,6 +525,7 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
     seg0 = k;
     seg_end0 = sg.end[k];
     nq = 0;
+    ts_dirty = 0;
   }
   __syncthreads();
   Src s{U, lds32, s0, ESTAGE};  // >= EW + 15 + 44: every phase-A read is staged
@@ -652,6 +655,7 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
     if (x < o.defer_cap) o.defer_pos[x] = t0 + i;
   };
   auto settle = [&](uint32_t i, uint32_t r) {  // a candidate's result (queue-driven paths)
+    if (r > 1) ts_dirty = 1;  // its bit is settled later (k_eager_xq / k_eager_defer) or unknown
     if (r == 1) {
       atomicOr(&res[i >> 5], 1u << (i & 31));
     } else if (r == EAGER_DEFER) {
@@ -849,6 +853,76 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
 #ifdef SBH_EPROBE
     c4 = __builtin_readcyclecounter();
 #endif
+    if (o.tsum) {
+      // each wave's quarter of the tile (EAGER_SUB positions, its lanes' result words): each true
+      // position's record step (its length field, staged) against the next true position of the
+      // quarter; the last one's step for k_verify_chain_w.  Wave-local: no barrier.
+      constexpr uint32_t TW = ETILE / 32 / T;  // result words per thread
+      static_assert(TW * T * 32 == ETILE && ETILE / NWV == EAGER_SUB, "whole result words per thread");
+      const uint32_t wt0 = threadIdx.x * TW;
+      uint32_t rw[TW];
+      bool any = false;
+#pragma unroll
+      for (uint32_t k = 0; k < TW; ++k) {
+        rw[k] = res[wt0 + k];
+        any = any || rw[k] != 0;
+      }
+      const uint64_t bal = __ballot(any);
+      uint32_t an = 0, af = ~0u;
+      uint64_t mystep = TS_NONE;
+      bool last = false;
+      if (any) {
+        uint32_t nx = ETILE;  // the first true position after this thread's words in the quarter
+        const uint64_t after = lane == WAVE - 1 ? 0ull : bal & (~0ull << (lane + 1));
+        if (after) {
+          const uint32_t tn = wid * WAVE + (uint32_t)__builtin_ctzll(after);
+#pragma unroll
+          for (uint32_t k = TW; k-- > 0;) {
+            const uint32_t x = res[tn * TW + k];
+            if (x) nx = 32 * (tn * TW + k) + __builtin_ctz(x);
+          }
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < TW; ++k) {
+          uint32_t x = rw[k];
+          while (x) {
+            const uint32_t i = 32 * (wt0 + k) + __builtin_ctz(x);
+            x &= x - 1;
+            uint32_t nxt = nx;
+            if (x) {
+              nxt = 32 * (wt0 + k) + __builtin_ctz(x);
+            } else {
+#pragma unroll
+              for (uint32_t k2 = k + 1; k2 < TW; ++k2)
+                if (rw[k2] && nxt == nx) nxt = 32 * (wt0 + k2) + __builtin_ctz(rw[k2]);
+            }
+            const uint64_t q = t0 + i;
+            const uint64_t total = q < e0 ? e0 : sg.end[seg_index(sg, q, k0)];
+            const uint64_t step = q + 4 > total ? TS_NONE : q + 4 + (int64_t)(int32_t)s.word_at(q);
+            if (nxt < ETILE) {
+              if (step != t0 + nxt) {
+                ++an;
+                af = min(af, i - wid * EAGER_SUB);
+              }
+            } else {
+              mystep = step;
+              last = true;
+            }
+          }
+        }
+      }
+      an = __builtin_amdgcn_readlane(wave_incl_scan(an), WAVE - 1);
+#pragma unroll
+      for (uint32_t o2 = 1; o2 < WAVE; o2 <<= 1) af = min(af, (uint32_t)__shfl_xor(af, o2, WAVE));
+      const uint64_t lb = __ballot(last);
+      uint64_t sl = TS_NONE;
+      if (lb) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(lb);
+        sl = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(mystep >> 32), l) << 32 |
+             (uint32_t)__builtin_amdgcn_readlane((uint32_t)mystep, l);
+      }
+      if (lane == 0) o.tsum[blockIdx.x * NWV + wid] = TileSum{ts_dirty ? TS_DIRTY : sl, an, af};
+    }
     write_res();
   } else {
     // ---- fallback (a survivor list overflowed, or rtc <= 0): per-thread survivor loop
@@ -916,6 +990,8 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
     if (lane == 0 && wt)
       atomicAdd(o.true_spread + ((blockIdx.x * NWV + wid) % TRUE_SLOTS) * TRUE_STRIDE, (unsigned long long)wt);
   }
+  if (o.tsum && !fast && lane == 0)  // (the fallback path leaves no summaries)
+    o.tsum[blockIdx.x * NWV + wid] = TileSum{TS_DIRTY, 0, ~0u};
 #ifdef SBH_EPROBE
   __shared__ uint32_t psurv, pcand, pexact, ntrue;
   if (threadIdx.x == 0) { psurv = 0; pcand = 0; pexact = 0; ntrue = 0; }
@@ -1534,8 +1610,10 @@ __global__ __launch_bounds__(256) void k_first_set(const uint32_t *bits, uint64_
 __global__ __launch_bounds__(256) void k_verify_chain_w(const uint8_t *U, const uint32_t *bits, uint64_t begin,
                                                          uint64_t bits_end, uint64_t from, uint64_t E, uint64_t total,
                                                          unsigned long long *n_anom, unsigned long long *first_anom,
-                                                         unsigned long long *exit_pos, unsigned long long *n_set) {
+                                                         unsigned long long *exit_pos, unsigned long long *n_set,
+                                                         const TileSum *tsum) {
   const uint32_t lane = threadIdx.x & (WAVE - 1);
+  constexpr uint32_t TWORDS = EAGER_SUB / 32;  // bitmap words per summarised quarter tile (from `begin`)
   const uint64_t W0 = (from - begin) / 32 & ~3ull;
   const uint64_t w_end = (E - begin + 31) / 32;
   const uint64_t w_lim = (bits_end - begin + 31) / 32;
@@ -1565,6 +1643,24 @@ __global__ __launch_bounds__(256) void k_verify_chain_w(const uint8_t *U, const 
     }
     const uint32_t cnt = __popc(v[0]) + __popc(v[1]) + __popc(v[2]) + __popc(v[3]);
     tot += cnt;
+    // a tile wholly inside [from, E) with a summary: its own pairs were checked by k_eager (their
+    // anomalies added once, by the lane of its first word); only its last true position's step
+    // is needed, from the summary, not from U
+    bool cov = false;
+    uint64_t tstep = TS_NONE, thi = 0;
+    if (tsum && w < w_end) {
+      const uint64_t tile = w / TWORDS, tlo = begin + tile * EAGER_SUB;
+      thi = tlo + EAGER_SUB;
+      if (tlo >= from && thi <= E) {
+        const TileSum ts = tsum[tile];
+        cov = ts.step_last != TS_DIRTY;
+        tstep = ts.step_last;
+        if (cov && w % TWORDS == 0 && ts.n_anom) {
+          atomicAdd(n_anom, (unsigned long long)ts.n_anom);
+          atomicMin(first_anom, (unsigned long long)(tlo + ts.first_anom));
+        }
+      }
+    }
     // the lane's first set position (successor of the previous non-empty lane's last bit)
     uint64_t f = ~0ull;
     for (int k = 3; k >= 0; --k)
@@ -1605,7 +1701,13 @@ __global__ __launch_bounds__(256) void k_verify_chain_w(const uint8_t *U, const 
       while (kn < 4 && !v[kn]) ++kn;
       const uint64_t nxt_set = kn < 4 ? begin + 32 * (w + kn) + __builtin_ctz(v[kn]) : lane_next;
       uint64_t step;
-      if (s + 4 > total) {
+      if (cov && nxt_set != ~0ull && nxt_set < thi) {  // a pair inside a summarised tile
+        k = kn;
+        continue;
+      }
+      if (cov) {
+        step = tstep;  // the tile's last true position
+      } else if (s + 4 > total) {
         step = ~0ull;  // getInt at EOF: the chain ends here
       } else {
         const uint32_t *g = reinterpret_cast<const uint32_t *>(U + (s & ~3ull));
@@ -1927,12 +2029,12 @@ static inline uint32_t ngrid(uint64_t n, uint32_t t) { return (uint32_t)((n + t 
 hipError_t launch_eager(const uint8_t *U, uint64_t u_pad, uint64_t begin, uint64_t end, const uint64_t *seg_end,
                         uint32_t nseg, uint32_t open_last, const int32_t *ctg, int32_t nctg, int32_t rtc,
                         uint32_t *bits, unsigned long long *counters, hipStream_t st, uint64_t front,
-                        uint64_t *defer_pos, uint64_t defer_cap, uint64_t *xq_pos, uint64_t xq_cap) {
+                        uint64_t *defer_pos, uint64_t defer_cap, uint64_t *xq_pos, uint64_t xq_cap, TileSum *tsum) {
   if (end <= begin) return hipSuccess;
   Segs sg{seg_end, nseg, open_last};
   Ctg c{ctg, nctg};
   EagerOut o{bits,   counters,     counters + 1, counters + 2, front, defer_pos, counters + 3, defer_cap,
-             xq_pos, counters + 4, xq_cap,       counters + TRUE_SPREAD_OFF};
+             xq_pos, counters + 4, xq_cap,       counters + TRUE_SPREAD_OFF, tsum};
   hipLaunchKernelGGL(k_eager, dim3(ngrid(end - begin, ETILE)), dim3(T), 0, st, U, u_pad, begin, end, sg, c,
                      rtc, o);
   hipLaunchKernelGGL(k_fold_true, dim3(1), dim3(WAVE), 0, st, counters + TRUE_SPREAD_OFF, counters);
@@ -2010,12 +2112,12 @@ hipError_t launch_first_set(const uint32_t *bits, uint64_t begin, uint64_t from,
 hipError_t launch_verify_chain_count(const uint8_t *U, const uint32_t *bits, uint64_t begin, uint64_t bits_end,
                                      uint64_t from, uint64_t E, uint64_t total, unsigned long long *n_anom,
                                      unsigned long long *first_anom, unsigned long long *exit_pos,
-                                     unsigned long long *n_set, hipStream_t st) {
+                                     unsigned long long *n_set, const TileSum *tsum, hipStream_t st) {
   if (E <= from) return hipSuccess;
   const uint64_t nw = (E - begin + 31) / 32 - ((from - begin) / 32 & ~3ull);
   const uint32_t grid = (uint32_t)std::min<uint64_t>(ngrid(nw, 1024), 2048);
   hipLaunchKernelGGL(k_verify_chain_w, dim3(grid), dim3(256), 0, st, U, bits, begin, bits_end, from, E, total,
-                     n_anom, first_anom, exit_pos, n_set);
+                     n_anom, first_anom, exit_pos, n_set, tsum);
   return hipGetLastError();
 }
 

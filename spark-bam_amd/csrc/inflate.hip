@@ -2365,6 +2365,16 @@ __device__ __forceinline__ uint4 pack8_u16(const uint32_t *c) {
 #ifndef SBH_ASM_CHASE
 #define SBH_ASM_CHASE 1  // k_lz's pointer chase as the hand-written loop below
 #endif
+#ifndef SBH_LZ_SLOT128
+#define SBH_LZ_SLOT128 1  // k_lz slot pass: a thread's 8 start values from one 16-byte read of its own slots
+#endif
+#ifndef SBH_LZ_SBMASK
+#define SBH_LZ_SBMASK 0  // 1: k_lz marks OR a thread's start bits per word (A/B r04e: +0.5..3% k_lz: kept off)
+#endif
+#ifndef SBH_LZ_LMARK_MIN
+#define SBH_LZ_LMARK_MIN 1  // k_lz: long matches per wave and token slot from which their threads mark them (A/B r04f: 1 best; 99 = wave-serial only: D +11%)
+#endif
+constexpr uint32_t LZ_LMARK_MIN = SBH_LZ_LMARK_MIN;
 #ifndef SBH_LZ_OVL_WAVE
 #define SBH_LZ_OVL_WAVE 0  // 1: overlapping short matches (dist < len) marked byte by byte by the wave (A/B r04c: k_lz +5% B, +26% D, +10% E: kept off)
 #endif
@@ -2438,7 +2448,8 @@ __global__ __launch_bounds__(LZ_THREADS, 4) void k_lz(const uint8_t *__restrict_
   uint32_t *wsum = sm.pp.wsum;
   const uint64_t b = blockIdx.x;
   if (b >= nblocks) return;
-  const uint32_t t = threadIdx.x, lane = t & (WAVE - 1);
+  const uint32_t t = threadIdx.x;
+  [[maybe_unused]] const uint32_t lane = t & (WAVE - 1);
   const uint32_t n = bl.ntok[b];
   const uint64_t G = bl.ustart[b];
   const uint32_t sh = (uint32_t)(G & 15);
@@ -2534,20 +2545,64 @@ __global__ __launch_bounds__(LZ_THREADS, 4) void k_lz(const uint8_t *__restrict_
 #pragma unroll
       for (uint32_t k = 0; k < LZ_TPT; ++k)
         wide[k] = match[k] && (len[k] > LZ_SHORT || (SBH_LZ_OVL_WAVE && dist[k] < len[k]));
+#if SBH_LZ_SBMASK
+      // start bits gathered per word first: a thread's short tokens span at most 3 words (2 x 32
+      // bytes), so 3 atomics at most (one when they share a word) instead of one per token
+      uint32_t wA = ~0u, mA = 0, mB = 0, mC = 0;
+#endif
 #pragma unroll
       for (uint32_t k = 0; k < LZ_TPT; ++k) {
         if (i0 + k >= n || wide[k] || !(off[k] - pb < plen)) continue;
         const uint32_t d = off[k] - abase;
         p16[d] = (uint16_t)(match[k] ? off[k] - dist[k] : off[k]);
         if (!match[k]) img[off[k]] = (uint8_t)(x[k] >> 8);
+#if SBH_LZ_SBMASK
+        const uint32_t w = d >> 5, bit = 1u << (d & 31);
+        wA = wA == ~0u ? w : wA;
+        const uint32_t r = w - wA;
+        mA |= r == 0 ? bit : 0u;
+        mB |= r == 1 ? bit : 0u;
+        mC |= r == 2 ? bit : 0u;
+        if (r > 2)  // (a long match between this thread's short tokens)
+          __hip_atomic_fetch_or(&sbits[w], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
         __hip_atomic_fetch_or(&sbits[d >> 5], 1u << (d & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
       }
+#if SBH_LZ_SBMASK
+      if (mA) __hip_atomic_fetch_or(&sbits[wA], mA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (mB) __hip_atomic_fetch_or(&sbits[wA + 1], mB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (mC) __hip_atomic_fetch_or(&sbits[wA + 2], mC, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
+      // long matches.  Few in a wave (short-read data: one or two): the wave writes every byte's
+      // pointer, match by match.  Many (long reads): each thread marks its own with a start every
+      // 32 bytes (a pointer and a start bit each), so the slot pass finds every byte's start
+      // within 31 slots back as for a short match; a marker at 32 m copies from
+      // o - dist + (32 m mod dist) (for an overlapping match the same byte periods earlier).
+      // (A/B r04e, k_lz: lane markers -12% on config D, +2.5% on B; wave-serial the reverse.)
 #pragma unroll
-      for (uint32_t k = 0; k < LZ_TPT; ++k) {  // long matches: the wave writes every byte's pointer
-        uint64_t lm = __ballot(i0 + k < n && wide[k] && off[k] - pb < plen);
+      for (uint32_t k = 0; k < LZ_TPT; ++k) {
+        const bool mine = i0 + k < n && wide[k] && off[k] - pb < plen;
+        uint64_t lm = __ballot(mine);
 #ifdef SBH_LZ_PROBE
         nlong += __builtin_popcountll(lm);
 #endif
+        if ((uint32_t)__builtin_popcountll(lm) >= LZ_LMARK_MIN) {
+          if (mine) {
+            const uint32_t d0 = off[k] - abase, D = dist[k], L = len[k];
+            const bool ov = D < L;
+            uint32_t r = 0;  // 32 m mod D (ov)
+            const uint32_t r32 = ov ? (D > 32 ? 32 : mod_small(32, D)) : 0;
+            for (uint32_t m = 0; m < L; m += 32) {
+              const uint32_t d = d0 + m;
+              p16[d] = (uint16_t)(off[k] - D + (ov ? r : m));
+              __hip_atomic_fetch_or(&sbits[d >> 5], 1u << (d & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              r += r32;
+              r = r >= D ? r - D : r;
+            }
+          }
+          continue;
+        }
         while (lm) {
           const uint32_t l = (uint32_t)__builtin_ctzll(lm);
           lm &= lm - 1;
@@ -2596,6 +2651,22 @@ __global__ __launch_bounds__(LZ_THREADS, 4) void k_lz(const uint8_t *__restrict_
         uint32_t st = low ? wi * 32 + 31 - __builtin_clz(low) : prev ? wi * 32 - 1 - __builtin_clz(prev) : s0;
         const uint32_t wb = cur >> sh8;
         uint32_t sidx[PTR_HALF], v[PTR_HALF];
+#if SBH_LZ_SLOT128
+        // the start values: the window's own 8 slots in one 16-byte read (lane h at 16 h bytes: no
+        // bank conflicts, where 8 u16 reads at a 16-byte lane stride were 4-way), the nearest start
+        // before the window in one u16 read; each slot takes its last start's value
+        const uint4 ow = reinterpret_cast<const uint4 *>(p16)[h];
+        const uint32_t od[4] = {ow.x, ow.y, ow.z, ow.w};
+        uint32_t vl = p16[st];
+#pragma unroll
+        for (uint32_t k = 0; k < PTR_HALF; ++k) {
+          const bool s = (wb >> k) & 1u;
+          st = s ? s0 + k : st;
+          sidx[k] = st;
+          vl = s ? (k & 1 ? od[k >> 1] >> 16 : od[k >> 1] & 0xffffu) : vl;
+          v[k] = vl;
+        }
+#else
 #pragma unroll
         for (uint32_t k = 0; k < PTR_HALF; ++k) {
           st = (wb >> k) & 1u ? s0 + k : st;
@@ -2603,6 +2674,7 @@ __global__ __launch_bounds__(LZ_THREADS, 4) void k_lz(const uint8_t *__restrict_
         }
 #pragma unroll
         for (uint32_t k = 0; k < PTR_HALF; ++k) v[k] = p16[sidx[k]];
+#endif
 #if SBH_LZ_OVL_WAVE
         // (no byte of a short start-marked match reaches past its distance: overlapping matches
         // had every byte marked with its final offset by the wave)

@@ -59,7 +59,7 @@ hipError_t build_chain(const uint8_t *comp, uint64_t n, const uint64_t *cand, ui
 hipError_t launch_eager(const uint8_t *U, uint64_t u_pad, uint64_t begin, uint64_t end, const uint64_t *seg_end,
                         uint32_t nseg, uint32_t open_last, const int32_t *ctg, int32_t nctg, int32_t rtc,
                         uint32_t *bits, unsigned long long *counters, hipStream_t st, uint64_t front,
-                        uint64_t *defer_pos, uint64_t defer_cap, uint64_t *xq_pos, uint64_t xq_cap);
+                        uint64_t *defer_pos, uint64_t defer_cap, uint64_t *xq_pos, uint64_t xq_cap, TileSum *tsum);
 hipError_t launch_eager_xq(const uint8_t *U, uint64_t begin, const uint64_t *seg_end, uint32_t nseg,
                            uint32_t open_last, const int32_t *ctg, int32_t nctg, int32_t rtc, uint32_t *bits,
                            unsigned long long *counters, uint64_t *xq_pos, uint64_t cap, hipStream_t st);
@@ -76,7 +76,7 @@ hipError_t launch_first_set(const uint32_t *bits, uint64_t begin, uint64_t from,
 hipError_t launch_verify_chain_count(const uint8_t *U, const uint32_t *bits, uint64_t begin, uint64_t bits_end,
                                      uint64_t from, uint64_t E, uint64_t total, unsigned long long *n_anom,
                                      unsigned long long *first_anom, unsigned long long *exit_pos,
-                                     unsigned long long *n_set, hipStream_t st);
+                                     unsigned long long *n_set, const TileSum *tsum, hipStream_t st);
 hipError_t launch_chain_walk(const uint8_t *U, uint64_t first, uint64_t E, uint64_t total,
                              unsigned long long *count, unsigned long long *last, hipStream_t st);
 }  // namespace sbh
@@ -150,6 +150,7 @@ struct sbh_shard {
   DBuf<int32_t> ctg;
   int32_t nctg = -1;
   DBuf<uint32_t> bits;
+  DBuf<TileSum> tsum;  // per quarter eager tile of bits (from bits_begin): the chain proof's summaries
   // chain marking (pointer doubling) over the set bits of [cm_first, cm_E) when the bitmap
   // is not the chain: node positions, per-word prefix counts, jumps, marks and their prefix
   DBuf<uint64_t> cm_pos, cm_wcnt, cm_wpre, cm_mark, cm_mpre;
@@ -783,6 +784,13 @@ static uint64_t xq_cap() {
   const char *e = std::getenv("SBH_XQ");
   return e && e[0] == '0' ? 0 : XQ_CAP_MAX;
 }
+// SBH_TSUM=1: k_eager writes per-quarter-tile chain summaries and the chain proof reads them
+// instead of every true position's record length from U (its 4.8x line over-read).  Off by
+// default: measured (r04g, config B) the proof 0.46 -> 0.36 ms per step but k_eager 3.00 -> 3.24 ms.
+static bool tsum_on() {
+  const char *e = std::getenv("SBH_TSUM");
+  return e && e[0] == '1';
+}
 
 static int eager_range(sbh_shard *sh, uint64_t begin, uint64_t end, int32_t rtc, uint64_t *n_true) {
   sbh_ctx *ctx = sh->ctx;
@@ -790,6 +798,7 @@ static int eager_range(sbh_shard *sh, uint64_t begin, uint64_t end, int32_t rtc,
   const uint64_t nwords = (end - begin + 31) / 32;
   sh->chain_ok = sh->cm_valid = false;
   HIPCHK(ctx, sh->bits.ensure(nwords + 1));
+  HIPCHK(ctx, sh->tsum.ensure((end - begin + EAGER_TILE - 1) / EAGER_TILE * 4 + 4));
   HIPCHK(ctx, sh->xq.ensure(2 * XQ_CAP_MAX));
   unsigned long long *c = sh->ctr.p;
   HIPCHK(ctx, hipMemsetAsync(c, 0, 48, st));
@@ -797,7 +806,7 @@ static int eager_range(sbh_shard *sh, uint64_t begin, uint64_t end, int32_t rtc,
   mark(sh, 4);
   HIPCHK(ctx, launch_eager(sh->U.p, sh->utotal + sh->pad, begin, end, sh->d_seg.p, (uint32_t)sh->seg_end.size(),
                            sh->open_last ? 1 : 0, sh->ctg.p, sh->nctg, rtc, sh->bits.p, c, st, ~0ull, nullptr, 0,
-                           sh->xq.p, xq_cap()));
+                           sh->xq.p, xq_cap(), tsum_on() ? sh->tsum.p : nullptr));
   HIPCHK(ctx, launch_eager_xq(sh->U.p, begin, sh->d_seg.p, (uint32_t)sh->seg_end.size(), sh->open_last ? 1 : 0,
                               sh->ctg.p, sh->nctg, rtc, sh->bits.p, c, sh->xq.p, xq_cap(), st));
   mark(sh, 5);
@@ -1011,7 +1020,7 @@ static int count_records_impl(sbh_shard *sh, uint64_t first, uint64_t E, uint64_
     // verify bitmap == chain and count the set bits in one pass (k_verify_chain_w: wave-
     // cooperative successors, so sparse bitmaps of long records cost no word-by-word scans)
     HIPCHK(ctx, launch_verify_chain_count(sh->U.p, sh->bits.p, sh->bits_begin, sh->bits_end, first, E, total, c,
-                                          c + 1, c + 3, c + 2, st));
+                                          c + 1, c + 3, c + 2, tsum_on() ? sh->tsum.p : nullptr, st));
     HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 16, c, 32, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipStreamSynchronize(st));
     const uint64_t n = sh->h_ctr[18];
@@ -1365,6 +1374,7 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
   const TokPlan P = tok_plan(sh, (nb + npipe - 1) / std::max<uint64_t>(npipe, 1));
   HIPCHK(ctx, sh->tok.ensure(P.tok_len));
   HIPCHK(ctx, sh->bits.ensure((E + 31) / 32 + 1));
+  HIPCHK(ctx, sh->tsum.ensure((E + EAGER_TILE - 1) / EAGER_TILE * 4 + 4));
   HIPCHK(ctx, sh->defer.ensure(DEFER_CAP));
   HIPCHK(ctx, sh->xq.ensure(2 * XQ_CAP_MAX));
   HIPCHK(ctx, hipMemsetAsync(sh->U.p + sh->utotal, 0, sh->pad, sa));
@@ -1410,7 +1420,8 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
       HIPCHK(ctx, hipEventRecord(e[4], se));
       HIPCHK(ctx, launch_eager(sh->U.p, sh->utotal + sh->pad, e_done, hi, sh->d_seg.p, (uint32_t)sh->seg_end.size(),
                                sh->open_last ? 1 : 0, sh->ctg.p, sh->nctg, rtc, sh->bits.p + e_done / 32, c, se,
-                               front, sh->defer.p, DEFER_CAP, sh->xq.p, xq_cap()));
+                               front, sh->defer.p, DEFER_CAP, sh->xq.p, xq_cap(),
+                               tsum_on() ? sh->tsum.p + e_done / EAGER_SUB : nullptr));
       HIPCHK(ctx, hipEventRecord(e[5], se));
       eager_launched[i] = 1;
       e_done = hi;

@@ -85,6 +85,19 @@ constexpr uint32_t INF_SERIAL = 0xffu; // (inside inflate only) left to the seri
 #endif
 constexpr uint64_t EAGER_TILE = SBH_ETILE;
 constexpr uint64_t EAGER_REACH = SBH_ETILE + 4096 + 512 + 64;
+constexpr uint64_t EAGER_SUB = EAGER_TILE / 4;  // one k_eager wave's share of a tile (4 waves)
+// Per quarter of an eager tile (EAGER_SUB positions, one k_eager wave's result words; written on
+// k_eager's fast path; the chain proof, k_verify_chain_w, reads it instead of every true
+// position's record length): the record step of the quarter's last true position, and the true
+// positions whose step misses the next true position of the same quarter.
+struct TileSum {
+  uint64_t step_last;   // TS_NONE: none, or the record ends the stream; TS_DIRTY: no summary
+  uint32_t n_anom;      // true positions whose step is not the tile's next true position
+  uint32_t first_anom;  // offset of the first of them in the quarter (~0u: none)
+};
+constexpr uint64_t TS_NONE = ~0ull;
+constexpr uint64_t TS_DIRTY = ~1ull;  // bits settled after k_eager (long-record queue, deferred,
+                                      // unknown positions) or by its fallback path
 // Bitmap set-bit prefix (launch_rec_positions_bits): one u64 per group of WPRE_GROUP
 // consecutive words of [first, E) -- the set bits before the group; a lookup adds the
 // popcounts of the group's earlier words (one 64-byte read).

@@ -441,6 +441,45 @@ def test_chain_count_with_false_positive_bits(ctx, synth_files, name):
         sh.close()
 
 
+@pytest.mark.parametrize("name", ["adversarial", "short_l6", "short_l0", "long"])
+def test_chain_proof_tile_summaries(ctx, synth_files, name, monkeypatch):
+    """The chain proof (k_verify_chain_w) reading k_eager's per-tile summaries gives the same
+    counts, exits and anomaly counts as reading every true position's length from U
+    (SBH_TSUM=1 vs 0), over the whole file (sbh_run_shard, pipelined eager) and over sub-ranges
+    that start and end inside tiles or on tile edges (sbh_check_eager's bitmap)."""
+    data = synth_files[name]
+    of = OracleFile(data)
+    tile = 16384
+
+    def run(flag):
+        monkeypatch.setenv("SBH_TSUM", flag)
+        sh = load(ctx, data, of.contig_len)
+        try:
+            r = sh.run(0, data.size)
+            _, _, first = sb.parse_bam_header(sh.read_flat(0, min(of.flat_size, 1 << 20)))
+            chain = of.record_chain(first)
+            sh.check_eager(0, of.flat_size)
+            out = [(r["count"], r["exit_flat"], r["anomalies"], r["n_true"])]
+            rng = np.random.default_rng(11)
+            for _ in range(8):
+                i = int(rng.integers(0, len(chain) - 1))
+                f = int(chain[i])
+                for e in (int(rng.integers(f + 1, of.flat_size + 1)), (f // tile + 3) * tile, of.flat_size):
+                    e = min(e, of.flat_size)
+                    want = int(np.count_nonzero((chain >= f) & (chain < e)))
+                    got = sh.count_records(f, e)
+                    assert got == want, (name, flag, f, e)
+                    out.append((f, e, got, sh.chain_from(f, e)))
+            return out, len(chain)
+        finally:
+            sh.close()
+
+    on, n_chain = run("1")
+    off, _ = run("0")
+    assert on == off
+    assert on[0][0] == n_chain
+
+
 @pytest.mark.parametrize("name", FIXTURES)
 def test_verify_crc_fixtures(ctx, name):
     """Every inflated block's bytes match its BGZF footer CRC32 (sbh_verify_crc)."""
