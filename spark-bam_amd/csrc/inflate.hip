@@ -2479,7 +2479,7 @@ __global__ __launch_bounds__(LZ_THREADS, 4) void k_lz(const uint8_t *__restrict_
 
   uint32_t base = 0;  // output offset of the chunk's first token
 #ifdef SBH_LZ_PROBE
-  uint64_t tp0 = __builtin_readcyclecounter(), t_pre = 0, t_rounds = 0, t_init = 0, t_w = 0, t_ch = 0, t_mk = 0;
+  uint64_t tp0 = __builtin_readcyclecounter(), t_pre = 0, t_rounds = 0, t_init = 0, t_w = 0, t_ch = 0, t_mk = 0, t_b1 = 0;
   uint32_t nrounds = 0, njumps = 0, nlong = 0;
 #endif
   uint32_t xn[LZ_TPT];  // next chunk's tokens, loaded one chunk ahead
@@ -2627,6 +2627,9 @@ __global__ __launch_bounds__(LZ_THREADS, 4) void k_lz(const uint8_t *__restrict_
       t_mk += __builtin_readcyclecounter() - tb;
 #endif
       __syncthreads();
+#ifdef SBH_LZ_PROBE
+      t_b1 += __builtin_readcyclecounter() - tb;
+#endif
       // slot pass: every byte's pointer from its token's start (at most LZ_SHORT - 1
       // slots back): byte j of a match that starts at slot s and copies from v points at
       // v + j, or v + (j mod (s - v)) when the match overlaps itself (rare); a literal
@@ -2799,11 +2802,11 @@ __global__ __launch_bounds__(LZ_THREADS, 4) void k_lz(const uint8_t *__restrict_
     for (uint32_t l = 0; l < WAVE; ++l) tot += __builtin_amdgcn_readlane(njumps, l);
     njumps = tot;
   }
-  if (lane == 0 && (b == 1 || b == 1000) && t < WAVE)
-    printf("lz blk %llu wave %u ntok %u cyc %llu pre %llu marks %llu marks+slots %llu init+bar %llu chase %llu resolve+bar %llu fallback %u chase_rounds %u long %u\n",
+  if (lane == 0 && (b == 1000 || (b == 1 && t < WAVE)))
+    printf("lz blk %llu wave %u ntok %u cyc %llu pre %llu marks %llu marks+bar %llu marks+slots %llu init+bar %llu chase %llu resolve+bar %llu fallback %u chase_rounds %u long %u\n",
            (unsigned long long)b, t / WAVE, n, (unsigned long long)(__builtin_readcyclecounter() - tp0),
-           (unsigned long long)t_pre, (unsigned long long)t_mk, (unsigned long long)t_w, (unsigned long long)t_init,
-           (unsigned long long)t_ch, (unsigned long long)t_rounds, nrounds, njumps, nlong);
+           (unsigned long long)t_pre, (unsigned long long)t_mk, (unsigned long long)t_b1, (unsigned long long)t_w,
+           (unsigned long long)t_init, (unsigned long long)t_ch, (unsigned long long)t_rounds, nrounds, njumps, nlong);
 #endif
   const uint32_t usize = base;
   // write the image: 16-byte granules aligned to the flat address
