@@ -1607,6 +1607,9 @@ __global__ __launch_bounds__(256) void k_first_set(const uint32_t *bits, uint64_
 // of the next non-empty lane (a readlane), and only the wave's last one looks past the
 // wave -- the whole wave scanning 64 words per step -- so each set bit costs one bitmap
 // load and one U load, and sparse bitmaps (long records) no longer scan word by word.
+#ifndef SBH_TSUM_CODE
+#define SBH_TSUM_CODE 1  // (A/B: 0 compiles the summaries' branches out of k_verify_chain_w)
+#endif
 __global__ __launch_bounds__(256) void k_verify_chain_w(const uint8_t *U, const uint32_t *bits, uint64_t begin,
                                                          uint64_t bits_end, uint64_t from, uint64_t E, uint64_t total,
                                                          unsigned long long *n_anom, unsigned long long *first_anom,
@@ -1648,7 +1651,7 @@ __global__ __launch_bounds__(256) void k_verify_chain_w(const uint8_t *U, const 
     // is needed, from the summary, not from U
     bool cov = false;
     uint64_t tstep = TS_NONE, thi = 0;
-    if (tsum && w < w_end) {
+    if (SBH_TSUM_CODE && tsum && w < w_end) {
       const uint64_t tile = w / TWORDS, tlo = begin + tile * EAGER_SUB;
       thi = tlo + EAGER_SUB;
       if (tlo >= from && thi <= E) {

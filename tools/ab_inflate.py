@@ -64,6 +64,9 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--child", default=None)
     ap.add_argument("--config", default="B", choices=sorted(CONFIGS))
+    ap.add_argument("--rounds", type=int, default=1,
+                    help="run the library list this many times, alternating its order (ABBA), and "
+                         "print each library's per-stage median over the rounds at the end")
     ap.add_argument("variants", nargs="*")
     a = ap.parse_args()
     if a.child is not None:
@@ -71,13 +74,26 @@ def main():
     vdir = os.path.join(ROOT, "spark-bam_amd/build/ab")
     named = [v if v.endswith(".so") else os.path.join(vdir, f"lib_{v}.so") for v in a.variants]
     libs = [""] + (named or sorted(glob.glob(os.path.join(vdir, "lib_*.so"))))
-    for lib in libs:
-        r = subprocess.run([sys.executable, __file__, "--child", lib, "--records", str(a.records),
-                            "--reps", str(a.reps), "--config", a.config], capture_output=True, text=True,
-                           timeout=900)
-        print(r.stdout.strip() or r.stderr[-2000:], flush=True)
-        if r.stderr and r.stdout:  # probe variants print their counters on stderr/stdout
-            print(r.stderr[-4000:], flush=True)
+    got = {}
+    for rnd in range(a.rounds):
+        for lib in (libs if rnd % 2 == 0 else libs[::-1]):
+            r = subprocess.run([sys.executable, __file__, "--child", lib, "--records", str(a.records),
+                                "--reps", str(a.reps), "--config", a.config], capture_output=True, text=True,
+                               timeout=900)
+            print(r.stdout.strip() or r.stderr[-2000:], flush=True)
+            if r.stderr and r.stdout:  # probe variants print their counters on stderr/stdout
+                print(r.stderr[-4000:], flush=True)
+            try:
+                d = json.loads(r.stdout.strip().splitlines()[-1])
+                got.setdefault(d["lib"], []).append((d["stage_ms"], d.get("sha1")))
+            except (ValueError, IndexError, KeyError):
+                pass
+    if a.rounds > 1:
+        import numpy as np
+        for lib, v in got.items():
+            med = np.median(np.asarray([x[0] for x in v]), axis=0).round(4).tolist()
+            print(json.dumps({"summary": lib, "rounds": len(v), "stage_ms_median": med,
+                              "sha1": sorted({x[1] for x in v})}), flush=True)
 
 
 if __name__ == "__main__":

@@ -46,7 +46,7 @@ ab)
   C=$1; N=$2; shift 2
   L=""
   for v in "$@"; do L="$L spark-bam_amd/build/ab/lib_$v.so"; done
-  timeout -k 10 500 python -u tools/ab_inflate.py --config $C --records $N $L > gpurun_out/${T}_ab$C.log 2>&1 || exit 6
+  timeout -k 10 900 python -u tools/ab_inflate.py --config $C --records $N --rounds ${AB_ROUNDS:-1} $L > gpurun_out/${T}_ab$C.log 2>&1 || exit 6
   ;;
 fullab)
   N=$1; shift
