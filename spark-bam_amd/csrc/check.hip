@@ -1059,6 +1059,9 @@ constexpr uint32_t FCCAP = 256;               // close calls buffered per workgr
 #ifndef SBH_FULL_FAST
 #define SBH_FULL_FAST 1  // tiles far from a segment end: full_first_win (no end-of-stream cases)
 #endif
+#ifndef SBH_FULL_HOT
+#define SBH_FULL_HOT 1  // fast tiles: the wave's most shared failure word counted by ballot (see k_full)
+#endif
 constexpr uint32_t FCTG = 1024;               // contig lengths staged in LDS (more: read from global)
 constexpr uint32_t FULL_SLOW = 0xFFFFFFFFu;   // "take the exact path" (no valid word has all bits)
 constexpr uint32_t FULL_PASS = 0xFFFFFFFEu;   // the first record passes: the chain decides
@@ -1423,6 +1426,26 @@ __global__ __launch_bounds__(T, 5) void k_full(const uint8_t *__restrict__ U, ui
     // queue overflows (more record starts in the tile than slowq holds) are kept as bits and
     // decided after the sweep, so the exact path is not inlined into every unrolled position
     uint32_t ovf = 0;
+#if SBH_FULL_HOT
+    // The wave's hot failure word: inside quality strings and sequences most of a wave's 64
+    // positions fail with one and the same word, and their per-flag LDS adds all land on the
+    // same counters (a same-address atomic serialises: the bulk of k_full's bank conflicts).
+    // Lanes whose word equals the hot word only count (one ballot popcount per wave); the count
+    // goes into the word's Counts row when the hot word changes (to a word more lanes share) and
+    // after the sweep.  Words with <= 2 flags (close calls, listed per position) are never hot.
+    uint32_t hotw = 0, hotn = 0;  // wave-uniform; 0 is no failure word
+    const uint32_t lane = threadIdx.x & (WAVE - 1);
+    auto hot_flush = [&]() {
+      if (hotn && lane == 0) {
+        uint32_t f = hotw;
+        uint32_t *row = myhist + __popc(f) * RW;
+        while (f) {
+          atomicAdd(&row[__builtin_ctz(f)], hotn);
+          f &= f - 1;
+        }
+      }
+    };
+#endif
     for (uint32_t step = 0; step < FTILE / (FPL * T); ++step) {
       const uint32_t j = threadIdx.x + step * T;
       const uint4 v0 = ldsv[j], v1 = ldsv[j + 1], v2 = ldsv[j + 2];
@@ -1442,12 +1465,34 @@ __global__ __launch_bounds__(T, 5) void k_full(const uint8_t *__restrict__ U, ui
           x.nidx = (int32_t)__builtin_amdgcn_alignbyte(D[b + 7], D[b + 6], sh);
           x.npos = (int32_t)__builtin_amdgcn_alignbyte(D[b + 8], D[b + 7], sh);
           const uint32_t r = full_first_win(s, bname, bop, q, x, c, oi);
-          if (r == FULL_SLOW || r == FULL_PASS) {  // record starts, long CIGARs: the balanced pass below
+          const bool queued = r == FULL_SLOW || r == FULL_PASS;
+#if SBH_FULL_HOT
+          uint64_t hm = __ballot(!queued && r == hotw);
+          const uint64_t om = __ballot(!queued && r != hotw);
+          if (__builtin_popcountll(om) > __builtin_popcountll(hm)) {  // uniform: try another hot word
+            const uint32_t cw = __builtin_amdgcn_readlane(r, (uint32_t)__builtin_ctzll(om));
+            const uint64_t cm = __ballot(!queued && r == cw);
+            if (__popc(cw) > 2 && __builtin_popcountll(cm) > __builtin_popcountll(hm)) {
+              hot_flush();
+              hotw = cw;
+              hotn = 0;
+              hm = cm;
+            }
+          }
+          hotn += (uint32_t)__builtin_popcountll(hm);
+#endif
+          if (queued) {  // record starts, long CIGARs: the balanced pass below
             const uint32_t qi = atomicAdd(&nslow, 1u);
             if (qi < SLOWCAP) slowq[qi] = q;
             else ovf |= 1u << (16 * step + 4 * b + sh);
             continue;
           }
+#if SBH_FULL_HOT
+          if ((hm >> lane) & 1ull) {
+            if (o.words) o.words[s0 + q - begin] = r;
+            continue;
+          }
+#endif
 #if SBH_FULL_ACCF
           account_fail(s0 + q, r);
 #else
@@ -1458,6 +1503,9 @@ __global__ __launch_bounds__(T, 5) void k_full(const uint8_t *__restrict__ U, ui
     }
 #if SBH_FULL_RUN
     run_flush();
+#endif
+#if SBH_FULL_HOT
+    hot_flush();
 #endif
     static_assert(FTILE / (FPL * T) * FPL <= 32, "overflow bits fit a word");
     while (ovf) {
