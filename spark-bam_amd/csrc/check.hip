@@ -1060,7 +1060,7 @@ constexpr uint32_t FCCAP = 256;               // close calls buffered per workgr
 #define SBH_FULL_FAST 1  // tiles far from a segment end: full_first_win (no end-of-stream cases)
 #endif
 #ifndef SBH_FULL_HOT
-#define SBH_FULL_HOT 1  // fast tiles: the wave's most shared failure word counted by ballot (see k_full)
+#define SBH_FULL_HOT 0  // 1: fast tiles count the wave's most shared failure word by ballot (A/B r04o: 7.40 -> 7.89 ms at 4 M records: off)
 #endif
 constexpr uint32_t FCTG = 1024;               // contig lengths staged in LDS (more: read from global)
 constexpr uint32_t FULL_SLOW = 0xFFFFFFFFu;   // "take the exact path" (no valid word has all bits)

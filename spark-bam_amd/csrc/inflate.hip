@@ -2378,93 +2378,76 @@ constexpr uint32_t LZ_LMARK_MIN = SBH_LZ_LMARK_MIN;
 #ifndef SBH_LZ_OVL_WAVE
 #define SBH_LZ_OVL_WAVE 0  // 1: overlapping short matches (dist < len) marked byte by byte by the wave (A/B r04c: k_lz +5% B, +26% D, +10% E: kept off)
 #endif
-#ifndef SBH_LZ_ROT
-#define SBH_LZ_ROT 0  // 1: k_lz chase / gather pointers rotated per lane, bank-conflict-free reads (A/B r04n: k_lz +5% B, +4% D, +2.5% E: kept off)
+#ifndef SBH_LZ_MOD
+#define SBH_LZ_MOD 1  // 1: a byte of an overlapping short match points at v + (j mod distance) (0: at v + j, a longer chase: A/B r04p k_lz +4% B, +2% D)
 #endif
+// (r04n-r04p, measured and removed -- profiles/r04_ab/: each lane's 8 pointers rotated by
+// 2 ((h >> 3) & 3) slots so the chase's u16 reads of lanes h, h + 8, h + 16, h + 24 (16 bytes
+// apart, one bank) hit four distinct dwords: k_lz +5% B, +4% D, +2.5% E; a thread's two half
+// granules chased in one loop (16 reads per round, a single-granule thread chasing a copy):
+// +17% B, +19% D, +17% E; the slot pass's two half granules as one straight-line body: +30% B;
+// 1024-token chunks (SBH_LZ_TPT=2): +10% B, +6% D.  Each variant that added LDS instructions or
+// VALU work per byte lost more than the latency it overlapped or the conflicts it removed.)
 
-// Lane h of a 32-lane LDS group owns slots [8h, 8h + 8): 16 bytes, so the same slot k of lanes
-// h, h + 8, h + 16, h + 24 falls on one bank (ds_read_u16 banks by dword mod 32) -- and inside a
-// match or a literal run the pointers keep that stride, so every chase read was a 4-way conflict
-// (the gather's byte reads 2-way).  Each lane keeps its 8 pointers rotated by 2 r slots, r =
-// (h >> 3) & 3: register k holds slot (k + 2 r) & 7, so those four lanes read four distinct dwords.
-// c'[k] = c[(k + 2 r) & 7] in two select stages (r's two bits).
-// (bit selects, not ?: -- the compiler turns a ?: of two array elements into a dynamically
-// indexed array, i.e. scratch)
-__device__ __forceinline__ void rot8(uint32_t (&c)[8], uint32_t r) {
-  const uint32_t m1 = 0u - (r & 1u), m2 = 0u - ((r >> 1) & 1u);
-  uint32_t u[8];
-#pragma unroll
-  for (uint32_t k = 0; k < 8; ++k) u[k] = (c[(k + 2) & 7] & m1) | (c[k] & ~m1);
-#pragma unroll
-  for (uint32_t k = 0; k < 8; ++k) c[k] = (u[(k + 4) & 7] & m2) | (u[k] & ~m2);
-}
 // k_lz's pointer chase for one half granule (8 slots) as hand-written code, the same rounds as
 // the C++ loop: every pointer at or past the pass start pb is replaced by its target's slot
-// value (u16 LDS reads at 2 * max(c, pb) + p16 - 2 * abase), the 8 slots written back as
-// 16 bytes, until no pointer of the lane moved to another in-pass position.  5 vector + 3
-// scalar instructions per pointer and round (the compiler's version: ~9 and ~3, plus a
-// register rotation of the 8 pointers every round).
-// With SBH_LZ_ROT the pointers arrive rotated (rot8), so the packed dwords a0..a3 are the
-// granule's dwords r, r + 1, r + 2, r + 3 (mod 4): pairs (a0, a2) and (a1, a3) go to dwords two
-// apart, written by ds_write2_b32 at per-lane bases wA / wB with the pair's order chosen by the
-// lane masks sA / sB (set where the pair's first dword is the higher one).
-__device__ __forceinline__ void chase8_asm(uint32_t (&c)[8], uint32_t pend, uint32_t pb, uint32_t off,
-                                           uint32_t waddr, uint32_t wB, uint64_t sA, uint64_t sB) {
-  const uint32_t sel = 0x05040100u;  // v_perm: the low halves of two dwords
-  uint32_t a0, a1, a2, a3, a4, a5, a6, a7, r0, r1, r2, r3, r4, r5, r6, r7;
-  uint64_t sv, sm, sx, sy, sc;
+// value (u16 LDS reads at 2 * max(c, pb) + p16 - 2 * abase, all 8 issued before the first is
+// waited for), the 8 slots written back as 16 bytes at w0, until no pointer of the lane moved to
+// another in-pass position.  5 vector + 3 scalar instructions per pointer and round (the
+// compiler's version: ~9 and ~3, plus a register rotation of the 8 pointers every round); a
+// read's address register takes its result (8 VGPRs fewer: k_lz -1% B).
 #define SBH_CH_ADDR(k) "v_max_u32 %[a" #k "], %[pb], %[c" #k "]\n\t" \
                        "v_lshl_add_u32 %[a" #k "], %[a" #k "], 1, %[off]\n\t" \
-                       "ds_read_u16 %[r" #k "], %[a" #k "]\n\t"
+                       "ds_read_u16 %[a" #k "], %[a" #k "]\n\t"
 #define SBH_CH_STEP(k, w) "s_waitcnt lgkmcnt(" #w ")\n\t" \
                           "v_cmp_le_u32 vcc, %[pb], %[c" #k "]\n\t" \
-                          "v_cmp_ne_u32 %[sx], %[r" #k "], %[c" #k "]\n\t" \
-                          "v_cmp_le_u32 %[sy], %[pb], %[r" #k "]\n\t" \
+                          "v_cmp_ne_u32 %[sx], %[a" #k "], %[c" #k "]\n\t" \
+                          "v_cmp_le_u32 %[sy], %[pb], %[a" #k "]\n\t" \
                           "s_and_b64 %[sx], %[sx], vcc\n\t" \
                           "s_and_b64 %[sx], %[sx], %[sy]\n\t" \
                           "s_or_b64 %[sc], %[sc], %[sx]\n\t" \
-                          "v_cndmask_b32_e32 %[c" #k "], %[c" #k "], %[r" #k "], vcc\n\t"
-  asm volatile(
-      "s_mov_b64 %[sv], exec\n\t"
-      "v_cmp_ne_u32 %[sm], 0, %[pend]\n\t"
-      "s_and_b64 exec, exec, %[sm]\n\t"
-      "s_cbranch_execz L_chend%=\n"
-      "L_round%=:\n\t"
+                          "v_cndmask_b32_e32 %[c" #k "], %[c" #k "], %[a" #k "], vcc\n\t"
+#define SBH_CH_WB(w, k0, k1, k2, k3, k4, k5, k6, k7) \
+  "v_perm_b32 %[a" #k0 "], %[c" #k1 "], %[c" #k0 "], %[sel]\n\t" \
+  "v_perm_b32 %[a" #k1 "], %[c" #k3 "], %[c" #k2 "], %[sel]\n\t" \
+  "v_perm_b32 %[a" #k2 "], %[c" #k5 "], %[c" #k4 "], %[sel]\n\t" \
+  "v_perm_b32 %[a" #k3 "], %[c" #k7 "], %[c" #k6 "], %[sel]\n\t" \
+  "ds_write2_b32 %[" #w "], %[a" #k0 "], %[a" #k1 "] offset1:1\n\t" \
+  "ds_write2_b32 %[" #w "], %[a" #k2 "], %[a" #k3 "] offset0:2 offset1:3\n\t"
+#define SBH_CH_HEAD "s_mov_b64 %[sv], exec\n\t" \
+                    "v_cmp_ne_u32 %[sm], 0, %[pend]\n\t" \
+                    "s_and_b64 exec, exec, %[sm]\n\t" \
+                    "s_cbranch_execz L_chend%=\n" \
+                    "L_round%=:\n\t"
+#define SBH_CH_TAIL "s_and_b64 exec, exec, %[sc]\n\t" \
+                    "s_cbranch_execnz L_round%=\n" \
+                    "L_chend%=:\n\t" \
+                    "s_mov_b64 exec, %[sv]"
+__device__ __forceinline__ void chase8_asm(uint32_t (&c)[8], uint32_t pend, uint32_t pb, uint32_t off,
+                                           uint32_t w0) {
+  const uint32_t sel = 0x05040100u;  // v_perm: the low halves of two dwords
+  uint32_t a0, a1, a2, a3, a4, a5, a6, a7;
+  uint64_t sv, sm, sx, sy, sc;
+  asm volatile(SBH_CH_HEAD
       SBH_CH_ADDR(0) SBH_CH_ADDR(1) SBH_CH_ADDR(2) SBH_CH_ADDR(3)
       SBH_CH_ADDR(4) SBH_CH_ADDR(5) SBH_CH_ADDR(6) SBH_CH_ADDR(7)
       "s_mov_b64 %[sc], 0\n\t"
       SBH_CH_STEP(0, 7) SBH_CH_STEP(1, 6) SBH_CH_STEP(2, 5) SBH_CH_STEP(3, 4)
       SBH_CH_STEP(4, 3) SBH_CH_STEP(5, 2) SBH_CH_STEP(6, 1) SBH_CH_STEP(7, 0)
-      "v_perm_b32 %[a0], %[c1], %[c0], %[sel]\n\t"
-      "v_perm_b32 %[a1], %[c3], %[c2], %[sel]\n\t"
-      "v_perm_b32 %[a2], %[c5], %[c4], %[sel]\n\t"
-      "v_perm_b32 %[a3], %[c7], %[c6], %[sel]\n\t"
-#if SBH_LZ_ROT
-      "v_cndmask_b32_e64 %[a4], %[a0], %[a2], %[sA]\n\t"
-      "v_cndmask_b32_e64 %[a5], %[a2], %[a0], %[sA]\n\t"
-      "v_cndmask_b32_e64 %[a6], %[a1], %[a3], %[sB]\n\t"
-      "v_cndmask_b32_e64 %[a7], %[a3], %[a1], %[sB]\n\t"
-      "ds_write2_b32 %[waddr], %[a4], %[a5] offset1:2\n\t"
-      "ds_write2_b32 %[wB], %[a6], %[a7] offset1:2\n\t"
-#else
-      "ds_write2_b32 %[waddr], %[a0], %[a1] offset1:1\n\t"
-      "ds_write2_b32 %[waddr], %[a2], %[a3] offset0:2 offset1:3\n\t"
-#endif
-      "s_and_b64 exec, exec, %[sc]\n\t"
-      "s_cbranch_execnz L_round%=\n"
-      "L_chend%=:\n\t"
-      "s_mov_b64 exec, %[sv]"
+      SBH_CH_WB(w0, 0, 1, 2, 3, 4, 5, 6, 7)
+      SBH_CH_TAIL
       : [c0] "+v"(c[0]), [c1] "+v"(c[1]), [c2] "+v"(c[2]), [c3] "+v"(c[3]), [c4] "+v"(c[4]), [c5] "+v"(c[5]),
         [c6] "+v"(c[6]), [c7] "+v"(c[7]), [a0] "=&v"(a0), [a1] "=&v"(a1), [a2] "=&v"(a2), [a3] "=&v"(a3),
-        [a4] "=&v"(a4), [a5] "=&v"(a5), [a6] "=&v"(a6), [a7] "=&v"(a7), [r0] "=&v"(r0), [r1] "=&v"(r1),
-        [r2] "=&v"(r2), [r3] "=&v"(r3), [r4] "=&v"(r4), [r5] "=&v"(r5), [r6] "=&v"(r6), [r7] "=&v"(r7),
+        [a4] "=&v"(a4), [a5] "=&v"(a5), [a6] "=&v"(a6), [a7] "=&v"(a7),
         [sv] "=&s"(sv), [sm] "=&s"(sm), [sx] "=&s"(sx), [sy] "=&s"(sy), [sc] "=&s"(sc)
-      : [pend] "v"(pend), [pb] "s"(pb), [off] "s"(off), [waddr] "v"(waddr), [sel] "s"(sel), [wB] "v"(wB),
-        [sA] "s"(sA), [sB] "s"(sB)
+      : [pend] "v"(pend), [pb] "s"(pb), [off] "s"(off), [w0] "v"(w0), [sel] "s"(sel)
       : "vcc", "scc", "memory");
+}
 #undef SBH_CH_ADDR
 #undef SBH_CH_STEP
-}
+#undef SBH_CH_WB
+#undef SBH_CH_HEAD
+#undef SBH_CH_TAIL
 
 // LZ77 resolution of one block per workgroup, LZ_CHUNK tokens per chunk (LZ_TPT consecutive
 // tokens per thread); bytes before the chunk are final.  A chunk whose output fits PTR_CAP
@@ -2720,6 +2703,15 @@ __global__ __launch_bounds__(LZ_THREADS, 4) void k_lz(const uint8_t *__restrict_
           const bool in = k - klo < khi - klo;
           c[hh][k] = in ? v[k] + (s0 + k - sidx[k]) : g0 + k;
         }
+#elif !SBH_LZ_MOD
+        // byte j of every match points at v + j = its position - distance: inside the match
+        // itself when the match overlaps (j >= distance), which is still an earlier byte of the
+        // same value; the chase follows it
+#pragma unroll
+        for (uint32_t k = 0; k < PTR_HALF; ++k) {
+          const bool in = k - klo < khi - klo;
+          c[hh][k] = in ? v[k] + (s0 + k - sidx[k]) : g0 + k;
+        }
 #else
         uint32_t ovl = 0;  // slots of overlapping matches
 #pragma unroll
@@ -2752,35 +2744,33 @@ __global__ __launch_bounds__(LZ_THREADS, 4) void k_lz(const uint8_t *__restrict_
       // writing shortened pointers back (other threads' chains pass through them); no
       // barriers.  A pointer is final when it is before the pass or names a literal (a
       // slot pointing at itself).  Then gather the bytes and store them.
+      // Plain loads: another thread may rewrite a slot concurrently, and either value (u16 LDS
+      // accesses are single-copy atomic) is a valid pointer.  Rounds are branch-free; settled
+      // slots reread their own final pointer's slot harmlessly.  Each round replaces every
+      // in-pass pointer by the one stored at its target (a final slot -- a literal -- stores
+      // itself, so it stays); a lane stops once no pointer of its own moved to another in-pass
+      // position.
+      auto gather8 = [&](const uint32_t *cp, uint32_t g0) {
+        uint32_t w[2];
+#pragma unroll
+        for (uint32_t q = 0; q < 2; ++q)
+          w[q] = (uint32_t)img[cp[4 * q]] | (uint32_t)img[cp[4 * q + 1]] << 8 | (uint32_t)img[cp[4 * q + 2]] << 16 |
+                 (uint32_t)img[cp[4 * q + 3]] << 24;
+        *reinterpret_cast<uint2 *>(img + g0) = make_uint2(w[0], w[1]);
+      };
+      const uint32_t p16a = (uint32_t)reinterpret_cast<uintptr_t>(p16);
+      [[maybe_unused]] const uint32_t choff = uni(p16a) - 2u * abase;  // LDS address of pointer c: choff + 2 c
 #pragma unroll
       for (uint32_t hh = 0; hh < NHP; ++hh) {
         const uint32_t h = t + hh * LZ_THREADS;
         if (h >= nh) continue;
         const uint32_t g0 = abase + PTR_HALF * h;  // image position of the half granule
-#if SBH_LZ_ROT
-        const uint32_t rr = (h >> 3) & 3u;  // register k holds slot (k + 2 rr) & 7
-        rot8(c[hh], rr);
-        const uint32_t wbase = (uint32_t)reinterpret_cast<uintptr_t>(p16) + 16u * h;
-        const uint32_t wA = wbase + 4u * (rr & 1u), wB = wbase + 4u * ((rr + 1u) & 1u);
-        const uint64_t sA = __ballot((rr & 2u) != 0), sB = __ballot(((rr + 1u) & 2u) != 0);
-#else
-        const uint32_t wA = (uint32_t)reinterpret_cast<uintptr_t>(p16) + 16u * h, wB = wA;
-        const uint64_t sA = 0, sB = 0;
-#endif
-        // Plain loads: another thread may rewrite a slot concurrently, and either value
-        // (u16 LDS accesses are single-copy atomic) is a valid pointer.  Rounds are
-        // branch-free; settled slots reread their own final pointer's slot harmlessly.
 #ifdef SBH_LZ_DEBUG
         uint32_t guard = 0;
 #endif
-        // Each round replaces every in-pass pointer by the one stored at its target (a
-        // final slot -- a literal -- stores itself, so it stays); a lane stops once no
-        // pointer of its own moved to another in-pass position.
 #if SBH_ASM_CHASE && !defined(SBH_LZ_DEBUG) && !defined(SBH_LZ_PROBE)
-        chase8_asm(c[hh], pend[hh], pb, uni((uint32_t)reinterpret_cast<uintptr_t>(p16)) - 2u * abase, wA, wB, sA,
-                   sB);
+        chase8_asm(c[hh], pend[hh], pb, choff, p16a + 16u * h);
 #else
-        (void)wA, (void)wB, (void)sA, (void)sB;
         bool more = pend[hh] != 0;
         while (__builtin_expect(more, 0)) {
 #ifdef SBH_LZ_DEBUG
@@ -2806,32 +2796,10 @@ __global__ __launch_bounds__(LZ_THREADS, 4) void k_lz(const uint8_t *__restrict_
           }
           // write back: settled and shortened pointers alike (literal and out-of-pass
           // slots keep pointing at themselves)
-#if SBH_LZ_ROT
-          uint32_t lc[PTR_HALF];
-#pragma unroll
-          for (uint32_t k = 0; k < PTR_HALF; ++k) lc[k] = c[hh][k];
-          rot8(lc, (4u - rr) & 3u);  // back to slot order
-          reinterpret_cast<uint4 *>(p16)[h] = pack8_u16(lc);
-#else
           reinterpret_cast<uint4 *>(p16)[h] = pack8_u16(c[hh]);
-#endif
         }
 #endif
-        uint32_t w[2];
-#pragma unroll
-        for (uint32_t q = 0; q < 2; ++q) {
-          w[q] = (uint32_t)img[c[hh][4 * q]] | (uint32_t)img[c[hh][4 * q + 1]] << 8 |
-                 (uint32_t)img[c[hh][4 * q + 2]] << 16 | (uint32_t)img[c[hh][4 * q + 3]] << 24;
-        }
-#if SBH_LZ_ROT
-        {  // byte k holds slot (k + 2 rr) & 7: rotate the 8 bytes left by 16 rr bits
-          const uint32_t m1 = 0u - (rr & 1u), m2 = 0u - ((rr >> 1) & 1u);
-          const uint32_t x0 = (w[1] & m2) | (w[0] & ~m2), x1 = (w[0] & m2) | (w[1] & ~m2);
-          w[0] = (__builtin_amdgcn_alignbit(x0, x1, 16) & m1) | (x0 & ~m1);
-          w[1] = (__builtin_amdgcn_alignbit(x1, x0, 16) & m1) | (x1 & ~m1);
-        }
-#endif
-        *reinterpret_cast<uint2 *>(img + g0) = make_uint2(w[0], w[1]);
+        gather8(c[hh], g0);
       }
 #ifdef SBH_LZ_PROBE
       t_ch += __builtin_readcyclecounter() - tc;
