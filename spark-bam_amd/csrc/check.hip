@@ -853,7 +853,7 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
 #ifdef SBH_EPROBE
     c4 = __builtin_readcyclecounter();
 #endif
-    if (o.tsum) {
+    if (SBH_TSUM_CODE && o.tsum) {
       // each wave's quarter of the tile (EAGER_SUB positions, its lanes' result words): each true
       // position's record step (its length field, staged) against the next true position of the
       // quarter; the last one's step for k_verify_chain_w.  Wave-local: no barrier.
@@ -990,7 +990,7 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
     if (lane == 0 && wt)
       atomicAdd(o.true_spread + ((blockIdx.x * NWV + wid) % TRUE_SLOTS) * TRUE_STRIDE, (unsigned long long)wt);
   }
-  if (o.tsum && !fast && lane == 0)  // (the fallback path leaves no summaries)
+  if (SBH_TSUM_CODE && o.tsum && !fast && lane == 0)  // (the fallback path leaves no summaries)
     o.tsum[blockIdx.x * NWV + wid] = TileSum{TS_DIRTY, 0, ~0u};
 #ifdef SBH_EPROBE
   __shared__ uint32_t psurv, pcand, pexact, ntrue;
@@ -1655,9 +1655,6 @@ __global__ __launch_bounds__(256) void k_first_set(const uint32_t *bits, uint64_
 // of the next non-empty lane (a readlane), and only the wave's last one looks past the
 // wave -- the whole wave scanning 64 words per step -- so each set bit costs one bitmap
 // load and one U load, and sparse bitmaps (long records) no longer scan word by word.
-#ifndef SBH_TSUM_CODE
-#define SBH_TSUM_CODE 1  // (A/B: 0 compiles the summaries' branches out of k_verify_chain_w)
-#endif
 __global__ __launch_bounds__(256) void k_verify_chain_w(const uint8_t *U, const uint32_t *bits, uint64_t begin,
                                                          uint64_t bits_end, uint64_t from, uint64_t E, uint64_t total,
                                                          unsigned long long *n_anom, unsigned long long *first_anom,

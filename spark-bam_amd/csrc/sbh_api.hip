@@ -284,7 +284,21 @@ int sbh_ctx_create(int device, sbh_ctx **out) {
   if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return SBH_E_HIP;
   sbh_ctx *c = new sbh_ctx();
   c->device = device;
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipSetDevice(device) != hipSuccess) {
+    delete c;
+    return SBH_E_HIP;
+  }
+  // SBH_SCHED=spin|yield|block: how a host thread waits in hipStreamSynchronize (the path's
+  // host round trips -- index sizes, block table, statuses -- each leave the GPU idle until the
+  // host thread wakes); unset: the runtime's default
+  if (const char *e = std::getenv("SBH_SCHED")) {
+    const unsigned f = !std::strcmp(e, "spin")    ? hipDeviceScheduleSpin
+                       : !std::strcmp(e, "yield") ? hipDeviceScheduleYield
+                       : !std::strcmp(e, "block") ? hipDeviceScheduleBlockingSync
+                                                  : hipDeviceScheduleAuto;
+    (void)hipSetDeviceFlags(f);
+  }
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return SBH_E_HIP;
   }
@@ -789,7 +803,7 @@ static uint64_t xq_cap() {
 // default: measured (r04g, config B) the proof 0.46 -> 0.36 ms per step but k_eager 3.00 -> 3.24 ms.
 static bool tsum_on() {
   const char *e = std::getenv("SBH_TSUM");
-  return e && e[0] == '1';
+  return SBH_TSUM_CODE && e && e[0] == '1';
 }
 
 static int eager_range(sbh_shard *sh, uint64_t begin, uint64_t end, int32_t rtc, uint64_t *n_true) {

@@ -86,6 +86,13 @@ constexpr uint32_t INF_SERIAL = 0xffu; // (inside inflate only) left to the seri
 constexpr uint64_t EAGER_TILE = SBH_ETILE;
 constexpr uint64_t EAGER_REACH = SBH_ETILE + 4096 + 512 + 64;
 constexpr uint64_t EAGER_SUB = EAGER_TILE / 4;  // one k_eager wave's share of a tile (4 waves)
+#ifndef SBH_TSUM_CODE
+// 1: compile the per-quarter-tile chain summaries (k_eager writes them, k_verify_chain_w reads
+// them; SBH_TSUM=1 at run time turns them on).  0 (default): measured net slower (proof 0.46 ->
+// 0.36 ms, k_eager 3.00 -> 3.24 ms per config-B step), and their branches alone cost the proof
+// 0.34 -> 0.42 ms with the summaries off (r04q kernel trace).
+#define SBH_TSUM_CODE 0
+#endif
 // Per quarter of an eager tile (EAGER_SUB positions, one k_eager wave's result words; written on
 // k_eager's fast path; the chain proof, k_verify_chain_w, reads it instead of every true
 // position's record length): the record step of the quarter's last true position, and the true
