@@ -2385,7 +2385,10 @@ constexpr uint32_t LZ_LMARK_MIN = SBH_LZ_LMARK_MIN;
 // 2 ((h >> 3) & 3) slots so the chase's u16 reads of lanes h, h + 8, h + 16, h + 24 (16 bytes
 // apart, one bank) hit four distinct dwords: k_lz +5% B, +4% D, +2.5% E; a thread's two half
 // granules chased in one loop (16 reads per round, a single-granule thread chasing a copy):
-// +17% B, +19% D, +17% E; the slot pass's two half granules as one straight-line body: +30% B;
+// +17% B, +19% D, +17% E, and only in the waves that have two (waves 0-3): +10% B, +8% D, +7% E
+// (chasing the lower granule first shortens the chains of the higher one); the slot pass's two
+// half granules as one straight-line body: +30% B; an all-literal half granule skipping its
+// gather: +3% B;
 // 1024-token chunks (SBH_LZ_TPT=2): +10% B, +6% D.  Each variant that added LDS instructions or
 // VALU work per byte lost more than the latency it overlapped or the conflicts it removed.)
 
