@@ -279,11 +279,14 @@ __global__ void k_mark_u64(const uint8_t *on, uint64_t *v, uint64_t nc) {
 }
 
 // Emit the chain as the block table (ordered by position).
+// (usz is zero beyond the chain, so the flat-offset scan may run over all nc entries; the chain
+// length is the last rank plus the last mark, read here rather than by the host)
 __global__ void k_chain_emit(const uint8_t *comp, uint64_t n, const uint64_t *cand, const uint8_t *on,
-                             const uint64_t *rank, uint64_t nc, DevBlocks bl,
-                             uint64_t *usz, uint64_t nchain, uint8_t *next18) {
+                             const uint64_t *rank, const uint64_t *v, uint64_t nc, DevBlocks bl,
+                             uint64_t *usz, uint8_t *next18) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nc || !on[i]) return;
+  const uint64_t nchain = rank[nc - 1] + v[nc - 1];
   const uint64_t r = rank[i];
   const uint64_t p = cand[i];
   const uint32_t xlen = u16_at(comp, p + 10);
@@ -379,9 +382,10 @@ hipError_t launch_cand_write(const uint8_t *comp, uint64_t n, uint64_t from, con
   return hipGetLastError();
 }
 
-// Build the chain from cand[0] over nc candidates.  Scratch: J0, J1 (int64 x nc),
-// on (u8 x nc), v/rank (u64 x nc each), tmp (scan).  Writes the block table and
-// usz (u64 per block); returns the block count via *nchain (host).
+// Build the chain from the candidate at start_rel over nc candidates.  Scratch: J0, J1 (int64 x
+// nc), on (u8 x nc), v/rank (u64 x nc each), tmp (scan).  Writes the block table and usz (u64
+// per block, zero past the chain); the block count is rank[nc - 1] + v[nc - 1] (no host round
+// trip here: the caller copies those two words back with the block table).
 hipError_t launch_pack_blocks(DevBlocks bl, uint64_t n, uint64_t file_off, uint64_t *out, hipStream_t st) {
   if (n) hipLaunchKernelGGL(k_pack_blocks, dim3(nblk(n, 256)), dim3(256), 0, st, bl, n, file_off, out);
   return hipGetLastError();
@@ -389,12 +393,12 @@ hipError_t launch_pack_blocks(DevBlocks bl, uint64_t n, uint64_t file_off, uint6
 
 hipError_t build_chain(const uint8_t *comp, uint64_t n, const uint64_t *cand, uint64_t nc, uint64_t start_rel,
                        int64_t *J0, int64_t *J1, uint8_t *on, uint64_t *v, uint64_t *rank, uint64_t *tmp,
-                       DevBlocks bl, uint64_t *usz, uint64_t *nchain, uint8_t *next18, hipStream_t st) {
-  *nchain = 0;
+                       DevBlocks bl, uint64_t *usz, uint8_t *next18, hipStream_t st) {
   if (nc == 0) return hipSuccess;
   const uint32_t T = 256;
   hipLaunchKernelGGL(k_cand_link, dim3(nblk(nc, T)), dim3(T), 0, st, comp, n, cand, nc, J0);
   hipError_t e = hipMemsetAsync(on, 0, nc, st);
+  if (e == hipSuccess) e = hipMemsetAsync(usz, 0, nc * sizeof(uint64_t), st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_mark_start, dim3(1), dim3(64), 0, st, cand, nc, start_rel, on);
   int64_t *a = J0, *b = J1;
@@ -409,16 +413,8 @@ hipError_t build_chain(const uint8_t *comp, uint64_t n, const uint64_t *cand, ui
   hipLaunchKernelGGL(k_mark_u64, dim3(nblk(nc, T)), dim3(T), 0, st, on, v, nc);
   e = scan_exclusive_u64(v, rank, nc, tmp, st);
   if (e != hipSuccess) return e;
-  uint64_t last_rank = 0, last_v = 0;
-  e = hipMemcpyAsync(&last_rank, rank + nc - 1, 8, hipMemcpyDeviceToHost, st);
-  if (e != hipSuccess) return e;
-  e = hipMemcpyAsync(&last_v, v + nc - 1, 8, hipMemcpyDeviceToHost, st);
-  if (e != hipSuccess) return e;
-  e = hipStreamSynchronize(st);
-  if (e != hipSuccess) return e;
-  *nchain = last_rank + last_v;
-  hipLaunchKernelGGL(k_chain_emit, dim3(nblk(nc, T)), dim3(T), 0, st, comp, n, cand, on, rank, nc, bl,
-                     usz, *nchain, next18);
+  hipLaunchKernelGGL(k_chain_emit, dim3(nblk(nc, T)), dim3(T), 0, st, comp, n, cand, on, rank, v, nc, bl, usz,
+                     next18);
   return hipGetLastError();
 }
 

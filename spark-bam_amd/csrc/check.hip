@@ -1659,7 +1659,13 @@ __global__ __launch_bounds__(256) void k_verify_chain_w(const uint8_t *U, const 
                                                          uint64_t bits_end, uint64_t from, uint64_t E, uint64_t total,
                                                          unsigned long long *n_anom, unsigned long long *first_anom,
                                                          unsigned long long *exit_pos, unsigned long long *n_set,
-                                                         const TileSum *tsum) {
+                                                         const TileSum *tsum, const unsigned long long *from_dev) {
+  // from_dev: the chain's first record as another kernel left it on the device (k_first_set's
+  // answer; ~0: none, nothing to prove)
+  if (from_dev) {
+    from = *from_dev;
+    if (from >= E) return;
+  }
   const uint32_t lane = threadIdx.x & (WAVE - 1);
   constexpr uint32_t TWORDS = EAGER_SUB / 32;  // bitmap words per summarised quarter tile (from `begin`)
   const uint64_t W0 = (from - begin) / 32 & ~3ull;
@@ -2160,12 +2166,13 @@ hipError_t launch_first_set(const uint32_t *bits, uint64_t begin, uint64_t from,
 hipError_t launch_verify_chain_count(const uint8_t *U, const uint32_t *bits, uint64_t begin, uint64_t bits_end,
                                      uint64_t from, uint64_t E, uint64_t total, unsigned long long *n_anom,
                                      unsigned long long *first_anom, unsigned long long *exit_pos,
-                                     unsigned long long *n_set, const TileSum *tsum, hipStream_t st) {
-  if (E <= from) return hipSuccess;
+                                     unsigned long long *n_set, const TileSum *tsum, hipStream_t st,
+                                     const unsigned long long *from_dev) {
+  if (E <= from) return hipSuccess;  // (with from_dev: from is a lower bound of *from_dev)
   const uint64_t nw = (E - begin + 31) / 32 - ((from - begin) / 32 & ~3ull);
   const uint32_t grid = (uint32_t)std::min<uint64_t>(ngrid(nw, 1024), 2048);
   hipLaunchKernelGGL(k_verify_chain_w, dim3(grid), dim3(256), 0, st, U, bits, begin, bits_end, from, E, total,
-                     n_anom, first_anom, exit_pos, n_set, tsum);
+                     n_anom, first_anom, exit_pos, n_set, tsum, from_dev);
   return hipGetLastError();
 }
 

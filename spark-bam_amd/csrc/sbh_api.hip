@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -54,8 +55,8 @@ hipError_t launch_cand_write(const uint8_t *comp, uint64_t n, uint64_t from, con
                              hipStream_t st);
 hipError_t launch_pack_blocks(DevBlocks bl, uint64_t n, uint64_t file_off, uint64_t *out, hipStream_t st);
 hipError_t build_chain(const uint8_t *comp, uint64_t n, const uint64_t *cand, uint64_t nc, uint64_t start_rel,
-                       int64_t *J0, int64_t *J1, uint8_t *on, uint64_t *v, uint64_t *rank, uint64_t *tmp, DevBlocks bl,
-                       uint64_t *usz, uint64_t *nchain, uint8_t *next18, hipStream_t st);
+                       int64_t *J0, int64_t *J1, uint8_t *on, uint64_t *v, uint64_t *rank, uint64_t *tmp,
+                       DevBlocks bl, uint64_t *usz, uint8_t *next18, hipStream_t st);
 hipError_t launch_eager(const uint8_t *U, uint64_t u_pad, uint64_t begin, uint64_t end, const uint64_t *seg_end,
                         uint32_t nseg, uint32_t open_last, const int32_t *ctg, int32_t nctg, int32_t rtc,
                         uint32_t *bits, unsigned long long *counters, hipStream_t st, uint64_t front,
@@ -76,7 +77,8 @@ hipError_t launch_first_set(const uint32_t *bits, uint64_t begin, uint64_t from,
 hipError_t launch_verify_chain_count(const uint8_t *U, const uint32_t *bits, uint64_t begin, uint64_t bits_end,
                                      uint64_t from, uint64_t E, uint64_t total, unsigned long long *n_anom,
                                      unsigned long long *first_anom, unsigned long long *exit_pos,
-                                     unsigned long long *n_set, const TileSum *tsum, hipStream_t st);
+                                     unsigned long long *n_set, const TileSum *tsum, hipStream_t st,
+                                     const unsigned long long *from_dev = nullptr);
 hipError_t launch_chain_walk(const uint8_t *U, uint64_t first, uint64_t E, uint64_t total,
                              unsigned long long *count, unsigned long long *last, hipStream_t st);
 }  // namespace sbh
@@ -150,7 +152,8 @@ struct sbh_shard {
   DBuf<int32_t> ctg;
   int32_t nctg = -1;
   DBuf<uint32_t> bits;
-  DBuf<TileSum> tsum;  // per quarter eager tile of bits (from bits_begin): the chain proof's summaries
+  DBuf<TileSum> tsum;
+  bool pipe_fallback = false;  // run_pipelined redid the eager pass (a deferral overflow)  // per quarter eager tile of bits (from bits_begin): the chain proof's summaries
   // chain marking (pointer doubling) over the set bits of [cm_first, cm_E) when the bitmap
   // is not the chain: node positions, per-word prefix counts, jumps, marks and their prefix
   DBuf<uint64_t> cm_pos, cm_wcnt, cm_wpre, cm_mark, cm_mpre;
@@ -534,21 +537,28 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
     HIPCHK(ctx, sh->b_status.ensure(nc));
     HIPCHK(ctx, sh->b_ntok.ensure(nc));
     HIPCHK(ctx, build_chain(sh->comp.p, n, sh->cand.p, nc, rel, sh->J0.p, sh->J1.p, sh->on.p, sh->v.p, sh->rank.p,
-                            sh->tmp.p, sh->dev_blocks(), sh->usz.p, &nchain, next18_dev, st));
-    HIPCHK(ctx, scan_exclusive_u64(sh->usz.p, sh->b_ustart.p, nchain, sh->tmp.p, st));
+                            sh->tmp.p, sh->dev_blocks(), sh->usz.p, next18_dev, st));
+    // flat offsets over all nc entries (usz is zero past the chain); the chain length comes back
+    // with the block table, so the table is packed and copied for all nc candidates and cut after
+    HIPCHK(ctx, scan_exclusive_u64(sh->usz.p, sh->b_ustart.p, nc, sh->tmp.p, st));
   }
   sh->ncand = nc;
   sh->cand_from = srel;
   // host copy of the block table (Pos mapping, segments)
   static_assert(sizeof(sbh_block) == 32, "k_pack_blocks writes 32-byte sbh_block records");
-  sh->hb.resize(nchain);
-  if (nchain) {
-    HIPCHK(ctx, sh->blkpack.ensure(4 * nchain));
-    HIPCHK(ctx, launch_pack_blocks(sh->dev_blocks(), nchain, sh->file_off, sh->blkpack.p, st));
-    HIPCHK(ctx, hipMemcpyAsync(sh->hb.data(), sh->blkpack.p, nchain * 32, hipMemcpyDeviceToHost, st));
+  sh->hb.resize(nc);
+  if (nc) {
+    unsigned long long *lastw = sh->h_ctr + 540;  // pinned: rank[nc - 1], v[nc - 1]
+    HIPCHK(ctx, sh->blkpack.ensure(4 * nc));
+    HIPCHK(ctx, launch_pack_blocks(sh->dev_blocks(), nc, sh->file_off, sh->blkpack.p, st));
+    HIPCHK(ctx, hipMemcpyAsync(sh->hb.data(), sh->blkpack.p, nc * 32, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(lastw, sh->rank.p + nc - 1, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(lastw + 1, sh->v.p + nc - 1, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipMemcpyAsync(nx, next18_dev, 18, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipStreamSynchronize(st));
+    nchain = lastw[0] + lastw[1];
   }
+  sh->hb.resize(nchain);
   // stream end: a truncated last block is not part of the resident stream
   sh->open_last = !sh->at_eof;
   sh->broken_end = false;
@@ -1373,7 +1383,11 @@ static hipEvent_t pev(sbh_shard *sh, size_t i) {
   return sh->pev[i];
 }
 
-static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_true) {
+// pre_sync (optional): more work enqueued on the main stream after the eager kernels and before
+// the one host round trip that brings back the inflate status and the eager counters (its
+// results are only meaningful when this returns SBH_OK without a fallback)
+static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_true,
+                         const std::function<hipError_t(hipStream_t)> &pre_sync = nullptr) {
   sbh_ctx *ctx = sh->ctx;
   if (!sh->indexed) return fail(ctx, SBH_E_STATE, "inflate before index");
   if (sh->nctg < 0) return fail(ctx, SBH_E_STATE, "contig lengths not set");
@@ -1396,6 +1410,7 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
   HIPCHK(ctx, hipMemsetAsync(c, 0, 48, sa));
   HIPCHK(ctx, hipMemsetAsync(c + 2, 0xff, 8, sa));
   sh->inflated = sh->bits_valid = sh->chain_ok = sh->cm_valid = false;
+  sh->pipe_fallback = false;
   const uint64_t nbat = P.batches.size();
   // events: per batch [huff start, huff end, lz start, lz end, eager start, eager end]
   for (size_t i = 0; i < 6 * nbat + 4; ++i)
@@ -1450,6 +1465,7 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
   HIPCHK(ctx, hipEventRecord(ev[6 * nbat + 3], se));
   HIPCHK(ctx, hipEventRecord(ev[6 * nbat + 1], se));
   HIPCHK(ctx, hipStreamWaitEvent(sa, ev[6 * nbat + 1], 0));
+  if (pre_sync) HIPCHK(ctx, pre_sync(sa));
   {
     const int rs = inflate_status(sh, sa, nullptr, c, sh->h_ctr, 48);
     if (rs) return rs;
@@ -1472,7 +1488,10 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
   if (std::getenv("SBH_XQ_DEBUG"))
     fprintf(stderr, "[sbh] eager: deferred %llu, long-record queue %llu (%llu past the pre-test)\n", sh->h_ctr[3],
             sh->h_ctr[4], sh->h_ctr[5]);
-  if (sh->h_ctr[3] > DEFER_CAP) return eager_range(sh, 0, E, rtc, n_true);  // deferral overflow: plain pass
+  if (sh->h_ctr[3] > DEFER_CAP) {  // deferral overflow: plain pass
+    sh->pipe_fallback = true;
+    return eager_range(sh, 0, E, rtc, n_true);
+  }
   sh->bits_valid = true;
   sh->bits_begin = 0;
   sh->bits_end = E;
@@ -1510,20 +1529,69 @@ int sbh_run_shard(sbh_shard *sh, uint64_t index_start, uint64_t own_end_file, in
   res->comp_bytes = cbytes;
   res->flat_bytes = E;
   mark(sh, 2);
-  rc = run_pipelined(sh, E, rtc, &res->n_true);
+  // The step's tail rides in the inflate-status round trip: FindRecordStart from flat 0 (the
+  // first set bit of the verified bitmap below min(segment end, maxReadSize, E)) and the chain
+  // proof from that record, which k_verify_chain_w reads from the device.  The answers are taken
+  // when the record lies in the first segment and the bitmap is exactly the chain; anything else
+  // (no bit found, an anomaly, a fallback inside run_pipelined) goes the long way below, as
+  // sbh_find_record_start and count_records_impl would on their own.
+  const uint64_t total0 = sh->seg_end.empty() ? 0 : sh->seg_end[0];
+  const uint64_t hi0 = std::min(std::min<uint64_t>(total0, (uint64_t)std::max(mrs, 0)), E);
+  const uint64_t E0 = std::min(E, total0);
+  unsigned long long *tbest = sh->ctr.p + 8, *tc = sh->ctr.p + 16;
+  bool tail = rtc >= 0 && hi0 > 0;
+  auto tail_launch = [&](hipStream_t s) -> hipError_t {
+    unsigned long long *init = sh->h_ctr + 600;  // pinned: anomalies, first anomaly, set bits, exit
+    init[0] = 0;
+    init[1] = ~0ull;
+    init[2] = 0;
+    init[3] = ~0ull;
+    hipError_t e = hipMemsetAsync(tbest, 0xff, 8, s);
+    if (e == hipSuccess) e = launch_first_set(sh->bits.p, 0, 0, hi0, tbest, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(tc, init, 32, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+      e = launch_verify_chain_count(sh->U.p, sh->bits.p, 0, E, 0, E0, total0, tc, tc + 1, tc + 3, tc + 2, nullptr, s,
+                                    tbest);
+    if (e == hipSuccess) e = hipMemcpyAsync(sh->h_ctr + 8, tbest, 8, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(sh->h_ctr + 16, tc, 32, hipMemcpyDeviceToHost, s);
+    return e;
+  };
+  rc = tail ? run_pipelined(sh, E, rtc, &res->n_true, tail_launch) : run_pipelined(sh, E, rtc, &res->n_true);
   mark(sh, 5);
   if (rc) { sh->timing = false; return res->status = rc; }
+  // (a deferral overflow re-ran the eager pass inside run_pipelined: the bitmap is new)
+  tail = tail && sh->bits_valid && sh->bits_begin == 0 && sh->bits_end == E && sh->bits_rtc == rtc &&
+         !sh->pipe_fallback;
   uint64_t first = 0;
   int32_t delta = 0;
-  rc = sbh_find_record_start(sh, 0, rtc, mrs, &first, &delta);
-  if (rc == SBH_E_NO_READ_FOUND) {
-    res->count = 0;
+  if (tail && sh->h_ctr[8] != ~0ull) {
+    first = sh->h_ctr[8];
     rc = SBH_OK;
-  } else if (rc == SBH_OK) {
-    rc = count_records_impl(sh, first, E, &res->count, &res->anomalies, &res->exit_flat);
+    if (first < E0 && sh->h_ctr[16] == 0 && sh->h_ctr[19] != ~0ull) {  // count_records_impl's proof, done
+      sh->cm_valid = false;
+      sh->chain_ok = true;
+      sh->chain_first = first;
+      sh->chain_E = E0;
+      res->count = sh->h_ctr[18];
+      res->anomalies = 0;
+      res->exit_flat = sh->h_ctr[19];
+    } else {
+      rc = count_records_impl(sh, first, E, &res->count, &res->anomalies, &res->exit_flat);
+    }
     uint64_t bp = 0;
     uint32_t off = 0;
     if (!rc && sbh_pos_of(sh, first, &bp, &off) == SBH_OK) res->first_vpos = (bp << 16) | off;
+  } else {
+    rc = sbh_find_record_start(sh, 0, rtc, mrs, &first, &delta);
+    if (rc == SBH_E_NO_READ_FOUND) {
+      res->count = 0;
+      rc = SBH_OK;
+    } else if (rc == SBH_OK) {
+      rc = count_records_impl(sh, first, E, &res->count, &res->anomalies, &res->exit_flat);
+      uint64_t bp = 0;
+      uint32_t off = 0;
+      if (!rc && sbh_pos_of(sh, first, &bp, &off) == SBH_OK) res->first_vpos = (bp << 16) | off;
+    }
   }
   if (res->count == 0) res->exit_flat = E;
   mark(sh, 6);
