@@ -2387,7 +2387,9 @@ constexpr uint32_t LZ_LMARK_MIN = SBH_LZ_LMARK_MIN;
 // granules chased in one loop (16 reads per round, a single-granule thread chasing a copy):
 // +17% B, +19% D, +17% E, and only in the waves that have two (waves 0-3): +10% B, +8% D, +7% E
 // (chasing the lower granule first shortens the chains of the higher one); the slot pass's two
-// half granules as one straight-line body: +30% B; an all-literal half granule skipping its
+// half granules as one straight-line body: +30% B, and only in the waves that have two, every
+// LDS read of both issued before either is waited for: +5% B, +3.5% D (the slot pass's time did
+// not move: not its round trips); an all-literal half granule skipping its
 // gather: +3% B;
 // 1024-token chunks (SBH_LZ_TPT=2): +10% B, +6% D.  Each variant that added LDS instructions or
 // VALU work per byte lost more than the latency it overlapped or the conflicts it removed.)
