@@ -2378,6 +2378,9 @@ constexpr uint32_t LZ_LMARK_MIN = SBH_LZ_LMARK_MIN;
 #ifndef SBH_LZ_OVL_WAVE
 #define SBH_LZ_OVL_WAVE 0  // 1: overlapping short matches (dist < len) marked byte by byte by the wave (A/B r04c: k_lz +5% B, +26% D, +10% E: kept off)
 #endif
+#ifndef SBH_LZ_NOCLAMP
+#define SBH_LZ_NOCLAMP 1  // the chase reads settled pointers' slots unclamped: one VALU + one SALU fewer per pointer (A/B r04v: k_lz -2.7% B, -2.8% D, -3.4% E)
+#endif
 #ifndef SBH_LZ_MOD
 #define SBH_LZ_MOD 1  // 1: a byte of an overlapping short match points at v + (j mod distance) (0: at v + j, a longer chase: A/B r04p k_lz +4% B, +2% D)
 #endif
@@ -2390,17 +2393,33 @@ constexpr uint32_t LZ_LMARK_MIN = SBH_LZ_LMARK_MIN;
 // half granules as one straight-line body: +30% B, and only in the waves that have two, every
 // LDS read of both issued before either is waited for: +5% B, +3.5% D (the slot pass's time did
 // not move: not its round trips); an all-literal half granule skipping its
-// gather: +3% B;
+// gather: +3% B; the slot pass without its range test in waves wholly inside the pass: +0.7% B,
+// -1% E; one pending flag per half granule instead of a bit per slot: +0.6% B, -4% E;
 // 1024-token chunks (SBH_LZ_TPT=2): +10% B, +6% D.  Each variant that added LDS instructions or
 // VALU work per byte lost more than the latency it overlapped or the conflicts it removed.)
 
 // k_lz's pointer chase for one half granule (8 slots) as hand-written code, the same rounds as
 // the C++ loop: every pointer at or past the pass start pb is replaced by its target's slot
-// value (u16 LDS reads at 2 * max(c, pb) + p16 - 2 * abase, all 8 issued before the first is
+// value (u16 LDS reads at 2 c + p16 - 2 * abase, all 8 issued before the first is
 // waited for), the 8 slots written back as 16 bytes at w0, until no pointer of the lane moved to
-// another in-pass position.  5 vector + 3 scalar instructions per pointer and round (the
-// compiler's version: ~9 and ~3, plus a register rotation of the 8 pointers every round); a
-// read's address register takes its result (8 VGPRs fewer: k_lz -1% B).
+// another in-pass position.  4 vector + 2 scalar instructions per pointer and round besides
+// the read (SBH_LZ_NOCLAMP; the compiler's version: ~9 and ~3, plus a register rotation of the
+// 8 pointers every round); a read's address register takes its result (8 VGPRs fewer: k_lz -1% B).
+#if SBH_LZ_NOCLAMP
+// (no clamp to the pass start: a settled pointer c < pb reads whatever LDS word 2 c + off names
+// -- the image below the slots, or nothing (an out-of-range LDS read returns 0) -- and the
+// value is dropped: c moves only when pb <= c.  A pointer moves on in the pass when
+// pb <= r < c: slot values never exceed their slot, so r != c is r < c)
+#define SBH_CH_ADDR(k) "v_lshl_add_u32 %[a" #k "], %[c" #k "], 1, %[off]\n\t" \
+                       "ds_read_u16 %[a" #k "], %[a" #k "]\n\t"
+#define SBH_CH_STEP(k, w) "s_waitcnt lgkmcnt(" #w ")\n\t" \
+                          "v_cmp_le_u32 vcc, %[pb], %[c" #k "]\n\t" \
+                          "v_cmp_lt_u32 %[sx], %[a" #k "], %[c" #k "]\n\t" \
+                          "v_cmp_le_u32 %[sy], %[pb], %[a" #k "]\n\t" \
+                          "s_and_b64 %[sx], %[sx], %[sy]\n\t" \
+                          "s_or_b64 %[sc], %[sc], %[sx]\n\t" \
+                          "v_cndmask_b32_e32 %[c" #k "], %[c" #k "], %[a" #k "], vcc\n\t"
+#else
 #define SBH_CH_ADDR(k) "v_max_u32 %[a" #k "], %[pb], %[c" #k "]\n\t" \
                        "v_lshl_add_u32 %[a" #k "], %[a" #k "], 1, %[off]\n\t" \
                        "ds_read_u16 %[a" #k "], %[a" #k "]\n\t"
@@ -2412,6 +2431,7 @@ constexpr uint32_t LZ_LMARK_MIN = SBH_LZ_LMARK_MIN;
                           "s_and_b64 %[sx], %[sx], %[sy]\n\t" \
                           "s_or_b64 %[sc], %[sc], %[sx]\n\t" \
                           "v_cndmask_b32_e32 %[c" #k "], %[c" #k "], %[a" #k "], vcc\n\t"
+#endif
 #define SBH_CH_WB(w, k0, k1, k2, k3, k4, k5, k6, k7) \
   "v_perm_b32 %[a" #k0 "], %[c" #k1 "], %[c" #k0 "], %[sel]\n\t" \
   "v_perm_b32 %[a" #k1 "], %[c" #k3 "], %[c" #k2 "], %[sel]\n\t" \
