@@ -881,7 +881,8 @@ __global__ __launch_bounds__(WAVES *WAVE) void k_huff_serial(const uint8_t *__re
 // Block-wide exclusive prefix sum over NT threads; *total gets the sum.  wsum: NT/64 words.
 template <uint32_t NT>
 __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t *wsum, uint32_t *total) {
-  const uint32_t lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+  // (the wave index through readfirstlane: uniform, so the sums below are scalar work)
+  const uint32_t lane = threadIdx.x & (WAVE - 1), w = uni(threadIdx.x / WAVE);
   const uint32_t x = wave_incl_scan(v);
   if (lane == WAVE - 1) wsum[w] = x;
   __syncthreads();
@@ -900,7 +901,7 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t *wsum, uint3
 // read or written by anything else between two calls' barriers.
 template <uint32_t NT>
 __device__ __forceinline__ uint32_t block_min(uint32_t v, uint32_t *wmin) {
-  const uint32_t lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+  const uint32_t lane = threadIdx.x & (WAVE - 1), w = uni(threadIdx.x / WAVE);
 #pragma unroll
   for (uint32_t off = WAVE / 2; off > 0; off >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, (int)off, WAVE));
   if (lane == 0) wmin[w] = v;
@@ -2381,6 +2382,9 @@ constexpr uint32_t LZ_LMARK_MIN = SBH_LZ_LMARK_MIN;
 #ifndef SBH_LZ_NOCLAMP
 #define SBH_LZ_NOCLAMP 1  // the chase reads settled pointers' slots unclamped: one VALU + one SALU fewer per pointer (A/B r04v: k_lz -2.7% B, -2.8% D, -3.4% E)
 #endif
+#ifndef SBH_LZ_NOHOIST
+#define SBH_LZ_NOHOIST 1  // keep the long-match marker mod inside its branch (see k_lz)
+#endif
 #ifndef SBH_LZ_MOD
 #define SBH_LZ_MOD 1  // 1: a byte of an overlapping short match points at v + (j mod distance) (0: at v + j, a longer chase: A/B r04p k_lz +4% B, +2% D)
 #endif
@@ -2631,7 +2635,13 @@ __global__ __launch_bounds__(LZ_THREADS, 4) void k_lz(const uint8_t *__restrict_
 #endif
         if ((uint32_t)__builtin_popcountll(lm) >= LZ_LMARK_MIN) {
           if (mine) {
-            const uint32_t d0 = off[k] - abase, D = dist[k], L = len[k];
+            uint32_t D = dist[k];
+#if SBH_LZ_NOHOIST
+            // (opaque to the compiler, which otherwise computes the mod below for every token of
+            // every chunk, ahead of this branch: ~36 VALU per chunk and wave)
+            asm volatile("" : "+v"(D));
+#endif
+            const uint32_t d0 = off[k] - abase, L = len[k];
             const bool ov = D < L;
             uint32_t r = 0;  // 32 m mod D (ov)
             const uint32_t r32 = ov ? (D > 32 ? 32 : mod_small(32, D)) : 0;
