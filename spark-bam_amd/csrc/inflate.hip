@@ -2388,12 +2388,7 @@ constexpr uint32_t LZ_LMARK_MIN = SBH_LZ_LMARK_MIN;
 #ifndef SBH_LZ_RUN1
 #define SBH_LZ_RUN1 1  // distance-1 matches point every byte at the source byte (no mod branch)
 #endif
-#ifndef SBH_LZ_OVL2
-#define SBH_LZ_OVL2 0  // 1: (with RUN1) an overlap byte with j < 2 d points one period back, no mod
-#endif
-#ifndef SBH_LZ_POW2
-#define SBH_LZ_POW2 0  // 1: (with RUN1) power-of-two distances take j & (d - 1), no mod
-#endif
+
 #ifndef SBH_LZ_MOD
 #define SBH_LZ_MOD 1  // 1: a byte of an overlapping short match points at v + (j mod distance) (0: at v + j, a longer chase: A/B r04p k_lz +4% B, +2% D)
 #endif
@@ -2408,7 +2403,9 @@ constexpr uint32_t LZ_LMARK_MIN = SBH_LZ_LMARK_MIN;
 // not move: not its round trips); an all-literal half granule skipping its
 // gather: +3% B; the slot pass without its range test in waves wholly inside the pass: +0.7% B,
 // -1% E; one pending flag per half granule instead of a bit per slot: +0.6% B, -4% E; full
-// chunks without the per-token bound tests: +0.3% B, +2.4% D, +1.6% E;
+// chunks without the per-token bound tests: +0.3% B, +2.4% D, +1.6% E; beyond distance 1,
+// overlap bytes with j < 2 d pointed one period back / power-of-two distances by a mask, both
+// without the mod: +5% / +2% B;
 // 1024-token chunks (SBH_LZ_TPT=2): +10% B, +6% D.  Each variant that added LDS instructions or
 // VALU work per byte lost more than the latency it overlapped or the conflicts it removed.)
 
@@ -2763,19 +2760,7 @@ __global__ __launch_bounds__(LZ_THREADS, 4) void k_lz(const uint8_t *__restrict_
         for (uint32_t k = 0; k < PTR_HALF; ++k) {
           const uint32_t j = s0 + k - sidx[k], dd = abase + sidx[k] - v[k];
           const bool in = k - klo < khi - klo;
-#if SBH_LZ_RUN1 && SBH_LZ_OVL2
-          // distance 1 (a run of one byte value): every byte copies the source byte; an overlap
-          // with j < 2 d: one period back (j - d); only j >= 2 d takes the mod below
-          const bool one = dd == 1, ov = in && j != 0 && j >= dd && !one;
-          ovl |= (ov && j >= 2 * dd) ? 1u << k : 0u;
-          c[hh][k] = in ? v[k] + (one ? 0u : ov ? j - dd : j) : g0 + k;
-#elif SBH_LZ_RUN1 && SBH_LZ_POW2
-          // a power-of-two distance (1 included: a run of one byte value): j mod d = j & (d - 1)
-          const uint32_t dm = dd - 1;
-          const bool p2 = (dd & dm) == 0;
-          ovl |= (in && j != 0 && j >= dd && !p2) ? 1u << k : 0u;
-          c[hh][k] = in ? v[k] + (p2 ? j & dm : j) : g0 + k;
-#elif SBH_LZ_RUN1
+#if SBH_LZ_RUN1
           // a match at distance 1 (a run of one byte value): every byte copies its source byte,
           // no mod needed (A/B r04h: k_lz -9.1% B, -6.2% D, -4.6% E)
           const bool one = dd == 1;
