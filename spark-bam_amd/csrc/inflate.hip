@@ -2389,6 +2389,9 @@ constexpr uint32_t LZ_LMARK_MIN = SBH_LZ_LMARK_MIN;
 #define SBH_LZ_RUN1 1  // distance-1 matches point every byte at the source byte (no mod branch)
 #endif
 
+#ifndef SBH_LZ_MOD2
+#define SBH_LZ_MOD2 1  // (with RUN1) overlaps at distance >= 2 chased instead of taking the mod
+#endif
 #ifndef SBH_LZ_MOD
 #define SBH_LZ_MOD 1  // 1: a byte of an overlapping short match points at v + (j mod distance) (0: at v + j, a longer chase: A/B r04p k_lz +4% B, +2% D)
 #endif
@@ -2760,9 +2763,15 @@ __global__ __launch_bounds__(LZ_THREADS, 4) void k_lz(const uint8_t *__restrict_
         for (uint32_t k = 0; k < PTR_HALF; ++k) {
           const uint32_t j = s0 + k - sidx[k], dd = abase + sidx[k] - v[k];
           const bool in = k - klo < khi - klo;
-#if SBH_LZ_RUN1
+#if SBH_LZ_RUN1 && SBH_LZ_MOD2
+          // distance 1 (a run of one byte value): every byte points at the source byte (A/B r04h:
+          // k_lz -9.1% B, -6.2% D, -4.6% E); a longer overlap (d >= 2) keeps v + j, an earlier
+          // byte of the match itself, which the chase follows -- no mod at all (A/B r04m2: k_lz
+          // -6.5% B, -6.4% D, -9.2% E; v + j is position - d, always an earlier byte of equal value)
+          c[hh][k] = in ? v[k] + (dd == 1 ? 0u : j) : g0 + k;
+#elif SBH_LZ_RUN1
           // a match at distance 1 (a run of one byte value): every byte copies its source byte,
-          // no mod needed (A/B r04h: k_lz -9.1% B, -6.2% D, -4.6% E)
+          // no mod needed
           const bool one = dd == 1;
           ovl |= (in && j != 0 && j >= dd && !one) ? 1u << k : 0u;
           c[hh][k] = in ? v[k] + (one ? 0u : j) : g0 + k;
