@@ -283,9 +283,12 @@ def main():
         if kt:
             traffic, traffic_src = kt["hbm_bytes"], tsrc
             traffic_fresh = tj.get("src_hash") == kernel_src_hash()
-            # k_huff's timed stage is launch_huff: the k_hdr header pre-pass, then k_huff
-            if dom == "k_huff" and tj["kernels"].get("k_hdr"):
-                traffic += tj["kernels"]["k_hdr"]["hbm_bytes"]
+            # k_huff's timed stage is launch_huff: the k_hdr header pre-pass, k_huff, the
+            # k_huff_tail finish of deferred final deflate blocks and the serial fallback
+            if dom == "k_huff":
+                for extra in ("k_hdr", "k_huff_tail", "k_huff_serial"):
+                    if tj["kernels"].get(extra):
+                        traffic += tj["kernels"][extra]["hbm_bytes"]
 
     def gbps(nbytes, ms):
         return round(nbytes / (ms * 1e-3) / 1e9, 2) if ms > 0 else None
@@ -411,6 +414,11 @@ def main():
                 "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                 "traffic_source": traffic_src,
                 "traffic_matches_kernels": traffic_fresh,  # collected from these kernel sources (hash)
+                # tools/pmc_collect.sh runs the default workload (config B): for another config the
+                # per-launch bytes are config B's
+                "traffic_workload": "B" if traffic_src and traffic_src != "--traffic" else None,
+                "traffic_same_workload": (args.config == "B") if traffic_src and traffic_src != "--traffic"
+                else None,
                 "alg_bytes_per_step": int(alg_bytes),
                 "alg_units": dom_units,
                 "limiter": limiter_text(dom, dom_ms, traffic),
