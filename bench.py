@@ -281,14 +281,8 @@ def main():
         tj, tsrc = latest_pmc("traffic.json")
         kt = tj["kernels"].get(dom) if tj else None
         if kt:
-            traffic, traffic_src = kt["hbm_bytes"], tsrc
+            traffic, traffic_src = stage_traffic(tj, dom), tsrc
             traffic_fresh = tj.get("src_hash") == kernel_src_hash()
-            # k_huff's timed stage is launch_huff: the k_hdr header pre-pass, k_huff, the
-            # k_huff_tail finish of deferred final deflate blocks and the serial fallback
-            if dom == "k_huff":
-                for extra in ("k_hdr", "k_huff_tail", "k_huff_serial"):
-                    if tj["kernels"].get(extra):
-                        traffic += tj["kernels"][extra]["hbm_bytes"]
 
     def gbps(nbytes, ms):
         return round(nbytes / (ms * 1e-3) / 1e9, 2) if ms > 0 else None
@@ -625,6 +619,18 @@ def latest_pmc(name):
     files = fresh or files
     with open(files[-1]) as fh:
         return json.load(fh), os.path.relpath(files[-1], ROOT)
+
+
+# The launches each timed stage's HIP events bracket: launch_huff is the k_hdr header pre-pass,
+# k_huff, the k_huff_tail finish of deferred final deflate blocks and the serial fallback.
+STAGE_KERNELS = {"k_huff": ("k_hdr", "k_huff", "k_huff_tail", "k_huff_serial")}
+
+
+def stage_traffic(tj, dom):
+    """HBM bytes per launch of the stage timed as `dom`, from a traffic.json (tools/pmc_traffic.py):
+    the sum over the kernels that stage launches that the counter passes saw."""
+    ks = tj["kernels"]
+    return sum(ks[k]["hbm_bytes"] for k in STAGE_KERNELS.get(dom, (dom,)) if ks.get(k))
 
 
 def limiter_text(kernel, ms=None, traffic=None):
