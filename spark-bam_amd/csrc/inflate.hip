@@ -1208,9 +1208,8 @@ __device__ __forceinline__ LaneRun spec_asm(const WaveSmem &t, const uint32_t *s
       "v_and_b32 %[a], 0x3ff, %[bits]\n\t"
       "v_lshl_add_u32 %[a], %[a], 2, %[tselb]\n\t"
       "ds_read_b32 %[e], %[a]\n\t"
-      "v_lshrrev_b32 %[a], 3, %[pos]\n\t"
-      "v_and_b32 %[a], -4, %[a]\n\t"
-      "v_add_u32 %[a], %[stb], %[a]\n\t"
+      "v_lshrrev_b32 %[a], 5, %[pos]\n\t"
+      "v_lshl_add_u32 %[a], %[a], 2, %[stb]\n\t"
       "ds_read_b32 %[nx], %[a]\n\t"
       // while the entry is in flight: token boundary (sA), cut (sC), checkpoint hit (sB)
       "v_cmp_eq_u32 %[sA], 0, %[vt]\n\t"
@@ -1371,9 +1370,8 @@ __device__ __forceinline__ LaneRun redo_asm(const WaveSmem &t, const uint32_t *s
       "v_and_b32 %[a], 0x3ff, %[bits]\n\t"
       "v_lshl_add_u32 %[a], %[a], 2, %[tselb]\n\t"
       "ds_read_b32 %[e], %[a]\n\t"
-      "v_lshrrev_b32 %[a], 3, %[pos]\n\t"
-      "v_and_b32 %[a], -4, %[a]\n\t"
-      "v_add_u32 %[a], %[stb], %[a]\n\t"
+      "v_lshrrev_b32 %[a], 5, %[pos]\n\t"
+      "v_lshl_add_u32 %[a], %[a], 2, %[stb]\n\t"
       "ds_read_b32 %[nx], %[a]\n\t"
       // while the entry is in flight: token boundary (sA), cut (sC), checkpoint hit (sB)
       "v_cmp_eq_u32 %[sA], 0, %[vt]\n\t"
@@ -1529,9 +1527,8 @@ __device__ __forceinline__ void emit_asm(const WaveSmem &t, const uint32_t *stag
       "v_and_b32 %[a], 0x3ff, %[bits]\n\t"
       "v_lshl_add_u32 %[a], %[a], 2, %[tselb]\n\t"
       "ds_read_b32 %[e], %[a]\n\t"
-      "v_lshrrev_b32 %[a], 3, %[pos]\n\t"
-      "v_and_b32 %[a], -4, %[a]\n\t"
-      "v_add_u32 %[a], %[stb], %[a]\n\t"
+      "v_lshrrev_b32 %[a], 5, %[pos]\n\t"
+      "v_lshl_add_u32 %[a], %[a], 2, %[stb]\n\t"
       "ds_read_b32 %[nx], %[a]\n\t"
       // while the entry is in flight: token boundary (sA), cut (sC), checkpoint hit (sB)
       "v_cmp_eq_u32 %[sA], 0, %[vt]\n\t"
