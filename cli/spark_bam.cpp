@@ -526,7 +526,7 @@ BlocksPartitions blocks_apply(const Args &a, const uint8_t *data, uint64_t size)
     R.bounds.push_back({i * split, (i + 1) * split});
   }
   R.parts.resize(idx.size());
-  std::vector<sbh_block> out(size / 4096 + 16);
+  std::vector<sbh_block> out(size / 16384 + 4096);  // BAM blocks average 15-25 KB; regrown if short
   uint64_t n = 0;
   for (;;) {
     chk(sbh_find_blocks(g_ctx, data, size, st.data(), en.data(), st.size(), a.blocks_to_check, 1ull << 30, out.data(),

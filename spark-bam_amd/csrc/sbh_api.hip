@@ -299,7 +299,11 @@ int sbh_ctx_create(int device, sbh_ctx **out) {
                        : !std::strcmp(e, "yield") ? hipDeviceScheduleYield
                        : !std::strcmp(e, "block") ? hipDeviceScheduleBlockingSync
                                                   : hipDeviceScheduleAuto;
-    (void)hipSetDeviceFlags(f);
+    // the flag only takes before the device's primary context is active; a refusal is reported
+    // (stderr) rather than silently ignored, so an A/B of wait modes shows whether it applied
+    const hipError_t fe = hipSetDeviceFlags(f);
+    std::fprintf(stderr, "sparkbam-hip: SBH_SCHED=%s %s (%s)\n", e, fe == hipSuccess ? "applied" : "NOT applied",
+                 hipGetErrorString(fe));
   }
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
@@ -402,7 +406,7 @@ int sbh_shard_destroy(sbh_shard *sh) {
   sh->counts.release(); sh->cfirst.release(); sh->offs.release(); sh->cand.release(); sh->v.release(); sh->rank.release();
   sh->tmp.release(); sh->J0.release(); sh->J1.release(); sh->on.release(); sh->d_seg.release();
   sh->U.release(); sh->ctg.release(); sh->bits.release(); sh->words.release(); sh->close_pos.release();
-  sh->close_word.release(); sh->ctr.release(); sh->opix.release();
+  sh->close_word.release(); sh->ctr.release(); sh->opix.release(); sh->tsum.release();
   for (hipEvent_t &e : sh->ev)
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t &e : sh->pev)
@@ -822,7 +826,7 @@ static int eager_range(sbh_shard *sh, uint64_t begin, uint64_t end, int32_t rtc,
   const uint64_t nwords = (end - begin + 31) / 32;
   sh->chain_ok = sh->cm_valid = false;
   HIPCHK(ctx, sh->bits.ensure(nwords + 1));
-  HIPCHK(ctx, sh->tsum.ensure((end - begin + EAGER_TILE - 1) / EAGER_TILE * 4 + 4));
+  if (tsum_on()) HIPCHK(ctx, sh->tsum.ensure((end - begin + EAGER_TILE - 1) / EAGER_TILE * 4 + 4));
   HIPCHK(ctx, sh->xq.ensure(2 * XQ_CAP_MAX));
   unsigned long long *c = sh->ctr.p;
   HIPCHK(ctx, hipMemsetAsync(c, 0, 48, st));
@@ -1402,7 +1406,7 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
   const TokPlan P = tok_plan(sh, (nb + npipe - 1) / std::max<uint64_t>(npipe, 1));
   HIPCHK(ctx, sh->tok.ensure(P.tok_len));
   HIPCHK(ctx, sh->bits.ensure((E + 31) / 32 + 1));
-  HIPCHK(ctx, sh->tsum.ensure((E + EAGER_TILE - 1) / EAGER_TILE * 4 + 4));
+  if (tsum_on()) HIPCHK(ctx, sh->tsum.ensure((E + EAGER_TILE - 1) / EAGER_TILE * 4 + 4));
   HIPCHK(ctx, sh->defer.ensure(DEFER_CAP));
   HIPCHK(ctx, sh->xq.ensure(2 * XQ_CAP_MAX));
   HIPCHK(ctx, hipMemsetAsync(sh->U.p + sh->utotal, 0, sh->pad, sa));

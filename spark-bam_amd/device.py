@@ -4,6 +4,8 @@ import weakref
 
 import numpy as np
 
+from .records import record_columns
+
 from ._lib import (SBH_OK, SbhBlock, SbhCheckOpts, SbhCheckResult, SbhRecordsOut, SbhRecordsSizes,
                    SbhShardResult, SbhStreamOpts, SbhStreamResult, SparkBamError, lib)
 
@@ -152,7 +154,9 @@ class Context:
         arr = data if isinstance(data, np.ndarray) else np.frombuffer(data, dtype=np.uint8)
         st = np.ascontiguousarray([a for a, _ in splits], dtype=np.uint64)
         en = np.ascontiguousarray([b for _, b in splits], dtype=np.uint64)
-        cap = max(16, int(arr.size) // 4096 + 16)  # (a BGZF block is >= 28 bytes; grown below if short)
+        # a realistic first guess (BAM blocks average 15-25 KB compressed); a file of smaller
+        # blocks reports the count it needs and is asked again with that capacity
+        cap = int(arr.size) // 16384 + 4096
         while True:
             out = (SbhBlock * cap)()
             n = C.c_uint64()
@@ -444,17 +448,7 @@ class Shard:
         return self._records_fetch(sz)
 
     def _records_fetch(self, sz):
-        n = sz.n
-        cols = {
-            "flat": np.empty(n, np.uint64), "ref_id": np.empty(n, np.int32), "pos": np.empty(n, np.int32),
-            "next_ref_id": np.empty(n, np.int32), "next_pos": np.empty(n, np.int32),
-            "tlen": np.empty(n, np.int32), "flag": np.empty(n, np.uint16), "bin": np.empty(n, np.uint16),
-            "mapq": np.empty(n, np.uint8), "name_off": np.empty(n + 1, np.uint64),
-            "cigar_off": np.empty(n + 1, np.uint64), "seq_off": np.empty(n + 1, np.uint64),
-            "aux_off": np.empty(n + 1, np.uint64), "names": np.empty(sz.name_bytes, np.uint8),
-            "cigar": np.empty(sz.cigar_ops, np.uint32), "seq": np.empty(sz.bases, np.uint8),
-            "qual": np.empty(sz.bases, np.uint8), "aux": np.empty(sz.aux_bytes, np.uint8),
-        }
+        cols = record_columns(sz.n, sz.name_bytes, sz.cigar_ops, sz.bases, sz.aux_bytes)
         out = SbhRecordsOut(**{k: v.ctypes.data if v.size else None for k, v in cols.items()})
         self._c(lib().sbh_records_fetch(self.h, C.byref(out)))
         return cols

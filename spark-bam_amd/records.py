@@ -12,6 +12,28 @@ import struct
 import numpy as np
 
 CIGAR_OPS = "MIDNSHP=X"
+
+# The columns sbh_records_fetch fills (sbh_records_out field order): name -> (dtype, length
+# from (n, name_bytes, cigar_ops, bases, aux_bytes)).  Offset columns hold n + 1 entries.
+RECORD_COLUMNS = (
+    ("flat", np.uint64, lambda n, nm, cg, bs, ax: n), ("ref_id", np.int32, lambda n, *_: n),
+    ("pos", np.int32, lambda n, *_: n), ("next_ref_id", np.int32, lambda n, *_: n),
+    ("next_pos", np.int32, lambda n, *_: n), ("tlen", np.int32, lambda n, *_: n),
+    ("flag", np.uint16, lambda n, *_: n), ("bin", np.uint16, lambda n, *_: n),
+    ("mapq", np.uint8, lambda n, *_: n), ("name_off", np.uint64, lambda n, *_: n + 1),
+    ("cigar_off", np.uint64, lambda n, *_: n + 1), ("seq_off", np.uint64, lambda n, *_: n + 1),
+    ("aux_off", np.uint64, lambda n, *_: n + 1), ("names", np.uint8, lambda n, nm, cg, bs, ax: nm),
+    ("cigar", np.uint32, lambda n, nm, cg, bs, ax: cg), ("seq", np.uint8, lambda n, nm, cg, bs, ax: bs),
+    ("qual", np.uint8, lambda n, nm, cg, bs, ax: bs), ("aux", np.uint8, lambda n, nm, cg, bs, ax: ax),
+)
+
+
+def record_columns(n=0, name_bytes=0, cigar_ops=0, bases=0, aux_bytes=0):
+    """Uninitialised columns for n records (offset columns zeroed when n == 0, so an empty
+    batch has the same schema as a full one)."""
+    z = (n, name_bytes, cigar_ops, bases, aux_bytes)
+    cols = {k: (np.zeros if n == 0 else np.empty)(f(*z), dt) for k, dt, f in RECORD_COLUMNS}
+    return cols
 _B_FMT = {"c": "b", "C": "B", "s": "h", "S": "H", "i": "i", "I": "I", "f": "f"}
 
 
@@ -85,8 +107,9 @@ class Reads:
         """One batch of the records of several, in order (windowed loadReads, api.iter_reads)."""
         batches = [b for b in batches if b.n]
         if not batches:
-            return cls({k: np.empty(1 if k in cls.OFFSETS else 0, np.uint64) for k in
-                        ("flat", "vpos", *cls.OFFSETS)}, ref_names)
+            cols = record_columns()
+            cols["vpos"] = np.empty(0, np.uint64)
+            return cls(cols, ref_names)
         cols = {}
         for k in batches[0].cols:
             if k in cls.OFFSETS:

@@ -586,3 +586,34 @@ def test_split_parameters(golden, z, rtc):
             assert status[k] == 0 and int(c[k]) == want_n and (want_n == 0 or int(v[k]) == want_v), (s, e, z, rtc)
         else:
             assert status[k] != 0, (s, e, z, rtc)
+
+
+def test_shard_lifecycle_frees_hbm(ctx):
+    """Creating and destroying shards (index, inflate, eager pass, whole run) leaves device
+    memory where it was: every buffer a shard grows is released by sbh_shard_destroy (ADVICE r04:
+    the eager tile-summary buffer was not)."""
+    import ctypes as C
+    hip = C.CDLL("libamdhip64.so")
+    free, total = C.c_size_t(), C.c_size_t()
+
+    def free_now():
+        assert hip.hipMemGetInfo(C.byref(free), C.byref(total)) == 0
+        return free.value
+
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tools"))
+    import synth
+    data = synth.make_bam(synth.params(0x5B4D0001), 100_000)[0]  # ~33 MB flat
+    of = OracleFile(data)
+
+    def cycle():
+        sh = load(ctx, data, of.contig_len)
+        sh.check_eager(0, of.flat_size)
+        sh.run(0, data.size)
+        sh.close()
+
+    cycle()
+    before = free_now()
+    for _ in range(12):
+        cycle()
+    assert before - free_now() < (1 << 20), (before, free_now())

@@ -55,3 +55,17 @@ def test_tags_text_types():
     assert sb.records.tags_text(np.frombuffer(aux, np.uint8)) == [
         "XA:A:q", "XC:i:-5", "XS:i:65535", "XI:i:-70000", "XZ:Z:hello", "XH:H:1AE3", "XB:B:s,-2",
         "XF:f:1.5"]
+
+
+def test_reads_concat_empty_has_full_schema():
+    """Reads.concat of no non-empty batch keeps every column of a decoded batch:
+    the columns sbh_records_fetch fills, zero-length (offset columns one zero), plus vpos."""
+    RECORD_COLUMNS, record_columns = sb.records.RECORD_COLUMNS, sb.records.record_columns
+    full = record_columns(3, 10, 4, 300, 20)
+    full["vpos"] = np.zeros(3, np.uint64)
+    empty = sb.Reads.concat([], ["1"])
+    assert empty.n == 0 and set(empty.cols) == set(full)
+    for k, dt, _ in RECORD_COLUMNS:
+        assert empty.cols[k].dtype == dt, k
+        want = [0] if k.endswith("_off") else []
+        assert empty.cols[k].tolist() == want, k

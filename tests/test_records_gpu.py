@@ -105,3 +105,19 @@ def test_records_chain_walk_path_and_subrange():
         empty = sh.records(first, first)
         assert empty["flat"].size == 0 and empty["name_off"].tolist() == [0]
         sh.close()
+
+
+def test_load_reads_windowed_header_only():
+    """A BAM with a header and no records: the windowed decode (Reads.concat of no non-empty
+    batch) has the resident decode's full column schema, every column empty."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tools"))
+    import synth
+    data = synth.make_bam(synth.params(0x5B4D0001), 0)[0]
+    one = sb.load_reads(data)
+    win = sb.load_reads(data, window=4096)
+    assert one.n == win.n == 0
+    assert set(win.cols) == set(one.cols)
+    for k in one.cols:
+        assert win.cols[k].dtype == one.cols[k].dtype, k
+        assert np.array_equal(win.cols[k], one.cols[k]), k
