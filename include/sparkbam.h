@@ -88,6 +88,19 @@ typedef struct {
 int sbh_ctx_create(int device, sbh_ctx **out);
 int sbh_ctx_destroy(sbh_ctx *ctx);
 const char *sbh_last_error(const sbh_ctx *ctx);
+/* The last error's status and the fields the reference's exception is constructed from;
+ * returns how many fields the error carries (fields[0..min(n, cap)) are written):
+ *   SBH_E_HEADER_PARSE         {header file offset, idx, actual, expected}  -> HeaderParseException(idx: Int,
+ *                              actual: Byte, expected: Byte) (bgzf/.../block/HeaderParseException.scala:6-11)
+ *   SBH_E_HEADER_SEARCH_FAILED {start, positionsAttempted}  -> HeaderSearchFailedException(path, start,
+ *                              positionsAttempted) (bgzf/.../block/HeaderSearchFailedException.scala:7-12)
+ *   SBH_E_NO_READ_FOUND        {start (file offset of a split, or the flat position searched from),
+ *                              maxReadSize} -> NoReadFoundException(path, start, maxReadSize)
+ *                              (check/.../spark/FindRecordStart.scala:66-71)
+ *   SBH_E_INFLATE_SIZE         {block start, expected bytes}  -> IOException (Stream.scala:52-54)
+ *   SBH_E_INFLATE_DATA         {block start}  -> DataFormatException
+ *   anything else              no fields */
+int32_t sbh_last_error_detail(const sbh_ctx *ctx, int32_t *code, int64_t *fields, int32_t cap);
 /* Use a caller-owned hipStream_t (e.g. torch.cuda.current_stream().cuda_stream). */
 int sbh_ctx_set_stream(sbh_ctx *ctx, void *hip_stream);
 int sbh_ctx_synchronize(sbh_ctx *ctx);

@@ -8,28 +8,68 @@
 //   check/src/main/scala/org/hammerlab/bam/check/full/Checker.scala:186-198  full makeChecker implicit
 //   check/src/main/scala/org/hammerlab/bam/check/full/error/Flags.scala:10-45 Result / Success / Flags
 //   bgzf/src/main/scala/org/hammerlab/bgzf/block/Stream.scala:16-75          StreamI (Block iterator)
-//   load/src/main/scala/org/hammerlab/bam/spark/load/CanLoadBam.scala:196-357 loadSplitsAndReads et al.
+//   load/src/main/scala/org/hammerlab/bam/spark/load/CanLoadBam.scala:61-405  loadBam / loadSplitsAndReads /
+//                                                                            loadReadsAndPositions / loadReads /
+//                                                                            loadBamIntervals (GpuCanLoadBam)
+//   check/src/main/scala/org/hammerlab/bam/spark/FindRecordStart.scala:11-71  FindRecordStart, NoReadFoundException
+//   bgzf/src/main/scala/org/hammerlab/bgzf/block/FindBlockStart.scala:8-36  FindBlockStart, HeaderSearchFailedException
+//   check/src/main/scala/org/hammerlab/bam/check/Blocks.scala:141-206       Blocks.apply's unindexed branch (GpuBlocks)
 //
 // Not compiled in this image (no JVM / sbt; SURVEY.md 8c); the C-ABI under it is the tested
-// contract (tests/test_abi.py, every -m gpu test calls it).
+// contract (tests/test_abi.py, every -m gpu test calls it), and the reference names this file
+// and the shim use -- classes, constructors, imports, overridden signatures -- are pinned
+// against the reference's own declarations by tests/test_jni_names.py.
 package org.hammerlab.bam.gpu
 
 import java.nio.{ ByteBuffer, ByteOrder }
 
+import hammerlab.iterator._
+import hammerlab.path._
+import htsjdk.samtools.{ DefaultSAMRecordFactory, SAMFileHeader, SAMRecord }
 import org.apache.spark.broadcast.Broadcast
-import org.hammerlab.bam.check.Checker.MakeChecker
+import org.apache.spark.rdd.RDD
+import org.hammerlab.bam.check.Checker.{ MakeChecker, default }
 import org.hammerlab.bam.check.{ Checker, MaxReadSize, ReadStartFinder, ReadsToCheck }
 import org.hammerlab.bam.check.full.error.{ Flags, Result, Success }
-import org.hammerlab.bam.header.ContigLengths
-import org.hammerlab.bgzf.Pos
-import org.hammerlab.bgzf.block.{ Block, StreamI }
+import org.hammerlab.bam.header.{ ContigLengths, Header }
+import org.hammerlab.bam.index.Index.Chunk
+import org.hammerlab.bam.spark.{ BAMRecordRDD, NoReadFoundException, Split }
+import org.hammerlab.bam.spark.load.{ CanLoadBam, SplitRDD }
+import org.hammerlab.bgzf.{ EstimatedCompressionRatio, Pos }
+import org.hammerlab.bgzf.block.{ BGZFBlocksToCheck, Block, HeaderSearchFailedException, Metadata, StreamI }
 import org.hammerlab.channel.{ ByteChannel, CachingChannel, SeekableByteChannel }
-import hammerlab.path._
+import org.hammerlab.genomics.loci.set.LociSet
+import org.hammerlab.hadoop.splits.{ FileSplits, MaxSplitSize }
+
+import scala.collection.JavaConverters._
 
 class NeedHaloException(msg: String) extends RuntimeException(msg)
 
+/** A library status the shim cannot turn into the reference's exception by itself: the
+  * reference class needs the file's Path, which only the Scala caller holds.  `fields` are
+  * sbh_last_error_detail's (include/sparkbam.h); Native.rethrow(path) builds the reference's
+  * exception from them. */
+class NativeException(val status: Int, msg: String, val fields: Array[Long]) extends RuntimeException(msg)
+
 object Native {
   System.loadLibrary("sparkbam_jni")
+
+  // include/sparkbam.h status codes the facades test for
+  val HEADER_SEARCH_FAILED = 11
+  val NO_READ_FOUND = 16
+  val NOT_FOUND = 19
+  val BAD_RECORD = 20
+
+  /** The reference's exception for a NativeException, given the file's path:
+    * HeaderSearchFailedException(path, start, positionsAttempted) (bgzf/.../block/
+    * HeaderSearchFailedException.scala:7-12) or NoReadFoundException(path, start, maxReadSize)
+    * (check/.../spark/FindRecordStart.scala:66-71). */
+  def rethrow[T](path: Path): PartialFunction[Throwable, T] = {
+    case e: NativeException if e.status == HEADER_SEARCH_FAILED ⇒
+      throw HeaderSearchFailedException(path, e.fields(0), e.fields(1).toInt)
+    case e: NativeException if e.status == NO_READ_FOUND ⇒
+      throw NoReadFoundException(path, e.fields(0), e.fields(1).toInt)
+  }
 
   @native def ctxCreate(device: Int): Long
   @native def ctxDestroy(ctx: Long): Unit
@@ -79,6 +119,22 @@ object Native {
     * returns the file length written into `out` (capacity >= bgzfBound(n)). */
   @native def bgzfBound(n: Long): Long
   @native def bgzfCompress(ctx: Long, src: ByteBuffer, n: Long, level: Int, out: ByteBuffer): Long
+  /** Blocks.apply's unindexed branch over a local file (mapped by the shim; sbh_find_blocks):
+    * 4 longs per block {split index, start, compressedSize, uncompressedSize}. */
+  @native def findBlocks(ctx: Long, path: String, starts: Array[Long], ends: Array[Long], blocksToCheck: Int,
+                         window: Long): Array[Long]
+  /** check-bam -s / full-check over the listed blocks of a local file of any size
+    * (sbh_check_stream): out = {nWindows, positions, compBytes, nTrue, tp, fp, fn, unknown,
+    * nSuccess, nClose, haloFinal}; null buffers skip their part. */
+  @native def checkStream(ctx: Long, path: String, contigs: Array[Int], blocks: Array[Long], truthVpos: ByteBuffer,
+                          nTruth: Long, full: Boolean, window: Long, halo: Long, readsToCheck: Int,
+                          fpVpos: ByteBuffer, fnVpos: ByteBuffer, mismatchCap: Long, counts: ByteBuffer,
+                          rbe: ByteBuffer, closeVpos: ByteBuffer, closeWord: ByteBuffer, closeCap: Long,
+                          out: Array[Long]): Unit
+  /** loadBamIntervals' record pass (sbh_records_scan_regions): out = {n, nameBytes, cigarOps,
+    * bases, auxBytes} for recordsFetch. */
+  @native def recordsScanRegions(ctx: Long, sh: Long, chunkBegin: Array[Long], chunkEnd: Array[Long],
+                                 ivRef: Array[Int], ivBegin: Array[Long], ivEnd: Array[Long], out: Array[Long]): Unit
 }
 
 /** One executor GPU (one sbh_ctx), shared by its tasks under a lock (the reference's checkers are
@@ -134,7 +190,8 @@ class GpuShard(comp: ByteBuffer, n: Long, val fileOffset: Long, fileSize: Long, 
       Native.findRecordStart(ctx, sh, from, readsToCheck, maxReadSize, out)
       Some((out(0), out(1).toInt))
     } catch {
-      case _: org.hammerlab.bam.check.NoReadFoundException ⇒ None
+      // eager.Checker.nextReadStartWithDelta's None (eager/Checker.scala:134-162)
+      case e: NativeException if e.status == Native.NO_READ_FOUND ⇒ None
     }
   }
   /** (status, firstVpos, count) per split, one batch (CanLoadBam.scala:283-297, 316-356). */
@@ -518,5 +575,360 @@ case class GpuStream(compressedBytes: ByteChannel with SeekableByteChannel, wind
     next += 1
     lo = start + csize
     Some(Block(shard.flat(ustart, usize.toInt), start, csize.toInt))
+  }
+}
+
+/** Drop-in for check/.../spark/FindRecordStart.scala:11-71 on the GPU: the first eager-true
+  * position at/after Pos(start, 0) within maxReadSize positions, searched on the device over a
+  * shard of the file from `start` (grown x4 while the search needs bytes past it).  Same
+  * signature; `uncompressedBytes` is not read (the device inflates the blocks itself). */
+object GpuFindRecordStart {
+  def apply(path: Path,
+            start: Long)(
+      implicit
+      uncompressedBytes: org.hammerlab.bgzf.block.SeekableUncompressedBytes,
+      contigLengths: ContigLengths,
+      readsToCheck: ReadsToCheck,
+      maxReadSize: MaxReadSize): Pos =
+    withDelta(path, Pos(start, 0))
+      .map(_._1)
+      .getOrElse(throw NoReadFoundException(path, start, maxReadSize))
+
+  /** FindRecordStart.withDelta: Some((pos, positions skipped)) or None */
+  def withDelta(path: Path, start: Pos, halo0: Long = 1L << 20)(
+      implicit
+      contigLengths: ContigLengths,
+      readsToCheck: ReadsToCheck,
+      maxReadSize: MaxReadSize): Option[(Pos, Int)] = {
+    val ch = SeekableByteChannel(path)
+    try {
+      var halo = halo0
+      while (true) {
+        val s = GpuShard.read(ch, start.blockPos, halo, GpuShard.contigArray(contigLengths))
+        try {
+          s.load(start.blockPos)
+          return s.findRecordStart(s.flatOf(start), readsToCheck.n, maxReadSize.n).map {
+            case (f, delta) ⇒ (s.posOf(f), delta)
+          }
+        } catch {
+          case e: NeedHaloException ⇒
+            if (start.blockPos + halo >= ch.size) throw e
+            halo *= 4
+        } finally s.close()
+      }
+      None
+    } finally ch.close()
+  }
+}
+
+/** RecordStream over the records a shard's device pass found (RecordStream.scala:16-41):
+  * (Pos, SAMRecord) in file order.  The record starts come from the GPU (sbh_records_scan /
+  * sbh_records_scan_regions left them, "flat" column); the records' bytes are read out of HBM in
+  * one copy and each SAMRecord is built exactly as htsjdk's BAMRecordCodec.decode builds it
+  * (the 32 fixed-field bytes after block_size, then SAMRecordFactory.createBAMRecord over the
+  * variable-length rest), so the objects equal the reference's.  `sizes` are the scan's
+  * {n, nameBytes, cigarOps, bases, auxBytes}.  Everything is copied out on construction: the
+  * shard may be closed right after. */
+class GpuRecordIterator(shard: GpuShard, sizes: Array[Long], header: SAMFileHeader)
+  extends Iterator[(Pos, SAMRecord)] {
+  private val n = sizes(0).toInt
+  private val flats: Array[Long] = {
+    val b = ByteBuffer.allocateDirect(math.max(8, 8 * n)).order(ByteOrder.LITTLE_ENDIAN)
+    val cols = new Array[ByteBuffer](18)  // only the "flat" column (sbh_records_out field 0)
+    cols(0) = b
+    Native.recordsFetch(Device.ctx, shard.sh, sizes, cols)
+    Array.tabulate(n)(i ⇒ b.getLong(8 * i))
+  }
+  // the block table, for Pos of each start (canonical: a start at a block's end is Pos(next, 0))
+  private val (bStart, bUstart) = {
+    val t = shard.blocks(0, shard.numBlocks)
+    val live = (0 until shard.numBlocks.toInt).filter(i ⇒ t(6 * i + 4) > 0)
+    (live.map(i ⇒ t(6 * i)).toArray, live.map(i ⇒ t(6 * i + 1)).toArray)
+  }
+  private def posOf(f: Long): Pos = {
+    var k = java.util.Arrays.binarySearch(bUstart, f)
+    if (k < 0) k = -k - 2
+    else while (k + 1 < bUstart.length && bUstart(k + 1) == f) k += 1
+    Pos(bStart(k), (f - bUstart(k)).toInt)
+  }
+  // the bytes of [first record, end of the last record), read once
+  private val (lo, raw) =
+    if (n == 0) (0L, ByteBuffer.allocate(0))
+    else {
+      val last = flats(n - 1)
+      val len4 = ByteBuffer.wrap(shard.flat(last, 4)).order(ByteOrder.LITTLE_ENDIAN).getInt(0)
+      val hi = last + 4 + (len4.toLong & 0xffffffffL)
+      val b = ByteBuffer.allocateDirect((hi - flats(0)).toInt).order(ByteOrder.LITTLE_ENDIAN)
+      Native.readFlat(Device.ctx, shard.sh, flats(0), hi - flats(0), b)
+      (flats(0), b)
+    }
+  private val factory = DefaultSAMRecordFactory.getInstance
+  private var i = 0
+
+  override def hasNext: Boolean = i < n
+
+  override def next(): (Pos, SAMRecord) = {
+    val f = flats(i)
+    i += 1
+    val o = (f - lo).toInt
+    val blockSize = raw.getInt(o)
+    val binMqNl = raw.getInt(o + 12)
+    val flagNc = raw.getInt(o + 16)
+    val rest = new Array[Byte](blockSize - 32)
+    val dup = raw.duplicate()
+    dup.position(o + 36)
+    dup.get(rest)
+    val rec = factory.createBAMRecord(
+      header,
+      raw.getInt(o + 4),                // referenceID
+      raw.getInt(o + 8) + 1,            // coordinate (1-based)
+      (binMqNl & 0xff).toShort,         // readNameLength
+      ((binMqNl >>> 8) & 0xff).toShort, // mappingQuality
+      binMqNl >>> 16,                   // indexingBin
+      flagNc & 0xffff,                  // cigarLen
+      flagNc >>> 16,                    // flags
+      raw.getInt(o + 20),               // readLen
+      raw.getInt(o + 24),               // mateReferenceID
+      raw.getInt(o + 28) + 1,           // mateCoordinate
+      raw.getInt(o + 32),               // insertSize
+      rest)
+    posOf(f) → rec
+  }
+}
+
+/** loadReadsAndPositions' per-split body (CanLoadBam.scala:316-356) on the executor's GPU: the
+  * split's compressed bytes [start, end) plus a halo in one shard; FindBlockStart(start), index +
+  * inflate from it, the eager check over the owned positions [0, flat(Pos(end, 0))),
+  * FindRecordStart from Pos(blockStart, 0), then the records from it while pos < Pos(end, 0)
+  * (RecordStream.takeWhile).  The halo grows x4 while an answer needs bytes past it.  Mirrored
+  * call for call by spark_bam_amd.canloadbam.split_partition (tests/test_canloadbam_gpu.py). */
+object GpuSplitPartition {
+  def apply(path: Path, start: Long, end: Long, header: SAMFileHeader, contigs: Array[Int],
+            bgzfBlocksToCheck: Int, readsToCheck: Int, maxReadSize: Int,
+            halo0: Long = 1L << 20): Iterator[(Pos, SAMRecord)] = {
+    val ch = SeekableByteChannel(path)
+    try {
+      var halo = halo0
+      while (true) {
+        val s = GpuShard.read(ch, start, end - start + halo, contigs)
+        try {
+          val b = try Native.findBlockStart(Device.ctx, s.sh, start, bgzfBlocksToCheck) catch Native.rethrow(path)
+          s.load(b)
+          val owned = s.flatBound(end)
+          if (!s.atEof && owned == s.flatSize) throw new NeedHaloException(s"no block past $end in the halo")
+          val first = s.findRecordStart(0, readsToCheck, maxReadSize)
+            .getOrElse(throw NoReadFoundException(path, b, maxReadSize))._1
+          if (first >= owned) return Iterator.empty
+          Native.checkEager(Device.ctx, s.sh, 0, owned, readsToCheck, null)
+          val sizes = new Array[Long](5)
+          Native.recordsScan(Device.ctx, s.sh, first, owned, sizes)
+          return new GpuRecordIterator(s, sizes, header)
+        } catch {
+          case e: NeedHaloException ⇒
+            if (end + halo >= ch.size) throw e
+            halo *= 4
+        } finally s.close()
+      }
+      Iterator.empty
+    } finally ch.close()
+  }
+}
+
+/** loadBamIntervals' per-partition body (CanLoadBam.scala:120-154) on the executor's GPU: the
+  * partition's chunks whose block ranges lie within `mergeGap` of each other share one shard
+  * [first chunk's block, last chunk's end block + halo); index + inflate, the eager check over
+  * the chunks' flat span, then sbh_records_scan_regions keeps the records starting in a chunk
+  * whose region meets the intervals (region(record) as in CanLoadBam.scala:447-454).  Mirrored
+  * by spark_bam_amd.canloadbam.intervals_partition. */
+object GpuIntervalsPartition {
+  def apply(path: Path, chunks: Seq[Chunk], ivRef: Array[Int], ivBegin: Array[Long], ivEnd: Array[Long],
+            header: SAMFileHeader, contigs: Array[Int], readsToCheck: Int,
+            halo0: Long = 1L << 18, mergeGap: Long = 1L << 20): Iterator[SAMRecord] = {
+    val groups = scala.collection.mutable.ArrayBuffer[(Long, Long, Seq[Chunk])]()
+    for (c ← chunks) {
+      val (lo, hi) = (c.start.blockPos, c.end.blockPos)
+      if (groups.nonEmpty && lo <= groups.last._2 + mergeGap) {
+        val g = groups.last
+        groups(groups.size - 1) = (g._1, math.max(g._2, hi), g._3 :+ c)
+      } else groups += ((lo, hi, Seq(c)))
+    }
+    val ch = SeekableByteChannel(path)
+    try {
+      groups.iterator.flatMap {
+        case (lo, hi, cs) ⇒
+          var halo = halo0
+          var out: Vector[SAMRecord] = null
+          while (out == null) {
+            val s = GpuShard.read(ch, lo, hi - lo + halo, contigs)
+            try {
+              s.load(lo)
+              def flat(p: Pos): Long = if (p.blockPos >= ch.size) s.flatSize else s.flatOf(p)
+              val fb = cs.map(c ⇒ flat(c.start)).toArray
+              val fe = cs.map(c ⇒ math.min(flat(c.end), s.flatSize)).toArray
+              if (fe.max > fb.min) Native.checkEager(Device.ctx, s.sh, fb.min, fe.max, readsToCheck, null)
+              val sizes = new Array[Long](5)
+              Native.recordsScanRegions(Device.ctx, s.sh, fb, fe, ivRef, ivBegin, ivEnd, sizes)
+              out = new GpuRecordIterator(s, sizes, header).map(_._2).toVector
+            } catch {
+              // an eager check reading on, a chunk end or a kept record past the shard: grow it
+              case e: NeedHaloException if hi + halo < ch.size ⇒ halo *= 4
+              case e: NativeException
+                if (e.status == Native.NOT_FOUND || e.status == Native.BAD_RECORD) && hi + halo < ch.size ⇒
+                halo *= 4
+            } finally s.close()
+          }
+          out
+      }.toVector.iterator
+    } finally ch.close()
+  }
+}
+
+/** CanLoadBam with the hot path on the GPU: the same five entry points with the reference's
+  * parameter lists (load/.../CanLoadBam.scala:61-405); Spark partitioning is the reference's
+  * (one task per Hadoop FileSplit through SplitRDD(FileSplits.asJava(path, splitSize)); one per
+  * cappedCostGroups chunk group for intervals), and each task's FindBlockStart / inflate /
+  * FindRecordStart / record boundaries run on its executor's GPU (GpuSplitPartition,
+  * GpuIntervalsPartition).  Records are htsjdk SAMRecords built from the records' bytes exactly as
+  * BAMRecordCodec builds them.  `import spark_bam_gpu._` in place of `import spark_bam._`
+  * (jni/spark_bam_gpu.scala) puts these methods on SparkContext. */
+trait GpuCanLoadBam extends CanLoadBam {
+
+  override def loadBam(path: Path,
+                       splitSize: MaxSplitSize = MaxSplitSize(),
+                       bgzfBlocksToCheck: BGZFBlocksToCheck = default[BGZFBlocksToCheck],
+                       readsToCheck: ReadsToCheck = default[ReadsToCheck],
+                       maxReadSize: MaxReadSize = default[MaxReadSize]
+                      ): RDD[SAMRecord] =
+    loadReadsAndPositions(path, splitSize, bgzfBlocksToCheck, readsToCheck, maxReadSize).values
+
+  override def loadSplitsAndReads(path: Path,
+                                  splitSize: MaxSplitSize = MaxSplitSize(),
+                                  bgzfBlocksToCheck: BGZFBlocksToCheck = default[BGZFBlocksToCheck],
+                                  readsToCheck: ReadsToCheck = default[ReadsToCheck],
+                                  maxReadSize: MaxReadSize = default[MaxReadSize]
+                                 ): BAMRecordRDD = {
+    val positionsAndReadsRDD = loadReadsAndPositions(path, splitSize, bgzfBlocksToCheck, readsToCheck, maxReadSize)
+    val endPos = Pos(path.size, 0)
+    // the first record of every non-empty partition, sliding2 with Pos(fileSize, 0) (:283-297)
+    val splits =
+      positionsAndReadsRDD
+        .mapPartitions(it ⇒ if (it.hasNext) Iterator(it.next._1) else Iterator())
+        .collect
+        .sliding2(endPos)
+        .map(Split(_))
+        .toVector
+    BAMRecordRDD(splits, positionsAndReadsRDD.values)
+  }
+
+  override def loadReadsAndPositions(path: Path,
+                                     splitSize: MaxSplitSize,
+                                     bgzfBlocksToCheck: BGZFBlocksToCheck,
+                                     readsToCheck: ReadsToCheck,
+                                     maxReadSize: MaxReadSize
+                                    ): RDD[(Pos, SAMRecord)] = {
+    val headerBroadcast = sc.broadcast(Header(path))
+    val contigs = GpuShard.contigArray(ContigLengths(path))
+    val (k, r, m) = (bgzfBlocksToCheck.n, readsToCheck.n, maxReadSize.n)
+    SplitRDD(FileSplits.asJava(path, splitSize))
+      .flatMap {
+        case (start, end) ⇒
+          GpuSplitPartition(path, start, end, headerBroadcast.value, contigs, k, r, m)
+      }
+  }
+
+  override def loadReads(path: Path,
+                         bgzfBlocksToCheck: BGZFBlocksToCheck = default[BGZFBlocksToCheck],
+                         readsToCheck: ReadsToCheck = default[ReadsToCheck],
+                         maxReadSize: MaxReadSize = default[MaxReadSize],
+                         splitSize: MaxSplitSize = MaxSplitSize()): RDD[SAMRecord] =
+    path.extension match {
+      case "bam" ⇒ loadBam(path, splitSize, bgzfBlocksToCheck, readsToCheck, maxReadSize)
+      case _ ⇒ super.loadReads(path, bgzfBlocksToCheck, readsToCheck, maxReadSize, splitSize)  // sam / cram
+    }
+
+  override def loadBamIntervals(path: Path,
+                                intervals: LociSet,
+                                splitSize: MaxSplitSize,
+                                estimatedCompressionRatio: EstimatedCompressionRatio): RDD[SAMRecord] = {
+    if (path.toString.endsWith(".sam"))
+      return super.loadBamIntervals(path, intervals, splitSize, estimatedCompressionRatio)
+    val header = Header(path)
+    val headerBroadcast = sc.broadcast(header)
+    val contigs = GpuShard.contigArray(header.contigLengths)
+    // the merged intervals, 0-based half-open, as (contig index, begin, end): the same
+    // htsjdk intervals getIntevalChunks queries the BAI with (CanLoadBam.scala:425-436)
+    val samHeader: SAMFileHeader = header
+    val dict = samHeader.getSequenceDictionary
+    val ivs = intervals.toHtsJDKIntervals.toArray
+      .map(i ⇒ (dict.getSequenceIndex(i.getContig), i.getStart - 1L, i.getEnd.toLong))
+      .sorted
+    val (ivRef, ivBegin, ivEnd) = (ivs.map(_._1), ivs.map(_._2), ivs.map(_._3))
+    val chunks = CanLoadBam.getIntevalChunks(path, intervals)
+    val chunkPartitions =
+      chunks
+        .cappedCostGroups(_.size(estimatedCompressionRatio), splitSize.toDouble)
+        .map(_.toVector)
+        .toVector
+    sc
+      .parallelize(chunkPartitions, math.max(1, chunkPartitions.size))
+      .mapPartitions {
+        groups ⇒
+          val h: SAMFileHeader = headerBroadcast.value
+          groups.flatMap(cs ⇒ GpuIntervalsPartition(path, cs, ivRef, ivBegin, ivEnd, h, contigs, 10))
+      }
+  }
+}
+
+/** Blocks.apply's unindexed branch (check/.../check/Blocks.scala:141-206) for a local file:
+  * FindBlockStart per split, then MetadataStream to the split's end, on the device
+  * (sbh_find_blocks); per split the Metadata(start, compressedSize, uncompressedSize) list. */
+object GpuBlocks {
+  def unindexed(path: Path, splits: Seq[(Long, Long)], bgzfBlocksToCheck: Int = 5,
+                window: Long = 1L << 30): Vector[Vector[Metadata]] = {
+    val v =
+      try Native.findBlocks(Device.ctx, path.toString, splits.map(_._1).toArray, splits.map(_._2).toArray,
+                            bgzfBlocksToCheck, window)
+      catch Native.rethrow(path)
+    val per = Array.fill(splits.size)(Vector.newBuilder[Metadata])
+    for (i ← 0 until v.length / 4)
+      per(v(4 * i).toInt) += Metadata(v(4 * i + 1), v(4 * i + 2).toInt, v(4 * i + 3).toInt)
+    per.map(_.result()).toVector
+  }
+}
+
+/** check-bam -s (CheckerApp.scala:65-227 + CallPartition.scala:23-54) and full-check
+  * (FullCheck.scala:65-86,142-192) over Blocks.apply's blocks of a local file of any size, the
+  * file streamed through HBM (sbh_check_stream): the totals the apps print, the mismatching
+  * positions (first mismatchCap), and with full the Counts / readsBeforeError histograms by
+  * numNonZeroFields and the close calls.  Mirrored by spark_bam_amd.api.check_bam / full_check. */
+object GpuCheckStream {
+  case class Totals(windows: Long, positions: Long, compressedBytes: Long, trueCalls: Long, tp: Long, fp: Long,
+                    fn: Long, unknown: Long, successes: Long, closeCalls: Long)
+
+  case class Calls(totals: Totals, falsePositives: Seq[Pos], falseNegatives: Seq[Pos], counts: Array[Long],
+                   readsBeforeError: Array[Long], close: Seq[(Pos, Int)])
+
+  def apply(path: Path, contigLengths: ContigLengths, blocks: Array[Long], records: Option[Array[Long]],
+            full: Boolean, readsToCheck: Int = 10, window: Long = 1L << 30, halo: Long = 4L << 20,
+            mismatchCap: Int = 1 << 20, closeCap: Int = 1 << 22): Calls = {
+    def longs(n: Int) = ByteBuffer.allocateDirect(8 * math.max(1, n)).order(ByteOrder.LITTLE_ENDIAN)
+    val truth = records.map { r ⇒ val b = longs(r.length); b.asLongBuffer.put(r); b }
+    val (fp, fn) = if (records.isDefined) (longs(mismatchCap), longs(mismatchCap)) else (null, null)
+    val (counts, rbe) = if (full) (longs(21 * 19), longs(21 * 64)) else (null, null)
+    val (cv, cw) =
+      if (full) (longs(closeCap), ByteBuffer.allocateDirect(4 * closeCap).order(ByteOrder.LITTLE_ENDIAN))
+      else (null, null)
+    val out = new Array[Long](11)
+    Native.checkStream(Device.ctx, path.toString, GpuShard.contigArray(contigLengths), blocks, truth.orNull,
+                       records.map(_.length.toLong).getOrElse(0L), full, window, halo, readsToCheck, fp, fn,
+                       mismatchCap, counts, rbe, cv, cw, closeCap, out)
+    val t = Totals(out(0), out(1), out(2), out(3), out(4), out(5), out(6), out(7), out(8), out(9))
+    def poss(b: ByteBuffer, n: Long) =
+      if (b == null) Seq() else (0 until math.min(n, mismatchCap.toLong).toInt).map(i ⇒ Pos(b.getLong(8 * i)))
+    def arr(b: ByteBuffer, n: Int) = if (b == null) Array.empty[Long] else Array.tabulate(n)(i ⇒ b.getLong(8 * i))
+    val close =
+      if (!full) Seq()
+      else (0 until math.min(t.closeCalls, closeCap.toLong).toInt).map(i ⇒ (Pos(cv.getLong(8 * i)), cw.getInt(4 * i)))
+    Calls(t, poss(fp, t.fp), poss(fn, t.fn), arr(counts, 21 * 19), arr(rbe, 21 * 64), close)
   }
 }

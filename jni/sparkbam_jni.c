@@ -3,42 +3,109 @@
  * (modules bgzf / check / load / cli) calls libsparkbam_hip.so (include/sparkbam.h).
  *
  * Java class: org.hammerlab.bam.gpu.Native (jni/Native.scala).  Handles are jlongs; byte
- * buffers are direct ByteBuffers (no copies through the JVM heap); status codes map onto
- * the reference's exception classes:
- *   SBH_E_HEADER_PARSE         -> org.hammerlab.bgzf.block.HeaderParseException
- *                                 (bgzf/.../block/Header.scala:50-57)
- *   SBH_E_HEADER_SEARCH_FAILED -> org.hammerlab.bgzf.block.HeaderSearchFailedException
- *                                 (bgzf/.../block/FindBlockStart.scala:31-35)
- *   SBH_E_INFLATE_SIZE         -> java.io.IOException (Stream.scala:52-54)
- *   SBH_E_INFLATE_DATA         -> java.util.zip.DataFormatException
- *   SBH_E_NO_READ_FOUND        -> org.hammerlab.bam.check.NoReadFoundException
- *                                 (check/.../spark/FindRecordStart.scala:66-71)
- *   SBH_E_NEED_HALO            -> org.hammerlab.bam.gpu.NeedHaloException (the façade re-reads
- *                                 a larger halo; never user-visible)
- *   anything else              -> java.lang.IllegalStateException(sbh_last_error)
+ * buffers are direct ByteBuffers (no copies through the JVM heap).  Failures become the
+ * reference's own exceptions, built with their real constructors (EXCEPTIONS below; the class
+ * names and constructor descriptors are pinned against the reference's declarations by
+ * tests/test_jni_names.py):
+ *   SBH_E_HEADER_PARSE  -> org.hammerlab.bgzf.block.HeaderParseException(idx: Int, actual: Byte,
+ *                          expected: Byte)   (bgzf/.../block/HeaderParseException.scala:6-11), from
+ *                          sbh_last_error_detail's fields
+ *   SBH_E_INFLATE_SIZE, SBH_E_BAD_ISIZE -> java.io.IOException(String) (bgzf/.../block/Stream.scala:52-54)
+ *   SBH_E_INFLATE_DATA  -> java.util.zip.DataFormatException(String) (Inflater.inflate)
+ *   SBH_E_TRUNCATED     -> java.io.EOFException(String)
+ *   SBH_E_ARG           -> java.lang.IllegalArgumentException(String)
+ *   SBH_E_NEED_HALO     -> org.hammerlab.bam.gpu.NeedHaloException(String) (the facade re-reads a
+ *                          larger halo; never user-visible)
+ *   SBH_E_NOT_FOUND, SBH_E_BAD_RECORD
+ *                       -> org.hammerlab.bam.gpu.NativeException (below): the facades grow a shard
+ *                          on them (a Pos or a record past the resident bytes)
+ *   SBH_E_HEADER_SEARCH_FAILED, SBH_E_NO_READ_FOUND
+ *                       -> org.hammerlab.bam.gpu.NativeException(status: Int, message: String,
+ *                          fields: Array[Long]): their reference classes take the file's Path
+ *                          (HeaderSearchFailedException(path, start, positionsAttempted),
+ *                          bgzf/.../block/HeaderSearchFailedException.scala:7-12;
+ *                          org.hammerlab.bam.spark.NoReadFoundException(path, start, maxReadSize),
+ *                          check/.../spark/FindRecordStart.scala:66-71), which only the Scala
+ *                          caller holds: Native.scala's `Native.rethrow(path)` builds them from the
+ *                          fields {start, positionsAttempted} / {start, maxReadSize}
+ *   anything else       -> java.lang.IllegalStateException(sbh_last_error)
  *
  * Built by jni/Makefile only when $JAVA_HOME/include/jni.h exists (no JDK in this image).
  */
+#include <fcntl.h>
 #include <jni.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include "sparkbam.h"
 
 #define CTX(x) ((sbh_ctx *)(intptr_t)(x))
 #define SH(x) ((sbh_shard *)(intptr_t)(x))
 
-static void throw_status(JNIEnv *env, sbh_ctx *ctx, int rc) {
-  const char *cls = rc == SBH_E_HEADER_PARSE           ? "org/hammerlab/bgzf/block/HeaderParseException"
-                    : rc == SBH_E_HEADER_SEARCH_FAILED ? "org/hammerlab/bgzf/block/HeaderSearchFailedException"
-                    : rc == SBH_E_INFLATE_SIZE         ? "java/io/IOException"
-                    : rc == SBH_E_INFLATE_DATA         ? "java/util/zip/DataFormatException"
-                    : rc == SBH_E_NO_READ_FOUND        ? "org/hammerlab/bam/check/NoReadFoundException"
-                    : rc == SBH_E_NEED_HALO            ? "org/hammerlab/bam/gpu/NeedHaloException"
-                                                       : "java/lang/IllegalStateException";
+#define STRING_CTOR "(Ljava/lang/String;)V"
+#define NATIVE_EXCEPTION "org/hammerlab/bam/gpu/NativeException"
+#define NATIVE_CTOR "(ILjava/lang/String;[J)V"
+
+/* status -> the class thrown and the constructor it is built with */
+static const struct {
+  int rc;
+  const char *cls, *ctor;
+} EXCEPTIONS[] = {
+    {SBH_E_HEADER_PARSE, "org/hammerlab/bgzf/block/HeaderParseException", "(IBB)V"},
+    {SBH_E_HEADER_SEARCH_FAILED, NATIVE_EXCEPTION, NATIVE_CTOR},
+    {SBH_E_NO_READ_FOUND, NATIVE_EXCEPTION, NATIVE_CTOR},
+    {SBH_E_NOT_FOUND, NATIVE_EXCEPTION, NATIVE_CTOR},  /* a Pos past the shard: the facade grows it */
+    {SBH_E_BAD_RECORD, NATIVE_EXCEPTION, NATIVE_CTOR}, /* a record past the shard (or malformed) */
+    {SBH_E_INFLATE_SIZE, "java/io/IOException", STRING_CTOR},
+    {SBH_E_BAD_ISIZE, "java/io/IOException", STRING_CTOR},
+    {SBH_E_INFLATE_DATA, "java/util/zip/DataFormatException", STRING_CTOR},
+    {SBH_E_TRUNCATED, "java/io/EOFException", STRING_CTOR},
+    {SBH_E_ARG, "java/lang/IllegalArgumentException", STRING_CTOR},
+    {SBH_E_NEED_HALO, "org/hammerlab/bam/gpu/NeedHaloException", STRING_CTOR},
+};
+static const char *const OTHER_EXCEPTION = "java/lang/IllegalStateException";
+
+/* new cls(args...) thrown; a class or constructor that cannot be found leaves its
+ * NoClassDefFoundError / NoSuchMethodError pending instead */
+static void throw_new(JNIEnv *env, const char *cls, const char *ctor, int rc, const char *msg, const int64_t *f,
+                      int nf) {
   jclass c = (*env)->FindClass(env, cls);
-  if (!c) return; /* NoClassDefFoundError is pending */
-  (*env)->ThrowNew(env, c, ctx ? sbh_last_error(ctx) : "libsparkbam_hip");
+  if (!c) return;
+  jmethodID init = (*env)->GetMethodID(env, c, "<init>", ctor);
+  if (!init) return;
+  jobject e = NULL;
+  if (ctor[1] == 'I' && ctor[2] == 'B') { /* HeaderParseException(idx, actual, expected) */
+    e = (*env)->NewObject(env, c, init, (jint)f[1], (jbyte)f[2], (jbyte)f[3]);
+  } else if (ctor[1] == 'I') { /* NativeException(status, message, fields) */
+    jstring m = (*env)->NewStringUTF(env, msg);
+    jlongArray a = (*env)->NewLongArray(env, nf);
+    if (!m || !a) return;
+    (*env)->SetLongArrayRegion(env, a, 0, nf, (const jlong *)f);
+    e = (*env)->NewObject(env, c, init, (jint)rc, m, a);
+  } else {
+    jstring m = (*env)->NewStringUTF(env, msg);
+    if (!m) return;
+    e = (*env)->NewObject(env, c, init, m);
+  }
+  if (e) (*env)->Throw(env, (jthrowable)e);
+}
+
+static void throw_status(JNIEnv *env, sbh_ctx *ctx, int rc) {
+  const char *msg = ctx ? sbh_last_error(ctx) : "libsparkbam_hip";
+  int64_t f[4] = {0, 0, 0, 0};
+  int32_t code = 0;
+  int nf = ctx ? (int)sbh_last_error_detail(ctx, &code, f, 4) : 0;
+  if (code != rc || nf > 4) nf = code == rc ? 4 : 0; /* fields of another error are not this one's */
+  const char *cls = OTHER_EXCEPTION, *ctor = STRING_CTOR;
+  for (size_t i = 0; i < sizeof EXCEPTIONS / sizeof EXCEPTIONS[0]; ++i)
+    if (EXCEPTIONS[i].rc == rc) cls = EXCEPTIONS[i].cls, ctor = EXCEPTIONS[i].ctor;
+  if (rc == SBH_E_HEADER_PARSE && nf < 4) /* no byte to report: the status alone */
+    cls = NATIVE_EXCEPTION, ctor = NATIVE_CTOR;
+  throw_new(env, cls, ctor, rc, msg, f, nf);
 }
 
 /* status check: throws and returns 1 on failure */
@@ -49,8 +116,7 @@ static int failed(JNIEnv *env, jlong ctx, int rc) {
 }
 
 static void throw_arg(JNIEnv *env, const char *msg) {
-  jclass c = (*env)->FindClass(env, "java/lang/IllegalArgumentException");
-  if (c) (*env)->ThrowNew(env, c, msg);
+  throw_new(env, "java/lang/IllegalArgumentException", STRING_CTOR, SBH_E_ARG, msg, NULL, 0);
 }
 
 /* The address of a direct ByteBuffer the library will read or write `need` bytes of.  A null
@@ -502,4 +568,185 @@ JNIEXPORT jlong JNICALL Java_org_hammerlab_bam_gpu_Native_00024_bgzfCompress(JNI
   if (failed(env, ctx, sbh_bgzf_compress_level(CTX(ctx), in, (uint64_t)n, 0, level, o, cap, &size, &nb, NULL)))
     return -1;
   return (jlong)size;
+}
+
+/* ---- files larger than a ByteBuffer: the file mapped read-only by the shim ---- */
+typedef struct {
+  void *p;
+  uint64_t n;
+} Mapped;
+
+/* path -> read-only mapping of the whole (local) file; throws IOException on failure */
+static int map_file(JNIEnv *env, jstring path, Mapped *m) {
+  m->p = NULL, m->n = 0;
+  const char *s = (*env)->GetStringUTFChars(env, path, NULL);
+  if (!s) return 1;
+  int fd = open(s, O_RDONLY);
+  struct stat st;
+  char msg[512];
+  int ok = fd >= 0 && fstat(fd, &st) == 0;
+  if (ok && st.st_size > 0) {
+    m->n = (uint64_t)st.st_size;
+    m->p = mmap(NULL, m->n, PROT_READ, MAP_PRIVATE, fd, 0);
+    ok = m->p != MAP_FAILED;
+    if (!ok) m->p = NULL;
+  }
+  snprintf(msg, sizeof msg, "%s: cannot map the file", s);
+  if (fd >= 0) close(fd);
+  (*env)->ReleaseStringUTFChars(env, path, s);
+  if (!ok) throw_new(env, "java/io/IOException", STRING_CTOR, 0, msg, NULL, 0);
+  return !ok;
+}
+
+static void unmap_file(Mapped *m) {
+  if (m->p) munmap(m->p, m->n);
+}
+
+/* Blocks.apply's unindexed branch (check/.../check/Blocks.scala:141-206): FindBlockStart per
+ * split, then MetadataStream to the split's end, windows through HBM (sbh_find_blocks).
+ * Returns 4 longs per block {split index, start, compressedSize, uncompressedSize}. */
+JNIEXPORT jlongArray JNICALL Java_org_hammerlab_bam_gpu_Native_00024_findBlocks(JNIEnv *env, jobject self, jlong ctx,
+                                                                                jstring path, jlongArray starts,
+                                                                                jlongArray ends, jint blocksToCheck,
+                                                                                jlong window) {
+  const jsize ns = (*env)->GetArrayLength(env, starts);
+  if ((*env)->GetArrayLength(env, ends) != ns) {
+    throw_arg(env, "findBlocks: split starts and ends of different lengths");
+    return NULL;
+  }
+  Mapped m;
+  if (map_file(env, path, &m)) return NULL;
+  uint64_t *se = (uint64_t *)malloc(sizeof(uint64_t) * 2 * (size_t)(ns > 0 ? ns : 1));
+  uint64_t cap = m.n / 16384 + 4096, n = 0; /* BAM blocks average 15-25 KB; regrown if short */
+  sbh_block *out = NULL;
+  jlongArray res = NULL;
+  if (!se) {
+    throw_status(env, NULL, SBH_E_NOMEM);
+    goto done;
+  }
+  (*env)->GetLongArrayRegion(env, starts, 0, ns, (jlong *)se);
+  (*env)->GetLongArrayRegion(env, ends, 0, ns, (jlong *)(se + ns));
+  for (;;) {
+    free(out);
+    out = (sbh_block *)malloc(sizeof(sbh_block) * (size_t)cap);
+    if (!out) {
+      throw_status(env, NULL, SBH_E_NOMEM);
+      goto done;
+    }
+    if (failed(env, ctx, sbh_find_blocks(CTX(ctx), m.p, m.n, se, se + ns, (uint64_t)ns, blocksToCheck,
+                                         (uint64_t)window, out, cap, &n)))
+      goto done;
+    if (n <= cap) break;
+    cap = n;
+  }
+  res = (*env)->NewLongArray(env, (jsize)(4 * n));
+  if (res) {
+    jlong *v = (jlong *)malloc(sizeof(jlong) * 4 * (size_t)(n ? n : 1));
+    if (!v) {
+      throw_status(env, NULL, SBH_E_NOMEM);
+      res = NULL;
+      goto done;
+    }
+    for (uint64_t i = 0; i < n; ++i) /* (sbh_find_blocks: ustart holds the split index) */
+      v[4 * i] = (jlong)out[i].ustart, v[4 * i + 1] = (jlong)out[i].start, v[4 * i + 2] = out[i].csize,
+      v[4 * i + 3] = out[i].usize;
+    (*env)->SetLongArrayRegion(env, res, 0, (jsize)(4 * n), v);
+    free(v);
+  }
+done:
+  free(out);
+  free(se);
+  unmap_file(&m);
+  return res;
+}
+
+/* check-bam -s / full-check over Blocks.apply's blocks of a file of any size
+ * (cli/.../CallPartition.scala:23-54, cli/.../full/FullCheck.scala:65-86; sbh_check_stream):
+ * blocks = file offsets of the block starts, ascending; truthVpos (direct, n_truth longs, or
+ * null) = the `.records` positions; fp/fn vpos and the full aggregation into direct buffers
+ * (null = skipped).  out = {nWindows, positions, compBytes, nTrue, tp, fp, fn, unknown,
+ * nSuccess, nClose, haloFinal}. */
+JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_checkStream(
+    JNIEnv *env, jobject self, jlong ctx, jstring path, jintArray contigs, jlongArray blocks, jobject truthVpos,
+    jlong nTruth, jboolean full, jlong window, jlong halo, jint readsToCheck, jobject fpVpos, jobject fnVpos,
+    jlong mismatchCap, jobject counts, jobject rbe, jobject closeVpos, jobject closeWord, jlong closeCap,
+    jlongArray out) {
+  const jsize nb = (*env)->GetArrayLength(env, blocks);
+  const uint64_t nt = nTruth > 0 ? (uint64_t)nTruth : 0, mc = mismatchCap > 0 ? (uint64_t)mismatchCap : 0,
+                 cc = closeCap > 0 ? (uint64_t)closeCap : 0;
+  int bad = 0;
+  sbh_check_opts o = {0};
+  o.window = (uint64_t)window, o.halo = (uint64_t)halo, o.reads_to_check = readsToCheck, o.full = full ? 1 : 0;
+  o.truth_vpos = (const uint64_t *)direct_n(env, truthVpos, 8 * nt, &bad);
+  o.n_truth = o.truth_vpos ? nt : 0;
+  o.fp_vpos = bad ? NULL : (uint64_t *)direct_n(env, fpVpos, 8 * mc, &bad);
+  o.fn_vpos = bad ? NULL : (uint64_t *)direct_n(env, fnVpos, 8 * mc, &bad);
+  o.fp_cap = o.fp_vpos ? mc : 0, o.fn_cap = o.fn_vpos ? mc : 0;
+  o.counts = bad ? NULL : (uint64_t *)direct_n(env, counts, 8ull * SBH_NNZ_MAX * 19, &bad);
+  o.rbe_hist = bad ? NULL : (uint64_t *)direct_n(env, rbe, 8ull * SBH_NNZ_MAX * SBH_RBE_MAX, &bad);
+  o.close_vpos = bad ? NULL : (uint64_t *)direct_n(env, closeVpos, 8 * cc, &bad);
+  o.close_word = bad ? NULL : (uint32_t *)direct_n(env, closeWord, 4 * cc, &bad);
+  o.close_cap = (o.close_vpos && o.close_word) ? cc : 0;
+  if (bad) return;
+  if (o.full && (!o.counts || !o.rbe_hist)) {
+    throw_arg(env, "checkStream: full needs the counts and rbe buffers");
+    return;
+  }
+  uint64_t *bl = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)(nb > 0 ? nb : 1));
+  if (!bl) {
+    throw_status(env, NULL, SBH_E_NOMEM);
+    return;
+  }
+  (*env)->GetLongArrayRegion(env, blocks, 0, nb, (jlong *)bl);
+  o.blocks = bl, o.n_blocks = (uint64_t)nb;
+  const jsize nc = (*env)->GetArrayLength(env, contigs);
+  jint *cl = (*env)->GetIntArrayElements(env, contigs, NULL);
+  Mapped m = {NULL, 0};
+  if (cl && !map_file(env, path, &m)) {
+    sbh_check_result r;
+    const int rc = sbh_check_stream(CTX(ctx), m.p, m.n, (const int32_t *)cl, (int32_t)nc, &o, &r);
+    if (!failed(env, ctx, rc)) {
+      jlong v[11] = {(jlong)r.n_windows, (jlong)r.positions, (jlong)r.comp_bytes, (jlong)r.n_true, (jlong)r.tp,
+                     (jlong)r.fp, (jlong)r.fn, (jlong)r.unknown, (jlong)r.n_success, (jlong)r.n_close,
+                     (jlong)r.halo_final};
+      put_longs(env, out, v, 11);
+    }
+    unmap_file(&m);
+  }
+  if (cl) (*env)->ReleaseIntArrayElements(env, contigs, cl, JNI_ABORT);
+  free(bl);
+}
+
+/* loadBamIntervals' record pass over a shard (load/.../CanLoadBam.scala:120-154;
+ * sbh_records_scan_regions): chunk flat ranges [chunkBegin[k], chunkEnd[k]) and the merged
+ * intervals (ref, begin, end) 0-based half-open; out = {n, nameBytes, cigarOps, bases,
+ * auxBytes} for recordsFetch. */
+JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_recordsScanRegions(
+    JNIEnv *env, jobject self, jlong ctx, jlong sh, jlongArray chunkBegin, jlongArray chunkEnd, jintArray ivRef,
+    jlongArray ivBegin, jlongArray ivEnd, jlongArray out) {
+  const jsize nch = (*env)->GetArrayLength(env, chunkBegin), niv = (*env)->GetArrayLength(env, ivRef);
+  if ((*env)->GetArrayLength(env, chunkEnd) != nch || (*env)->GetArrayLength(env, ivBegin) != niv ||
+      (*env)->GetArrayLength(env, ivEnd) != niv) {
+    throw_arg(env, "recordsScanRegions: arrays of different lengths");
+    return;
+  }
+  uint64_t *cb = (uint64_t *)malloc(sizeof(uint64_t) * 2 * (size_t)(nch > 0 ? nch : 1));
+  int64_t *iv = (int64_t *)malloc(sizeof(int64_t) * 2 * (size_t)(niv > 0 ? niv : 1));
+  int32_t *ir = (int32_t *)malloc(sizeof(int32_t) * (size_t)(niv > 0 ? niv : 1));
+  if (cb && iv && ir) {
+    (*env)->GetLongArrayRegion(env, chunkBegin, 0, nch, (jlong *)cb);
+    (*env)->GetLongArrayRegion(env, chunkEnd, 0, nch, (jlong *)(cb + nch));
+    (*env)->GetLongArrayRegion(env, ivBegin, 0, niv, (jlong *)iv);
+    (*env)->GetLongArrayRegion(env, ivEnd, 0, niv, (jlong *)(iv + niv));
+    (*env)->GetIntArrayRegion(env, ivRef, 0, niv, (jint *)ir);
+    sbh_records_sizes z;
+    if (!failed(env, ctx, sbh_records_scan_regions(SH(sh), cb, cb + nch, (uint64_t)nch, ir, iv, iv + niv,
+                                                   (uint32_t)niv, &z))) {
+      jlong v[5] = {(jlong)z.n, (jlong)z.name_bytes, (jlong)z.cigar_ops, (jlong)z.bases, (jlong)z.aux_bytes};
+      put_longs(env, out, v, 5);
+    }
+  } else {
+    throw_status(env, NULL, SBH_E_NOMEM);
+  }
+  free(cb), free(iv), free(ir);
 }

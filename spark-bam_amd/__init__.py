@@ -11,7 +11,8 @@ Import name: ``spark_bam_amd`` (the directory name contains a hyphen, so load it
           (CanLoadBam), FileSplits, read_bai (bam.index.Index)
 """
 from ._lib import (BLOCK_EMPTY, BLOCK_TRUNCATED, FULL_FLAGS_MASK, FULL_N_SHIFT,  # noqa: F401
-                   FULL_SUCCESS, FULL_UNKNOWN, SparkBamError, lib)
+                   FULL_SUCCESS, FULL_UNKNOWN, HeaderParseException, HeaderSearchFailedException,
+                   NoReadFoundException, SparkBamError, lib)
 from .device import Context, PinnedBuffer, Shard  # noqa: F401
 from .api import (FLAG_NAMES, htsjdk_rewrite, Header, Metadata, Pos, Split, bam_header, check_bam,  # noqa: F401
                   file_splits, full_check, load_bam_count, load_reads, load_splits_and_reads,
@@ -23,7 +24,8 @@ from .intervals import (Chunk, Index, get_interval_chunks, load_bam_intervals,  
 
 __all__ = [
     "htsjdk_rewrite",
-    "Context", "PinnedBuffer", "Shard", "SparkBamError", "Pos", "Header", "Metadata", "Split", "FLAG_NAMES",
+    "Context", "PinnedBuffer", "Shard", "SparkBamError", "HeaderParseException", "HeaderSearchFailedException",
+    "NoReadFoundException", "Pos", "Header", "Metadata", "Split", "FLAG_NAMES",
     "file_splits", "load_splits_and_reads", "load_bam_count", "check_bam", "full_check",
     "bam_header", "parse_bam_header", "lib", "load_reads", "Reads", "Chunk", "Index",
     "read_bai", "parse_loci", "get_interval_chunks", "load_bam_intervals",

@@ -30,7 +30,7 @@ BLOCK_EMPTY, BLOCK_TRUNCATED = 1, 2
 
 # Every symbol include/sparkbam.h declares (checked by tests/test_abi.py).
 EXPORTS = [
-    "sbh_ctx_create", "sbh_ctx_destroy", "sbh_last_error", "sbh_ctx_set_stream",
+    "sbh_ctx_create", "sbh_ctx_destroy", "sbh_last_error", "sbh_last_error_detail", "sbh_ctx_set_stream",
     "sbh_ctx_synchronize", "sbh_version", "sbh_host_alloc", "sbh_host_free", "sbh_header_make", "sbh_shard_create",
     "sbh_shard_destroy", "sbh_shard_comp_device_ptr", "sbh_find_block_start", "sbh_index",
     "sbh_get_blocks", "sbh_inflate", "sbh_read_flat", "sbh_flat_device_ptr", "sbh_flat_of",
@@ -100,12 +100,63 @@ class SbhRecordsOut(C.Structure):  # host buffers (sbh_records_out); NULL = not 
 
 
 class SparkBamError(RuntimeError):
-    """Maps an SBH_E_* status onto the reference's exception vocabulary."""
+    """Maps an SBH_E_* status onto the reference's exception vocabulary.  `fields` are the
+    values sbh_last_error_detail returned (what the reference's exception is built from)."""
 
-    def __init__(self, code, message=""):
+    def __init__(self, code, message="", fields=()):
         self.code = code
+        self.fields = tuple(fields)
         super().__init__(f"{STATUS_NAMES.get(code, code)}: {message}")
 
+
+class HeaderParseException(SparkBamError):
+    """bgzf/.../block/HeaderParseException.scala:6-11: HeaderParseException(idx, actual, expected)."""
+
+    def __init__(self, code, message="", fields=()):
+        super().__init__(code, message, fields)
+        _, self.idx, self.actual, self.expected = (list(fields) + [None] * 4)[:4]
+
+
+class HeaderSearchFailedException(SparkBamError):
+    """bgzf/.../block/HeaderSearchFailedException.scala:7-12: (path, start, positionsAttempted);
+    the library knows no path: the caller that does sets it (with_path)."""
+
+    def __init__(self, code, message="", fields=(), path=None):
+        super().__init__(code, message, fields)
+        self.start, self.positions_attempted = (list(fields) + [None] * 2)[:2]
+        self.path = path
+
+    def with_path(self, path):
+        self.path = path
+        return self
+
+
+class NoReadFoundException(SparkBamError):
+    """check/.../spark/FindRecordStart.scala:66-71: NoReadFoundException(path, start, maxReadSize)."""
+
+    def __init__(self, code, message="", fields=(), path=None):
+        super().__init__(code, message, fields)
+        self.start, self.max_read_size = (list(fields) + [None] * 2)[:2]
+        self.path = path
+
+    def with_path(self, path, start=None):
+        self.path = path
+        if start is not None:
+            self.start = start
+        return self
+
+
+# the status -> exception class the JNI shim throws (jni/sparkbam_jni.c EXCEPTIONS)
+EXCEPTION_CLASSES = {}  # filled below, after the status constants
+
+
+def error_for(code, message="", fields=()):
+    return EXCEPTION_CLASSES.get(code, SparkBamError)(code, message, fields)
+
+
+EXCEPTION_CLASSES.update({SBH_E_HEADER_PARSE: HeaderParseException,
+                          SBH_E_HEADER_SEARCH_FAILED: HeaderSearchFailedException,
+                          SBH_E_NO_READ_FOUND: NoReadFoundException})
 
 _lib = None
 
@@ -173,6 +224,8 @@ def lib():
     L.sbh_stage_times.restype = C.c_int
     L.sbh_last_error.argtypes = [P]
     L.sbh_last_error.restype = C.c_char_p
+    L.sbh_last_error_detail.argtypes = [P, PI32, C.POINTER(C.c_int64), I32]
+    L.sbh_last_error_detail.restype = I32
     L.sbh_version.argtypes = []
     L.sbh_version.restype = C.c_char_p
     for name in ("sbh_shard_comp_device_ptr", "sbh_flat_device_ptr"):

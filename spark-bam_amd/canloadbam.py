@@ -1,0 +1,194 @@
+"""Python twin of the Scala load-API facade (jni/Native.scala `GpuCanLoadBam`,
+`GpuSplitPartition`, `GpuIntervalsPartition`): the same C-ABI calls in the same order, per
+Spark task, so the tests can run the facade's exact call sequence on the GPU.
+
+The reference's partitioning is kept: one task per Hadoop FileSplit (`SplitRDD(FileSplits.
+asJava(path, splitSize))`, load/.../CanLoadBam.scala:205,314) for loadBam / loadSplitsAndReads /
+loadReadsAndPositions / loadReads, one per `cappedCostGroups` chunk group for loadBamIntervals
+(:105-112).  A task's records come back as a columnar `Reads` batch with a `vpos` column (the
+Scala facade builds htsjdk SAMRecords from the same record starts and bytes).
+
+Failures are the reference's exceptions: HeaderSearchFailedException(path, start,
+positionsAttempted) from FindBlockStart, NoReadFoundException(path, blockStart, maxReadSize) from
+FindRecordStart (check/.../spark/FindRecordStart.scala:11-30,66-71).
+"""
+import os
+
+import numpy as np
+
+from ._lib import (SBH_E_BAD_RECORD, SBH_E_NEED_HALO, SBH_E_NOT_FOUND, HeaderSearchFailedException,
+                   NoReadFoundException, SparkBamError)
+from .api import (DEFAULT_BGZF_BLOCKS_TO_CHECK, DEFAULT_MAX_READ_SIZE, DEFAULT_READS_TO_CHECK, Pos, Split,
+                  file_splits)
+from .api import DEFAULT_SPLIT_SIZE as DEFAULT_MAX_SPLIT_SIZE
+from .device import Context
+from .intervals import (DEFAULT_COMPRESSION_RATIO, _flat_of_pos, _vpos_of_flat, capped_cost_groups, chunk_size,
+                        get_interval_chunks, parse_loci, read_bai)
+from .intervals import DEFAULT_SPLIT_SIZE
+from .records import Reads, record_columns
+
+
+def _reader(path):
+    from .sharded import bytes_reader, file_reader
+    if isinstance(path, (bytes, bytearray, memoryview, np.ndarray)):
+        return bytes_reader(path), "<bytes>"
+    return file_reader(path), str(path)
+
+
+def _empty():
+    cols = record_columns()
+    cols["vpos"] = np.zeros(0, np.uint64)
+    return cols
+
+
+def split_partition(ctx, read, size, path, start, end, contigs, bgzf_blocks_to_check=DEFAULT_BGZF_BLOCKS_TO_CHECK,
+                    reads_to_check=DEFAULT_READS_TO_CHECK, max_read_size=DEFAULT_MAX_READ_SIZE, halo0=1 << 20):
+    """GpuSplitPartition: loadReadsAndPositions' body for the FileSplit [start, end)
+    (CanLoadBam.scala:316-356).  Returns the split's records (columns + vpos)."""
+    halo = halo0
+    while True:
+        sh = ctx.shard(read(start, min(size, end + halo)), file_offset=start, file_size=size)
+        try:
+            sh.set_contigs(contigs)  # (GpuShard's constructor)
+            try:
+                b = sh.find_block_start(start, bgzf_blocks_to_check)
+            except HeaderSearchFailedException as e:
+                raise e.with_path(path)
+            sh.index(b)  # indexAndInflate
+            sh.inflate()
+            owned = sh.flat_bound(end)
+            at_eof = sh.file_offset + sh.n == size
+            if not at_eof and owned == sh.flat_size:
+                raise SparkBamError(SBH_E_NEED_HALO, f"no block past {end} in the halo")
+            try:
+                first, _ = sh.find_record_start(0, reads_to_check, max_read_size)
+            except NoReadFoundException as e:
+                raise e.with_path(path, start=b)
+            if first >= owned:
+                return _empty()
+            sh.check_eager(0, owned, reads_to_check, want_bits=False)
+            cols = sh.records(first, owned)
+            cols["vpos"] = _vpos_of_flat(sh.blocks(), cols["flat"]) if cols["flat"].size else np.zeros(0, np.uint64)
+            return cols
+        except SparkBamError as e:
+            if e.code != SBH_E_NEED_HALO or end + halo >= size:
+                raise
+            halo *= 4
+        finally:
+            sh.close()
+
+
+def load_reads_and_positions(path, split_size=DEFAULT_MAX_SPLIT_SIZE,
+                             bgzf_blocks_to_check=DEFAULT_BGZF_BLOCKS_TO_CHECK,
+                             reads_to_check=DEFAULT_READS_TO_CHECK, max_read_size=DEFAULT_MAX_READ_SIZE, ctx=None):
+    """GpuCanLoadBam.loadReadsAndPositions: one partition per FileSplit, each a Reads batch
+    (its vpos column = the reference's Pos keys)."""
+    from .sharded import read_header
+    read, name = _reader(path)
+    size = read.size
+    own = ctx is None
+    ctx = ctx or Context(0)
+    try:
+        names, lens, _ = read_header(ctx, read, size)
+        parts = []
+        for start, end in file_splits(size, split_size):
+            cols = split_partition(ctx, read, size, name, start, end, lens, bgzf_blocks_to_check, reads_to_check,
+                                   max_read_size)
+            parts.append(Reads(cols, names))
+        return parts
+    finally:
+        if own:
+            ctx.close()
+
+
+def load_bam(path, split_size=DEFAULT_MAX_SPLIT_SIZE, bgzf_blocks_to_check=DEFAULT_BGZF_BLOCKS_TO_CHECK,
+             reads_to_check=DEFAULT_READS_TO_CHECK, max_read_size=DEFAULT_MAX_READ_SIZE, ctx=None):
+    """GpuCanLoadBam.loadBam = loadReadsAndPositions(...).values: the partitions' records."""
+    return load_reads_and_positions(path, split_size, bgzf_blocks_to_check, reads_to_check, max_read_size, ctx)
+
+
+def load_splits_and_reads(path, split_size=DEFAULT_MAX_SPLIT_SIZE, bgzf_blocks_to_check=DEFAULT_BGZF_BLOCKS_TO_CHECK,
+                          reads_to_check=DEFAULT_READS_TO_CHECK, max_read_size=DEFAULT_MAX_READ_SIZE, ctx=None):
+    """GpuCanLoadBam.loadSplitsAndReads (CanLoadBam.scala:268-302): BAMRecordRDD(splits, reads),
+    splits = the first record of every non-empty partition, sliding2 with Pos(fileSize, 0)."""
+    parts = load_reads_and_positions(path, split_size, bgzf_blocks_to_check, reads_to_check, max_read_size, ctx)
+    size = _reader(path)[0].size
+    firsts = [Pos.from_htsjdk(int(p.cols["vpos"][0])) for p in parts if p.n]
+    splits = [Split(a, b) for a, b in zip(firsts, firsts[1:] + [Pos(size, 0)])]
+    return splits, parts
+
+
+def load_reads(path, bgzf_blocks_to_check=DEFAULT_BGZF_BLOCKS_TO_CHECK, reads_to_check=DEFAULT_READS_TO_CHECK,
+               max_read_size=DEFAULT_MAX_READ_SIZE, split_size=DEFAULT_MAX_SPLIT_SIZE, ctx=None):
+    """GpuCanLoadBam.loadReads (CanLoadBam.scala:371-405): .bam through loadBam; the reference's
+    sam / cram branches are not on the GPU path."""
+    if isinstance(path, (str, os.PathLike)) and not str(path).endswith(".bam"):
+        raise SparkBamError(1, f"Can't load reads from path on the GPU path: {path} (sam / cram stay the reference's)")
+    return load_bam(path, split_size, bgzf_blocks_to_check, reads_to_check, max_read_size, ctx)
+
+
+def intervals_partition(ctx, read, size, chunks, intervals, contigs, reads_to_check=DEFAULT_READS_TO_CHECK,
+                        halo0=1 << 18, merge_gap=1 << 20):
+    """GpuIntervalsPartition: one chunk group's records (CanLoadBam.scala:120-154); chunks whose
+    block ranges lie within merge_gap share a shard, grown x4 while an answer needs more."""
+    groups = []
+    for c in chunks:
+        lo, hi = c.start.block_pos, c.end.block_pos
+        if groups and lo <= groups[-1][1] + merge_gap:
+            groups[-1][1] = max(groups[-1][1], hi)
+            groups[-1][2].append(c)
+        else:
+            groups.append([lo, hi, [c]])
+    out = []
+    for lo, hi, cs in groups:
+        halo = halo0
+        while True:
+            sh = ctx.shard(read(lo, min(size, hi + halo)), file_offset=lo, file_size=size)
+            try:
+                sh.set_contigs(contigs)  # (GpuShard's constructor)
+                sh.index(lo)  # indexAndInflate
+                sh.inflate()
+                fb = [_flat_of_pos(sh, c.start) for c in cs]
+                fe = [min(_flat_of_pos(sh, c.end), sh.flat_size) for c in cs]
+                if max(fe) > min(fb):
+                    sh.check_eager(min(fb), max(fe), reads_to_check, want_bits=False)
+                cols = sh.records_regions(list(zip(fb, fe)), intervals)
+                cols["vpos"] = _vpos_of_flat(sh.blocks(), cols["flat"]) if cols["flat"].size \
+                    else np.zeros(0, np.uint64)
+                out.append(cols)
+                break
+            except SparkBamError as e:
+                if e.code not in (SBH_E_NEED_HALO, SBH_E_NOT_FOUND, SBH_E_BAD_RECORD) or hi + halo >= size:
+                    raise
+                halo *= 4
+            finally:
+                sh.close()
+    return out
+
+
+def load_bam_intervals(path, intervals, split_size=DEFAULT_SPLIT_SIZE,
+                       estimated_compression_ratio=DEFAULT_COMPRESSION_RATIO, bai=None,
+                       reads_to_check=DEFAULT_READS_TO_CHECK, ctx=None):
+    """GpuCanLoadBam.loadBamIntervals(path, LociSet, splitSize, ratio): one partition per
+    cappedCostGroups chunk group (getNumPartitions = max(1, groups)), each a Reads batch."""
+    from .sharded import read_header
+    read, _ = _reader(path)
+    size = read.size
+    index = read_bai(bai if bai is not None else str(path) + ".bai")
+    own = ctx is None
+    ctx = ctx or Context(0)
+    try:
+        names, lens, _ = read_header(ctx, read, size)
+        names = list(names)
+        loci = parse_loci(intervals, dict(zip(names, (int(x) for x in lens))))
+        ivs = sorted((names.index(c), a, e) for c, rs in loci.items() for a, e in rs)
+        chunks = get_interval_chunks(index, loci, names)
+        groups = capped_cost_groups(chunks, lambda c: chunk_size(c, estimated_compression_ratio), float(split_size))
+        parts = []
+        for g in groups:
+            batches = intervals_partition(ctx, read, size, g, ivs, lens, reads_to_check)
+            parts.append(Reads.concat([Reads(b, names) for b in batches], names))
+        return parts if parts else [Reads.concat([], names)]
+    finally:
+        if own:
+            ctx.close()

@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <initializer_list>
 #include <string>
 #include <vector>
 
@@ -93,6 +94,10 @@ struct sbh_ctx {
   hipStream_t stream = nullptr;
   bool own_stream = false;
   std::string err;
+  // the last error's structured fields (sbh_last_error_detail): what the reference's exception
+  // is constructed from (e.g. HeaderParseException(idx, actual, expected))
+  int32_t err_code = 0, err_n = 0;
+  int64_t err_fields[4] = {0, 0, 0, 0};
   StreamCache *sc = nullptr;
 };
 
@@ -239,15 +244,33 @@ static void stream_cache_free(StreamCache *sc) {
   delete sc;
 }
 
-static int fail(sbh_ctx *ctx, int code, const char *fmt, ...) {
+static int vfail(sbh_ctx *ctx, int code, std::initializer_list<int64_t> fields, const char *fmt, va_list ap) {
   if (ctx) {
     char buf[512];
-    va_list ap;
-    va_start(ap, fmt);
     vsnprintf(buf, sizeof buf, fmt, ap);
-    va_end(ap);
     ctx->err = buf;
+    ctx->err_code = code;
+    ctx->err_n = 0;
+    for (int64_t f : fields)
+      if (ctx->err_n < 4) ctx->err_fields[ctx->err_n++] = f;
   }
+  return code;
+}
+
+static int fail(sbh_ctx *ctx, int code, const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vfail(ctx, code, {}, fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+// fail() with the fields the reference's exception takes (sbh_last_error_detail)
+static int fail_with(sbh_ctx *ctx, int code, std::initializer_list<int64_t> fields, const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vfail(ctx, code, fields, fmt, ap);
+  va_end(ap);
   return code;
 }
 
@@ -330,6 +353,14 @@ int sbh_ctx_destroy(sbh_ctx *ctx) {
 }
 
 const char *sbh_last_error(const sbh_ctx *ctx) { return ctx ? ctx->err.c_str() : "no context"; }
+
+int32_t sbh_last_error_detail(const sbh_ctx *ctx, int32_t *code, int64_t *fields, int32_t cap) {
+  if (!ctx) return 0;
+  if (code) *code = ctx->err_code;
+  const int32_t n = fields ? std::min(ctx->err_n, std::max(cap, 0)) : 0;
+  for (int32_t i = 0; i < n; ++i) fields[i] = ctx->err_fields[i];
+  return ctx->err_n;
+}
 
 int sbh_host_alloc(uint64_t n, void **out) {
   if (!out) return SBH_E_ARG;
@@ -468,8 +499,11 @@ int sbh_find_block_start(sbh_shard *sh, uint64_t start, int32_t k, uint64_t *out
   HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr, best, 8, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   const unsigned long long b = sh->h_ctr[0];
-  if (b == ~0ull) return fail(ctx, SBH_E_HEADER_SEARCH_FAILED, "no BGZF block start in [%llu, %llu)",
-                              (unsigned long long)start, (unsigned long long)(start + 65536));
+  // HeaderSearchFailedException(path, start, positionsAttempted): the search tried every
+  // pos < MAX_BLOCK_SIZE (FindBlockStart.scala:18-35)
+  if (b == ~0ull)
+    return fail_with(ctx, SBH_E_HEADER_SEARCH_FAILED, {(int64_t)start, 65536}, "no BGZF block start in [%llu, %llu)",
+                     (unsigned long long)start, (unsigned long long)(start + 65536));
   const uint32_t outcome = (uint32_t)(b & 0xff);
   const uint64_t pos = b >> 8;
   if (outcome == 2) return fail(ctx, SBH_E_TRUNCATED, "truncated BGZF block near %llu", (unsigned long long)(start + pos));
@@ -493,8 +527,16 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
   // the start must itself be a header (its 18 bytes come back with the candidate count)
   uint8_t *h18 = reinterpret_cast<uint8_t *>(sh->h_ctr + 512);  // pinned
   auto start_is_header = [&]() -> int {
-    if (sbh_header_make(h18, 18, nullptr, nullptr) != SBH_OK)
-      return fail(ctx, SBH_E_HEADER_PARSE, "no BGZF header at %llu", (unsigned long long)start);
+    if (sbh_header_make(h18, 18, nullptr, nullptr) != SBH_OK) {
+      // HeaderParseException(idx, actual, expected): the first byte Header.make's checks
+      // reject, in its order (Header.scala:48-71)
+      static const uint8_t idx[7] = {0, 1, 2, 3, 12, 13, 14}, want[7] = {31, 139, 8, 4, 66, 67, 2};
+      int k = 0;
+      while (k < 6 && h18[idx[k]] == want[k]) ++k;
+      return fail_with(ctx, SBH_E_HEADER_PARSE, {(int64_t)start, idx[k], (int8_t)h18[idx[k]], (int8_t)want[k]},
+                       "Position %d: %d != %d (BGZF header at %llu)", idx[k], (int8_t)h18[idx[k]], (int8_t)want[k],
+                       (unsigned long long)start);
+    }
     return SBH_OK;
   };
   if (rel + 18 <= n) HIPCHK(ctx, hipMemcpyAsync(h18, sh->comp.p + rel, 18, hipMemcpyDeviceToHost, st));
@@ -624,10 +666,11 @@ static int inflate_status(sbh_shard *sh, hipStream_t st, uint64_t *bad_block, co
   if (bad_block) *bad_block = i;
   const sbh_block &b = sh->hb[i];
   if (*hs == INF_SIZE)
-    return fail(ctx, SBH_E_INFLATE_SIZE, "block %llu: expected %u decompressed bytes", (unsigned long long)b.start,
-                b.usize);
+    return fail_with(ctx, SBH_E_INFLATE_SIZE, {(int64_t)b.start, b.usize},
+                     "Expected %u decompressed bytes (block %llu)", b.usize, (unsigned long long)b.start);
   if (*hs == INF_BAD_ISIZE) return fail(ctx, SBH_E_BAD_ISIZE, "block %llu: ISIZE %u", (unsigned long long)b.start, b.usize);
-  return fail(ctx, SBH_E_INFLATE_DATA, "block %llu: invalid deflate data", (unsigned long long)b.start);
+  return fail_with(ctx, SBH_E_INFLATE_DATA, {(int64_t)b.start}, "block %llu: invalid deflate data",
+                   (unsigned long long)b.start);
 }
 
 static DevBlocks blocks_from(DevBlocks d, uint64_t b) {
@@ -1013,8 +1056,8 @@ int sbh_find_record_start(sbh_shard *sh, uint64_t from, int32_t rtc, int32_t max
   }
   if (lo >= seg && seg_is_open(sh, from) && (uint64_t)max_read_size > seg - from)
     return fail(ctx, SBH_E_NEED_HALO, "record search from %llu runs past the shard", (unsigned long long)from);
-  return fail(ctx, SBH_E_NO_READ_FOUND, "no read start within %d positions of flat %llu", max_read_size,
-              (unsigned long long)from);
+  return fail_with(ctx, SBH_E_NO_READ_FOUND, {(int64_t)from, max_read_size},
+                   "no read start within %d positions of flat %llu", max_read_size, (unsigned long long)from);
 }
 
 // Records of the chain from `first` whose start is < E; *exit_flat (optional) = the
@@ -1130,11 +1173,13 @@ int sbh_split(sbh_shard *sh, uint64_t start, uint64_t end, int32_t k, int32_t rt
   const int64_t bi = block_index_of(sh, b);
   if (bi < 0) {
     if (b >= sh->file_size || (sh->at_eof && b >= sh->file_off + sh->n))
-      return fail(ctx, SBH_E_NO_READ_FOUND, "split at %llu: no blocks left", (unsigned long long)start);
+      return fail_with(ctx, SBH_E_NO_READ_FOUND, {(int64_t)start, mrs}, "split at %llu: no blocks left",
+                       (unsigned long long)start);
     return fail(ctx, SBH_E_NOT_FOUND, "block start %llu is not on the indexed chain", (unsigned long long)b);
   }
   if (sh->hb[bi].flags & SBH_BLOCK_EMPTY)  // the stream from an empty block ends at once
-    return fail(ctx, SBH_E_NO_READ_FOUND, "split at %llu starts at an empty block", (unsigned long long)start);
+    return fail_with(ctx, SBH_E_NO_READ_FOUND, {(int64_t)start, mrs}, "split at %llu starts at an empty block",
+                     (unsigned long long)start);
   uint64_t first = 0;
   int32_t delta = 0;
   rc = sbh_find_record_start(sh, sh->hb[bi].ustart, rtc, mrs, &first, &delta);

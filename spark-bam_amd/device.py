@@ -7,13 +7,19 @@ import numpy as np
 from .records import record_columns
 
 from ._lib import (SBH_OK, SbhBlock, SbhCheckOpts, SbhCheckResult, SbhRecordsOut, SbhRecordsSizes,
-                   SbhShardResult, SbhStreamOpts, SbhStreamResult, SparkBamError, lib)
+                   SbhShardResult, SbhStreamOpts, SbhStreamResult, SparkBamError, error_for, lib)
 
 
 def _check(ctx_handle, rc):
     if rc != SBH_OK:
         msg = lib().sbh_last_error(ctx_handle) if ctx_handle else b""
-        raise SparkBamError(rc, (msg or b"").decode(errors="replace"))
+        fields = ()
+        if ctx_handle:
+            code, f = C.c_int32(), (C.c_int64 * 4)()
+            n = lib().sbh_last_error_detail(ctx_handle, C.byref(code), f, 4)
+            if code.value == rc:
+                fields = tuple(f[:min(n, 4)])
+        raise error_for(rc, (msg or b"").decode(errors="replace"), fields)
 
 
 def _ptr(a):

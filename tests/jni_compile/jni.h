@@ -7,10 +7,12 @@
 #include <stdint.h>
 typedef int32_t jint;
 typedef int64_t jlong;
+typedef int8_t jbyte;
 typedef unsigned char jboolean;
 typedef jint jsize;
 typedef struct _jobject *jobject;
-typedef jobject jclass, jarray, jlongArray, jintArray, jobjectArray;
+typedef jobject jclass, jarray, jlongArray, jintArray, jobjectArray, jstring, jthrowable;
+typedef struct _jmethodID *jmethodID;
 #define JNIEXPORT __attribute__((visibility("default")))
 #define JNICALL
 #define JNI_ABORT 2
@@ -28,5 +30,13 @@ struct JNINativeInterface_ {
   jint *(*GetIntArrayElements)(JNIEnv *, jintArray, unsigned char *);
   void (*ReleaseIntArrayElements)(JNIEnv *, jintArray, jint *, jint);
   jobject (*GetObjectArrayElement)(JNIEnv *, jobjectArray, jsize);
+  jmethodID (*GetMethodID)(JNIEnv *, jclass, const char *, const char *);
+  jobject (*NewObject)(JNIEnv *, jclass, jmethodID, ...);
+  jint (*Throw)(JNIEnv *, jthrowable);
+  jstring (*NewStringUTF)(JNIEnv *, const char *);
+  jlongArray (*NewLongArray)(JNIEnv *, jsize);
+  const char *(*GetStringUTFChars)(JNIEnv *, jstring, jboolean *);
+  void (*ReleaseStringUTFChars)(JNIEnv *, jstring, const char *);
+  void (*GetIntArrayRegion)(JNIEnv *, jintArray, jsize, jsize, jint *);
 };
 #endif
