@@ -15,7 +15,7 @@
 
 #include <hip/hip_runtime.h>
 
-#include "../../include/sparkbam.h"
+#include "sbh_internal.h"
 
 namespace {
 
@@ -161,20 +161,63 @@ int sbh_check_stream(sbh_ctx *ctx, const void *host_file, uint64_t file_size, co
     *v = bp << 16 | off;
     return r;
   };
+  // window k: the listed blocks [i, j) starting in [B[i], B[i] + window), loaded with a halo
+  // past the last one, and its truth slice (the `.records` of those blocks)
+  auto window_end = [&](uint64_t i) {
+    uint64_t j = i + 1;
+    while (j < nb && B[j] < B[i] + window) ++j;
+    return j;
+  };
+  auto truth_slice = [&](uint64_t lo, uint64_t last, uint64_t *t0, uint64_t *t1) {
+    const uint64_t *T = o->truth_vpos;
+    *t0 = truth ? (uint64_t)(std::lower_bound(T, T + o->n_truth, lo << 16) - T) : 0;
+    *t1 = truth ? (uint64_t)(std::lower_bound(T, T + o->n_truth, (last + 1) << 16) - T) : 0;
+  };
+  // The next window's bytes (and truth slice) are copied by a host thread while this window's
+  // kernels run (sbh::shard_prefetch); a window redone with a larger halo loads synchronously.
+  struct PrefetchGuard {  // no copy thread outlives the call
+    sbh_shard *sh;
+    ~PrefetchGuard() {
+      if (sbh::shard_prefetch_pending(sh, nullptr, nullptr)) (void)sbh::shard_prefetch_finish(sh, false);
+    }
+  } pf_guard{sh};
   for (uint64_t i = 0; i < nb;) {
     const uint64_t lo = B[i];
-    uint64_t j = i + 1;
-    while (j < nb && B[j] < lo + window) ++j;
+    const uint64_t j = window_end(i);
     const uint64_t last = B[j - 1];
+    uint64_t t0i = 0, t1i = 0;
+    truth_slice(lo, last, &t0i, &t1i);
     for (;;) {  // this window, grown until its answers fit the halo
       const uint64_t ld = std::min(file_size, last + halo);
       const bool at_eof = ld == file_size;
       A = Acc{};
       A.counts.assign(SBH_NNZ_MAX * 19, 0);
       A.rbe.assign(SBH_NNZ_MAX * SBH_RBE_MAX, 0);
-      const auto th = Clock::now();
-      rc = sbh_shard_load(sh, src + lo, ld - lo, lo, 0);
-      res->ms_h2d += ms_since(th);
+      uint64_t poff = 0, pn = 0;
+      bool truth_resident = false;
+      if (sbh::shard_prefetch_pending(sh, &poff, &pn)) {
+        const bool use = poff == lo && pn == ld - lo;
+        double cms = 0;
+        rc = sbh::shard_prefetch_finish(sh, use, &cms);
+        res->ms_h2d += cms;
+        truth_resident = use && truth;
+        if (!rc && !use) {
+          const auto th = Clock::now();
+          rc = sbh_shard_load(sh, src + lo, ld - lo, lo, 0);
+          res->ms_h2d += ms_since(th);
+        }
+      } else {
+        const auto th = Clock::now();
+        rc = sbh_shard_load(sh, src + lo, ld - lo, lo, 0);
+        res->ms_h2d += ms_since(th);
+      }
+      if (!rc && j < nb) {  // the next window starts copying now
+        const uint64_t lo2 = B[j], last2 = B[window_end(j) - 1];
+        const uint64_t ld2 = std::min(file_size, last2 + halo);
+        uint64_t u0 = 0, u1 = 0;
+        truth_slice(lo2, last2, &u0, &u1);
+        rc = sbh::shard_prefetch(sh, src + lo2, ld2 - lo2, lo2, truth ? o->truth_vpos + u0 : nullptr, u1 - u0);
+      }
       uint64_t nblk = 0;
       if (!rc) rc = sbh_index(sh, lo, &nblk, nullptr);
       std::vector<sbh_block> t;
@@ -199,13 +242,13 @@ int sbh_check_stream(sbh_ctx *ctx, const void *host_file, uint64_t file_size, co
       // eager calls, against the truth when given
       if (!rc && truth) {
         const uint64_t *T = o->truth_vpos;
-        const uint64_t t0i = (uint64_t)(std::lower_bound(T, T + o->n_truth, lo << 16) - T);
-        const uint64_t t1i = (uint64_t)(std::lower_bound(T, T + o->n_truth, (last + 1) << 16) - T);
         fl.assign(o->fp_cap + 1, 0);
         fl2.assign(o->fn_cap + 1, 0);
         uint64_t r4[4] = {0, 0, 0, 0};
-        rc = sbh_check_records(sh, rb.data(), re.data(), rb.size(), rtc, T + t0i, t1i - t0i, r4, fl.data(), o->fp_cap,
-                               fl2.data(), o->fn_cap);
+        rc = truth_resident ? sbh::check_records_resident(sh, rb.data(), re.data(), rb.size(), rtc, t1i - t0i, r4,
+                                                          fl.data(), o->fp_cap, fl2.data(), o->fn_cap)
+                            : sbh_check_records(sh, rb.data(), re.data(), rb.size(), rtc, T + t0i, t1i - t0i, r4,
+                                                fl.data(), o->fp_cap, fl2.data(), o->fn_cap);
         if (!rc) {
           A.tp = r4[0], A.fp = r4[1], A.fn = r4[2], A.unk = r4[3];
           A.n_true = A.tp + A.fp;

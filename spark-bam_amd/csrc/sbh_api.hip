@@ -10,6 +10,7 @@
 #include <functional>
 #include <initializer_list>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "sbh_internal.h"
@@ -210,6 +211,16 @@ struct sbh_shard {
   DBuf<unsigned long long> sp_count;
   DBuf<uint32_t> tbits;
   DBuf<uint64_t> t_rb, t_re, t_fp, t_fn;
+  // the next window prefetched by a host thread (shard_prefetch): spare compressed bytes and
+  // a u64 array riding with them (check-bam's truth slice; sp_vpos once used)
+  DBuf<uint8_t> comp2;
+  DBuf<uint64_t> aux2;
+  std::thread pf;
+  hipStream_t pf_stream = nullptr;
+  hipError_t pf_err = hipSuccess;
+  bool pf_active = false;
+  uint64_t pf_off = 0, pf_n = 0, pf_naux = 0;
+  double pf_ms = 0;  // the copy's wall time on its thread
   hipEvent_t ev[9] = {};
   bool ev_ok = false, timing = false;
   double stage_ms[6] = {0, 0, 0, 0, 0, 0};
@@ -426,6 +437,7 @@ int sbh_shard_create(sbh_ctx *ctx, const void *src, uint64_t n, uint64_t file_of
 
 int sbh_shard_destroy(sbh_shard *sh) {
   if (!sh) return SBH_OK;
+  if (sh->pf_active) (void)shard_prefetch_finish(sh, false);
   (void)hipSetDevice(sh->ctx->device);
   (void)hipStreamSynchronize(sh->ctx->stream);
   sh->comp.release();
@@ -438,6 +450,8 @@ int sbh_shard_destroy(sbh_shard *sh) {
   sh->tmp.release(); sh->J0.release(); sh->J1.release(); sh->on.release(); sh->d_seg.release();
   sh->U.release(); sh->ctg.release(); sh->bits.release(); sh->words.release(); sh->close_pos.release();
   sh->close_word.release(); sh->ctr.release(); sh->opix.release(); sh->tsum.release();
+  sh->comp2.release(); sh->aux2.release();
+  if (sh->pf_stream) (void)hipStreamDestroy(sh->pf_stream);
   for (hipEvent_t &e : sh->ev)
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t &e : sh->pev)
@@ -483,6 +497,79 @@ int sbh_shard_load(sbh_shard *sh, const void *src, uint64_t n, uint64_t file_off
   sh->nblocks = sh->utotal = 0;
   return SBH_OK;
 }
+
+}  // extern "C"
+
+namespace sbh {
+
+int shard_prefetch(sbh_shard *sh, const void *src, uint64_t n, uint64_t file_offset, const uint64_t *aux,
+                   uint64_t n_aux) {
+  if (!sh || (!src && n) || (!aux && n_aux) || file_offset + n > sh->file_size || sh->pf_active) return SBH_E_ARG;
+  sbh_ctx *ctx = sh->ctx;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  // buffers are sized here, on the calling thread (the copy thread only copies)
+  HIPCHK(ctx, sh->comp2.ensure(n + sh->pad));
+  HIPCHK(ctx, sh->aux2.ensure(n_aux + 1));
+  if (!sh->pf_stream) HIPCHK(ctx, hipStreamCreateWithFlags(&sh->pf_stream, hipStreamNonBlocking));
+  sh->pf_active = true;
+  sh->pf_off = file_offset, sh->pf_n = n, sh->pf_naux = n_aux;
+  sh->pf_err = hipSuccess;
+  const int dev = ctx->device;
+  uint8_t *dst = sh->comp2.p;
+  uint64_t *adst = sh->aux2.p;
+  const uint64_t pad = sh->pad;
+  hipStream_t cs = sh->pf_stream;
+  // host memory that is not page-locked makes hipMemcpyAsync return only once copied: a thread
+  // of its own keeps the caller's kernels going meanwhile
+  sh->pf = std::thread([=]() {
+    const auto t0 = std::chrono::steady_clock::now();
+    hipError_t e = hipSetDevice(dev);
+    if (e == hipSuccess && n) e = hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, cs);
+    if (e == hipSuccess) e = hipMemsetAsync(dst + n, 0, pad, cs);
+    if (e == hipSuccess && n_aux) e = hipMemcpyAsync(adst, aux, 8 * n_aux, hipMemcpyHostToDevice, cs);
+    if (e == hipSuccess) e = hipStreamSynchronize(cs);
+    sh->pf_err = e;
+    sh->pf_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  });
+  return SBH_OK;
+}
+
+bool shard_prefetch_pending(const sbh_shard *sh, uint64_t *file_offset, uint64_t *n) {
+  if (!sh || !sh->pf_active) return false;
+  if (file_offset) *file_offset = sh->pf_off;
+  if (n) *n = sh->pf_n;
+  return true;
+}
+
+int shard_prefetch_finish(sbh_shard *sh, bool use, double *copy_ms) {
+  if (!sh || !sh->pf_active) return SBH_E_STATE;
+  sbh_ctx *ctx = sh->ctx;
+  if (sh->pf.joinable()) sh->pf.join();
+  sh->pf_active = false;
+  if (copy_ms) *copy_ms = sh->pf_ms;
+  if (sh->pf_err != hipSuccess) return fail(ctx, SBH_E_HIP, "window prefetch: %s", hipGetErrorString(sh->pf_err));
+  if (!use) return SBH_OK;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));  // (no kernel may still read the old bytes)
+  std::swap(sh->comp, sh->comp2);
+  std::swap(sh->sp_vpos, sh->aux2);
+  sh->file_off = sh->pf_off;
+  sh->n = sh->pf_n;
+  sh->at_eof = sh->file_off + sh->n == sh->file_size;
+  sh->indexed = sh->inflated = sh->bits_valid = sh->chain_ok = sh->cm_valid = false;
+  sh->rec.valid = false;
+  sh->ncand = 0;
+  sh->scan_from = ~0ull;
+  sh->hb.clear();
+  sh->nblocks = sh->utotal = 0;
+  return SBH_OK;
+}
+
+}  // namespace sbh
+
+extern "C" {
 
 const void *sbh_shard_comp_device_ptr(sbh_shard *sh) { return sh ? sh->comp.p : nullptr; }
 
@@ -1342,10 +1429,36 @@ int sbh_split_starts(sbh_shard *sh, const uint64_t *starts, const uint64_t *ends
 // (optional) receive up to fp_cap / fn_cap mismatching flat positions, sorted: all of them
 // when there are at most that many, otherwise an arbitrary subset (the compaction is in
 // atomic order), not the first ones by position.
+static int check_records_impl(sbh_shard *sh, const uint64_t *range_begin, const uint64_t *range_end,
+                              uint64_t n_ranges, int32_t rtc, const uint64_t *rec_vpos, uint64_t n_rec,
+                              bool resident, uint64_t *out, uint64_t *fp_flat, uint64_t fp_cap, uint64_t *fn_flat,
+                              uint64_t fn_cap);
+
 int sbh_check_records(sbh_shard *sh, const uint64_t *range_begin, const uint64_t *range_end, uint64_t n_ranges,
                       int32_t rtc, const uint64_t *rec_vpos, uint64_t n_rec, uint64_t *out /*tp, fp, fn, unknown*/,
                       uint64_t *fp_flat, uint64_t fp_cap, uint64_t *fn_flat, uint64_t fn_cap) {
   if (!sh || !out || (n_ranges && (!range_begin || !range_end)) || (n_rec && !rec_vpos)) return SBH_E_ARG;
+  return check_records_impl(sh, range_begin, range_end, n_ranges, rtc, rec_vpos, n_rec, false, out, fp_flat, fp_cap,
+                            fn_flat, fn_cap);
+}
+
+}  // extern "C"
+
+int sbh::check_records_resident(sbh_shard *sh, const uint64_t *range_begin, const uint64_t *range_end,
+                                uint64_t n_ranges, int32_t rtc, uint64_t n_rec, uint64_t *out, uint64_t *fp_flat,
+                                uint64_t fp_cap, uint64_t *fn_flat, uint64_t fn_cap) {
+  if (!sh || !out || (n_ranges && (!range_begin || !range_end)) || (n_rec && sh->sp_vpos.cap < n_rec))
+    return SBH_E_ARG;
+  return check_records_impl(sh, range_begin, range_end, n_ranges, rtc, nullptr, n_rec, true, out, fp_flat, fp_cap,
+                            fn_flat, fn_cap);
+}
+
+extern "C" {
+
+static int check_records_impl(sbh_shard *sh, const uint64_t *range_begin, const uint64_t *range_end,
+                              uint64_t n_ranges, int32_t rtc, const uint64_t *rec_vpos, uint64_t n_rec,
+                              bool resident, uint64_t *out, uint64_t *fp_flat, uint64_t fp_cap, uint64_t *fn_flat,
+                              uint64_t fn_cap) {
   sbh_ctx *ctx = sh->ctx;
   for (uint64_t r = 0; r < n_ranges; ++r)
     if (range_begin[r] > range_end[r] || (r && range_begin[r] < range_end[r - 1]))
@@ -1368,8 +1481,10 @@ int sbh_check_records(sbh_shard *sh, const uint64_t *range_begin, const uint64_t
   const uint64_t nw = (end - hb0 + 31) / 32;
   HIPCHK(ctx, sh->tbits.ensure(nw + 1));
   HIPCHK(ctx, hipMemsetAsync(sh->tbits.p, 0, 4 * (nw + 1), st));
-  HIPCHK(ctx, sh->sp_vpos.ensure(n_rec + 1));
-  if (n_rec) HIPCHK(ctx, hipMemcpyAsync(sh->sp_vpos.p, rec_vpos, 8 * n_rec, hipMemcpyHostToDevice, st));
+  if (!resident) {
+    HIPCHK(ctx, sh->sp_vpos.ensure(n_rec + 1));
+    if (n_rec) HIPCHK(ctx, hipMemcpyAsync(sh->sp_vpos.p, rec_vpos, 8 * n_rec, hipMemcpyHostToDevice, st));
+  }
   HIPCHK(ctx, sh->t_rb.ensure(n_ranges));
   HIPCHK(ctx, sh->t_re.ensure(n_ranges));
   HIPCHK(ctx, hipMemcpyAsync(sh->t_rb.p, range_begin, 8 * n_ranges, hipMemcpyHostToDevice, st));

@@ -239,4 +239,19 @@ hipError_t launch_truth_compare(const uint32_t *ebits, uint64_t ebegin, const ui
                                 unsigned long long *acc, uint64_t *fp_pos, uint64_t fp_cap, uint64_t *fn_pos,
                                 uint64_t fn_cap, hipStream_t st);
 
+// Host-side streaming over a shard (sbh_check_stream, check_stream.hip): the next window's
+// compressed bytes -- and optionally a host array of u64 riding with it (check-bam's truth
+// slice) -- copied into the shard's spare device buffers by a host thread while the current
+// window's kernels run.  shard_prefetch starts the copy; shard_prefetch_finish waits for it and,
+// with `use`, makes it the shard's bytes exactly as sbh_shard_load(src, n, file_offset) would
+// (the u64 array becomes the resident truth of check_records_resident); without, drops it.
+int shard_prefetch(sbh_shard *sh, const void *src, uint64_t n, uint64_t file_offset, const uint64_t *aux,
+                   uint64_t n_aux);
+int shard_prefetch_finish(sbh_shard *sh, bool use, double *copy_ms = nullptr);
+bool shard_prefetch_pending(const sbh_shard *sh, uint64_t *file_offset, uint64_t *n);
+// sbh_check_records with the truth already on the device (the prefetched u64 array, n_rec of it)
+int check_records_resident(sbh_shard *sh, const uint64_t *range_begin, const uint64_t *range_end, uint64_t n_ranges,
+                           int32_t rtc, uint64_t n_rec, uint64_t *out, uint64_t *fp_flat, uint64_t fp_cap,
+                           uint64_t *fn_flat, uint64_t fn_cap);
+
 }  // namespace sbh
