@@ -193,24 +193,19 @@ int sbh_check_stream(sbh_ctx *ctx, const void *host_file, uint64_t file_size, co
       A = Acc{};
       A.counts.assign(SBH_NNZ_MAX * 19, 0);
       A.rbe.assign(SBH_NNZ_MAX * SBH_RBE_MAX, 0);
+      // this window's bytes: the prefetch started during the previous window when it matches
+      // (a window redone with a larger halo does not), else a copy of its own (the same copy
+      // threads, waited for at once)
       uint64_t poff = 0, pn = 0;
-      bool truth_resident = false;
-      if (sbh::shard_prefetch_pending(sh, &poff, &pn)) {
-        const bool use = poff == lo && pn == ld - lo;
-        double cms = 0;
-        rc = sbh::shard_prefetch_finish(sh, use, &cms);
-        res->ms_h2d += cms;
-        truth_resident = use && truth;
-        if (!rc && !use) {
-          const auto th = Clock::now();
-          rc = sbh_shard_load(sh, src + lo, ld - lo, lo, 0);
-          res->ms_h2d += ms_since(th);
-        }
-      } else {
-        const auto th = Clock::now();
-        rc = sbh_shard_load(sh, src + lo, ld - lo, lo, 0);
-        res->ms_h2d += ms_since(th);
-      }
+      rc = SBH_OK;
+      if (sbh::shard_prefetch_pending(sh, &poff, &pn) && !(poff == lo && pn == ld - lo))
+        rc = sbh::shard_prefetch_finish(sh, false);
+      if (!rc && !sbh::shard_prefetch_pending(sh, nullptr, nullptr))
+        rc = sbh::shard_prefetch(sh, src + lo, ld - lo, lo, truth ? o->truth_vpos + t0i : nullptr, t1i - t0i);
+      double cms = 0;
+      if (!rc) rc = sbh::shard_prefetch_finish(sh, true, &cms);
+      res->ms_h2d += cms;
+      const bool truth_resident = truth;
       if (!rc && j < nb) {  // the next window starts copying now
         const uint64_t lo2 = B[j], last2 = B[window_end(j) - 1];
         const uint64_t ld2 = std::min(file_size, last2 + halo);

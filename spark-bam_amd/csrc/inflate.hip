@@ -2326,7 +2326,10 @@ __global__ __launch_bounds__(WAVE) void k_huff_tail(const uint8_t *__restrict__ 
 constexpr uint32_t LZ_TPT = SBH_LZ_TPT;                       // tokens per thread per chunk
 constexpr uint32_t LZ_CHUNK = LZ_THREADS * LZ_TPT;      // tokens per chunk
 constexpr uint32_t PTR_HALF = 8;                        // pointer slots per thread and pass
-constexpr uint32_t PTR_CAP = 7552;                      // bytes one pointer-chasing pass resolves
+#ifndef SBH_LZ_PTR_CAP
+#define SBH_LZ_PTR_CAP 7552
+#endif
+constexpr uint32_t PTR_CAP = SBH_LZ_PTR_CAP;            // bytes one pointer-chasing pass resolves
 constexpr uint32_t SB_WORDS = PTR_CAP / 32;             // token-start bitmap words
 constexpr uint32_t NHP = 2;                             // half granules (8 slots) per k_lz thread, at most
 static_assert(PTR_CAP <= NHP * LZ_THREADS * PTR_HALF, "slot pass covers the slots");
@@ -2336,8 +2339,8 @@ struct LzSmem {
   struct {
     uint16_t p16[PTR_CAP];     // per pass byte: its source pointer (token starts first)
     uint32_t sbits[SB_WORDS];  // per pass byte: starts a token (every byte of a long match)
-    uint32_t wsum[8];          // block_scan scratch
-    uint32_t wmin[8];          // block_min scratch (a pass cut)
+    uint32_t wsum[LZ_THREADS / WAVE];  // block_scan scratch
+    uint32_t wmin[LZ_THREADS / WAVE];  // block_min scratch (a pass cut)
   } pp;
 };
 // two workgroups per CU, counting the 256 B of LDS the compiler adds
@@ -2495,7 +2498,10 @@ __device__ __forceinline__ void chase8_asm(uint32_t (&c)[8], uint32_t pend, uint
 // passes of at most PTR_CAP bytes, each cut at a token start, so every chunk takes the
 // pointer path (the dependency-rounds fallback this replaced cost ~100 k cycles per
 // overflowing chunk: 2-4 per block of long-read data).
-__global__ __launch_bounds__(LZ_THREADS, 4) void k_lz(const uint8_t *__restrict__ comp, DevBlocks bl, uint64_t nblocks,
+#ifndef SBH_LZ_WAVES_PER_EU
+#define SBH_LZ_WAVES_PER_EU 4  // (the register budget: 512 VGPRs / waves per SIMD)
+#endif
+__global__ __launch_bounds__(LZ_THREADS, SBH_LZ_WAVES_PER_EU) void k_lz(const uint8_t *__restrict__ comp, DevBlocks bl, uint64_t nblocks,
                                                     const uint32_t *__restrict__ tok, uint8_t *__restrict__ U) {
   __shared__ LzSmem sm;
   uint32_t *wsum = sm.pp.wsum;

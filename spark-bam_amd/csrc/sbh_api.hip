@@ -215,12 +215,12 @@ struct sbh_shard {
   // a u64 array riding with them (check-bam's truth slice; sp_vpos once used)
   DBuf<uint8_t> comp2;
   DBuf<uint64_t> aux2;
-  std::thread pf;
-  hipStream_t pf_stream = nullptr;
-  hipError_t pf_err = hipSuccess;
+  std::vector<std::thread> pf;
+  std::vector<hipStream_t> pf_stream;
+  std::vector<hipError_t> pf_err;
   bool pf_active = false;
   uint64_t pf_off = 0, pf_n = 0, pf_naux = 0;
-  double pf_ms = 0;  // the copy's wall time on its thread
+  std::vector<double> pf_ms;  // each copy thread's wall time
   hipEvent_t ev[9] = {};
   bool ev_ok = false, timing = false;
   double stage_ms[6] = {0, 0, 0, 0, 0, 0};
@@ -451,7 +451,7 @@ int sbh_shard_destroy(sbh_shard *sh) {
   sh->U.release(); sh->ctg.release(); sh->bits.release(); sh->words.release(); sh->close_pos.release();
   sh->close_word.release(); sh->ctr.release(); sh->opix.release(); sh->tsum.release();
   sh->comp2.release(); sh->aux2.release();
-  if (sh->pf_stream) (void)hipStreamDestroy(sh->pf_stream);
+  for (hipStream_t st : sh->pf_stream) (void)hipStreamDestroy(st);
   for (hipEvent_t &e : sh->ev)
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t &e : sh->pev)
@@ -502,36 +502,58 @@ int sbh_shard_load(sbh_shard *sh, const void *src, uint64_t n, uint64_t file_off
 
 namespace sbh {
 
+// copy threads per prefetch (SBH_PREFETCH_THREADS, default 4): host memory that is not
+// page-locked is staged by the runtime on the calling thread, so one thread's copy runs at that
+// thread's memcpy rate; several threads on their own streams copy disjoint parts of the window
+static uint32_t prefetch_threads() {
+  const char *e = std::getenv("SBH_PREFETCH_THREADS");
+  const long v = e ? std::atol(e) : 4;
+  return (uint32_t)std::min<long>(std::max<long>(v, 1), 16);
+}
+
 int shard_prefetch(sbh_shard *sh, const void *src, uint64_t n, uint64_t file_offset, const uint64_t *aux,
                    uint64_t n_aux) {
   if (!sh || (!src && n) || (!aux && n_aux) || file_offset + n > sh->file_size || sh->pf_active) return SBH_E_ARG;
   sbh_ctx *ctx = sh->ctx;
   int rc = set_device(ctx);
   if (rc) return rc;
-  // buffers are sized here, on the calling thread (the copy thread only copies)
+  // buffers are sized here, on the calling thread (the copy threads only copy)
   HIPCHK(ctx, sh->comp2.ensure(n + sh->pad));
   HIPCHK(ctx, sh->aux2.ensure(n_aux + 1));
-  if (!sh->pf_stream) HIPCHK(ctx, hipStreamCreateWithFlags(&sh->pf_stream, hipStreamNonBlocking));
+  const uint32_t nt = prefetch_threads();
+  while (sh->pf_stream.size() < nt) {
+    hipStream_t st = nullptr;
+    HIPCHK(ctx, hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    sh->pf_stream.push_back(st);
+  }
   sh->pf_active = true;
   sh->pf_off = file_offset, sh->pf_n = n, sh->pf_naux = n_aux;
-  sh->pf_err = hipSuccess;
+  sh->pf_err.assign(nt, hipSuccess);
+  sh->pf_ms.assign(nt, 0.0);
+  sh->pf.clear();
   const int dev = ctx->device;
   uint8_t *dst = sh->comp2.p;
   uint64_t *adst = sh->aux2.p;
-  const uint64_t pad = sh->pad;
-  hipStream_t cs = sh->pf_stream;
-  // host memory that is not page-locked makes hipMemcpyAsync return only once copied: a thread
-  // of its own keeps the caller's kernels going meanwhile
-  sh->pf = std::thread([=]() {
-    const auto t0 = std::chrono::steady_clock::now();
-    hipError_t e = hipSetDevice(dev);
-    if (e == hipSuccess && n) e = hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, cs);
-    if (e == hipSuccess) e = hipMemsetAsync(dst + n, 0, pad, cs);
-    if (e == hipSuccess && n_aux) e = hipMemcpyAsync(adst, aux, 8 * n_aux, hipMemcpyHostToDevice, cs);
-    if (e == hipSuccess) e = hipStreamSynchronize(cs);
-    sh->pf_err = e;
-    sh->pf_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  });
+  const uint64_t pad = sh->pad, part = (n / nt + 4095) & ~4095ull;
+  const auto t0 = std::chrono::steady_clock::now();
+  // (host memory that is not page-locked makes hipMemcpyAsync return only once copied: threads
+  // of their own keep the caller's kernels going meanwhile)
+  for (uint32_t k = 0; k < nt; ++k) {
+    const uint64_t lo = std::min(n, k * part), hi = k + 1 == nt ? n : std::min(n, (k + 1) * part);
+    hipStream_t cs = sh->pf_stream[k];
+    hipError_t *err = &sh->pf_err[k];
+    double *ms = &sh->pf_ms[k];
+    sh->pf.emplace_back([=]() {
+      hipError_t e = hipSetDevice(dev);
+      if (e == hipSuccess && hi > lo)
+        e = hipMemcpyAsync(dst + lo, static_cast<const uint8_t *>(src) + lo, hi - lo, hipMemcpyHostToDevice, cs);
+      if (e == hipSuccess && k == 0) e = hipMemsetAsync(dst + n, 0, pad, cs);
+      if (e == hipSuccess && k == 0 && n_aux) e = hipMemcpyAsync(adst, aux, 8 * n_aux, hipMemcpyHostToDevice, cs);
+      if (e == hipSuccess) e = hipStreamSynchronize(cs);
+      *err = e;
+      *ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    });
+  }
   return SBH_OK;
 }
 
@@ -545,10 +567,13 @@ bool shard_prefetch_pending(const sbh_shard *sh, uint64_t *file_offset, uint64_t
 int shard_prefetch_finish(sbh_shard *sh, bool use, double *copy_ms) {
   if (!sh || !sh->pf_active) return SBH_E_STATE;
   sbh_ctx *ctx = sh->ctx;
-  if (sh->pf.joinable()) sh->pf.join();
+  for (std::thread &th : sh->pf)
+    if (th.joinable()) th.join();
+  sh->pf.clear();
   sh->pf_active = false;
-  if (copy_ms) *copy_ms = sh->pf_ms;
-  if (sh->pf_err != hipSuccess) return fail(ctx, SBH_E_HIP, "window prefetch: %s", hipGetErrorString(sh->pf_err));
+  if (copy_ms) *copy_ms = sh->pf_ms.empty() ? 0.0 : *std::max_element(sh->pf_ms.begin(), sh->pf_ms.end());
+  for (hipError_t e : sh->pf_err)
+    if (e != hipSuccess) return fail(ctx, SBH_E_HIP, "window prefetch: %s", hipGetErrorString(e));
   if (!use) return SBH_OK;
   int rc = set_device(ctx);
   if (rc) return rc;
