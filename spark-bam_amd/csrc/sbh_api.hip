@@ -506,16 +506,22 @@ int sbh_shard_load(sbh_shard *sh, const void *src, uint64_t n, uint64_t file_off
 
 namespace sbh {
 
-// copy threads per prefetch (SBH_PREFETCH_THREADS, default 4).  Host memory that is not
-// page-locked (a mapped file, a numpy array) is copied through page-locked staging chunks: each
-// thread memcpys a chunk into its staging slot and DMAs it on its own stream while it fills the
-// next slot (2 slots of 8 MiB per thread).  hipMemcpyAsync straight from pageable memory ran at
-// ~46 GB/s whatever the number of threads (r05f: the runtime's own staging); page-locked host
-// memory is DMAed directly.
+// copy threads per prefetch (SBH_PREFETCH_THREADS, default 4), each hipMemcpyAsync-ing its
+// part on its own stream.  SBH_PREFETCH_STAGE=1: host memory that is not page-locked (a mapped
+// file, a numpy array) goes through page-locked staging chunks instead -- each thread memcpys a
+// chunk into its slot and DMAs it while it fills the next (2 slots of 8 MiB per thread).  Measured
+// on configs[2]'s 100.9 GiB file (pageable numpy): direct 2.34 s of copies (r05f, ~46 GB/s, the
+// same with 1 or 4 threads), staged 2.32 s (r05h) and slower on a 5 GiB file (136 vs 118 ms):
+// the host's memory bandwidth share, not the runtime's staging, is the limit, so staging is off
+// by default.  Page-locked host memory is DMAed directly (~56 GB/s).
 static uint32_t prefetch_threads() {
   const char *e = std::getenv("SBH_PREFETCH_THREADS");
   const long v = e ? std::atol(e) : 4;
   return (uint32_t)std::min<long>(std::max<long>(v, 1), 16);
+}
+static bool prefetch_stage() {
+  const char *e = std::getenv("SBH_PREFETCH_STAGE");
+  return e && std::atol(e) == 1;
 }
 static constexpr uint32_t PF_SLOTS = 2;
 static constexpr uint64_t PF_CHUNK = 8ull << 20;
@@ -538,7 +544,8 @@ int shard_prefetch(sbh_shard *sh, const void *src, uint64_t n, uint64_t file_off
   hipPointerAttribute_t pa{};
   const bool pinned = n && hipPointerGetAttributes(&pa, src) == hipSuccess && pa.type == hipMemoryTypeHost;
   (void)hipGetLastError();
-  if (!pinned) {
+  const bool stage = !pinned && prefetch_stage();
+  if (stage) {
     while (sh->pf_pin.size() < (size_t)nt * PF_SLOTS) {
       void *p = nullptr;
       HIPCHK(ctx, hipHostMalloc(&p, PF_CHUNK, hipHostMallocDefault));
@@ -563,13 +570,13 @@ int shard_prefetch(sbh_shard *sh, const void *src, uint64_t n, uint64_t file_off
     hipStream_t cs = sh->pf_stream[k];
     hipError_t *err = &sh->pf_err[k];
     double *ms = &sh->pf_ms[k];
-    uint8_t *const *pin = pinned ? nullptr : sh->pf_pin.data() + (size_t)k * PF_SLOTS;
-    hipEvent_t *ev = pinned ? nullptr : sh->pf_ev.data() + (size_t)k * PF_SLOTS;
+    uint8_t *const *pin = stage ? sh->pf_pin.data() + (size_t)k * PF_SLOTS : nullptr;
+    hipEvent_t *ev = stage ? sh->pf_ev.data() + (size_t)k * PF_SLOTS : nullptr;
     sh->pf.emplace_back([=]() {
       uint32_t used = 0;  // staging chunks issued by this thread
       // [from, from + len) of host memory to device memory at to
       auto copy = [&](uint8_t *to, const uint8_t *from, uint64_t len) -> hipError_t {
-        if (pinned) return len ? hipMemcpyAsync(to, from, len, hipMemcpyHostToDevice, cs) : hipSuccess;
+        if (!stage) return len ? hipMemcpyAsync(to, from, len, hipMemcpyHostToDevice, cs) : hipSuccess;
         for (uint64_t o = 0; o < len; o += PF_CHUNK, ++used) {
           const uint32_t slot = used % PF_SLOTS;
           const uint64_t m = std::min(PF_CHUNK, len - o);
