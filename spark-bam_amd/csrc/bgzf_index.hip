@@ -212,10 +212,15 @@ constexpr int64_t TERM_END = -2;     // chain reaches the end of the resident by
 constexpr int64_t TERM_TRUNC = -3;   // block runs past the resident bytes
 constexpr int64_t TERM_BROKEN = -4;  // next offset is not a block header
 
-// Link each candidate to the candidate at (pos + csize).
+// Link each candidate to the candidate at (pos + csize).  (Thread 0 also zeroes the empty-block
+// count k_chain_emit keeps beside the next 18 bytes.)
 __global__ void k_cand_link(const uint8_t *comp, uint64_t n, const uint64_t *cand, uint64_t nc,
-                            int64_t *next) {
+                            int64_t *next, uint8_t *next18) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) {
+    *reinterpret_cast<uint32_t *>(next18 + NEXT18_NEMPTY) = 0;
+    next18[NEXT18_NONLIN] = 0;
+  }
   if (i >= nc) return;
   const uint64_t p = cand[i];
   const uint64_t cs = u16_at(comp, p + 16) + 1;
@@ -272,6 +277,34 @@ __global__ void k_mark_start(const uint64_t *cand, uint64_t nc, uint64_t start_r
   if (lo < nc && cand[lo] == start_rel) on[lo] = 1;
 }
 
+// The common chain: every candidate from the start on is the next one's predecessor (no
+// candidate inside a block's bytes, no break).  The start's index by binary search, then each
+// candidate's mark / rank directly -- no pointer-jumping rounds -- while every link is checked:
+// a candidate whose link is not the next candidate (or a last one that links on) sets
+// next18[NEXT18_NONLIN], and the host rebuilds the chain by pointer jumping (build_chain with
+// linear = false).  The marks and ranks equal the jumping path's whenever the flag stays clear.
+__global__ void k_linear_start(const uint64_t *cand, uint64_t nc, uint64_t start_rel, uint64_t *sidx) {
+  if (threadIdx.x != 0) return;
+  uint64_t lo = 0, hi = nc;
+  while (lo < hi) {
+    const uint64_t m = (lo + hi) >> 1;
+    if (cand[m] < start_rel) lo = m + 1;
+    else hi = m;
+  }
+  *sidx = lo < nc && cand[lo] == start_rel ? lo : nc;  // nc: the start is not a candidate (empty chain)
+}
+__global__ void k_linear_chain(const int64_t *J, const uint64_t *sidx, uint8_t *on, uint64_t *v, uint64_t *rank,
+                               uint64_t nc, uint8_t *next18) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nc) return;
+  const uint64_t s = *sidx;
+  const bool m = i >= s;
+  on[i] = m ? 1 : 0;
+  v[i] = m ? 1 : 0;
+  rank[i] = m ? i - s : 0;
+  if (m && (i + 1 < nc ? J[i] != (int64_t)(i + 1) : J[i] >= 0)) next18[NEXT18_NONLIN] = 1;
+}
+
 __global__ void k_mark_u64(const uint8_t *on, uint64_t *v, uint64_t nc) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nc) return;
@@ -280,7 +313,9 @@ __global__ void k_mark_u64(const uint8_t *on, uint64_t *v, uint64_t nc) {
 
 // Emit the chain as the block table (ordered by position).
 // (usz is zero beyond the chain, so the flat-offset scan may run over all nc entries; the chain
-// length is the last rank plus the last mark, read here rather than by the host)
+// length is the last rank plus the last mark, read here rather than by the host; the chain's
+// empty blocks are counted at next18 + NEXT18_NEMPTY, so that the host walks the table for its
+// segment ends only when there are any)
 __global__ void k_chain_emit(const uint8_t *comp, uint64_t n, const uint64_t *cand, const uint8_t *on,
                              const uint64_t *rank, const uint64_t *v, uint64_t nc, DevBlocks bl,
                              uint64_t *usz, uint8_t *next18) {
@@ -297,7 +332,10 @@ __global__ void k_chain_emit(const uint8_t *comp, uint64_t n, const uint64_t *ca
     flags |= BLK_TRUNCATED;
   } else {
     us = u32_at(comp, p + cs - 4);
-    if ((int32_t)cs - (int32_t)hs - 8 == 2) flags |= BLK_EMPTY;
+    if ((int32_t)cs - (int32_t)hs - 8 == 2) {
+      flags |= BLK_EMPTY;
+      atomicAdd(reinterpret_cast<uint32_t *>(next18 + NEXT18_NEMPTY), 1u);
+    }
   }
   bl.cstart[r] = p;
   bl.csize[r] = cs;
@@ -393,26 +431,32 @@ hipError_t launch_pack_blocks(DevBlocks bl, uint64_t n, uint64_t file_off, uint6
 
 hipError_t build_chain(const uint8_t *comp, uint64_t n, const uint64_t *cand, uint64_t nc, uint64_t start_rel,
                        int64_t *J0, int64_t *J1, uint8_t *on, uint64_t *v, uint64_t *rank, uint64_t *tmp,
-                       DevBlocks bl, uint64_t *usz, uint8_t *next18, hipStream_t st) {
+                       DevBlocks bl, uint64_t *usz, uint8_t *next18, uint64_t *sidx, bool linear, hipStream_t st) {
   if (nc == 0) return hipSuccess;
   const uint32_t T = 256;
-  hipLaunchKernelGGL(k_cand_link, dim3(nblk(nc, T)), dim3(T), 0, st, comp, n, cand, nc, J0);
-  hipError_t e = hipMemsetAsync(on, 0, nc, st);
-  if (e == hipSuccess) e = hipMemsetAsync(usz, 0, nc * sizeof(uint64_t), st);
+  hipLaunchKernelGGL(k_cand_link, dim3(nblk(nc, T)), dim3(T), 0, st, comp, n, cand, nc, J0, next18);
+  hipError_t e = hipMemsetAsync(usz, 0, nc * sizeof(uint64_t), st);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_mark_start, dim3(1), dim3(64), 0, st, cand, nc, start_rel, on);
-  int64_t *a = J0, *b = J1;
-  for (uint64_t span = 1; span < nc; span <<= 1) {
-    hipLaunchKernelGGL(k_jump_round, dim3(nblk(nc, T)), dim3(T), 0, st, a, b, on, nc);
-    int64_t *t = a;
-    a = b;
-    b = t;
+  if (linear) {  // (3 launches instead of ~log2(nc) + 6)
+    hipLaunchKernelGGL(k_linear_start, dim3(1), dim3(64), 0, st, cand, nc, start_rel, sidx);
+    hipLaunchKernelGGL(k_linear_chain, dim3(nblk(nc, T)), dim3(T), 0, st, J0, sidx, on, v, rank, nc, next18);
+  } else {
+    e = hipMemsetAsync(on, 0, nc, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_mark_start, dim3(1), dim3(64), 0, st, cand, nc, start_rel, on);
+    int64_t *a = J0, *b = J1;
+    for (uint64_t span = 1; span < nc; span <<= 1) {
+      hipLaunchKernelGGL(k_jump_round, dim3(nblk(nc, T)), dim3(T), 0, st, a, b, on, nc);
+      int64_t *t = a;
+      a = b;
+      b = t;
+    }
+    hipLaunchKernelGGL(k_jump_mark, dim3(nblk(nc, T)), dim3(T), 0, st, a, on, nc);
+    // ranks of marked nodes
+    hipLaunchKernelGGL(k_mark_u64, dim3(nblk(nc, T)), dim3(T), 0, st, on, v, nc);
+    e = scan_exclusive_u64(v, rank, nc, tmp, st);
+    if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(k_jump_mark, dim3(nblk(nc, T)), dim3(T), 0, st, a, on, nc);
-  // ranks of marked nodes
-  hipLaunchKernelGGL(k_mark_u64, dim3(nblk(nc, T)), dim3(T), 0, st, on, v, nc);
-  e = scan_exclusive_u64(v, rank, nc, tmp, st);
-  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_chain_emit, dim3(nblk(nc, T)), dim3(T), 0, st, comp, n, cand, on, rank, v, nc, bl, usz,
                      next18);
   return hipGetLastError();

@@ -2282,14 +2282,18 @@ __global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__rest
 #ifndef SBH_TAIL_DW
 #define SBH_TAIL_DW 256  // (A/B: 1024 -> 256 dwords: k_huff incl. tail 2.324 -> 2.214 ms at 4 M records; more tails per CU)
 #endif
-constexpr uint32_t TAIL_DW = SBH_TAIL_DW;
-using TailSmem = HuffSmemT<WAVE, TAIL_DW>;
-__global__ __launch_bounds__(WAVE) void k_huff_tail(const uint8_t *__restrict__ comp, DevBlocks bl, uint64_t nblocks,
-                                                    uint32_t *__restrict__ tok) {
+#ifndef SBH_TAIL_NT
+#define SBH_TAIL_NT 64  // lanes per tail (one wave; 128: the header's two tables built by two waves)
+#endif
+constexpr uint32_t TAIL_DW = SBH_TAIL_DW, TAIL_NT = SBH_TAIL_NT;
+static_assert(TAIL_NT % WAVE == 0 && TAIL_NT <= 256, "whole waves per tail");
+using TailSmem = HuffSmemT<TAIL_NT, TAIL_DW>;
+__global__ __launch_bounds__(TAIL_NT) void k_huff_tail(const uint8_t *__restrict__ comp, DevBlocks bl, uint64_t nblocks,
+                                                       uint32_t *__restrict__ tok) {
   __shared__ TailSmem sm;
   const uint64_t b = blockIdx.x;
   if (b >= nblocks || uni(bl.status[b]) != INF_TAIL) return;
-  const uint32_t lane = threadIdx.x;
+  const uint32_t tid = threadIdx.x, lane = tid & (WAVE - 1), wid = uni(tid / WAVE);
   const uint64_t cstart = bl.cstart[b];
   const uint32_t csize = bl.csize[b], hsize = bl.hsize[b], usize = bl.usize[b];
   const uint64_t G = bl.ustart[b];
@@ -2306,15 +2310,15 @@ __global__ __launch_bounds__(WAVE) void k_huff_tail(const uint8_t *__restrict__ 
   uint32_t n2 = 0, rc;
   if (ndw <= TAIL_DW) {
     const uint32_t *g = reinterpret_cast<const uint32_t *>(dbase);
-    for (uint32_t i = lane; i < ndw; i += WAVE) sm.stage[i] = g[i];
+    for (uint32_t i = tid; i < ndw; i += TAIL_NT) sm.stage[i] = g[i];
     __syncthreads();
-    rc = inflate_par<true>(sm, dbase, skip, limit, usize - out1, tk, lane, lane, 0, n2, false, 0, 0, out1, false,
+    rc = inflate_par<true>(sm, dbase, skip, limit, usize - out1, tk, tid, lane, wid, n2, false, 0, 0, out1, false,
                            nullptr, nullptr);
   } else {
-    rc = inflate_par<false>(sm, dbase, skip, limit, usize - out1, tk, lane, lane, 0, n2, false, 0, 0, out1, false,
+    rc = inflate_par<false>(sm, dbase, skip, limit, usize - out1, tk, tid, lane, wid, n2, false, 0, 0, out1, false,
                             nullptr, nullptr);
   }
-  if (lane == 0) {
+  if (tid == 0) {
     bl.status[b] = uni(rc) == PAR_OK ? INF_OK : INF_SERIAL;
     bl.ntok[b] = n1 + n2;
   }
@@ -2946,7 +2950,7 @@ hipError_t launch_huff(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, 
                      comp, blocks, nblocks, tok);
   hipLaunchKernelGGL(k_huff, dim3((uint32_t)nblocks), dim3(HT), 0, stream, comp, blocks, nblocks, tok);
 #if SBH_TAIL
-  hipLaunchKernelGGL(k_huff_tail, dim3((uint32_t)nblocks), dim3(WAVE), 0, stream, comp, blocks, nblocks, tok);
+  hipLaunchKernelGGL(k_huff_tail, dim3((uint32_t)nblocks), dim3(TAIL_NT), 0, stream, comp, blocks, nblocks, tok);
 #endif
   const uint64_t grid = (nblocks + WAVES - 1) / WAVES;
   hipLaunchKernelGGL(k_huff_serial<true>, dim3((uint32_t)grid), dim3(WAVES * WAVE), 0, stream, comp, blocks, nblocks,

@@ -58,7 +58,7 @@ hipError_t launch_cand_write(const uint8_t *comp, uint64_t n, uint64_t from, con
 hipError_t launch_pack_blocks(DevBlocks bl, uint64_t n, uint64_t file_off, uint64_t *out, hipStream_t st);
 hipError_t build_chain(const uint8_t *comp, uint64_t n, const uint64_t *cand, uint64_t nc, uint64_t start_rel,
                        int64_t *J0, int64_t *J1, uint8_t *on, uint64_t *v, uint64_t *rank, uint64_t *tmp,
-                       DevBlocks bl, uint64_t *usz, uint8_t *next18, hipStream_t st);
+                       DevBlocks bl, uint64_t *usz, uint8_t *next18, uint64_t *sidx, bool linear, hipStream_t st);
 hipError_t launch_eager(const uint8_t *U, uint64_t u_pad, uint64_t begin, uint64_t end, const uint64_t *seg_end,
                         uint32_t nseg, uint32_t open_last, const int32_t *ctg, int32_t nctg, int32_t rtc,
                         uint32_t *bits, unsigned long long *counters, hipStream_t st, uint64_t front,
@@ -671,6 +671,13 @@ int sbh_find_block_start(sbh_shard *sh, uint64_t start, int32_t k, uint64_t *out
   return SBH_OK;
 }
 
+// SBH_CHAIN_JUMP=1: the index always builds the block chain by pointer jumping (the path a
+// chain with false-positive candidates takes), for tests and A/B.
+static bool chain_jump_only() {
+  const char *e = std::getenv("SBH_CHAIN_JUMP");
+  return e && e[0] == '1';
+}
+
 // MetadataStream from `start` (bgzf/.../block/MetadataStream.scala:16-58)
 int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_size) {
   if (!sh || start < sh->file_off || start > sh->file_off + sh->n) return SBH_E_ARG;
@@ -741,11 +748,6 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
     HIPCHK(ctx, sh->b_flags.ensure(nc));
     HIPCHK(ctx, sh->b_status.ensure(nc));
     HIPCHK(ctx, sh->b_ntok.ensure(nc));
-    HIPCHK(ctx, build_chain(sh->comp.p, n, sh->cand.p, nc, rel, sh->J0.p, sh->J1.p, sh->on.p, sh->v.p, sh->rank.p,
-                            sh->tmp.p, sh->dev_blocks(), sh->usz.p, next18_dev, st));
-    // flat offsets over all nc entries (usz is zero past the chain); the chain length comes back
-    // with the block table, so the table is packed and copied for all nc candidates and cut after
-    HIPCHK(ctx, scan_exclusive_u64(sh->usz.p, sh->b_ustart.p, nc, sh->tmp.p, st));
   }
   sh->ncand = nc;
   sh->cand_from = srel;
@@ -755,12 +757,26 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
   if (nc) {
     unsigned long long *lastw = sh->h_ctr + 540;  // pinned: rank[nc - 1], v[nc - 1]
     HIPCHK(ctx, sh->blkpack.ensure(4 * nc));
-    HIPCHK(ctx, launch_pack_blocks(sh->dev_blocks(), nc, sh->file_off, sh->blkpack.p, st));
-    HIPCHK(ctx, hipMemcpyAsync(sh->hb.data(), sh->blkpack.p, nc * 32, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipMemcpyAsync(lastw, sh->rank.p + nc - 1, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipMemcpyAsync(lastw + 1, sh->v.p + nc - 1, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipMemcpyAsync(nx, next18_dev, 18, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipStreamSynchronize(st));
+    // the linear chain first (every candidate from the start on is chained: no pointer jumping);
+    // its flag comes back with the table, and a chain that is not linear is rebuilt by jumping
+    for (int pass = chain_jump_only() ? 1 : 0; pass < 2; ++pass) {
+      HIPCHK(ctx, build_chain(sh->comp.p, n, sh->cand.p, nc, rel, sh->J0.p, sh->J1.p, sh->on.p, sh->v.p, sh->rank.p,
+                              sh->tmp.p, sh->dev_blocks(), sh->usz.p, next18_dev,
+                              reinterpret_cast<uint64_t *>(sh->ctr.p + CTR_NEXT18 + 3),
+                              pass == 0, st));
+      // flat offsets over all nc entries (usz is zero past the chain); the chain length comes
+      // back with the block table, so the table is packed and copied for all nc candidates and
+      // cut after
+      HIPCHK(ctx, scan_exclusive_u64(sh->usz.p, sh->b_ustart.p, nc, sh->tmp.p, st));
+      HIPCHK(ctx, launch_pack_blocks(sh->dev_blocks(), nc, sh->file_off, sh->blkpack.p, st));
+      HIPCHK(ctx, hipMemcpyAsync(sh->hb.data(), sh->blkpack.p, nc * 32, hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipMemcpyAsync(lastw, sh->rank.p + nc - 1, 8, hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipMemcpyAsync(lastw + 1, sh->v.p + nc - 1, 8, hipMemcpyDeviceToHost, st));
+      // (+ the not-linear flag and the empty-block count)
+      HIPCHK(ctx, hipMemcpyAsync(nx, next18_dev, 24, hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipStreamSynchronize(st));
+      if (pass == 1 || !nx[NEXT18_NONLIN]) break;
+    }
     nchain = lastw[0] + lastw[1];
   }
   sh->hb.resize(nchain);
@@ -780,11 +796,21 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
       }
     }
   }
+  // segments: each empty block ends one (the table is walked only when the chain has any: a
+  // walk over a 1 GB shard's 46 k blocks took ~85 us of host time per step); the flat end is
+  // that of the last block with bytes
   uint64_t total = 0;
   sh->seg_end.clear();
-  for (const sbh_block &b : sh->hb) {
-    if (b.flags & SBH_BLOCK_EMPTY) sh->seg_end.push_back(b.ustart);
-    if (!(b.flags & SBH_BLOCK_EMPTY) && b.usize <= 65536) total = b.ustart + b.usize;
+  const uint32_t nempty = nc ? *reinterpret_cast<const uint32_t *>(nx + NEXT18_NEMPTY) : 0u;
+  if (nempty)
+    for (const sbh_block &b : sh->hb)
+      if (b.flags & SBH_BLOCK_EMPTY) sh->seg_end.push_back(b.ustart);
+  for (size_t i = sh->hb.size(); i-- > 0;) {
+    const sbh_block &b = sh->hb[i];
+    if (!(b.flags & SBH_BLOCK_EMPTY) && b.usize <= 65536) {
+      total = b.ustart + b.usize;
+      break;
+    }
   }
   sh->seg_end.push_back(total);
   HIPCHK(ctx, sh->d_seg.ensure(sh->seg_end.size()));
@@ -860,11 +886,13 @@ static TokPlan tok_plan(const sbh_shard *sh, uint64_t max_blocks) {
   P.reuse = sh->utotal + 64 > cap;
   uint64_t b0 = 0;
   while (b0 < nb) {
-    uint64_t b1 = b0 + 1;
     const uint64_t u0 = sh->hb[b0].ustart;
-    while (b1 < nb && b1 - b0 < max_blocks &&
-           (!P.reuse || sh->hb[b1].ustart + sh->hb[b1].usize - u0 <= cap))
-      ++b1;
+    // (no block walk unless the budget binds; max_blocks may be ~0)
+    uint64_t b1 = max_blocks >= nb - b0 ? nb : b0 + std::max<uint64_t>(max_blocks, 1);
+    if (P.reuse) {
+      b1 = b0 + 1;
+      while (b1 < nb && b1 - b0 < max_blocks && sh->hb[b1].ustart + sh->hb[b1].usize - u0 <= cap) ++b1;
+    }
     P.batches.emplace_back(b0, b1);
     const uint64_t ext = sh->hb[b1 - 1].ustart + sh->hb[b1 - 1].usize - u0;
     P.tok_len = std::max(P.tok_len, ext);
@@ -1758,9 +1786,13 @@ int sbh_run_shard(sbh_shard *sh, uint64_t index_start, uint64_t own_end_file, in
     sh->timing = false;
     return res->status = fail(ctx, SBH_E_NEED_HALO, "no halo past %llu", (unsigned long long)own_end_file);
   }
-  uint64_t owned_blocks = 0, cbytes = 0;
-  for (const sbh_block &b : sh->hb)
-    if (b.start < own_end_file) { ++owned_blocks; cbytes += b.csize; }
+  // the blocks starting before own_end_file (the chain is contiguous: each block starts where
+  // the one before it ends, so their bytes are one span)
+  const uint64_t owned_blocks = (uint64_t)(std::lower_bound(sh->hb.begin(), sh->hb.end(), own_end_file,
+                                                           [](const sbh_block &b, uint64_t v) { return b.start < v; }) -
+                                           sh->hb.begin());
+  const uint64_t cbytes =
+      owned_blocks ? sh->hb[owned_blocks - 1].start + sh->hb[owned_blocks - 1].csize - sh->hb[0].start : 0;
   res->n_blocks = owned_blocks;
   res->comp_bytes = cbytes;
   res->flat_bytes = E;

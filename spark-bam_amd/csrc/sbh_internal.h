@@ -197,12 +197,16 @@ hipError_t launch_member_footer(const uint8_t *src, uint64_t n, uint64_t b0, uin
 //   persistent [CTR_TRUE_SPREAD, +CTR_TRUE_WORDS)  k_eager's per-wave true counts: must be
 //                                 zero before every k_eager launch; k_fold_true folds them
 //                                 into n_true and zeroes them again
-//   per call  [CTR_NEXT18, +3)    the 18 bytes after an index's last chained block
+//   per call  [CTR_NEXT18, +4)    the 18 bytes after an index's last chained block, at byte
+//                                 NEXT18_NONLIN the linear chain's "not linear" flag (u8), at
+//                                 byte NEXT18_NEMPTY the chain's empty-block count (u32), then
+//                                 the linear chain's start index (u64, device only)
 constexpr uint32_t CTR_WORDS = 4096;
+constexpr uint32_t NEXT18_NONLIN = 18, NEXT18_NEMPTY = 20;
 constexpr uint32_t CTR_CALL_END = 4 + 21 * 19 + 21 * 64;
 constexpr uint32_t CTR_TRUE_SPREAD = 2048, CTR_TRUE_WORDS = 64 * 16;
 constexpr uint32_t CTR_NEXT18 = CTR_TRUE_SPREAD + CTR_TRUE_WORDS;
-static_assert(CTR_CALL_END <= CTR_TRUE_SPREAD && CTR_NEXT18 + 3 <= CTR_WORDS, "counter buffer layout");
+static_assert(CTR_CALL_END <= CTR_TRUE_SPREAD && CTR_NEXT18 + 4 <= CTR_WORDS, "counter buffer layout");
 
 constexpr uint32_t SPLIT_OK = 0;    // first record and flat end decided on the device
 constexpr uint32_t SPLIT_HOST = 1;  // off the common path: the exact per-split host path decides

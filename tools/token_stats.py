@@ -53,12 +53,16 @@ def huff(lens):
     return t
 
 
+LAST_LEN = [0]  # code length of the last symbol sym() decoded
+
+
 def sym(br, t):
     code = L = 0
     while True:
         code = (code << 1) | br.get(1)
         L += 1
         if (L, code) in t:
+            LAST_LEN[0] = L
             return t[(L, code)]
 
 
@@ -72,7 +76,7 @@ def tokens(raw):
             n = br.get(16)
             br.get(16)
             for _ in range(n):
-                out.append(("L", br.get(8)))
+                out.append(("L", br.get(8), 8))
         else:
             if typ == 1:
                 lit = huff([8] * 144 + [9] * 112 + [7] * 24 + [8] * 8)
@@ -98,15 +102,17 @@ def tokens(raw):
             while True:
                 s = sym(br, lit)
                 if s < 256:
-                    out.append(("L", s))
+                    out.append(("L", s, LAST_LEN[0]))
                 elif s == 256:
                     break
                 else:
                     s -= 257
+                    cl = LAST_LEN[0] + LEXT[s]
                     L = LBASE[s] + br.get(LEXT[s])
                     d = sym(br, dist)
                     D = DBASE[d] + br.get(DEXT[d])
-                    out.append(("M", L, D))
+                    out.append(("M", L, D, cl, LAST_LEN[0] + DEXT[d]))
+            out.append(("E",))  # end of a deflate block
         if final:
             return out
 
@@ -129,6 +135,34 @@ def main():
         xlen = blk[10] | blk[11] << 8
         raw = blk[12 + xlen:n - 8]
         t = tokens(raw)
+        # two literals per table lookup: a pair of consecutive literal codes (same deflate block)
+        # whose lengths sum to <= W bits is decodable from one W-bit lookup
+        i = 0
+        while i < len(t):
+            x = t[i]
+            if x[0] == "L":
+                for W in (10, 11, 12):
+                    if i + 1 < len(t) and t[i + 1][0] == "L" and x[2] + t[i + 1][2] <= W:
+                        tot["pair%d" % W] = tot.get("pair%d" % W, 0) + 1
+                tot["litbits"] = tot.get("litbits", 0) + x[2]
+            elif x[0] == "M":
+                tot["lenbits"] = tot.get("lenbits", 0) + x[3]
+                tot["distbits"] = tot.get("distbits", 0) + x[4]
+            i += 1
+        # greedy pairing at W bits: lookups needed for the literals
+        for W in (10, 11, 12):
+            i = look = 0
+            while i < len(t):
+                if t[i][0] == "L" and i + 1 < len(t) and t[i + 1][0] == "L" and t[i][2] + t[i + 1][2] <= W:
+                    i += 2
+                elif t[i][0] == "E":
+                    i += 1
+                    continue
+                else:
+                    i += 1
+                look += 1
+            tot["look%d" % W] = tot.get("look%d" % W, 0) + look
+        t = [x for x in t if x[0] != "E"]
         lit = sum(1 for x in t if x[0] == "L")
         tot["tok"] += len(t)
         tot["lit"] += lit
@@ -151,6 +185,11 @@ def main():
     for k in (2, 3, 4):
         n = m + tot["pack%d" % k]
         print(f"  literals packed {k} per token: {n} tokens ({n / tot['tok']:.1%} of today's)")
+    print(f"  mean code bits: literal {tot['litbits'] / tot['lit']:.2f}, length {tot['lenbits'] / max(m, 1):.2f}, "
+          f"distance {tot['distbits'] / max(m, 1):.2f}")
+    for W in (10, 11, 12):
+        print(f"  {W}-bit lookups decoding two literals when both codes fit: {tot['look%d' % W]} lookups for "
+              f"{tot['tok']} tokens ({tot['look%d' % W] / tot['tok']:.1%})")
     hist = sorted(runs.items())
     tot_runs = sum(runs.values())
     print("  literal runs:", tot_runs, "; length histogram (len: share of runs):",
