@@ -976,7 +976,7 @@ constexpr uint32_t INF_TAIL = 0xfeu;  // (inside inflate only) k_huff_tail finis
 #ifdef SBH_HUFF_PROBE
 // whole-kernel phase sums (cycles): 0 stage, 1 header, 2 pass 1, 3 repair, 4 emit, 5 repair
 // rounds, 6 deflate blocks, 7 whole block, 8-10 header: CL table / walk / tables, 11 tokens
-__device__ unsigned long long hp_acc[16];
+__device__ unsigned long long hp_acc[16];  // [14]: blocks timed
 __device__ unsigned int hp_done;
 #endif
 template <uint32_t NT_, uint32_t SDW_>
@@ -1498,6 +1498,9 @@ __device__ __forceinline__ LaneRun redo_asm(const WaveSmem &t, const uint32_t *s
 #ifndef SBH_ASM_EMIT
 #define SBH_ASM_EMIT 1  // pass 3 (RUN_EMIT over the LDS stage) as the hand-written loop below
 #endif
+#ifndef SBH_EMIT_X4
+#define SBH_EMIT_X4 1  // emit_asm: a lane's tokens stored four at a time (16-byte stores from v124..v127; A/B r05m/r05n: k_huff -7% E, +-0.2% B and D)
+#endif
 // RUN_EMIT over the LDS stage as hand-written code (lane_run<RUN_EMIT>'s results): the decode
 // loop of spec_asm without the checkpoints, each token stored once (a literal at its code, a
 // match at its distance code) through a 32-bit offset from the block's token base `tk` (wave-
@@ -1514,7 +1517,7 @@ __device__ __forceinline__ void emit_asm(const WaveSmem &t, const uint32_t *stag
   const uint64_t tkp = reinterpret_cast<uint64_t>(tk);
   const uint64_t tkb = (uint64_t)uni((uint32_t)tkp) | (uint64_t)uni((uint32_t)(tkp >> 32)) << 32;
   uint32_t pos = A, lo = stage[A >> 5], hi = stage[(A >> 5) + 1];
-  uint32_t vt = 0, tselb = tabb, ntok = 0, acc = 0, ml = 0, voff = tidx * 4u, badv = 0;
+  uint32_t vt = 0, tselb = tabb, ntok = 0, acc = 0, ml = 0, voff = tidx * 4u, badv = 0, cnt = 0;
   const uint32_t om1 = out0 - 1u;
   const uint32_t bad_e = 1u | PE_SPECIAL;
   uint32_t e = 0, bits, a, nx, x, ex, val, np, tmp, r15, q, p11, p12, p13, p14, p15, d, sh, vtn, vtok, vb;
@@ -1629,8 +1632,25 @@ __device__ __forceinline__ void emit_asm(const WaveSmem &t, const uint32_t *stag
       "s_and_b64 %[sE], %[sA], %[sL]\n\t"
       "s_mov_b64 %[sB], exec\n\t"
       "s_andn2_b64 exec, exec, %[sE]\n\t"
+#if SBH_EMIT_X4
+      // tokens gather in v124..v127 (oldest first) and leave four at a time in one 16-byte store
+      "v_mov_b32 v124, v125\n\t"
+      "v_mov_b32 v125, v126\n\t"
+      "v_mov_b32 v126, v127\n\t"
+      "v_mov_b32 v127, %[vtok]\n\t"
+      "v_add_u32 %[cnt], 1, %[cnt]\n\t"
+      "v_cmp_eq_u32 %[sE], 4, %[cnt]\n\t"
+      "s_and_b64 exec, exec, %[sE]\n\t"
+      "s_cbranch_execz L_nofl%=\n\t"
+      "global_store_dwordx4 %[voff], v[124:127], %[tkb]\n\t"
+      "s_nop 1\n\t"  // (a VALU write of a > 8-byte store's data VGPRs waits for the store to read them)
+      "v_add_u32 %[voff], 16, %[voff]\n\t"
+      "v_mov_b32 %[cnt], 0\n"
+      "L_nofl%=:\n\t"
+#else
       "global_store_dword %[voff], %[vtok], %[tkb]\n\t"
       "v_add_u32 %[voff], 4, %[voff]\n\t"
+#endif
       "s_mov_b64 exec, %[sB]\n\t"
       "v_addc_co_u32_e64 %[ntok], vcc, 0, %[ntok], %[sA]\n\t"
       "v_mov_b32 %[vt], %[vtn]\n\t"
@@ -1640,9 +1660,26 @@ __device__ __forceinline__ void emit_asm(const WaveSmem &t, const uint32_t *stag
       "L_end%=:\n\t"
       "s_waitcnt lgkmcnt(0)\n\t"
       "s_mov_b64 exec, %[sv]\n\t"
+#if SBH_EMIT_X4
+      // the last cnt (< 4) tokens of each lane: v127 (newest) at voff + 4 (cnt - 1), v126 before it, ...
+      "v_cmp_le_u32 %[sE], 1, %[cnt]\n\t"
+      "s_and_b64 exec, exec, %[sE]\n\t"
+      "s_cbranch_execz L_fld%=\n\t"
+      "v_lshl_add_u32 %[tmp], %[cnt], 2, %[voff]\n\t"
+      "global_store_dword %[tmp], v127, %[tkb] offset:-4\n\t"
+      "v_cmp_le_u32 %[sE], 2, %[cnt]\n\t"
+      "s_and_b64 exec, exec, %[sE]\n\t"
+      "global_store_dword %[tmp], v126, %[tkb] offset:-8\n\t"
+      "v_cmp_le_u32 %[sE], 3, %[cnt]\n\t"
+      "s_and_b64 exec, exec, %[sE]\n\t"
+      "global_store_dword %[tmp], v125, %[tkb] offset:-12\n"
+      "L_fld%=:\n\t"
+      "s_mov_b64 exec, %[sv]\n\t"
+#endif
       "v_cndmask_b32_e64 %[badv], 0, 1, %[sBad]"
       : [pos] "+v"(pos), [lo] "+v"(lo), [hi] "+v"(hi), [vt] "+v"(vt), [tselb] "+v"(tselb), [ntok] "+v"(ntok),
-        [acc] "+v"(acc), [ml] "+v"(ml), [voff] "+v"(voff), [badv] "+v"(badv), [e] "+v"(e), [bits] "=&v"(bits),
+        [acc] "+v"(acc), [ml] "+v"(ml), [voff] "+v"(voff), [badv] "+v"(badv), [cnt] "+v"(cnt), [e] "+v"(e),
+        [bits] "=&v"(bits),
         [a] "=&v"(a), [nx] "=&v"(nx), [x] "=&v"(x), [ex] "=&v"(ex), [val] "=&v"(val), [np] "=&v"(np),
         [tmp] "=&v"(tmp), [r15] "=&v"(r15), [q] "=&v"(q), [p11] "=&v"(p11), [p12] "=&v"(p12), [p13] "=&v"(p13),
         [p14] "=&v"(p14), [p15] "=&v"(p15), [d] "=&v"(d), [sh] "=&v"(sh), [vtn] "=&v"(vtn), [vtok] "=&v"(vtok),
@@ -1650,7 +1687,11 @@ __device__ __forceinline__ void emit_asm(const WaveSmem &t, const uint32_t *stag
         [sL] "=&s"(sL), [sBad] "=&s"(sBad), [sv] "=&s"(sv)
       : [stop] "v"(stop2), [tabb] "s"(tabb), [stb] "s"(stb), [pkb] "s"(pkb), [sentb] "s"(sentb),
         [sentd] "s"(sentd), [bad_e] "v"(bad_e), [om1] "v"(om1), [tkb] "s"(tkb)
-      : "vcc", "scc", "memory");
+      : "vcc", "scc", "memory"
+#if SBH_EMIT_X4
+      , "v124", "v125", "v126", "v127"
+#endif
+  );
   bad |= badv;
 }
 
@@ -1834,7 +1875,7 @@ __device__ __forceinline__ bool par_header(SM &sm, S src, uint32_t p, uint32_t l
   fill_tables();
   __syncthreads();
 #ifdef SBH_HUFF_PROBE
-  if (wid == 0 && lane == 0) {
+  if (NT == HT && wid == 0 && lane == 0) {
     atomicAdd(&hp_acc[8], h1 - h0);
     atomicAdd(&hp_acc[9], h2 - h1);
     atomicAdd(&hp_acc[10], __builtin_readcyclecounter() - h2);
@@ -1942,8 +1983,8 @@ __device__ __forceinline__ uint32_t inflate_par(SM &sm, const uint8_t *__restric
       xa = xb;
       xb = xt;
 #ifdef SBH_HUFF_PROBE
-      if (tid == 0 && nrounds == 1) atomicAdd(&hp_acc[12], __builtin_readcyclecounter() - tp1);
-      if (tid == 0 && nrounds == 2) atomicAdd(&hp_acc[13], __builtin_readcyclecounter() - tp1);
+      if (SM::NT == HT && tid == 0 && nrounds == 1) atomicAdd(&hp_acc[12], __builtin_readcyclecounter() - tp1);
+      if (SM::NT == HT && tid == 0 && nrounds == 2) atomicAdd(&hp_acc[13], __builtin_readcyclecounter() - tp1);
 #endif
       if (!again) break;
     }
@@ -1961,6 +2002,7 @@ __device__ __forceinline__ uint32_t inflate_par(SM &sm, const uint8_t *__restric
         sm.wsum[wid] = it;
         sm.wsum2[wid] = io;
       }
+
       if (lane == (wf < WAVE ? wf : 0u)) {
         sm.wk[wid] = wf < WAVE ? tid : NT;
         sm.wkt[wid] = it;
@@ -2000,7 +2042,7 @@ __device__ __forceinline__ uint32_t inflate_par(SM &sm, const uint8_t *__restric
     }
 #ifdef SBH_HUFF_PROBE
     const uint64_t tp3 = __builtin_readcyclecounter();
-    if (tid == 0) {
+    if (SM::NT == HT && tid == 0) {  // (k_huff only: the tail kernel's passes are not in the report)
       atomicAdd(&hp_acc[1], tph - tp0);
       atomicAdd(&hp_acc[2], tp1 - tph);
       atomicAdd(&hp_acc[3], tp3 - tp1);
@@ -2033,7 +2075,7 @@ __device__ __forceinline__ uint32_t inflate_par(SM &sm, const uint8_t *__restric
     }
     if (__syncthreads_or(bad)) return PAR_FAIL;
 #ifdef SBH_HUFF_PROBE
-    if (tid == 0) atomicAdd(&hp_acc[4], __builtin_readcyclecounter() - tp3);
+    if (SM::NT == HT && tid == 0) atomicAdd(&hp_acc[4], __builtin_readcyclecounter() - tp3);
 #endif
     ntok += ttot;
     out += otot;
@@ -2156,6 +2198,28 @@ __global__ __launch_bounds__(WAVE * HDR_WAVES) void k_hdr(const uint8_t *__restr
   if (lane == 0) out[HDR_STATUS] = ok ? HDR_OK : 0u;
 }
 
+#ifdef SBH_HUFF_PROBE
+// (probe) one BGZF block done: its whole-block cycles when `timed` (the parallel path; tails
+// counted up to the hand-off), and the per-launch report once every block of the launch is done
+__device__ void huff_probe_done(uint32_t tid, uint64_t nblocks, uint64_t hk0, bool timed) {
+  if (tid != 0) return;
+  if (timed) {
+    atomicAdd(&hp_acc[7], __builtin_readcyclecounter() - hk0);
+    atomicAdd(&hp_acc[14], 1ull);
+  }
+  __threadfence();
+  if (atomicAdd(&hp_done, 1u) == (uint32_t)nblocks - 1) {
+    unsigned long long a[15];
+    for (int k = 0; k < 15; ++k) a[k] = atomicExch(&hp_acc[k], 0ull);
+    hp_done = 0;
+    const double n = (double)(a[14] ? a[14] : 1), d = (double)(a[6] ? a[6] : 1);
+    printf("huffprobe blocks %llu (parallel %.0f) deflate %.0f per-BGZF-block cycles: stage %.0f hdr %.0f (cl %.0f walk %.0f tables %.0f) p1 %.0f p2 %.0f (rounds/defl %.2f) p3 %.0f whole %.0f tokens/defl %.0f | p2 to end of round1 %.0f round2 %.0f\n",
+           (unsigned long long)nblocks, n, d, a[0] / n, a[1] / n, a[8] / n, a[9] / n, a[10] / n, a[2] / n, a[3] / n,
+           a[5] / d, a[4] / n, a[7] / n, a[11] / d, a[12] / n, a[13] / n);
+  }
+}
+#endif
+
 __global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__restrict__ comp, DevBlocks bl, uint64_t nblocks,
                                               uint32_t *__restrict__ tok) {
   __shared__ HuffSmem sm;
@@ -2177,6 +2241,9 @@ __global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__rest
         bl.status[b] = INF_OK;
         bl.ntok[b] = NTOK_STORED;
       }
+#ifdef SBH_HUFF_PROBE
+      huff_probe_done(tid, nblocks, 0, false);
+#endif
       return;
     }
   }
@@ -2246,6 +2313,9 @@ __global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__rest
         bl.ntok[b] = ntok;
         bl.status[b] = INF_TAIL;
       }
+#ifdef SBH_HUFF_PROBE
+      huff_probe_done(tid, nblocks, hk0, true);
+#endif
       return;
     }
     if (uni(rc) == PAR_OK) {
@@ -2254,24 +2324,15 @@ __global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__rest
         bl.ntok[b] = ntok;
       }
 #ifdef SBH_HUFF_PROBE
-      if (tid == 0) {
-        atomicAdd(&hp_acc[7], __builtin_readcyclecounter() - hk0);
-        __threadfence();
-        if (atomicAdd(&hp_done, 1u) == (uint32_t)nblocks - 1) {  // (serial blocks not counted)
-          unsigned long long a[14];
-          for (int k = 0; k < 14; ++k) a[k] = atomicExch(&hp_acc[k], 0ull);
-          hp_done = 0;
-          const double n = (double)nblocks, d = (double)a[6];
-          printf("huffprobe blocks %.0f deflate %.0f per-BGZF-block cycles: stage %.0f hdr %.0f (cl %.0f walk %.0f tables %.0f) p1 %.0f p2 %.0f (rounds/defl %.2f) p3 %.0f whole %.0f tokens/defl %.0f | p2 to end of round1 %.0f round2 %.0f\n",
-                 n, d, a[0] / n, a[1] / n, a[8] / n, a[9] / n, a[10] / n, a[2] / n, a[3] / n, a[5] / d, a[4] / n,
-                 a[7] / n, a[11] / d, a[12] / n, a[13] / n);
-        }
-      }
+      huff_probe_done(tid, nblocks, hk0, true);
 #endif
       return;
     }
   }
   if (tid == 0) bl.status[b] = INF_SERIAL;  // k_huff_serial<true> decodes it
+#ifdef SBH_HUFF_PROBE
+  huff_probe_done(tid, nblocks, hk0, false);
+#endif
 }
 
 // The rest of a block k_huff deferred (INF_TAIL: a short final deflate block, typically),
