@@ -1251,8 +1251,11 @@ int sbh_find_record_start(sbh_shard *sh, uint64_t from, int32_t rtc, int32_t max
 // first chain record at/after E (the successor of the last counted record, clamped to
 // the stream end) -- what the next shard's first record must equal when stitching.
 
+// `known`: the four chain-proof counters (anomalies, first anomaly, set bits, exit) that a
+// k_verify_chain_w launch over this same [first, E) and bitmap already left in h_ctr[16..19]
+// (sbh_run_shard's tail): the proof is not run again.
 static int count_records_impl(sbh_shard *sh, uint64_t first, uint64_t E, uint64_t *count, int32_t *anomalies,
-                              uint64_t *exit_flat = nullptr) {
+                              uint64_t *exit_flat = nullptr, bool known = false) {
   sbh_ctx *ctx = sh->ctx;
   hipStream_t st = ctx->stream;
   const uint64_t total = seg_end_of(sh, first);
@@ -1274,13 +1277,15 @@ static int count_records_impl(sbh_shard *sh, uint64_t first, uint64_t E, uint64_
     init[1] = ~0ull;
     init[2] = 0;
     init[3] = ~0ull;
-    HIPCHK(ctx, hipMemcpyAsync(c, init, 32, hipMemcpyHostToDevice, st));
-    // verify bitmap == chain and count the set bits in one pass (k_verify_chain_w: wave-
-    // cooperative successors, so sparse bitmaps of long records cost no word-by-word scans)
-    HIPCHK(ctx, launch_verify_chain_count(sh->U.p, sh->bits.p, sh->bits_begin, sh->bits_end, first, E, total, c,
-                                          c + 1, c + 3, c + 2, tsum_on() ? sh->tsum.p : nullptr, st));
-    HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 16, c, 32, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipStreamSynchronize(st));
+    if (!known) {
+      HIPCHK(ctx, hipMemcpyAsync(c, init, 32, hipMemcpyHostToDevice, st));
+      // verify bitmap == chain and count the set bits in one pass (k_verify_chain_w: wave-
+      // cooperative successors, so sparse bitmaps of long records cost no word-by-word scans)
+      HIPCHK(ctx, launch_verify_chain_count(sh->U.p, sh->bits.p, sh->bits_begin, sh->bits_end, first, E, total, c,
+                                            c + 1, c + 3, c + 2, tsum_on() ? sh->tsum.p : nullptr, st));
+      HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 16, c, 32, hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipStreamSynchronize(st));
+    }
     const uint64_t n = sh->h_ctr[18];
     if (sh->h_ctr[16] == 0 && sh->h_ctr[19] != ~0ull) {
       sh->chain_ok = true;
@@ -1844,7 +1849,9 @@ int sbh_run_shard(sbh_shard *sh, uint64_t index_start, uint64_t own_end_file, in
       res->anomalies = 0;
       res->exit_flat = sh->h_ctr[19];
     } else {
-      rc = count_records_impl(sh, first, E, &res->count, &res->anomalies, &res->exit_flat);
+      // (the tail's proof covered [first, E0) of this bitmap: its counters are reused when first
+      // lies in the first segment, which is the range count_records_impl proves)
+      rc = count_records_impl(sh, first, E, &res->count, &res->anomalies, &res->exit_flat, first < E0);
     }
     uint64_t bp = 0;
     uint32_t off = 0;
