@@ -17,6 +17,7 @@
 // wave ballots.  Results are a bit per position (2 KiB per tile, 16-byte stores) or a word
 // per position.
 #include <algorithm>
+#include <cstdlib>
 
 #include "sbh_internal.h"
 
@@ -1800,7 +1801,7 @@ __global__ __launch_bounds__(256) void k_verify_chain_w(const uint8_t *U, const 
 // Since every step moves forward, the nodes reachable from node 0 are exactly the chain.
 __global__ void k_cm_succ(const uint8_t *U, const uint32_t *bits, uint64_t begin, uint64_t from, uint64_t E,
                           uint64_t total, const uint64_t *pos, const uint64_t *wpre, uint64_t n, uint32_t *J,
-                          uint32_t *J0, uint64_t *mark) {
+                          uint32_t *J0, uint64_t *mark, uint32_t *indeg) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t s = pos[i];
@@ -1836,7 +1837,44 @@ __global__ void k_cm_succ(const uint8_t *U, const uint32_t *bits, uint64_t begin
   }
   J[i] = j;
   J0[i] = j;
-  mark[i] = i == 0;
+  if (indeg) {  // (the peeling path: every node starts marked, predecessors counted)
+    mark[i] = 1;
+    if (j < n) atomicAdd(&indeg[j], 1u);
+  } else {
+    mark[i] = i == 0;
+  }
+}
+
+// Chain marking by peeling instead of doubling (launch_chain_mark).  Edges only go forward, so a
+// node other than node 0 is off the chain exactly when every predecessor is: the nodes nobody
+// steps to are the roots of the off-chain set (k_cm_roots), and each root walks forward,
+// taking one predecessor off each successor and continuing while it took the last one
+// (k_cm_peel).  False positives are roots whose walks end at once (their successor is a chain
+// record with a chained predecessor), so this is ~3 passes where doubling took log2(n) rounds
+// over every node.  A walk longer than CM_PEEL_MAX (the chain itself breaking: everything after
+// the break is off) gives up and marks the result unusable, so the host takes the exact walk
+// as it does for a broken chain.
+constexpr uint32_t CM_PEEL_MAX = 4096;
+__global__ void k_cm_roots(const uint32_t *indeg, uint64_t *mark, uint64_t n, uint32_t *code) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) *code = (uint32_t)n;
+  if (i == 0 || i >= n) return;
+  if (indeg[i] == 0) mark[i] = 2;
+}
+__global__ void k_cm_peel(const uint32_t *J0, uint32_t *indeg, uint64_t *mark, uint64_t n, uint32_t *code) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || mark[i] != 2) return;
+  mark[i] = 0;
+  uint32_t j = J0[i];
+  for (uint32_t steps = 0; j < n; ++steps) {
+    if (steps == CM_PEEL_MAX) {
+      atomicMax(code, (uint32_t)n + 2);  // (not n: the host walks exactly)
+      return;
+    }
+    if (atomicSub(&indeg[j], 1u) != 1u) return;  // j keeps a predecessor
+    mark[j] = 0;
+    j = J0[j];
+  }
 }
 
 // One doubling round: nodes at distance < 2^k are marked; mark their 2^k-successors
@@ -1854,11 +1892,13 @@ __global__ void k_cm_round(const uint32_t *Jin, uint32_t *Jout, uint64_t *mark, 
   }
 }
 
-// The chain's last counted node (marked, J0 terminal): its successor is the exit.
+// The chain's last counted node (marked, J0 terminal): its successor is the exit.  (code: the
+// peeling path's verdict -- a chained node whose step leaves the set bits makes it unusable.)
 __global__ void k_cm_exit(const uint8_t *U, const uint64_t *pos, const uint32_t *J0, const uint64_t *mark,
-                          uint64_t n, uint64_t total, unsigned long long *exit_pos) {
+                          uint64_t n, uint64_t total, unsigned long long *exit_pos, uint32_t *code) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || !mark[i] || J0[i] < n) return;
+  if (code && J0[i] != (uint32_t)n) atomicMax(code, J0[i]);  // (broken: n + 1)
   const uint64_t s = pos[i];
   uint64_t x = total;
   if (s + 4 <= total) {
@@ -2190,14 +2230,30 @@ hipError_t launch_chain_mark(const uint8_t *U, const uint32_t *bits, uint64_t be
                              uint32_t *final_code, hipStream_t st) {
   if (!n) return hipSuccess;
   const uint32_t g = ngrid(n, 256);
-  hipLaunchKernelGGL(k_cm_succ, dim3(g), dim3(256), 0, st, U, bits, begin, from, E, total, pos, wpre, n, J, J0, mark);
-  uint32_t *a = J, *b = J2;
-  for (uint64_t span = 1; span < n; span <<= 1) {
-    hipLaunchKernelGGL(k_cm_round, dim3(g), dim3(256), 0, st, a, b, mark, n);
-    std::swap(a, b);
+  const char *dbl = std::getenv("SBH_CM_DOUBLING");  // 1: the pointer-doubling marking (A/B, tests)
+  if (dbl && dbl[0] == '1') {
+    hipLaunchKernelGGL(k_cm_succ, dim3(g), dim3(256), 0, st, U, bits, begin, from, E, total, pos, wpre, n, J, J0,
+                       mark, nullptr);
+    uint32_t *a = J, *b = J2;
+    for (uint64_t span = 1; span < n; span <<= 1) {
+      hipLaunchKernelGGL(k_cm_round, dim3(g), dim3(256), 0, st, a, b, mark, n);
+      std::swap(a, b);
+    }
+    hipLaunchKernelGGL(k_cm_exit, dim3(g), dim3(256), 0, st, U, pos, J0, mark, n, total, exit_pos, nullptr);
+    hipError_t e = hipMemcpyAsync(final_code, a, 4, hipMemcpyDeviceToHost, st);
+    if (e != hipSuccess) return e;
+    return hipGetLastError();
   }
-  hipLaunchKernelGGL(k_cm_exit, dim3(g), dim3(256), 0, st, U, pos, J0, mark, n, total, exit_pos);
-  hipError_t e = hipMemcpyAsync(final_code, a, 4, hipMemcpyDeviceToHost, st);
+  // peeling: J2 holds the predecessor counts, the word after exit_pos the verdict (n: usable)
+  uint32_t *indeg = J2, *code = reinterpret_cast<uint32_t *>(exit_pos + 1);
+  hipError_t e = hipMemsetAsync(indeg, 0, n * sizeof(uint32_t), st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_cm_succ, dim3(g), dim3(256), 0, st, U, bits, begin, from, E, total, pos, wpre, n, J, J0, mark,
+                     indeg);
+  hipLaunchKernelGGL(k_cm_roots, dim3(g), dim3(256), 0, st, indeg, mark, n, code);
+  hipLaunchKernelGGL(k_cm_peel, dim3(g), dim3(256), 0, st, J0, indeg, mark, n, code);
+  hipLaunchKernelGGL(k_cm_exit, dim3(g), dim3(256), 0, st, U, pos, J0, mark, n, total, exit_pos, code);
+  e = hipMemcpyAsync(final_code, code, 4, hipMemcpyDeviceToHost, st);
   if (e != hipSuccess) return e;
   return hipGetLastError();
 }

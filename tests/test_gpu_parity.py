@@ -411,11 +411,14 @@ def test_pipelined_run_matches_separate_calls(ctx, synth_files, name, batch_bloc
     sh.close()
 
 
+@pytest.mark.parametrize("marking", ["peel", "doubling"])
 @pytest.mark.parametrize("name", ["adversarial", "short_l6", "long"])
-def test_chain_count_with_false_positive_bits(ctx, synth_files, name):
+def test_chain_count_with_false_positive_bits(ctx, synth_files, name, marking, monkeypatch):
     """Record counts / exits / record starts over an eager bitmap that holds false
-    positives (config E's bait): the pointer-doubling chain marker must give exactly the
-    PosStream chain (oracle walk), for ranges starting at true records."""
+    positives (config E's bait): the chain marker -- off-chain nodes peeled from the nodes no
+    record steps to (default), or pointer doubling (SBH_CM_DOUBLING=1) -- must give exactly
+    the PosStream chain (oracle walk), for ranges starting at true records."""
+    monkeypatch.setenv("SBH_CM_DOUBLING", "1" if marking == "doubling" else "0")
     data = synth_files[name]
     of = OracleFile(data)
     sh = load(ctx, data, of.contig_len)
