@@ -385,7 +385,10 @@ __device__ __forceinline__ bool long_candidate(const Src &s, uint64_t p, const C
 }
 
 constexpr uint32_t ETILE = SBH_ETILE;     // eager tile: positions per workgroup
-constexpr uint32_t ELA = 4096;            // look-ahead: chains of short reads stay inside
+#ifndef SBH_ELA
+#define SBH_ELA 4096
+#endif
+constexpr uint32_t ELA = SBH_ELA;         // look-ahead: chains of short reads stay inside
 constexpr uint32_t EW = ETILE + ELA;      // eager window: single-record predicate evaluated here
 constexpr uint32_t ESTAGE = EW + 512;     // staged bytes (records near the end fit)
 #ifndef SBH_EQ_CHUNK
