@@ -2391,16 +2391,32 @@ __global__ __launch_bounds__(TAIL_NT) void k_huff_tail(const uint8_t *__restrict
 constexpr uint32_t LZ_TPT = SBH_LZ_TPT;                       // tokens per thread per chunk
 constexpr uint32_t LZ_CHUNK = LZ_THREADS * LZ_TPT;      // tokens per chunk
 constexpr uint32_t PTR_HALF = 8;                        // pointer slots per thread and pass
+#ifndef SBH_LZ_RING
+// k_lz's block image as a ring of 32 KiB of history + one pass, flushed to U pass by pass, so that
+// three workgroups fit a CU (6656-byte passes, 80 VGPRs: 6 waves per SIMD) instead of two with the
+// whole 64 KiB image (A/B r05y, output identical: k_lz -13% B, -15% D, -11% E)
+#define SBH_LZ_RING 1
+#endif
 #ifndef SBH_LZ_PTR_CAP
-#define SBH_LZ_PTR_CAP 7552
+#define SBH_LZ_PTR_CAP (SBH_LZ_RING ? 6656 : 7552)
 #endif
 constexpr uint32_t PTR_CAP = SBH_LZ_PTR_CAP;            // bytes one pointer-chasing pass resolves
 constexpr uint32_t SB_WORDS = PTR_CAP / 32;             // token-start bitmap words
 constexpr uint32_t NHP = 2;                             // half granules (8 slots) per k_lz thread, at most
 static_assert(PTR_CAP <= NHP * LZ_THREADS * PTR_HALF, "slot pass covers the slots");
 
+// image bytes: the whole block, or (ring) the deflate window before a pass plus the pass itself
+// (a pass's pointers reach at most 32768 bytes before its first byte), a multiple of 16 so
+// granules stay whole; image position q lives at q mod LZ_IMG (q < 2 LZ_IMG always)
+constexpr uint32_t LZ_IMG = SBH_LZ_RING ? (32768u + PTR_CAP + 16u + 15u) / 16u * 16u : 65536u + 16u;
+static_assert(!SBH_LZ_RING || 65536u + 16u < 2 * LZ_IMG, "one subtraction maps an image position into the ring");
+__device__ __forceinline__ uint32_t lz_ri(uint32_t q) {
+  if (!SBH_LZ_RING) return q;
+  const uint32_t r = q - LZ_IMG;
+  return r < q ? r : q;  // (q < LZ_IMG: r wraps above q)
+}
 struct LzSmem {
-  uint8_t img[65536 + 16];  // block image, placed at (ustart & 15) so granules align with HBM
+  uint8_t img[LZ_IMG];  // block image (or its ring), placed at (ustart & 15) so granules align with HBM
   struct {
     uint16_t p16[PTR_CAP];     // per pass byte: its source pointer (token starts first)
     uint32_t sbits[SB_WORDS];  // per pass byte: starts a token (every byte of a long match)
@@ -2408,8 +2424,9 @@ struct LzSmem {
     uint32_t wmin[LZ_THREADS / WAVE];  // block_min scratch (a pass cut)
   } pp;
 };
-// two workgroups per CU, counting the 256 B of LDS the compiler adds
+// two workgroups per CU (three with the ring), counting the 256 B of LDS the compiler adds
 static_assert(sizeof(LzSmem) * 2 + 512 <= 160 * 1024, "two k_lz workgroups per CU");
+static_assert(!SBH_LZ_RING || sizeof(LzSmem) * 3 + 768 <= 160 * 1024, "three k_lz workgroups per CU with the ring");
 
 // k mod d for k < 2^17, d >= 1 (one reciprocal, one correction).
 __device__ __forceinline__ uint32_t mod_small(uint32_t k, uint32_t d) {
@@ -2564,7 +2581,7 @@ __device__ __forceinline__ void chase8_asm(uint32_t (&c)[8], uint32_t pend, uint
 // pointer path (the dependency-rounds fallback this replaced cost ~100 k cycles per
 // overflowing chunk: 2-4 per block of long-read data).
 #ifndef SBH_LZ_WAVES_PER_EU
-#define SBH_LZ_WAVES_PER_EU 4  // (the register budget: 512 VGPRs / waves per SIMD)
+#define SBH_LZ_WAVES_PER_EU (SBH_LZ_RING ? 6 : 4)  // (the register budget: 512 VGPRs / waves per SIMD)
 #endif
 __global__ __launch_bounds__(LZ_THREADS, SBH_LZ_WAVES_PER_EU) void k_lz(const uint8_t *__restrict__ comp, DevBlocks bl, uint64_t nblocks,
                                                     const uint32_t *__restrict__ tok, uint8_t *__restrict__ U) {
@@ -2598,8 +2615,24 @@ __global__ __launch_bounds__(LZ_THREADS, SBH_LZ_WAVES_PER_EU) void k_lz(const ui
     }
     return;
   }
-  uint8_t *img = sm.img + sh;
+  [[maybe_unused]] uint8_t *img = sm.img + sh;
   const uint32_t *tk = tok + G;
+  const uint64_t g0u = G & ~15ull;  // flat address of image position 0
+#if SBH_LZ_RING
+  uint32_t fl = 0;  // image position of the first granule not yet in U (uniform)
+  // granules [fl, to) of the ring to U (the first one partial: the image starts at sh)
+  auto lz_flush = [&](uint32_t &from, uint32_t to) {
+    for (uint32_t q = from / 16 + t; q < to / 16; q += LZ_THREADS) {
+      const uint32_t lo = q * 16;
+      if (lo >= sh) {
+        *reinterpret_cast<uint4 *>(U + g0u + lo) = *reinterpret_cast<const uint4 *>(sm.img + lz_ri(lo));
+      } else {
+        for (uint32_t k = sh; k < 16; ++k) U[g0u + k] = sm.img[k];
+      }
+    }
+    from = to > from ? to : from;
+  };
+#endif
 
   uint32_t base = 0;  // output offset of the chunk's first token
 #ifdef SBH_LZ_PROBE
@@ -2643,6 +2676,11 @@ __global__ __launch_bounds__(LZ_THREADS, SBH_LZ_WAVES_PER_EU) void k_lz(const ui
     // case); long-match chunks take a few instead of a slower resolution.
     uint32_t pb = base;
     for (;;) {
+#if SBH_LZ_RING
+      // every byte before pb is final (the scan's or the last pass's barrier): its whole granules
+      // leave the ring for U before the ring wraps onto them
+      lz_flush(fl, (sh + pb) & ~15u);
+#endif
       // slots start at the 16-byte LDS granule holding `pb`, so that each thread's 16
       // slots are one granule of the image
       const uint32_t lead = (sh + pb) & 15, abase = pb - lead;
@@ -2679,7 +2717,7 @@ __global__ __launch_bounds__(LZ_THREADS, SBH_LZ_WAVES_PER_EU) void k_lz(const ui
         if (i0 + k >= n || wide[k] || !(off[k] - pb < plen)) continue;
         const uint32_t d = off[k] - abase;
         p16[d] = (uint16_t)(match[k] ? off[k] - dist[k] : off[k]);
-        if (!match[k]) img[off[k]] = (uint8_t)(x[k] >> 8);
+        if (!match[k]) sm.img[lz_ri(sh + off[k])] = (uint8_t)(x[k] >> 8);
 #if SBH_LZ_SBMASK
         const uint32_t w = d >> 5, bit = 1u << (d & 31);
         wA = wA == ~0u ? w : wA;
@@ -2879,11 +2917,20 @@ __global__ __launch_bounds__(LZ_THREADS, SBH_LZ_WAVES_PER_EU) void k_lz(const ui
       // position.
       auto gather8 = [&](const uint32_t *cp, uint32_t g0) {
         uint32_t w[2];
+#if SBH_LZ_RING
+        const uint8_t *rb = sm.img;
+#pragma unroll
+        for (uint32_t q = 0; q < 2; ++q)
+          w[q] = (uint32_t)rb[lz_ri(sh + cp[4 * q])] | (uint32_t)rb[lz_ri(sh + cp[4 * q + 1])] << 8 |
+                 (uint32_t)rb[lz_ri(sh + cp[4 * q + 2])] << 16 | (uint32_t)rb[lz_ri(sh + cp[4 * q + 3])] << 24;
+        *reinterpret_cast<uint2 *>(sm.img + lz_ri(sh + g0)) = make_uint2(w[0], w[1]);
+#else
 #pragma unroll
         for (uint32_t q = 0; q < 2; ++q)
           w[q] = (uint32_t)img[cp[4 * q]] | (uint32_t)img[cp[4 * q + 1]] << 8 | (uint32_t)img[cp[4 * q + 2]] << 16 |
                  (uint32_t)img[cp[4 * q + 3]] << 24;
         *reinterpret_cast<uint2 *>(img + g0) = make_uint2(w[0], w[1]);
+#endif
       };
       const uint32_t p16a = (uint32_t)reinterpret_cast<uintptr_t>(p16);
       [[maybe_unused]] const uint32_t choff = uni(p16a) - 2u * abase;  // LDS address of pointer c: choff + 2 c
@@ -2965,17 +3012,22 @@ __global__ __launch_bounds__(LZ_THREADS, SBH_LZ_WAVES_PER_EU) void k_lz(const ui
            (unsigned long long)t_init, (unsigned long long)t_ch, (unsigned long long)t_rounds, nrounds, njumps, nlong);
 #endif
   const uint32_t usize = base;
-  // write the image: 16-byte granules aligned to the flat address
-  const uint64_t g0 = G & ~15ull;
+  // write the image: 16-byte granules aligned to the flat address (the ring: those not yet written)
+  const uint64_t g0 = g0u;
   const uint32_t ngran = (sh + usize + 15) / 16;
-  for (uint32_t q = t; q < ngran; q += LZ_THREADS) {
+#if SBH_LZ_RING
+  const uint32_t q0 = fl / 16;
+#else
+  const uint32_t q0 = 0;
+#endif
+  for (uint32_t q = q0 + t; q < ngran; q += LZ_THREADS) {
     const uint32_t lo = q * 16;  // image offset (relative to sm.img) of the granule
     if (lo >= sh && lo + 16 <= sh + usize) {
-      *reinterpret_cast<uint4 *>(U + g0 + lo) = *reinterpret_cast<const uint4 *>(sm.img + lo);
+      *reinterpret_cast<uint4 *>(U + g0 + lo) = *reinterpret_cast<const uint4 *>(sm.img + lz_ri(lo));
     } else {
       for (uint32_t k = 0; k < 16; ++k) {
         const uint32_t a = lo + k;
-        if (a >= sh && a < sh + usize) U[g0 + a] = sm.img[a];
+        if (a >= sh && a < sh + usize) U[g0 + a] = sm.img[lz_ri(a)];
       }
     }
   }
