@@ -2639,6 +2639,12 @@ __global__ __launch_bounds__(LZ_THREADS, SBH_LZ_WAVES_PER_EU) void k_lz(const ui
   uint64_t tp0 = __builtin_readcyclecounter(), t_pre = 0, t_rounds = 0, t_init = 0, t_w = 0, t_ch = 0, t_mk = 0, t_b1 = 0;
   uint32_t nrounds = 0, njumps = 0, nlong = 0;
 #endif
+#ifndef SBH_LZ_PREFETCH
+// the next chunk's tokens loaded one chunk ahead (0: at the chunk's top).  At the ring's 80 VGPRs
+// the prefetched tokens were spilled to scratch right after their load (which then waited for
+// them): off for the ring (A/B r05za: k_lz -5% B, -6% D, -5% E, output identical)
+#define SBH_LZ_PREFETCH (!SBH_LZ_RING)
+#endif
   uint32_t xn[LZ_TPT];  // next chunk's tokens, loaded one chunk ahead
 #pragma unroll
   for (uint32_t k = 0; k < LZ_TPT; ++k) xn[k] = LZ_TPT * t + k < n ? tk[LZ_TPT * t + k] : 0;
@@ -2653,8 +2659,12 @@ __global__ __launch_bounds__(LZ_THREADS, SBH_LZ_WAVES_PER_EU) void k_lz(const ui
     uint32_t mysum = 0;
 #pragma unroll
     for (uint32_t k = 0; k < LZ_TPT; ++k) {
+#if SBH_LZ_PREFETCH
       x[k] = xn[k];
       xn[k] = i0 + LZ_CHUNK + k < n ? tk[i0 + LZ_CHUNK + k] : 0;
+#else
+      x[k] = i0 + k < n ? tk[i0 + k] : 0;
+#endif
       match[k] = i0 + k < n && (x[k] & TOK_MATCH) != 0;
       len[k] = i0 + k >= n ? 0 : match[k] ? (x[k] >> 16) & 0x1ff : 1;
       dist[k] = x[k] & 0xffff;
