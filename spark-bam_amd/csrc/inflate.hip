@@ -2220,22 +2220,12 @@ __device__ void huff_probe_done(uint32_t tid, uint64_t nblocks, uint64_t hk0, bo
 }
 #endif
 
-#ifndef SBH_HUFF_BIG
-// blocks whose deflate bytes exceed k_huff's 24 KiB stage (long-read and level-1 data: 11% of
-// config D's blocks, 66% of E's) go to a second instantiation with a 40 KiB stage at three
-// workgroups per CU instead of reading their bits from global memory at four
-#define SBH_HUFF_BIG 1
-#endif
-constexpr uint32_t INF_BIG = 0xfdu;  // (inside inflate only) left to k_huff<BIG_STAGE_DW, true>
-constexpr uint32_t BIG_STAGE_DW = 10240;
-template <uint32_t SDW, bool BIG>
-__device__ __forceinline__ void huff_block(const uint8_t *__restrict__ comp, DevBlocks bl, uint64_t nblocks,
-                                           uint32_t *__restrict__ tok) {
-  __shared__ HuffSmemT<HT, SDW> sm;
+__global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__restrict__ comp, DevBlocks bl, uint64_t nblocks,
+                                              uint32_t *__restrict__ tok) {
+  __shared__ HuffSmem sm;
   const uint32_t tid = threadIdx.x, lane = tid & (WAVE - 1), wid = uni(tid / WAVE);
   const uint64_t b = blockIdx.x;
   if (b >= nblocks) return;
-  if (BIG && uni(bl.status[b]) != INF_BIG) return;
   const uint64_t cstart = bl.cstart[b];
   const uint32_t csize = bl.csize[b], hsize = bl.hsize[b], usize = bl.usize[b];
   const uint64_t G = bl.ustart[b];
@@ -2252,7 +2242,7 @@ __device__ __forceinline__ void huff_block(const uint8_t *__restrict__ comp, Dev
         bl.ntok[b] = NTOK_STORED;
       }
 #ifdef SBH_HUFF_PROBE
-      if (!BIG) huff_probe_done(tid, nblocks, 0, false);
+      huff_probe_done(tid, nblocks, 0, false);
 #endif
       return;
     }
@@ -2298,14 +2288,7 @@ __device__ __forceinline__ void huff_block(const uint8_t *__restrict__ comp, Dev
         else if (i < 352) sm.t.pk[(i - 320) >> 4][(i - 320) & 15] = sv[k];
       }
     };
-    if (!BIG && SBH_HUFF_BIG && ndw > SDW && ndw <= BIG_STAGE_DW) {  // the big-stage kernel decodes it
-      if (tid == 0) bl.status[b] = INF_BIG;
-#ifdef SBH_HUFF_PROBE
-      huff_probe_done(tid, nblocks, 0, false);
-#endif
-      return;
-    }
-    if (ndw <= SDW) {
+    if (ndw <= STAGE_DW) {
       const uint32_t *g = reinterpret_cast<const uint32_t *>(dbase);
       for (uint32_t i = tid; i < ndw; i += HT) sm.stage[i] = g[i];
       if (pre) put_tables();
@@ -2331,7 +2314,7 @@ __device__ __forceinline__ void huff_block(const uint8_t *__restrict__ comp, Dev
         bl.status[b] = INF_TAIL;
       }
 #ifdef SBH_HUFF_PROBE
-      if (!BIG) huff_probe_done(tid, nblocks, hk0, true);
+      huff_probe_done(tid, nblocks, hk0, true);
 #endif
       return;
     }
@@ -2341,24 +2324,15 @@ __device__ __forceinline__ void huff_block(const uint8_t *__restrict__ comp, Dev
         bl.ntok[b] = ntok;
       }
 #ifdef SBH_HUFF_PROBE
-      if (!BIG) huff_probe_done(tid, nblocks, hk0, true);
+      huff_probe_done(tid, nblocks, hk0, true);
 #endif
       return;
     }
   }
   if (tid == 0) bl.status[b] = INF_SERIAL;  // k_huff_serial<true> decodes it
 #ifdef SBH_HUFF_PROBE
-  if (!BIG) huff_probe_done(tid, nblocks, hk0, false);
+  huff_probe_done(tid, nblocks, hk0, false);
 #endif
-}
-
-__global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__restrict__ comp, DevBlocks bl,
-                                                         uint64_t nblocks, uint32_t *__restrict__ tok) {
-  huff_block<STAGE_DW, false>(comp, bl, nblocks, tok);
-}
-__global__ __launch_bounds__(HT, 3) void k_huff_big(const uint8_t *__restrict__ comp, DevBlocks bl, uint64_t nblocks,
-                                                    uint32_t *__restrict__ tok) {
-  huff_block<BIG_STAGE_DW, true>(comp, bl, nblocks, tok);
 }
 
 // The rest of a block k_huff deferred (INF_TAIL: a short final deflate block, typically),
@@ -3098,9 +3072,6 @@ hipError_t launch_huff(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, 
   hipLaunchKernelGGL(k_hdr, dim3((uint32_t)((nblocks + HDR_WAVES - 1) / HDR_WAVES)), dim3(WAVE * HDR_WAVES), 0, stream,
                      comp, blocks, nblocks, tok);
   hipLaunchKernelGGL(k_huff, dim3((uint32_t)nblocks), dim3(HT), 0, stream, comp, blocks, nblocks, tok);
-#if SBH_HUFF_BIG
-  hipLaunchKernelGGL(k_huff_big, dim3((uint32_t)nblocks), dim3(HT), 0, stream, comp, blocks, nblocks, tok);
-#endif
 #if SBH_TAIL
   hipLaunchKernelGGL(k_huff_tail, dim3((uint32_t)nblocks), dim3(TAIL_NT), 0, stream, comp, blocks, nblocks, tok);
 #endif
