@@ -1050,7 +1050,10 @@ constexpr uint32_t FNV = FTILE / 16 + 256;    // staged 16-byte vectors: tile + 
                                               // 10 short records stay in LDS)
 constexpr uint32_t FSN = FNV * 16;            // staged bytes
 constexpr uint32_t FBW = FSN / 32;            // bitmap words
-constexpr uint32_t FCCAP = 256;               // close calls buffered per workgroup
+#ifndef SBH_FULL_FCCAP
+#define SBH_FULL_FCCAP 256
+#endif
+constexpr uint32_t FCCAP = SBH_FULL_FCCAP;    // close calls buffered per workgroup
 #ifndef SBH_FULL_CTG_LDS
 #define SBH_FULL_CTG_LDS 1
 #endif
@@ -1261,7 +1264,10 @@ __device__ uint32_t chain_full(const Src &s, const uint32_t *bname, const uint32
   }
 }
 
-__global__ __launch_bounds__(T, 5) void k_full(const uint8_t *__restrict__ U, uint64_t u_pad, uint64_t begin,
+#ifndef SBH_FULL_WGS
+#define SBH_FULL_WGS 5  // workgroups per CU the register budget allows
+#endif
+__global__ __launch_bounds__(T, SBH_FULL_WGS) void k_full(const uint8_t *__restrict__ U, uint64_t u_pad, uint64_t begin,
                                             uint64_t end, Segs sg, Ctg c, int32_t rtc, FullOut o, OpIdx oi) {
 #ifndef SBH_FULL_PACKED
 #define SBH_FULL_PACKED 0  // 1: Counts replicas as 16-bit counter pairs (A/B: 7.53 -> 7.72 ms, not kept)
