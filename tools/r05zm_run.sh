@@ -1,0 +1,10 @@
+# round 5, late: provisional tokens, interleaved groups, the copy storing 16 bytes at a time --
+# one group index contiguous) -- parity tests, then the inflate A/B against lib_pv0 on B, D, E, and
+# the Huffman phase probe (lib_hp) on B.
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest -m gpu --timeout 120 --timeout-method thread -x -q tests/test_gpu_parity.py \
+  > gpurun_out/r05zm_pytest_parity.log 2>&1 || exit 1
+AB_ROUNDS=2 timeout -k 10 900 bash tools/gpu_round.sh ab r05zm B 4000000 pv0 || exit 3
+AB_ROUNDS=1 timeout -k 10 600 bash tools/gpu_round.sh ab r05zmp B 4000000 hp || exit 4
+echo done
