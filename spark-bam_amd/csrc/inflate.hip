@@ -1498,6 +1498,9 @@ __device__ __forceinline__ LaneRun redo_asm(const WaveSmem &t, const uint32_t *s
 #ifndef SBH_ASM_EMIT
 #define SBH_ASM_EMIT 1  // pass 3 (RUN_EMIT over the LDS stage) as the hand-written loop below
 #endif
+#ifndef SBH_EMIT_NOCHK
+#define SBH_EMIT_NOCHK 1  // emit_asm: no too-far-back test per distance code (k_lz tests each match token once)
+#endif
 #ifndef SBH_EMIT_X4
 #define SBH_EMIT_X4 1  // emit_asm: a lane's tokens stored four at a time (16-byte stores from v124..v127; A/B r05m/r05n: k_huff -7% E, +-0.2% B and D)
 #endif
@@ -1613,10 +1616,18 @@ __device__ __forceinline__ void emit_asm(const WaveSmem &t, const uint32_t *stag
       "v_mov_b32 %[pos], %[np]\n\t"
       // the token: a literal (byte << 8) or the match completed by this distance code
       "v_lshlrev_b32 %[vtok], 8, %[val]\n\t"
+#if SBH_EMIT_NOCHK
+      // (ml: the match token's upper half, TOK_MATCH | length << 16, set by every code -- only a
+      // length code's is ever read, by the distance code after it)
+      "v_or_b32 %[np], %[ml], %[val]\n\t"
+      "v_lshl_add_u32 %[ml], %[val], 16, %[mlk]\n\t"
+#else
       "v_add_u32 %[tmp], 1, %[ml]\n\t"
       "v_lshl_or_b32 %[np], %[tmp], 16, %[val]\n\t"
       "v_or_b32 %[np], 0x80000000, %[np]\n\t"
+#endif
       "v_cndmask_b32_e64 %[vtok], %[np], %[vtok], %[sA]\n\t"
+#if !SBH_EMIT_NOCHK
       // too far back: a distance past the bytes before its match
       "v_lshrrev_b32 %[vb], 12, %[acc]\n\t"
       "v_sub_u32 %[vb], %[vb], %[ml]\n\t"
@@ -1625,6 +1636,7 @@ __device__ __forceinline__ void emit_asm(const WaveSmem &t, const uint32_t *stag
       "s_andn2_b64 %[sB], %[sB], %[sA]\n\t"
       "s_or_b64 %[sBad], %[sBad], %[sB]\n\t"
       "v_cndmask_b32_e64 %[ml], %[ml], %[val], %[sL]\n\t"
+#endif
       "s_waitcnt lgkmcnt(0)\n\t"
       "v_cndmask_b32_e32 %[lo], %[lo], %[hi], vcc\n\t"
       "v_cndmask_b32_e32 %[hi], %[hi], %[nx], vcc\n\t"
@@ -1686,7 +1698,7 @@ __device__ __forceinline__ void emit_asm(const WaveSmem &t, const uint32_t *stag
         [vb] "=&v"(vb), [sA] "=&s"(sA), [sB] "=&s"(sB), [sC] "=&s"(sC), [sD] "=&s"(sD), [sE] "=&s"(sE),
         [sL] "=&s"(sL), [sBad] "=&s"(sBad), [sv] "=&s"(sv)
       : [stop] "v"(stop2), [tabb] "s"(tabb), [stb] "s"(stb), [pkb] "s"(pkb), [sentb] "s"(sentb),
-        [sentd] "s"(sentd), [bad_e] "v"(bad_e), [om1] "v"(om1), [tkb] "s"(tkb)
+        [sentd] "s"(sentd), [bad_e] "v"(bad_e), [om1] "v"(om1), [tkb] "s"(tkb), [mlk] "s"(0x80010000u)
       : "vcc", "scc", "memory"
 #if SBH_EMIT_X4
       , "v124", "v125", "v126", "v127"
@@ -2676,6 +2688,17 @@ __global__ __launch_bounds__(LZ_THREADS, SBH_LZ_WAVES_PER_EU) void k_lz(const ui
 #pragma unroll
     for (uint32_t k = 1; k < LZ_TPT; ++k) off[k] = off[k - 1] + len[k - 1];
     const uint32_t chunk_end = base + chunk_len;
+#if SBH_EMIT_NOCHK
+    // too far back (zlib's "invalid distance too far back"): a match reaching before the block's
+    // first byte fails the block as the serial decoder would (INF_DATA); the Huffman passes no
+    // longer test each distance code (a block another path already failed keeps its status)
+    {
+      bool far = false;
+#pragma unroll
+      for (uint32_t k = 0; k < LZ_TPT; ++k) far = far || (match[k] && dist[k] > off[k]);
+      if (far && bl.status[b] == INF_OK) bl.status[b] = INF_DATA;
+    }
+#endif
 #ifdef SBH_LZ_PROBE
     const uint64_t tb = __builtin_readcyclecounter();
     t_pre += tb - ta;
