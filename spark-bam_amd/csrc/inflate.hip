@@ -1523,7 +1523,7 @@ __device__ __forceinline__ void emit_asm(const WaveSmem &t, const uint32_t *stag
   uint32_t vt = 0, tselb = tabb, ntok = 0, acc = 0, ml = 0, voff = tidx * 4u, badv = 0, cnt = 0;
   const uint32_t om1 = out0 - 1u;
   const uint32_t bad_e = 1u | PE_SPECIAL;
-  uint32_t e = 0, bits, a, nx, x, ex, val, np, tmp, r15, q, p11, p12, p13, p14, p15, d, sh, vtn, vtok, vb;
+  uint32_t e = 0, bits, a, nx, x, ex, val, np, tmp, r15, q, p11, p12, p13, p14, p15, d, sh, vtok, vb;
   uint64_t sA, sB, sC, sD, sE, sL, sBad, sv;
   asm volatile(
       "s_mov_b64 %[sv], exec\n\t"
@@ -1609,9 +1609,9 @@ __device__ __forceinline__ void emit_asm(const WaveSmem &t, const uint32_t *stag
       "v_bfe_u32 %[ex], %[bits], %[e], %[x]\n\t"
       "v_add3_u32 %[np], %[pos], %[tmp], %[x]\n\t"
       "v_add_u32_sdwa %[val], %[ex], %[e] dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
-      "v_and_b32 %[vtn], 0x1000, %[e]\n\t"
+      "v_and_b32 %[vt], 0x1000, %[e]\n\t"  // (the next code's state; this one's is in sA)
       "v_xor_b32 %[tmp], %[np], %[pos]\n\t"
-      "v_cmp_ne_u32 %[sL], 0, %[vtn]\n\t"  // a length code
+      "v_cmp_ne_u32 %[sL], 0, %[vt]\n\t"  // a length code
       "v_cmp_lt_u32 vcc, 31, %[tmp]\n\t"
       "v_mov_b32 %[pos], %[np]\n\t"
       // the token: a literal (byte << 8) or the match completed by this distance code
@@ -1664,10 +1664,11 @@ __device__ __forceinline__ void emit_asm(const WaveSmem &t, const uint32_t *stag
       "v_add_u32 %[voff], 4, %[voff]\n\t"
 #endif
       "s_mov_b64 exec, %[sB]\n\t"
+#if !SBH_EMIT_NOCHK  // (the token and byte counts feed the distance test only)
       "v_addc_co_u32_e64 %[ntok], vcc, 0, %[ntok], %[sA]\n\t"
-      "v_mov_b32 %[vt], %[vtn]\n\t"
-      "v_add_u32 %[tselb], %[tabb], %[vt]\n\t"
       "v_mad_u32_u24 %[acc], %[vt], %[val], %[acc]\n\t"
+#endif
+      "v_add_u32 %[tselb], %[tabb], %[vt]\n\t"
       "s_branch L_top%=\n"
       "L_end%=:\n\t"
       "s_waitcnt lgkmcnt(0)\n\t"
@@ -1694,7 +1695,7 @@ __device__ __forceinline__ void emit_asm(const WaveSmem &t, const uint32_t *stag
         [bits] "=&v"(bits),
         [a] "=&v"(a), [nx] "=&v"(nx), [x] "=&v"(x), [ex] "=&v"(ex), [val] "=&v"(val), [np] "=&v"(np),
         [tmp] "=&v"(tmp), [r15] "=&v"(r15), [q] "=&v"(q), [p11] "=&v"(p11), [p12] "=&v"(p12), [p13] "=&v"(p13),
-        [p14] "=&v"(p14), [p15] "=&v"(p15), [d] "=&v"(d), [sh] "=&v"(sh), [vtn] "=&v"(vtn), [vtok] "=&v"(vtok),
+        [p14] "=&v"(p14), [p15] "=&v"(p15), [d] "=&v"(d), [sh] "=&v"(sh), [vtok] "=&v"(vtok),
         [vb] "=&v"(vb), [sA] "=&s"(sA), [sB] "=&s"(sB), [sC] "=&s"(sC), [sD] "=&s"(sD), [sE] "=&s"(sE),
         [sL] "=&s"(sL), [sBad] "=&s"(sBad), [sv] "=&s"(sv)
       : [stop] "v"(stop2), [tabb] "s"(tabb), [stb] "s"(stb), [pkb] "s"(pkb), [sentb] "s"(sentb),
