@@ -39,6 +39,9 @@ namespace {
 #define SBH_HUFF_WAVES 4
 #endif
 constexpr int LIT_FAST = SBH_LIT_FAST;
+#ifndef SBH_HUFF_PAIRS
+#define SBH_HUFF_PAIRS 1  // literal-pair table entries and two-byte literal tokens (see PE_PAIR)
+#endif
 constexpr int DIST_FAST = 8;
 constexpr int CL_FAST = 7;
 constexpr int PDIST_FAST = 10;  // PAR-format distance table: one dword per entry, as wide as the literal one
@@ -53,6 +56,7 @@ constexpr uint32_t LZ_THREADS = SBH_LZ_THREADS;
 constexpr uint32_t LZ_SHORT = SBH_LZ_SHORT;  // longer matches get their pointers from the whole wave
 static_assert(LZ_SHORT <= 33, "k_lz finds a short match's start within 32 slots back");
 constexpr uint32_t NTOK_STORED = 0xffffffffu;  // ntok of a block whose payload is one stored deflate block
+constexpr uint32_t TOK_PAIR = 1u << 24;  // a literal token of two bytes (byte2 at [23:16])
 constexpr uint32_t TOK_MATCH = 0x80000000u;  // token: literal = byte << 8 (bit 31 clear); match = bit31 | len << 16 | dist
 
 // Table entries (32-bit; laid out so the asm hot loop decodes with few scalar ops):
@@ -83,6 +87,11 @@ constexpr uint32_t PE_LEN = 1u << 12;      // a length code: a distance code fol
 constexpr uint32_t PE_EOB = 1u << 13;      // (with PE_SPECIAL) end of block
 constexpr uint32_t PE_SLOW = 1u << 14;     // (with PE_SPECIAL) code longer than the table: slow_lane
 constexpr uint32_t PE_SPECIAL = 1u << 31;  // not a token: end of block, invalid, or long code
+// (SBH_HUFF_PAIRS) a literal entry that decodes two literal codes at once (their lengths summed in
+// [4:0]; the first byte at [23:16], the second's low 7 bits at [30:24] and its bit 7 at PE_L2B7):
+// one token of two bytes, (byte1 << 8) | (byte2 << 16) | TOK_PAIR
+constexpr uint32_t PE_L2B7 = 1u << 9;
+constexpr uint32_t PE_PAIR = 1u << 10;
 
 struct __attribute__((aligned(16))) WaveSmem {
   union {
@@ -330,6 +339,21 @@ __device__ __forceinline__ uint32_t ptable_entry(const SM &sm, const uint32_t *l
   return sm.sent[(kind ? 288 : 0) + (((sm.pk[kind][len] & 0xffffu) + (c15 >> (15 - len))) & 0xffffu)];
 }
 
+// Entry i of the literal/length table (PAR format), paired (SBH_HUFF_PAIRS): a literal code of
+// L1 < LIT_FAST bits whose next LIT_FAST - L1 bits hold a whole literal code gives both at once.
+// (The entry of i >> L1 is that second code's whatever the bits past the window: codes are
+// prefix-free, and a code of at most LIT_FAST - L1 bits lies inside it.)
+template <class SM>
+__device__ __forceinline__ uint32_t ptable_lit_entry(const SM &sm, const uint32_t *lj, uint32_t i) {
+  const uint32_t e1 = ptable_entry(sm, lj, 0, LIT_FAST, i);
+  if (!SBH_HUFF_PAIRS || (int32_t)e1 < 0 || (e1 & PE_LEN) || (e1 & 31) >= (uint32_t)LIT_FAST) return e1;
+  const uint32_t L1 = e1 & 31;
+  const uint32_t e2 = ptable_entry(sm, lj, 0, LIT_FAST, i >> L1);
+  if ((int32_t)e2 < 0 || (e2 & PE_LEN) || L1 + (e2 & 31) > (uint32_t)LIT_FAST) return e1;
+  const uint32_t b2 = (e2 >> 16) & 0xffu;
+  return (L1 + (e2 & 31)) | (e1 & 0x00ff0000u) | ((b2 & 0x7fu) << 24) | ((b2 >> 7) ? PE_L2B7 : 0u) | PE_PAIR;
+}
+
 // Canonical table in the PAR format (kind 0 lit/len, 1 dist), same validity rules as
 // build_table, built by one wave.  Returns 0 ok, 1 error, 2 empty.
 __device__ __forceinline__ uint32_t build_ptable(WaveSmem &sm, const uint8_t *lens, uint32_t nsym, uint32_t kind,
@@ -341,7 +365,8 @@ __device__ __forceinline__ uint32_t build_ptable(WaveSmem &sm, const uint8_t *le
 #pragma unroll
   for (uint32_t v = 1; v <= 15; ++v) lj[v] = sm.pk[kind][v] >> 16;
 #pragma unroll 4
-  for (uint32_t i = lane; i < (1u << fast); i += WAVE) tab[i] = ptable_entry(sm, lj, kind, fast, i);
+  for (uint32_t i = lane; i < (1u << fast); i += WAVE)
+    tab[i] = kind == 0 && fast == (uint32_t)LIT_FAST ? ptable_lit_entry(sm, lj, i) : ptable_entry(sm, lj, kind, fast, i);
   __builtin_amdgcn_wave_barrier();
   return rc;
 }
@@ -1132,7 +1157,7 @@ __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, S src, uint32_t A
     const uint32_t tnew = e & PE_LEN;
     if (MODE == RUN_EMIT) {
       if (atb && !tnew) {
-        dst[ntok] = val << 8;  // a literal
+        dst[ntok] = (val << 8) | ((e & (PE_L2B7 | PE_PAIR)) << 14);  // a literal (or a pair: TOK_PAIR)
       } else if (!atb) {       // a distance completing a match (started at token ntok - 1)
         dst[ntok - 1] = TOK_MATCH | ((ml + 1) << 16) | val;
         // bytes before the match: out0 + tokens before it + the earlier matches' extra bytes
@@ -1142,6 +1167,7 @@ __device__ __forceinline__ LaneRun lane_run(const WaveSmem &t, S src, uint32_t A
     }
     ntok += atb ? 1u : 0u;
     acc += (uint32_t)__umul24(tnew, val);  // (tnew: 0 or 4096; one v_mad_u32_u24)
+    acc += (e & PE_PAIR) << 2;              // a literal pair: one byte more than its token
     tsel = tnew;
   }
   if (MODE == RUN_SPEC) {  // oldest first: CK1's boundary in p1
@@ -1313,6 +1339,10 @@ __device__ __forceinline__ LaneRun spec_asm(const WaveSmem &t, const uint32_t *s
       "v_addc_co_u32_e64 %[ntok], vcc, 0, %[ntok], %[sA]\n\t"
       "v_add_u32 %[tselb], %[tabb], %[vt]\n\t"
       "v_mad_u32_u24 %[acc], %[vt], %[val], %[acc]\n\t"
+#if SBH_HUFF_PAIRS
+      "v_and_b32 %[tmp], 0x400, %[e]\n\t"  // a literal pair (PE_PAIR): one byte more than its token
+      "v_lshl_add_u32 %[acc], %[tmp], 2, %[acc]\n\t"
+#endif
       "s_branch L_top%=\n"
       "L_end%=:\n\t"
       "s_waitcnt lgkmcnt(0)\n\t"
@@ -1463,6 +1493,10 @@ __device__ __forceinline__ LaneRun redo_asm(const WaveSmem &t, const uint32_t *s
       "v_addc_co_u32_e64 %[ntok], vcc, 0, %[ntok], %[sA]\n\t"
       "v_add_u32 %[tselb], %[tabb], %[vt]\n\t"
       "v_mad_u32_u24 %[acc], %[vt], %[val], %[acc]\n\t"
+#if SBH_HUFF_PAIRS
+      "v_and_b32 %[tmp], 0x400, %[e]\n\t"  // a literal pair (PE_PAIR): one byte more than its token
+      "v_lshl_add_u32 %[acc], %[tmp], 2, %[acc]\n\t"
+#endif
       "s_branch L_top%=\n"
       "L_end%=:\n\t"
       "s_waitcnt lgkmcnt(0)\n\t"
@@ -1616,6 +1650,10 @@ __device__ __forceinline__ void emit_asm(const WaveSmem &t, const uint32_t *stag
       "v_mov_b32 %[pos], %[np]\n\t"
       // the token: a literal (byte << 8) or the match completed by this distance code
       "v_lshlrev_b32 %[vtok], 8, %[val]\n\t"
+#if SBH_HUFF_PAIRS
+      "v_and_b32 %[tmp], 0x600, %[e]\n\t"  // (a literal pair: byte2's bit 7 and TOK_PAIR)
+      "v_lshl_or_b32 %[vtok], %[tmp], 14, %[vtok]\n\t"
+#endif
 #if SBH_EMIT_NOCHK
       // (ml: the match token's upper half, TOK_MATCH | length << 16, set by every code -- only a
       // length code's is ever read, by the distance code after it)
@@ -1667,6 +1705,10 @@ __device__ __forceinline__ void emit_asm(const WaveSmem &t, const uint32_t *stag
 #if !SBH_EMIT_NOCHK  // (the token and byte counts feed the distance test only)
       "v_addc_co_u32_e64 %[ntok], vcc, 0, %[ntok], %[sA]\n\t"
       "v_mad_u32_u24 %[acc], %[vt], %[val], %[acc]\n\t"
+#if SBH_HUFF_PAIRS
+      "v_and_b32 %[tmp], 0x400, %[e]\n\t"
+      "v_lshl_add_u32 %[acc], %[tmp], 2, %[acc]\n\t"
+#endif
 #endif
       "v_add_u32 %[tselb], %[tabb], %[vt]\n\t"
       "s_branch L_top%=\n"
@@ -1815,7 +1857,7 @@ __device__ __forceinline__ void fill_ptables(WaveSmem &t, uint32_t tid) {
     lj1[v] = t.pk[1][v] >> 16;
   }
 #pragma unroll 4
-  for (uint32_t i = tid; i < (1u << LIT_FAST); i += NT) t.lit[i] = ptable_entry(t, lj0, 0, LIT_FAST, i);
+  for (uint32_t i = tid; i < (1u << LIT_FAST); i += NT) t.lit[i] = ptable_lit_entry(t, lj0, i);
 #pragma unroll 4
   for (uint32_t i = tid; i < (1u << PDIST_FAST); i += NT) t.dist[i] = ptable_entry(t, lj1, 1, PDIST_FAST, i);
 }
@@ -2197,7 +2239,7 @@ __global__ __launch_bounds__(WAVE * HDR_WAVES) void k_hdr(const uint8_t *__restr
       lj1[v] = t.pk[1][v] >> 16;
     }
 #pragma unroll 4
-    for (uint32_t i = lane; i < (1u << LIT_FAST); i += WAVE) out[i] = ptable_entry(t, lj0, 0, LIT_FAST, i);
+    for (uint32_t i = lane; i < (1u << LIT_FAST); i += WAVE) out[i] = ptable_lit_entry(t, lj0, i);
 #pragma unroll 4
     for (uint32_t i = lane; i < (1u << PDIST_FAST); i += WAVE)
       out[(1u << LIT_FAST) + i] = ptable_entry(t, lj1, 1, PDIST_FAST, i);
@@ -2474,6 +2516,9 @@ constexpr uint32_t LZ_LMARK_MIN = SBH_LZ_LMARK_MIN;
 #ifndef SBH_LZ_OVL_WAVE
 #define SBH_LZ_OVL_WAVE 0  // 1: overlapping short matches (dist < len) marked byte by byte by the wave (A/B r04c: k_lz +5% B, +26% D, +10% E: kept off)
 #endif
+#ifndef SBH_LZ_CARRY
+#define SBH_LZ_CARRY 1  // k_lz: a chunk that overflows its pass ends at the cut; the next chunk starts there
+#endif
 #ifndef SBH_LZ_NOCLAMP
 #define SBH_LZ_NOCLAMP 1  // the chase reads settled pointers' slots unclamped: one VALU + one SALU fewer per pointer (A/B r04v: k_lz -2.7% B, -2.8% D, -3.4% E)
 #endif
@@ -2658,10 +2703,17 @@ __global__ __launch_bounds__(LZ_THREADS, SBH_LZ_WAVES_PER_EU) void k_lz(const ui
 // them): off for the ring (A/B r05za: k_lz -5% B, -6% D, -5% E, output identical)
 #define SBH_LZ_PREFETCH (!SBH_LZ_RING)
 #endif
+static_assert(!(SBH_LZ_CARRY && SBH_LZ_PREFETCH), "the token prefetch assumes chunks of LZ_CHUNK tokens");
   uint32_t xn[LZ_TPT];  // next chunk's tokens, loaded one chunk ahead
 #pragma unroll
   for (uint32_t k = 0; k < LZ_TPT; ++k) xn[k] = LZ_TPT * t + k < n ? tk[LZ_TPT * t + k] : 0;
+#if SBH_LZ_CARRY
+  uint32_t c0n = 0;  // the next chunk's first token
+  for (uint32_t c0 = 0; c0 < n; c0 = c0n) {
+    c0n = c0 + LZ_CHUNK;
+#else
   for (uint32_t c0 = 0; c0 < n; c0 += LZ_CHUNK) {
+#endif
 #ifdef SBH_LZ_PROBE
     uint64_t ta = __builtin_readcyclecounter();
 #endif
@@ -2679,7 +2731,7 @@ __global__ __launch_bounds__(LZ_THREADS, SBH_LZ_WAVES_PER_EU) void k_lz(const ui
       x[k] = i0 + k < n ? tk[i0 + k] : 0;
 #endif
       match[k] = i0 + k < n && (x[k] & TOK_MATCH) != 0;
-      len[k] = i0 + k >= n ? 0 : match[k] ? (x[k] >> 16) & 0x1ff : 1;
+      len[k] = i0 + k >= n ? 0 : match[k] ? (x[k] >> 16) & 0x1ff : 1 + ((x[k] >> 24) & 1u);  // (TOK_PAIR: 2)
       dist[k] = x[k] & 0xffff;
       mysum += len[k];
     }
@@ -2709,6 +2761,7 @@ __global__ __launch_bounds__(LZ_THREADS, SBH_LZ_WAVES_PER_EU) void k_lz(const ui
     // that would end past the pass's slots.  One pass when the chunk fits (the common
     // case); long-match chunks take a few instead of a slower resolution.
     uint32_t pb = base;
+    [[maybe_unused]] uint32_t cend = chunk_end;  // (SBH_LZ_CARRY) where this chunk's pass ended
     for (;;) {
 #if SBH_LZ_RING
       // every byte before pb is final (the scan's or the last pass's barrier): its whole granules
@@ -2719,6 +2772,20 @@ __global__ __launch_bounds__(LZ_THREADS, SBH_LZ_WAVES_PER_EU) void k_lz(const ui
       // slots are one granule of the image
       const uint32_t lead = (sh + pb) & 15, abase = pb - lead;
       uint32_t pe = chunk_end;
+#if SBH_LZ_CARRY
+      // (carry: a chunk is one pass; the tokens from the cut on start the next chunk, so every
+      // chunk but the last of a block fills its pass instead of leaving a short second one)
+      static_assert(LZ_CHUNK <= 2048 && 65536u + 16u + 258u < (1u << 21), "cut keys: offset << 11 | token");
+      if (chunk_end - abase > PTR_CAP) {  // uniform: cut the chunk
+        uint32_t cut = ~0u;
+#pragma unroll
+        for (uint32_t k = 0; k < LZ_TPT; ++k)
+          if (i0 + k < n && off[k] + len[k] - abase > PTR_CAP) cut = min(cut, off[k] << 11 | (LZ_TPT * t + k));
+        const uint32_t key = block_min<LZ_THREADS>(cut, sm.pp.wmin);
+        pe = key >> 11;
+        c0n = c0 + (key & 0x7ffu);
+      }
+#else
       if (chunk_end - abase > PTR_CAP) {  // uniform: cut the chunk
         uint32_t cut = chunk_end;
 #pragma unroll
@@ -2726,6 +2793,7 @@ __global__ __launch_bounds__(LZ_THREADS, SBH_LZ_WAVES_PER_EU) void k_lz(const ui
           if (i0 + k < n && off[k] >= pb && off[k] + len[k] - abase > PTR_CAP) cut = min(cut, off[k]);
         pe = block_min<LZ_THREADS>(cut, sm.pp.wmin);
       }
+#endif
       const uint32_t plen = pe - pb;
 #ifdef SBH_LZ_PROBE
       nrounds += pe != chunk_end || pb != base;
@@ -2751,7 +2819,17 @@ __global__ __launch_bounds__(LZ_THREADS, SBH_LZ_WAVES_PER_EU) void k_lz(const ui
         if (i0 + k >= n || wide[k] || !(off[k] - pb < plen)) continue;
         const uint32_t d = off[k] - abase;
         p16[d] = (uint16_t)(match[k] ? off[k] - dist[k] : off[k]);
-        if (!match[k]) sm.img[lz_ri(sh + off[k])] = (uint8_t)(x[k] >> 8);
+        if (!match[k]) {
+          const uint32_t ia = lz_ri(sh + off[k]);
+          sm.img[ia] = (uint8_t)(x[k] >> 8);
+          // a literal pair's second byte: no start of its own (the slot pass points it at v + 1,
+          // itself); its image index from the first's (the ring wraps at LZ_IMG), computed here
+          if (x[k] & TOK_PAIR) {
+            uint32_t ib = ia + 1;
+            asm volatile("" : "+v"(ib));
+            sm.img[SBH_LZ_RING && ib == LZ_IMG ? 0u : ib] = (uint8_t)(x[k] >> 16);
+          }
+        }
 #if SBH_LZ_SBMASK
         const uint32_t w = d >> 5, bit = 1u << (d & 31);
         wA = wA == ~0u ? w : wA;
@@ -3012,13 +3090,21 @@ __global__ __launch_bounds__(LZ_THREADS, SBH_LZ_WAVES_PER_EU) void k_lz(const ui
 #ifdef SBH_LZ_PROBE
       t_ch += __builtin_readcyclecounter() - tc;
 #endif
+#if SBH_LZ_CARRY
+      cend = pe;
+      break;  // (one pass per chunk)
+#endif
       if (pe == chunk_end) break;
       __syncthreads();  // the pass's slots and start bits are reused by the next pass
       for (uint32_t w = t; w < SB_WORDS; w += LZ_THREADS) sm.pp.sbits[w] = 0;
       pb = pe;
       __syncthreads();
     }
+#if SBH_LZ_CARRY
+    base = cend;  // (chunk_end unless cut: the cut token starts the next chunk)
+#else
     base += chunk_len;
+#endif
 #if !SBH_LZ_NO_END_BAR
     __syncthreads();  // slots / wsum are reused by the next chunk
 #endif
