@@ -90,6 +90,14 @@ def main():
     ap.add_argument("--split-mib", type=float, default=32.0, help="Hadoop split size of the --file-gib file")
     ap.add_argument("--no-crc", action="store_true", help="--file-gib: skip the in-run CRC32 check")
     ap.add_argument("--no-pin", action="store_true", help="--file-gib: pageable host memory for the rank's bytes")
+    ap.add_argument("--no-facade", action="store_true",
+                    help="skip the load-API facade side measurement (loadReadsAndPositions per 32 MiB split)")
+    ap.add_argument("--facade-threads", type=int, default=4,
+                    help="concurrent task threads of the facade measurement (a Spark executor's cores)")
+    ap.add_argument("--facade-modes", default="hbm,pinned_host,hbm_records,calls_r05",
+                    help="facade modes to run (comma list; see facade_bench)")
+    ap.add_argument("--facade-only", action="store_true",
+                    help="skip full-check / e2e / CPU baseline side lines (facade iteration)")
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes per launch of the dominant kernel (default: the committed "
                          "rocprofv3 --pmc summary, profiles/*_pmc_traffic.json)")
@@ -290,6 +298,15 @@ def main():
     # Full-checker mode, reported separately: full.Checker at every owned
     # position with the FullCheck Counts aggregation (no per-position words), on the
     # inflated shard the last step left; wall time of the synchronous call, best of 2.
+    if args.facade_only:
+        args.no_full = args.no_e2e = args.no_cpu_baseline = True
+    facade = None
+    if (not args.no_facade and rank == 0 and world == 1 and shard is not None and not seg.file_offset
+            and seg.comp.size == seg.file_size):
+        facade = facade_bench(sb, ctx, seg.comp, seg.file_size, contig_len, args.facade_threads, torch, r,
+                              split_last, stream_splits, value_ref=total_flat * args.steps / elapsed / 1e9,
+                              modes=args.facade_modes.split(","))
+
     full = None
     if not args.no_full and shard is not None:
         f0 = max(0, shard.flat_bound(seg.file_offset)) if seg.file_offset else 0
@@ -425,6 +442,7 @@ def main():
                 "per_kernel_GBps": {k: gbps(v[0], v[1]) for k, v in kern.items()},
             },
             "full_check": full,
+            "facade": facade,
             "e2e_h2d": e2e,
             "cpu_baseline": cpu,
         }
@@ -584,6 +602,132 @@ def main_strong(args, rank, world, local_rank, device, backend, xdev, coll, dist
     if ranks_seen != args.gpus:
         log(f"ranks_seen {ranks_seen} != --gpus {args.gpus}")
         sys.exit(4)
+
+
+def facade_bench(sb, ctx, comp, file_size, contig_len, threads, torch, run, split_last, splits, value_ref,
+                 modes=("hbm", "pinned_host", "hbm_records", "calls_r05")):
+    """The load-API drop-in path (GpuCanLoadBam.loadReadsAndPositions, CanLoadBam.scala:316-356;
+    its twin spark_bam_amd.canloadbam): one task per 32 MiB Hadoop FileSplit, `threads` task threads
+    sharing the context (a Spark executor's cores), each with its own reused shard + pinned buffer
+    (SplitWorker) and ONE library call per split (sbh_split_records).  Modes:
+      hbm           the file's bytes already in HBM (device-to-device per split): the per-split
+                    overhead against `value`'s one resident shard
+      pinned_host   the file's bytes in page-locked host memory (a host read + H2D per split)
+      hbm_records   as hbm, plus what jni/Native.scala's GpuRecordIterator copies out of HBM to build
+                    htsjdk SAMRecords: the record starts and the records' bytes (into the task
+                    thread's page-locked buffer)
+      calls_r05     round 5's sequence (a shard per split, seven calls), one thread, from host memory
+    Wall time over every split; record starts -> vpos on the host; the per-split counts and first
+    records must equal the resident run's sbh_split_starts (checked against the oracle in tests/)."""
+    import threading
+
+    clb = __import__(sb.__name__ + ".canloadbam", fromlist=["x"])
+    read = __import__(sb.__name__ + ".sharded", fromlist=["x"]).bytes_reader(comp)
+    want_n = [int(x) for x in split_last["split_count"]]
+    want_v = [int(v) for v in split_last["split_vpos"]]
+    flat_total = int(run["flat_bytes"])
+    dev = torch.from_numpy(comp).to("cuda")
+    torch.cuda.synchronize()
+    pin = sb.PinnedBuffer(comp.size)
+    pin.array[:] = comp
+    pread = __import__(sb.__name__ + ".sharded", fromlist=["x"]).bytes_reader(pin.array)
+
+    def one_pass(mode, nthreads):
+        got = [None] * len(splits)
+        tm = [None] * len(splits)
+        it = iter(range(len(splits)))
+        lock = threading.Lock()
+        errs = []
+
+        def task():
+            w = clb.SplitWorker(ctx, file_size, contig_len,
+                                device_file=dev.data_ptr() if mode.startswith("hbm") else None)
+            out_pin = None
+            try:
+                while True:
+                    with lock:
+                        i = next(it, None)
+                    if i is None:
+                        return
+                    a, e = splits[i]
+                    t0 = time.perf_counter()
+                    cols = w.split(pread if mode == "pinned_host" else read, "bench.bam", a, e, decode=False)
+                    if mode == "hbm_records" and cols["flat"].size:
+                        # GpuRecordIterator: [first record, end of the last record) in one copy
+                        f = cols["flat"]
+                        last = int(f[-1])
+                        l4 = int(w.sh.read_flat(last, 4).view(np.uint32)[0])
+                        lo, hi = int(f[0]), last + 4 + l4
+                        if out_pin is None or out_pin.array.size < hi - lo:
+                            if out_pin is not None:
+                                out_pin.close()
+                            out_pin = sb.PinnedBuffer(int((hi - lo) * 1.25))
+                        w.sh.read_flat_into(lo, hi - lo, out_pin.array)
+                    got[i] = (int(cols["vpos"].size), int(cols["vpos"][0]) if cols["vpos"].size else None)
+                    tm[i] = time.perf_counter() - t0
+            except BaseException as ex:  # noqa: B902 (reported below)
+                errs.append(ex)
+            finally:
+                w.close()
+                if out_pin is not None:
+                    out_pin.close()
+
+        t0 = time.perf_counter()
+        if mode == "calls_r05":
+            for i, (a, e) in enumerate(splits):
+                ts = time.perf_counter()
+                cols = clb.split_partition_calls(ctx, read, file_size, "bench.bam", a, e, contig_len)
+                got[i] = (int(cols["vpos"].size), int(cols["vpos"][0]) if cols["vpos"].size else None)
+                tm[i] = time.perf_counter() - ts
+        else:
+            ts = [threading.Thread(target=task) for _ in range(nthreads)]
+            for t in ts:
+                t.start()
+            for t in ts:
+                t.join()
+        wall = time.perf_counter() - t0
+        if errs:
+            raise errs[0]
+        return wall, got, tm
+
+    out = {"splits": len(splits), "split_bytes": 32 << 20, "threads": threads, "value_ref_GBps": round(value_ref, 2)}
+    for mode in modes:
+        nth = 1 if mode == "calls_r05" else threads
+        reps = 1 if mode == "calls_r05" else 3
+        best = None
+        if mode != "calls_r05":
+            one_pass(mode, nth)  # warm: each thread's shard and pinned buffer reach their size
+        for _ in range(reps):
+            wall, got, tm = one_pass(mode, nth)
+            if best is None or wall < best[0]:
+                best = (wall, got, tm)
+        wall, got, tm = best
+        counts = [g[0] for g in got]
+        firsts = [g[1] for g in got]
+        ok = (counts == want_n and sum(counts) == int(run["count"]) and
+              all(f == v for f, v, n in zip(firsts, want_v, want_n) if n))
+        out[mode] = {"GBps_decompressed": round(flat_total / wall / 1e9, 2),
+                     "compressed_GBps": round(comp.size / wall / 1e9, 2),
+                     "records_per_s": round(sum(counts) / wall, 1), "ms": round(wall * 1e3, 2),
+                     "per_split_ms": {"mean": round(1e3 * float(np.mean(tm)), 3),
+                                      "max": round(1e3 * float(np.max(tm)), 3)},
+                     "threads": nth, "records": int(sum(counts)), "records_match": bool(ok),
+                     "frac_of_value": round(flat_total / wall / 1e9 / value_ref, 3) if value_ref else None}
+        log(f"facade {mode}: {out[mode]}")
+    # per-split device stages of one split (HIP events of its sbh_run_shard), thread-free
+    w = clb.SplitWorker(ctx, file_size, contig_len, device_file=dev.data_ptr())
+    try:
+        a, e = splits[len(splits) // 2]
+        w.split(read, "bench.bam", a, e, decode=False)
+        out["one_split_stages_ms"] = dict(zip(["index", "inflate+eager", "k_eager", "split/count", "k_huff", "k_lz"],
+                                              [round(x, 3) for x in w.sh.stage_times()]))
+    finally:
+        w.close()
+    pin.close()
+    del dev
+    out["note"] = ("GpuCanLoadBam.loadReadsAndPositions' per-split path (sbh_split_records per FileSplit, per-thread "
+                   "reused shard + pinned buffer, record starts -> vpos); not `value`")
+    return out
 
 
 def kernel_src_hash():

@@ -11,9 +11,19 @@
  *  - Every call returns an int status: SBH_OK or one of SBH_E_*, which map one-to-one
  *    onto the reference's exceptions (see below).  sbh_last_error() gives the message.
  *  - The caller owns every host buffer.  A context owns its device memory.
- *  - One context per device.  Calls on distinct contexts are thread-safe; a single
- *    context (and its shards) must be externally synchronized, like the reference's
- *    Checker instances (check/.../PosChecker.scala:19-20 share buffers).
+ *  - Threading.  One context per device per process, shared by every thread (a Spark
+ *    executor's concurrent tasks).  Any number of threads may call into one context at once
+ *    as long as each SHARD is used by one thread at a time -- the reference's model, where
+ *    each task builds its own channel and Checker (load/.../CanLoadBam.scala:316-320,
+ *    check/.../PosChecker.scala:19-20 share buffers inside one checker only).  Each shard
+ *    enqueues its device work on its own HIP stream, so two tasks' shards run concurrently
+ *    and one task's waits cover its own work only; context-level calls (sbh_run_stream2,
+ *    sbh_check_stream, sbh_find_blocks, sbh_bgzf_compress*) build their own shards per call
+ *    (sbh_run_stream2 takes a window cache from a pool in the context, one per concurrent
+ *    caller).  sbh_last_error / sbh_last_error_detail report the calling THREAD's last failed
+ *    call on that context, so a task always reads back its own failure.  sbh_ctx_set_stream
+ *    and sbh_ctx_destroy are setup/teardown calls: no other call may run on the context then
+ *    (shards created after sbh_ctx_set_stream enqueue on the caller's stream instead of their own).
  *  - Offsets: "file offsets" are byte offsets in the compressed BGZF file; "flat"
  *    offsets index the shard's concatenated uncompressed bytes (the reference's
  *    UncompressedBytes view, bgzf/.../block/UncompressedBytes.scala:13-87).  A
@@ -411,6 +421,32 @@ typedef struct {
 } sbh_records_out;
 int sbh_records_scan(sbh_shard *sh, uint64_t first_flat, uint64_t end_flat, sbh_records_sizes *out);
 int sbh_records_fetch(sbh_shard *sh, const sbh_records_out *out);
+
+/* One Hadoop FileSplit [start, end) of loadReadsAndPositions in ONE call (load/.../CanLoadBam.scala:
+ * 316-356, the body of its fileSplitsRDD.flatMap): FindBlockStart(start, bgzf_blocks_to_check)
+ * (FindBlockStart.scala:8-36), MetadataStream + inflate from that block, the eager check at every
+ * position of [Pos(blockStart, 0), Pos(end, 0)), FindRecordStart from Pos(blockStart, 0)
+ * (FindRecordStart.scala:11-30), and the records from it while pos < Pos(end, 0) (RecordStream.
+ * takeWhile): their starts, and with decode != 0 BAMRecordCodec.decode's columns, for
+ * sbh_records_fetch (decode == 0: only its `flat` column may be asked for).  The shard must hold
+ * the split's bytes from `start` plus a halo (sbh_shard_load reuses one shard for every split a
+ * thread runs).  Errors: SBH_E_HEADER_SEARCH_FAILED {start, positionsAttempted};
+ * SBH_E_NO_READ_FOUND {blockStart, maxReadSize} (NoReadFoundException(path, blockStart,
+ * maxReadSize)); SBH_E_NEED_HALO when an answer needs bytes past the resident range (reload with
+ * a larger halo) -- a last record running past the halo included. */
+typedef struct {
+  uint64_t block_start;     /* FindBlockStart(start)                                        */
+  uint64_t n_blocks;        /* blocks indexed from it (sbh_get_blocks), halo included        */
+  uint64_t flat_size;       /* their uncompressed bytes                                      */
+  uint64_t owned_flat;      /* flat image of Pos(end, 0): the split's positions [0, owned)   */
+  uint64_t first_flat;      /* FindRecordStart(Pos(blockStart, 0)) (may be >= owned_flat)    */
+  uint64_t first_vpos;      /* its htsjdk virtual position (when sizes.n > 0)                */
+  uint64_t n_true;          /* eager-true positions of [0, owned_flat)                       */
+  sbh_records_sizes sizes;  /* sizes.n = the split's records; column sizes when decoded      */
+} sbh_split_records_result;
+int sbh_split_records(sbh_shard *sh, uint64_t start, uint64_t end, int32_t bgzf_blocks_to_check,
+                      int32_t reads_to_check, int32_t max_read_size, int32_t decode,
+                      sbh_split_records_result *out);
 
 /* ---- loadBamIntervals ----
  * CanLoadBam.loadBamIntervals (load/.../CanLoadBam.scala:78-154) after the host has turned

@@ -78,6 +78,8 @@ object Native {
 
   @native def shardCreate(ctx: Long, comp: ByteBuffer, n: Long, fileOffset: Long, fileSize: Long): Long
   @native def shardDestroy(sh: Long): Unit
+  /** sbh_shard_load: new resident bytes [fileOffset, fileOffset + n) of the same file, device buffers kept */
+  @native def shardLoad(ctx: Long, sh: Long, comp: ByteBuffer, n: Long, fileOffset: Long): Unit
   @native def findBlockStart(ctx: Long, sh: Long, start: Long, blocksToCheck: Int): Long
   @native def indexAndInflate(ctx: Long, sh: Long, start: Long, out: Array[Long]): Unit
   @native def blocks(ctx: Long, sh: Long, first: Long, count: Long, out: Array[Long]): Unit
@@ -111,6 +113,10 @@ object Native {
                               blocksToCheck: Int, readsToCheck: Int, maxReadSize: Int, verifyCrc: Boolean,
                               splitStarts: Array[Long], splitEnds: Array[Long], splitOut: Array[Long],
                               out: Array[Long]): Unit
+  /** sbh_split_records: one FileSplit of loadReadsAndPositions in one call; out = {blockStart, nBlocks,
+    * flatSize, ownedFlat, firstFlat, firstVpos, nTrue, nRecords, nameBytes, cigarOps, bases, auxBytes} */
+  @native def splitRecords(ctx: Long, sh: Long, start: Long, end: Long, blocksToCheck: Int, readsToCheck: Int,
+                           maxReadSize: Int, decode: Boolean, out: Array[Long]): Unit
   /** out = {nRecords, nameBytes, cigarOps, bases, auxBytes} */
   @native def recordsScan(ctx: Long, sh: Long, first: Long, endFlat: Long, out: Array[Long]): Unit
   /** 18 direct buffers in sbh_records_out order, sized from recordsScan's `sizes` */
@@ -137,21 +143,38 @@ object Native {
                                  ivRef: Array[Int], ivBegin: Array[Long], ivEnd: Array[Long], out: Array[Long]): Unit
 }
 
-/** One executor GPU (one sbh_ctx), shared by its tasks under a lock (the reference's checkers are
-  * single-threaded per task, PosChecker.scala:19-20). */
+/** One executor GPU: one sbh_ctx, shared WITHOUT a lock by every task thread of the executor.  The
+  * library allows any number of threads on one context as long as each shard is used by one thread
+  * at a time (include/sparkbam.h, threading): every task below makes or reuses shards of its own
+  * (GpuShard, GpuSplitWorker), each shard runs on its own HIP stream, and a failed call's detail is
+  * kept per thread, so the shim's exception is always the calling task's.  This is the reference's
+  * model, where each task builds its own channel and checker (CanLoadBam.scala:316-320,
+  * PosChecker.scala:19-20).  (`lazy val` initialization is itself synchronized.) */
 object Device {
   lazy val ctx: Long = Native.ctxCreate(sys.env.getOrElse("LOCAL_RANK", "0").toInt)
 }
 
-/** Compressed bytes [fileOffset, fileOffset + n) of a BGZF file, resident in HBM. */
-class GpuShard(comp: ByteBuffer, n: Long, val fileOffset: Long, fileSize: Long, contigs: Array[Int])
+/** Compressed bytes [fileOffset, fileOffset + n) of a BGZF file, resident in HBM.  Used by one
+  * thread at a time; `reload` moves it to other bytes of the same file, keeping its device buffers. */
+class GpuShard(comp: ByteBuffer, private var n: Long, private var offset: Long, fileSize: Long, contigs: Array[Int])
   extends AutoCloseable {
   private val ctx = Device.ctx
-  val sh: Long = Native.shardCreate(ctx, comp, n, fileOffset, fileSize)
+  val sh: Long = Native.shardCreate(ctx, comp, n, offset, fileSize)
   Native.setContigs(ctx, sh, contigs)
-  val atEof: Boolean = fileOffset + n == fileSize
+  def fileOffset: Long = offset
+  def atEof: Boolean = offset + n == fileSize
   private val nf = new Array[Long](2)
   def load(start: Long): Unit = Native.indexAndInflate(ctx, sh, start, nf)
+  /** the resident bytes become [fileOffset, fileOffset + n) of the same file (sbh_shard_load) */
+  def reload(comp: ByteBuffer, n: Long, fileOffset: Long): Unit = {
+    Native.shardLoad(ctx, sh, comp, n, fileOffset)
+    this.n = n
+    this.offset = fileOffset
+    nf(0) = 0
+    nf(1) = 0
+  }
+  /** the block table a combined call (splitRecords) built: its size, for blocks() */
+  def indexed(numBlocks: Long, flatSize: Long): Unit = { nf(0) = numBlocks; nf(1) = flatSize }
   def numBlocks: Long = nf(0)
   def flatSize: Long = nf(1)
   def flatOf(pos: Pos): Long = Native.flatOf(ctx, sh, pos.toHTSJDK)
@@ -696,38 +719,93 @@ class GpuRecordIterator(shard: GpuShard, sizes: Array[Long], header: SAMFileHead
   }
 }
 
+/** One executor task thread's reusable device state for GpuSplitPartition: a page-locked buffer the
+  * split's bytes are read into and ONE shard whose device buffers (compressed bytes, tokens, flat
+  * bytes, bitmap, block table, record starts) serve every split the thread runs (sbh_shard_load,
+  * grow-only), so a split costs no host or device allocation.  Per thread (ThreadLocal): Spark runs
+  * an executor's tasks on a pool of threads, and a shard is one thread's at a time.  Mirrored by
+  * spark_bam_amd.canloadbam.SplitWorker. */
+class GpuSplitWorker(val contigs: Array[Int]) extends AutoCloseable {
+  private var buf: ByteBuffer = _
+  private var shard: GpuShard = _
+  private var fileSize = -1L
+
+  /** the thread's shard holding [lo, min(size, lo + n)) of the channel's file */
+  def load(ch: SeekableByteChannel, lo: Long, n: Long): GpuShard = {
+    val size = ch.size
+    val m = math.min(size - lo, n)
+    if (buf == null || buf.capacity < m) {
+      if (buf != null) Native.hostFree(buf)
+      buf = Native.hostAlloc(math.max(m + (m >> 3), 1L << 20))  // (room for a grown halo)
+    }
+    buf.clear()
+    buf.limit(m.toInt)
+    ch.seek(lo)
+    ch.readFully(buf)
+    buf.flip()
+    if (shard == null || fileSize != size) {
+      if (shard != null) shard.close()
+      shard = new GpuShard(buf, m, lo, size, contigs)
+      fileSize = size
+    } else shard.reload(buf, m, lo)
+    shard
+  }
+
+  override def close(): Unit = {
+    if (shard != null) { shard.close(); shard = null }
+    if (buf != null) { Native.hostFree(buf); buf = null }
+  }
+}
+
+object GpuSplitWorker {
+  private val local = new ThreadLocal[GpuSplitWorker]
+  /** the calling thread's worker; the contig lengths are set on its shard, so another file's
+    * contigs replace it */
+  def get(contigs: Array[Int]): GpuSplitWorker = {
+    val w = local.get
+    if (w != null && java.util.Arrays.equals(w.contigs, contigs)) w
+    else {
+      if (w != null) w.close()
+      val n = new GpuSplitWorker(contigs)
+      local.set(n)
+      n
+    }
+  }
+}
+
 /** loadReadsAndPositions' per-split body (CanLoadBam.scala:316-356) on the executor's GPU: the
-  * split's compressed bytes [start, end) plus a halo in one shard; FindBlockStart(start), index +
-  * inflate from it, the eager check over the owned positions [0, flat(Pos(end, 0))),
-  * FindRecordStart from Pos(blockStart, 0), then the records from it while pos < Pos(end, 0)
-  * (RecordStream.takeWhile).  The halo grows x4 while an answer needs bytes past it.  Mirrored
-  * call for call by spark_bam_amd.canloadbam.split_partition (tests/test_canloadbam_gpu.py). */
+  * split's compressed bytes [start, end) plus a halo in the task thread's reused shard, then ONE
+  * library call (sbh_split_records): FindBlockStart(start), index + inflate from it, the eager check
+  * over the owned positions [0, flat(Pos(end, 0))), FindRecordStart from Pos(blockStart, 0), and
+  * the record starts while pos < Pos(end, 0) (RecordStream.takeWhile).  The halo grows x4 while an
+  * answer -- the split's last record included -- needs bytes past it.  Mirrored call for call by
+  * spark_bam_amd.canloadbam.SplitWorker.split (tests/test_canloadbam_gpu.py, tests/test_threads_gpu.py). */
 object GpuSplitPartition {
   def apply(path: Path, start: Long, end: Long, header: SAMFileHeader, contigs: Array[Int],
             bgzfBlocksToCheck: Int, readsToCheck: Int, maxReadSize: Int,
             halo0: Long = 1L << 20): Iterator[(Pos, SAMRecord)] = {
     val ch = SeekableByteChannel(path)
+    val w = GpuSplitWorker.get(contigs)
     try {
       var halo = halo0
       while (true) {
-        val s = GpuShard.read(ch, start, end - start + halo, contigs)
+        val s = w.load(ch, start, end - start + halo)
         try {
-          val b = try Native.findBlockStart(Device.ctx, s.sh, start, bgzfBlocksToCheck) catch Native.rethrow(path)
-          s.load(b)
-          val owned = s.flatBound(end)
-          if (!s.atEof && owned == s.flatSize) throw new NeedHaloException(s"no block past $end in the halo")
-          val first = s.findRecordStart(0, readsToCheck, maxReadSize)
-            .getOrElse(throw NoReadFoundException(path, b, maxReadSize))._1
-          if (first >= owned) return Iterator.empty
-          Native.checkEager(Device.ctx, s.sh, 0, owned, readsToCheck, null)
-          val sizes = new Array[Long](5)
-          Native.recordsScan(Device.ctx, s.sh, first, owned, sizes)
-          return new GpuRecordIterator(s, sizes, header)
+          val out = new Array[Long](12)
+          try Native.splitRecords(Device.ctx, s.sh, start, end, bgzfBlocksToCheck, readsToCheck, maxReadSize,
+                                  false, out)
+          catch Native.rethrow(path)
+          s.indexed(out(1), out(2))
+          // (the iterator copies the starts and the records' bytes out: the shard is free again)
+          return new GpuRecordIterator(s, out.slice(7, 12), header)
         } catch {
-          case e: NeedHaloException ⇒
-            if (end + halo >= ch.size) throw e
+          case e: NeedHaloException if end + halo < ch.size ⇒ halo *= 4
+          // a record (or the chain's next one) past the resident bytes: more halo, as the reference
+          // would simply read on
+          case e: NativeException
+            if (e.status == Native.NOT_FOUND || e.status == Native.BAD_RECORD) && end + halo < ch.size ⇒
             halo *= 4
-        } finally s.close()
+        }
       }
       Iterator.empty
     } finally ch.close()

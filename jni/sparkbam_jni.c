@@ -197,6 +197,17 @@ JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_shardDestroy(JNIE
   sbh_shard_destroy(SH(sh));
 }
 
+/* sbh_shard_load: the shard's resident bytes replaced by [fileOffset, fileOffset + n) of the same
+ * file, its device buffers kept (a task thread's GpuSplitWorker reuses one shard for every split) */
+JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_shardLoad(JNIEnv *env, jobject self, jlong ctx,
+                                                                         jlong sh, jobject buf, jlong n,
+                                                                         jlong fileOffset) {
+  int bad = 0;
+  const void *comp = direct_n(env, buf, (uint64_t)n, &bad);
+  if (bad) return;
+  (void)failed(env, ctx, sbh_shard_load(SH(sh), comp, (uint64_t)n, (uint64_t)fileOffset, 0));
+}
+
 /* FindBlockStart.apply (bgzf/.../block/FindBlockStart.scala:8-36) */
 JNIEXPORT jlong JNICALL Java_org_hammerlab_bam_gpu_Native_00024_findBlockStart(JNIEnv *env, jobject self, jlong ctx,
                                                                                jlong sh, jlong start,
@@ -469,6 +480,24 @@ JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_recordsScan(JNIEn
   if (failed(env, ctx, sbh_records_scan(SH(sh), (uint64_t)first, (uint64_t)endFlat, &z))) return;
   jlong v[5] = {(jlong)z.n, (jlong)z.name_bytes, (jlong)z.cigar_ops, (jlong)z.bases, (jlong)z.aux_bytes};
   put_longs(env, out, v, 5);
+}
+
+/* One FileSplit of loadReadsAndPositions in one call (sbh_split_records, CanLoadBam.scala:316-356):
+ * out = {blockStart, nBlocks, flatSize, ownedFlat, firstFlat, firstVpos, nTrue, n, nameBytes,
+ * cigarOps, bases, auxBytes}; out[7..11] are recordsFetch's sizes */
+JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_splitRecords(JNIEnv *env, jobject self, jlong ctx,
+                                                                            jlong sh, jlong start, jlong end,
+                                                                            jint blocksToCheck, jint readsToCheck,
+                                                                            jint maxReadSize, jboolean decode,
+                                                                            jlongArray out) {
+  sbh_split_records_result r;
+  if (failed(env, ctx, sbh_split_records(SH(sh), (uint64_t)start, (uint64_t)end, blocksToCheck, readsToCheck,
+                                         maxReadSize, decode ? 1 : 0, &r)))
+    return;
+  jlong v[12] = {(jlong)r.block_start, (jlong)r.n_blocks, (jlong)r.flat_size, (jlong)r.owned_flat,
+                 (jlong)r.first_flat, (jlong)r.first_vpos, (jlong)r.n_true, (jlong)r.sizes.n,
+                 (jlong)r.sizes.name_bytes, (jlong)r.sizes.cigar_ops, (jlong)r.sizes.bases, (jlong)r.sizes.aux_bytes};
+  put_longs(env, out, v, 12);
 }
 
 JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_recordsFetch(JNIEnv *env, jobject self, jlong ctx,

@@ -39,7 +39,7 @@ EXPORTS = [
     "sbh_check_records", "sbh_run_shard",
     "sbh_stage_times", "sbh_run_stream", "sbh_run_stream2", "sbh_records_scan", "sbh_records_fetch", "sbh_records_scan_regions", "sbh_verify_crc",
     "sbh_bgzf_compress_bound", "sbh_bgzf_compress", "sbh_bgzf_compress_level",
-    "sbh_shard_load", "sbh_find_blocks", "sbh_check_stream",
+    "sbh_shard_load", "sbh_find_blocks", "sbh_check_stream", "sbh_split_records",
 ]
 LEVEL_HTSJDK, LEVEL_FAST = 5, -1  # sbh_bgzf_compress_level: htsjdk's zlib level 5 / this library's own coder
 
@@ -91,6 +91,12 @@ class SbhCheckResult(C.Structure):
 class SbhRecordsSizes(C.Structure):
     _fields_ = [("n", C.c_uint64), ("name_bytes", C.c_uint64), ("cigar_ops", C.c_uint64),
                 ("bases", C.c_uint64), ("aux_bytes", C.c_uint64)]
+
+
+class SbhSplitRecordsResult(C.Structure):
+    _fields_ = [("block_start", C.c_uint64), ("n_blocks", C.c_uint64), ("flat_size", C.c_uint64),
+                ("owned_flat", C.c_uint64), ("first_flat", C.c_uint64),
+                ("first_vpos", C.c_uint64), ("n_true", C.c_uint64), ("sizes", SbhRecordsSizes)]
 
 
 class SbhRecordsOut(C.Structure):  # host buffers (sbh_records_out); NULL = not copied
@@ -206,6 +212,7 @@ def lib():
                             C.POINTER(SbhStreamResult)],
         "sbh_records_scan": [P, U64, U64, C.POINTER(SbhRecordsSizes)],
         "sbh_records_fetch": [P, C.POINTER(SbhRecordsOut)],
+        "sbh_split_records": [P, U64, U64, I32, I32, I32, I32, C.POINTER(SbhSplitRecordsResult)],
         "sbh_records_scan_regions": [P, P, P, U64, P, P, P, C.c_uint32, C.POINTER(SbhRecordsSizes)],
         "sbh_verify_crc": [P, PU64, PU64],
         "sbh_shard_load": [P, P, U64, U64, C.c_int],

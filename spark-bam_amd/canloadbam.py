@@ -21,7 +21,7 @@ from ._lib import (SBH_E_BAD_RECORD, SBH_E_NEED_HALO, SBH_E_NOT_FOUND, HeaderSea
 from .api import (DEFAULT_BGZF_BLOCKS_TO_CHECK, DEFAULT_MAX_READ_SIZE, DEFAULT_READS_TO_CHECK, Pos, Split,
                   file_splits)
 from .api import DEFAULT_SPLIT_SIZE as DEFAULT_MAX_SPLIT_SIZE
-from .device import Context
+from .device import Context, PinnedBuffer
 from .intervals import (DEFAULT_COMPRESSION_RATIO, _flat_of_pos, _vpos_of_flat, capped_cost_groups, chunk_size,
                         get_interval_chunks, parse_loci, read_bai)
 from .intervals import DEFAULT_SPLIT_SIZE
@@ -41,10 +41,101 @@ def _empty():
     return cols
 
 
+class SplitWorker:
+    """One task thread's reusable device state (jni/Native.scala `GpuSplitWorker`): a page-locked
+    buffer the split's bytes are read into and ONE shard whose device buffers (compressed bytes,
+    tokens, flat bytes, bitmap, block table, record columns) serve every split the thread runs
+    (sbh_shard_load, grow-only), so a split costs no host or device allocation.  A worker belongs
+    to one thread at a time (include/sparkbam.h, threading); a context is shared by all of them."""
+
+    def __init__(self, ctx, size, contigs, device_file=None):
+        self.ctx, self.size = ctx, int(size)
+        self.contigs = np.ascontiguousarray(np.asarray(contigs, dtype=np.int32))
+        self.sh = None
+        self.pin = None
+        # device_file: a device pointer to the whole file's bytes already in HBM (the facade bench's
+        # resident mode: the split's bytes are copied device-to-device, no host read or H2D)
+        self.device_file = device_file
+
+    def load(self, read, lo, hi):
+        """The shard holding file bytes [lo, hi), read into the page-locked buffer first."""
+        n = hi - lo
+        if self.device_file is not None:
+            if self.sh is None:
+                self.sh = self.ctx.shard(self.device_file + lo, file_offset=lo, file_size=self.size, on_device=True,
+                                         nbytes=n)
+                self.sh.set_contigs(self.contigs)
+            else:
+                self.sh.load(self.device_file + lo, lo, on_device=True, nbytes=n)
+            return self.sh
+        if self.pin is None or self.pin.array.size < n:
+            if self.pin is not None:
+                self.pin.close()
+            self.pin = PinnedBuffer(max(n, 1 << 20) + (n >> 3))  # (room for a grown halo)
+        buf = self.pin.array[:n]
+        np.copyto(buf, read(lo, hi))
+        if self.sh is None:
+            self.sh = self.ctx.shard(buf, file_offset=lo, file_size=self.size)
+            self.sh.set_contigs(self.contigs)  # (kept across sbh_shard_load)
+        else:
+            self.sh.load(buf, lo)
+        return self.sh
+
+    def split(self, read, path, start, end, bgzf_blocks_to_check=DEFAULT_BGZF_BLOCKS_TO_CHECK,
+              reads_to_check=DEFAULT_READS_TO_CHECK, max_read_size=DEFAULT_MAX_READ_SIZE, decode=True,
+              halo0=1 << 20):
+        """GpuSplitPartition: loadReadsAndPositions' body for the FileSplit [start, end)
+        (CanLoadBam.scala:316-356) in one library call (sbh_split_records), the halo grown x4
+        while an answer needs bytes past it.  Returns the split's records (columns + vpos; only
+        flat + vpos without decode)."""
+        halo = halo0
+        while True:
+            sh = self.load(read, start, min(self.size, end + halo))
+            try:
+                info, cols = sh.split_records(start, end, bgzf_blocks_to_check, reads_to_check, max_read_size, decode)
+            except HeaderSearchFailedException as e:
+                raise e.with_path(path)
+            except NoReadFoundException as e:
+                raise e.with_path(path)
+            except SparkBamError as e:
+                # a record (or the chain's next one) past the resident bytes: more halo
+                if e.code not in (SBH_E_NEED_HALO, SBH_E_NOT_FOUND, SBH_E_BAD_RECORD) or end + halo >= self.size:
+                    raise
+                halo *= 4
+                continue
+            cols["vpos"] = sh.vpos_of_flat(cols["flat"]) if cols["flat"].size else np.zeros(0, np.uint64)
+            self.last = info
+            return cols
+
+    def close(self):
+        if self.sh is not None:
+            self.sh.close()
+            self.sh = None
+        if self.pin is not None:
+            self.pin.close()
+            self.pin = None
+
+
 def split_partition(ctx, read, size, path, start, end, contigs, bgzf_blocks_to_check=DEFAULT_BGZF_BLOCKS_TO_CHECK,
-                    reads_to_check=DEFAULT_READS_TO_CHECK, max_read_size=DEFAULT_MAX_READ_SIZE, halo0=1 << 20):
+                    reads_to_check=DEFAULT_READS_TO_CHECK, max_read_size=DEFAULT_MAX_READ_SIZE, halo0=1 << 20,
+                    worker=None):
     """GpuSplitPartition: loadReadsAndPositions' body for the FileSplit [start, end)
-    (CanLoadBam.scala:316-356).  Returns the split's records (columns + vpos)."""
+    (CanLoadBam.scala:316-356).  Returns the split's records (columns + vpos).  `worker`: the
+    calling thread's SplitWorker (one is made for the call when absent)."""
+    own = worker is None
+    w = worker or SplitWorker(ctx, size, contigs)
+    try:
+        return w.split(read, path, start, end, bgzf_blocks_to_check, reads_to_check, max_read_size, True, halo0)
+    finally:
+        if own:
+            w.close()
+
+
+def split_partition_calls(ctx, read, size, path, start, end, contigs, bgzf_blocks_to_check=DEFAULT_BGZF_BLOCKS_TO_CHECK,
+                          reads_to_check=DEFAULT_READS_TO_CHECK, max_read_size=DEFAULT_MAX_READ_SIZE, halo0=1 << 20):
+    """The same split as separate C-ABI calls (round 5's GpuSplitPartition: a shard per split,
+    FindBlockStart, index, inflate, flat_bound, FindRecordStart, check_eager, records_scan), kept
+    as the cross-check of sbh_split_records and as the facade bench's "before" line."""
     halo = halo0
     while True:
         sh = ctx.shard(read(start, min(size, end + halo)), file_offset=start, file_size=size)
@@ -71,7 +162,7 @@ def split_partition(ctx, read, size, path, start, end, contigs, bgzf_blocks_to_c
             cols["vpos"] = _vpos_of_flat(sh.blocks(), cols["flat"]) if cols["flat"].size else np.zeros(0, np.uint64)
             return cols
         except SparkBamError as e:
-            if e.code != SBH_E_NEED_HALO or end + halo >= size:
+            if e.code not in (SBH_E_NEED_HALO, SBH_E_NOT_FOUND, SBH_E_BAD_RECORD) or end + halo >= size:
                 raise
             halo *= 4
         finally:
@@ -80,9 +171,11 @@ def split_partition(ctx, read, size, path, start, end, contigs, bgzf_blocks_to_c
 
 def load_reads_and_positions(path, split_size=DEFAULT_MAX_SPLIT_SIZE,
                              bgzf_blocks_to_check=DEFAULT_BGZF_BLOCKS_TO_CHECK,
-                             reads_to_check=DEFAULT_READS_TO_CHECK, max_read_size=DEFAULT_MAX_READ_SIZE, ctx=None):
+                             reads_to_check=DEFAULT_READS_TO_CHECK, max_read_size=DEFAULT_MAX_READ_SIZE, ctx=None,
+                             threads=1):
     """GpuCanLoadBam.loadReadsAndPositions: one partition per FileSplit, each a Reads batch
-    (its vpos column = the reference's Pos keys)."""
+    (its vpos column = the reference's Pos keys).  threads > 1 runs the splits on that many
+    concurrent task threads sharing the context (a Spark executor's cores)."""
     from .sharded import read_header
     read, name = _reader(path)
     size = read.size
@@ -90,11 +183,47 @@ def load_reads_and_positions(path, split_size=DEFAULT_MAX_SPLIT_SIZE,
     ctx = ctx or Context(0)
     try:
         names, lens, _ = read_header(ctx, read, size)
-        parts = []
-        for start, end in file_splits(size, split_size):
-            cols = split_partition(ctx, read, size, name, start, end, lens, bgzf_blocks_to_check, reads_to_check,
-                                   max_read_size)
-            parts.append(Reads(cols, names))
+        splits = file_splits(size, split_size)
+        parts = [None] * len(splits)
+        if threads <= 1:
+            w = SplitWorker(ctx, size, lens)
+            try:
+                for i, (start, end) in enumerate(splits):
+                    parts[i] = Reads(w.split(read, name, start, end, bgzf_blocks_to_check, reads_to_check,
+                                             max_read_size), names)
+            finally:
+                w.close()
+            return parts
+        # an executor's concurrent tasks: `threads` task threads share the context, each with its
+        # own worker (shard + pinned buffer), taking the splits in order like Spark's task queue
+        import threading
+        nxt = iter(range(len(splits)))
+        lock = threading.Lock()
+        errors = []
+
+        def task():
+            w = SplitWorker(ctx, size, lens)
+            try:
+                while True:
+                    with lock:
+                        i = next(nxt, None)
+                    if i is None or errors:
+                        return
+                    start, end = splits[i]
+                    parts[i] = Reads(w.split(read, name, start, end, bgzf_blocks_to_check, reads_to_check,
+                                             max_read_size), names)
+            except BaseException as e:  # (re-raised on the calling thread)
+                errors.append(e)
+            finally:
+                w.close()
+
+        ts = [threading.Thread(target=task) for _ in range(threads)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        if errors:
+            raise errors[0]
         return parts
     finally:
         if own:
@@ -102,16 +231,19 @@ def load_reads_and_positions(path, split_size=DEFAULT_MAX_SPLIT_SIZE,
 
 
 def load_bam(path, split_size=DEFAULT_MAX_SPLIT_SIZE, bgzf_blocks_to_check=DEFAULT_BGZF_BLOCKS_TO_CHECK,
-             reads_to_check=DEFAULT_READS_TO_CHECK, max_read_size=DEFAULT_MAX_READ_SIZE, ctx=None):
+             reads_to_check=DEFAULT_READS_TO_CHECK, max_read_size=DEFAULT_MAX_READ_SIZE, ctx=None, threads=1):
     """GpuCanLoadBam.loadBam = loadReadsAndPositions(...).values: the partitions' records."""
-    return load_reads_and_positions(path, split_size, bgzf_blocks_to_check, reads_to_check, max_read_size, ctx)
+    return load_reads_and_positions(path, split_size, bgzf_blocks_to_check, reads_to_check, max_read_size, ctx,
+                                    threads)
 
 
 def load_splits_and_reads(path, split_size=DEFAULT_MAX_SPLIT_SIZE, bgzf_blocks_to_check=DEFAULT_BGZF_BLOCKS_TO_CHECK,
-                          reads_to_check=DEFAULT_READS_TO_CHECK, max_read_size=DEFAULT_MAX_READ_SIZE, ctx=None):
+                          reads_to_check=DEFAULT_READS_TO_CHECK, max_read_size=DEFAULT_MAX_READ_SIZE, ctx=None,
+                          threads=1):
     """GpuCanLoadBam.loadSplitsAndReads (CanLoadBam.scala:268-302): BAMRecordRDD(splits, reads),
     splits = the first record of every non-empty partition, sliding2 with Pos(fileSize, 0)."""
-    parts = load_reads_and_positions(path, split_size, bgzf_blocks_to_check, reads_to_check, max_read_size, ctx)
+    parts = load_reads_and_positions(path, split_size, bgzf_blocks_to_check, reads_to_check, max_read_size, ctx,
+                                     threads)
     size = _reader(path)[0].size
     firsts = [Pos.from_htsjdk(int(p.cols["vpos"][0])) for p in parts if p.n]
     splits = [Split(a, b) for a, b in zip(firsts, firsts[1:] + [Pos(size, 0)])]

@@ -2748,7 +2748,14 @@ static_assert(!(SBH_LZ_CARRY && SBH_LZ_PREFETCH), "the token prefetch assumes ch
     {
       bool far = false;
 #pragma unroll
-      for (uint32_t k = 0; k < LZ_TPT; ++k) far = far || (match[k] && dist[k] > off[k]);
+      for (uint32_t k = 0; k < LZ_TPT; ++k) {
+        const bool fk = match[k] && dist[k] > off[k];
+        far = far || fk;
+        // the block's bytes no longer matter, but its pointers must stay well formed: the bad
+        // match copies from itself (distance 0: every byte's pointer is its own slot, a final
+        // pointer), never from before the block (a wrapped u16 the chase would follow)
+        dist[k] = fk ? 0u : dist[k];
+      }
       if (far && bl.status[b] == INF_OK) bl.status[b] = INF_DATA;
     }
 #endif
@@ -2870,7 +2877,7 @@ static_assert(!(SBH_LZ_CARRY && SBH_LZ_PREFETCH), "the token prefetch assumes ch
             asm volatile("" : "+v"(D));
 #endif
             const uint32_t d0 = off[k] - abase, L = len[k];
-            const bool ov = D < L;
+            const bool ov = D != 0 && D < L;  // (D = 0: a too-far-back match, marked at itself)
             uint32_t r = 0;  // 32 m mod D (ov)
             const uint32_t r32 = ov ? (D > 32 ? 32 : mod_small(32, D)) : 0;
             for (uint32_t m = 0; m < L; m += 32) {
@@ -2888,8 +2895,9 @@ static_assert(!(SBH_LZ_CARRY && SBH_LZ_PREFETCH), "the token prefetch assumes ch
           lm &= lm - 1;
           const uint32_t o = __builtin_amdgcn_readlane(off[k], l), d = __builtin_amdgcn_readlane(dist[k], l);
           const uint32_t L = __builtin_amdgcn_readlane(len[k], l);
-          uint32_t s = lane < d ? lane : mod_small(lane, d);
-          const uint32_t step = WAVE < d ? WAVE : mod_small(WAVE, d);
+          // (d = 0: a too-far-back match, every byte pointing at itself)
+          uint32_t s = lane < d || d == 0 ? lane : mod_small(lane, d);
+          const uint32_t step = WAVE < d || d == 0 ? WAVE : mod_small(WAVE, d);
           for (uint32_t j = lane; j < L; j += WAVE) {
             p16[o - abase + j] = (uint16_t)(o - d + s);
             s += step;
@@ -2991,10 +2999,11 @@ static_assert(!(SBH_LZ_CARRY && SBH_LZ_PREFETCH), "the token prefetch assumes ch
           // a match at distance 1 (a run of one byte value): every byte copies its source byte,
           // no mod needed
           const bool one = dd == 1;
-          ovl |= (in && j != 0 && j >= dd && !one) ? 1u << k : 0u;
+          // (dd = 0: a literal pair's second byte or a too-far-back match -- its own slot, final)
+          ovl |= (in && j != 0 && dd != 0 && j >= dd && !one) ? 1u << k : 0u;
           c[hh][k] = in ? v[k] + (one ? 0u : j) : g0 + k;
 #else
-          ovl |= (in && j != 0 && j >= dd) ? 1u << k : 0u;
+          ovl |= (in && j != 0 && dd != 0 && j >= dd) ? 1u << k : 0u;
           c[hh][k] = in ? v[k] + j : g0 + k;
 #endif
         }

@@ -9,6 +9,7 @@
 #include <cstring>
 #include <functional>
 #include <initializer_list>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -90,17 +91,34 @@ using namespace sbh;
 struct StreamCache;  // sbh_run_stream's window shard, buffers and copy stream (kept between calls)
 static void stream_cache_free(StreamCache *sc);
 
+// Threading (include/sparkbam.h): one context serves every thread of its process on its device
+// -- a Spark executor's concurrent tasks share it (jni/Native.scala Device).  What a context holds
+// is therefore either immutable after creation (device, the context stream used by context-level
+// calls) or guarded by `mu` (the pool of streaming-window caches).  Each shard has its own HIP
+// stream (sbh_shard_create), so two tasks' shards run concurrently on the device and a task's
+// hipStreamSynchronize waits for its own work only; a shard itself belongs to one thread at a time.
+// The last error (message, status, the reference exception's fields) is kept per thread and per
+// context (t_err below), so one task's failure never overwrites what another task reads back.
 struct sbh_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   bool own_stream = false;
-  std::string err;
-  // the last error's structured fields (sbh_last_error_detail): what the reference's exception
-  // is constructed from (e.g. HeaderParseException(idx, actual, expected))
-  int32_t err_code = 0, err_n = 0;
-  int64_t err_fields[4] = {0, 0, 0, 0};
-  StreamCache *sc = nullptr;
+  std::mutex mu;                       // guards sc_free
+  std::vector<StreamCache *> sc_free;  // idle sbh_run_stream2 window caches (one per concurrent caller)
 };
+
+namespace {
+// the calling thread's last failed call: which context it was on, the message, the status and the
+// fields the reference's exception is constructed from (e.g. HeaderParseException(idx, actual,
+// expected)); sbh_last_error / sbh_last_error_detail read it back on the same thread
+struct ErrRec {
+  const sbh_ctx *ctx = nullptr;
+  std::string msg;
+  int32_t code = 0, n = 0;
+  int64_t fields[4] = {0, 0, 0, 0};
+};
+thread_local ErrRec t_err;
+}  // namespace
 
 namespace {
 
@@ -128,6 +146,10 @@ struct DBuf {  // grow-only device buffer
 
 struct sbh_shard {
   sbh_ctx *ctx = nullptr;
+  // the shard's own stream (every device call on the shard is enqueued here), or the caller's
+  // stream when the context was given one (sbh_ctx_set_stream)
+  hipStream_t st = nullptr;
+  bool own_st = false;
   uint64_t file_off = 0, n = 0, file_size = 0;
   bool at_eof = false;
   DBuf<uint8_t> comp;
@@ -171,6 +193,7 @@ struct sbh_shard {
   uint64_t chain_first = 0, chain_E = 0;
   bool bits_valid = false;
   uint64_t bits_begin = 0, bits_end = 0;
+  uint64_t run_first = ~0ull;  // sbh_run_shard's first record (flat), ~0: none found
   int32_t bits_rtc = 0;
   DBuf<uint32_t> words;
   DBuf<uint32_t> opix;  // the full checker's bad-CIGAR-op index (launch_full)
@@ -196,6 +219,7 @@ struct sbh_shard {
     DBuf<uint32_t> cigar;
     sbh_records_sizes sz{};
     bool valid = false;
+    bool decoded = false;  // the columns were decoded (else only the starts, sbh_split_records decode = 0)
     void release() {
       for (auto *b : {&pos, &wcnt, &wpre, &nm, &cg, &sq, &ax, &nmo, &cgo, &sqo, &axo, &keep, &kpre, &pos2}) b->release();
       iv_b.release(); iv_e.release(); iv_ref.release();
@@ -261,11 +285,13 @@ static int vfail(sbh_ctx *ctx, int code, std::initializer_list<int64_t> fields, 
   if (ctx) {
     char buf[512];
     vsnprintf(buf, sizeof buf, fmt, ap);
-    ctx->err = buf;
-    ctx->err_code = code;
-    ctx->err_n = 0;
+    ErrRec &E = t_err;
+    E.ctx = ctx;
+    E.msg = buf;
+    E.code = code;
+    E.n = 0;
     for (int64_t f : fields)
-      if (ctx->err_n < 4) ctx->err_fields[ctx->err_n++] = f;
+      if (E.n < 4) E.fields[E.n++] = f;
   }
   return code;
 }
@@ -300,7 +326,7 @@ static void mark(sbh_shard *sh, int i) {
     for (hipEvent_t &e : sh->ev)
       if (hipEventCreate(&e) != hipSuccess) sh->ev_ok = false;
   }
-  if (sh->ev_ok) (void)hipEventRecord(sh->ev[i], sh->ctx->stream);
+  if (sh->ev_ok) (void)hipEventRecord(sh->ev[i], sh->st);
 }
 
 static int set_device(sbh_ctx *ctx) {
@@ -352,10 +378,10 @@ int sbh_ctx_create(int device, sbh_ctx **out) {
 
 int sbh_ctx_destroy(sbh_ctx *ctx) {
   if (!ctx) return SBH_OK;
-  if (ctx->sc) {
+  if (!ctx->sc_free.empty()) {
     (void)hipSetDevice(ctx->device);
-    stream_cache_free(ctx->sc);
-    ctx->sc = nullptr;
+    for (StreamCache *sc : ctx->sc_free) stream_cache_free(sc);
+    ctx->sc_free.clear();
   }
   if (ctx->own_stream && ctx->stream) {
     (void)hipSetDevice(ctx->device);
@@ -365,14 +391,20 @@ int sbh_ctx_destroy(sbh_ctx *ctx) {
   return SBH_OK;
 }
 
-const char *sbh_last_error(const sbh_ctx *ctx) { return ctx ? ctx->err.c_str() : "no context"; }
+const char *sbh_last_error(const sbh_ctx *ctx) {
+  if (!ctx) return "no context";
+  return t_err.ctx == ctx ? t_err.msg.c_str() : "";
+}
 
 int32_t sbh_last_error_detail(const sbh_ctx *ctx, int32_t *code, int64_t *fields, int32_t cap) {
   if (!ctx) return 0;
-  if (code) *code = ctx->err_code;
-  const int32_t n = fields ? std::min(ctx->err_n, std::max(cap, 0)) : 0;
-  for (int32_t i = 0; i < n; ++i) fields[i] = ctx->err_fields[i];
-  return ctx->err_n;
+  const ErrRec &E = t_err;
+  const bool mine = E.ctx == ctx;
+  if (code) *code = mine ? E.code : 0;
+  if (!mine) return 0;
+  const int32_t n = fields ? std::min(E.n, std::max(cap, 0)) : 0;
+  for (int32_t i = 0; i < n; ++i) fields[i] = E.fields[i];
+  return E.n;
 }
 
 int sbh_host_alloc(uint64_t n, void **out) {
@@ -393,7 +425,11 @@ int sbh_ctx_set_stream(sbh_ctx *ctx, void *hip_stream) {
 
 int sbh_ctx_synchronize(sbh_ctx *ctx) {
   if (!ctx) return SBH_E_ARG;
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  // the context's work is on its own stream and on its shards' streams: wait for the device
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  HIPCHK(ctx, hipDeviceSynchronize());
   return SBH_OK;
 }
 
@@ -415,6 +451,15 @@ int sbh_shard_create(sbh_ctx *ctx, const void *src, uint64_t n, uint64_t file_of
   if (rc) return rc;
   sbh_shard *sh = new sbh_shard();
   sh->ctx = ctx;
+  if (ctx->own_stream) {
+    if (hipStreamCreateWithFlags(&sh->st, hipStreamNonBlocking) != hipSuccess) {
+      delete sh;
+      return fail(ctx, SBH_E_HIP, "shard create: no stream");
+    }
+    sh->own_st = true;
+  } else {
+    sh->st = sh->st;
+  }
   sh->file_off = file_offset;
   sh->n = n;
   sh->file_size = file_size;
@@ -422,13 +467,13 @@ int sbh_shard_create(sbh_ctx *ctx, const void *src, uint64_t n, uint64_t file_of
   hipError_t e = sh->comp.ensure(n + sh->pad);
   if (e == hipSuccess && n)
     e = hipMemcpyAsync(sh->comp.p, src, n, comp_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
-                       ctx->stream);
-  if (e == hipSuccess) e = hipMemsetAsync(sh->comp.p + n, 0, sh->pad, ctx->stream);
+                       sh->st);
+  if (e == hipSuccess) e = hipMemsetAsync(sh->comp.p + n, 0, sh->pad, sh->st);
   if (e == hipSuccess) e = sh->ctr.ensure(CTR_WORDS);
   // (layout: sbh_internal.h; k_eager's true-count slots must start zero, k_fold_true keeps them so)
-  if (e == hipSuccess) e = hipMemsetAsync(sh->ctr.p, 0, CTR_WORDS * sizeof(unsigned long long), ctx->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(sh->ctr.p, 0, CTR_WORDS * sizeof(unsigned long long), sh->st);
   if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&sh->h_ctr), CTR_WORDS * sizeof(unsigned long long));
-  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(sh->st);
   if (e != hipSuccess) {
     sbh_shard_destroy(sh);
     return fail(ctx, SBH_E_HIP, "shard create: %s", hipGetErrorString(e));
@@ -441,7 +486,7 @@ int sbh_shard_destroy(sbh_shard *sh) {
   if (!sh) return SBH_OK;
   if (sh->pf_active) (void)shard_prefetch_finish(sh, false);
   (void)hipSetDevice(sh->ctx->device);
-  (void)hipStreamSynchronize(sh->ctx->stream);
+  (void)hipStreamSynchronize(sh->st);
   sh->comp.release();
   sh->b_cstart.release(); sh->b_ustart.release(); sh->usz.release(); sh->blkpack.release();
   sh->b_csize.release(); sh->b_hsize.release(); sh->b_usize.release(); sh->b_flags.release();
@@ -474,6 +519,7 @@ int sbh_shard_destroy(sbh_shard *sh) {
   sh->cm_pos.release(); sh->cm_wcnt.release(); sh->cm_wpre.release(); sh->cm_mark.release(); sh->cm_mpre.release();
   sh->cm_j.release(); sh->cm_j2.release(); sh->cm_j0.release();
   if (sh->h_ctr) (void)hipHostFree(sh->h_ctr);
+  if (sh->own_st && sh->st) (void)hipStreamDestroy(sh->st);
   delete sh;
   return SBH_OK;
 }
@@ -483,13 +529,13 @@ int sbh_shard_load(sbh_shard *sh, const void *src, uint64_t n, uint64_t file_off
   sbh_ctx *ctx = sh->ctx;
   int rc = set_device(ctx);
   if (rc) return rc;
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));  // (no kernel may still read the old bytes)
+  HIPCHK(ctx, hipStreamSynchronize(sh->st));  // (no kernel may still read the old bytes)
   HIPCHK(ctx, sh->comp.ensure(n + sh->pad));
   if (n)
     HIPCHK(ctx, hipMemcpyAsync(sh->comp.p, src, n, comp_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
-                               ctx->stream));
-  HIPCHK(ctx, hipMemsetAsync(sh->comp.p + n, 0, sh->pad, ctx->stream));
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+                               sh->st));
+  HIPCHK(ctx, hipMemsetAsync(sh->comp.p + n, 0, sh->pad, sh->st));
+  HIPCHK(ctx, hipStreamSynchronize(sh->st));
   sh->file_off = file_offset;
   sh->n = n;
   sh->at_eof = file_offset + n == sh->file_size;
@@ -624,7 +670,7 @@ int shard_prefetch_finish(sbh_shard *sh, bool use, double *copy_ms) {
   if (!use) return SBH_OK;
   int rc = set_device(ctx);
   if (rc) return rc;
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));  // (no kernel may still read the old bytes)
+  HIPCHK(ctx, hipStreamSynchronize(sh->st));  // (no kernel may still read the old bytes)
   std::swap(sh->comp, sh->comp2);
   std::swap(sh->sp_vpos, sh->aux2);
   sh->file_off = sh->pf_off;
@@ -653,10 +699,10 @@ int sbh_find_block_start(sbh_shard *sh, uint64_t start, int32_t k, uint64_t *out
   if (rc) return rc;
   const uint64_t rel = start - sh->file_off;
   unsigned long long *best = sh->ctr.p;
-  HIPCHK(ctx, hipMemsetAsync(best, 0xff, 8, ctx->stream));
-  HIPCHK(ctx, launch_find_block_start(sh->comp.p, sh->n, rel, k, sh->at_eof ? 1 : 0, best, ctx->stream));
-  HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr, best, 8, hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  HIPCHK(ctx, hipMemsetAsync(best, 0xff, 8, sh->st));
+  HIPCHK(ctx, launch_find_block_start(sh->comp.p, sh->n, rel, k, sh->at_eof ? 1 : 0, best, sh->st));
+  HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr, best, 8, hipMemcpyDeviceToHost, sh->st));
+  HIPCHK(ctx, hipStreamSynchronize(sh->st));
   const unsigned long long b = sh->h_ctr[0];
   // HeaderSearchFailedException(path, start, positionsAttempted): the search tried every
   // pos < MAX_BLOCK_SIZE (FindBlockStart.scala:18-35)
@@ -682,7 +728,7 @@ static bool chain_jump_only() {
 int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_size) {
   if (!sh || start < sh->file_off || start > sh->file_off + sh->n) return SBH_E_ARG;
   sbh_ctx *ctx = sh->ctx;
-  hipStream_t st = ctx->stream;
+  hipStream_t st = sh->st;
   int rc = set_device(ctx);
   if (rc) return rc;
   sh->indexed = sh->inflated = sh->bits_valid = sh->chain_ok = sh->cm_valid = false;
@@ -910,7 +956,7 @@ int sbh_inflate(sbh_shard *sh, uint64_t *bad_block) {
   if (!sh->indexed) return fail(ctx, SBH_E_STATE, "inflate before index");
   int rc = set_device(ctx);
   if (rc) return rc;
-  hipStream_t st = ctx->stream;
+  hipStream_t st = sh->st;
   HIPCHK(ctx, sh->U.ensure(sh->utotal + sh->pad));
   const TokPlan P = tok_plan(sh, ~0ull);
   HIPCHK(ctx, sh->tok.ensure(P.tok_len));
@@ -938,7 +984,7 @@ int sbh_verify_crc(sbh_shard *sh, uint64_t *n_bad, uint64_t *first_bad) {
   if (!sh->inflated) return fail(ctx, SBH_E_STATE, "verify_crc before inflate");
   int rc = set_device(ctx);
   if (rc) return rc;
-  hipStream_t st = ctx->stream;
+  hipStream_t st = sh->st;
   unsigned long long *c = sh->ctr.p + 32;
   HIPCHK(ctx, hipMemsetAsync(c, 0, 8, st));
   HIPCHK(ctx, hipMemsetAsync(c + 1, 0xff, 8, st));
@@ -956,8 +1002,8 @@ int sbh_read_flat(sbh_shard *sh, uint64_t flat, uint64_t n, uint8_t *out) {
   if (flat + n > sh->utotal) return SBH_E_ARG;
   int rc = set_device(sh->ctx);
   if (rc) return rc;
-  HIPCHK(sh->ctx, hipMemcpyAsync(out, sh->U.p + flat, n, hipMemcpyDeviceToHost, sh->ctx->stream));
-  HIPCHK(sh->ctx, hipStreamSynchronize(sh->ctx->stream));
+  HIPCHK(sh->ctx, hipMemcpyAsync(out, sh->U.p + flat, n, hipMemcpyDeviceToHost, sh->st));
+  HIPCHK(sh->ctx, hipStreamSynchronize(sh->st));
   return SBH_OK;
 }
 
@@ -1019,8 +1065,8 @@ int sbh_set_contigs(sbh_shard *sh, const int32_t *lens, int32_t n) {
   int rc = set_device(sh->ctx);
   if (rc) return rc;
   HIPCHK(sh->ctx, sh->ctg.ensure(n + 1));
-  if (n) HIPCHK(sh->ctx, hipMemcpyAsync(sh->ctg.p, lens, (uint64_t)n * 4, hipMemcpyHostToDevice, sh->ctx->stream));
-  HIPCHK(sh->ctx, hipStreamSynchronize(sh->ctx->stream));
+  if (n) HIPCHK(sh->ctx, hipMemcpyAsync(sh->ctg.p, lens, (uint64_t)n * 4, hipMemcpyHostToDevice, sh->st));
+  HIPCHK(sh->ctx, hipStreamSynchronize(sh->st));
   sh->nctg = n;
   sh->bits_valid = sh->chain_ok = sh->cm_valid = false;
   return SBH_OK;
@@ -1052,7 +1098,7 @@ static bool tsum_on() {
 
 static int eager_range(sbh_shard *sh, uint64_t begin, uint64_t end, int32_t rtc, uint64_t *n_true) {
   sbh_ctx *ctx = sh->ctx;
-  hipStream_t st = ctx->stream;
+  hipStream_t st = sh->st;
   const uint64_t nwords = (end - begin + 31) / 32;
   sh->chain_ok = sh->cm_valid = false;
   HIPCHK(ctx, sh->bits.ensure(nwords + 1));
@@ -1092,8 +1138,8 @@ int sbh_check_eager(sbh_shard *sh, uint64_t begin, uint64_t end, int32_t rtc, ui
   rc = eager_range(sh, begin, end, rtc, n_true);
   if (rc) return rc;
   if (out_bits && end > begin) {
-    HIPCHK(sh->ctx, hipMemcpyAsync(out_bits, sh->bits.p, (end - begin + 7) / 8, hipMemcpyDeviceToHost, sh->ctx->stream));
-    HIPCHK(sh->ctx, hipStreamSynchronize(sh->ctx->stream));
+    HIPCHK(sh->ctx, hipMemcpyAsync(out_bits, sh->bits.p, (end - begin + 7) / 8, hipMemcpyDeviceToHost, sh->st));
+    HIPCHK(sh->ctx, hipStreamSynchronize(sh->st));
   }
   return SBH_OK;
 }
@@ -1109,8 +1155,8 @@ int sbh_eager_bits(sbh_shard *sh, uint64_t begin, uint64_t end, uint8_t *out_bit
   int rc = set_device(sh->ctx);
   if (rc) return rc;
   const uint8_t *src = reinterpret_cast<const uint8_t *>(sh->bits.p) + (begin - sh->bits_begin) / 8;
-  HIPCHK(sh->ctx, hipMemcpyAsync(out_bits, src, (end - begin + 7) / 8, hipMemcpyDeviceToHost, sh->ctx->stream));
-  HIPCHK(sh->ctx, hipStreamSynchronize(sh->ctx->stream));
+  HIPCHK(sh->ctx, hipMemcpyAsync(out_bits, src, (end - begin + 7) / 8, hipMemcpyDeviceToHost, sh->st));
+  HIPCHK(sh->ctx, hipStreamSynchronize(sh->st));
   return SBH_OK;
 }
 
@@ -1123,7 +1169,7 @@ int sbh_check_full(sbh_shard *sh, uint64_t begin, uint64_t end, int32_t rtc, uin
   rc = set_device(sh->ctx);
   if (rc) return rc;
   sbh_ctx *ctx = sh->ctx;
-  hipStream_t st = ctx->stream;
+  hipStream_t st = sh->st;
   const uint64_t nctr = 4 + 21 * 19 + 21 * 64;
   unsigned long long *c = sh->ctr.p;
   HIPCHK(ctx, hipMemsetAsync(c, 0, nctr * 8, st));
@@ -1196,7 +1242,7 @@ int sbh_find_record_start(sbh_shard *sh, uint64_t from, int32_t rtc, int32_t max
   if (rc) return rc;
   rc = set_device(ctx);
   if (rc) return rc;
-  hipStream_t st = ctx->stream;
+  hipStream_t st = sh->st;
   const uint64_t seg = seg_end_of(sh, from);
   const uint64_t limit = std::min<uint64_t>(seg, from + (uint64_t)std::max(max_read_size, 0));
   uint64_t lo = from;
@@ -1257,7 +1303,7 @@ int sbh_find_record_start(sbh_shard *sh, uint64_t from, int32_t rtc, int32_t max
 static int count_records_impl(sbh_shard *sh, uint64_t first, uint64_t E, uint64_t *count, int32_t *anomalies,
                               uint64_t *exit_flat = nullptr, bool known = false) {
   sbh_ctx *ctx = sh->ctx;
-  hipStream_t st = ctx->stream;
+  hipStream_t st = sh->st;
   const uint64_t total = seg_end_of(sh, first);
   E = std::min(E, total);
   if (anomalies) *anomalies = 0;
@@ -1420,7 +1466,7 @@ int sbh_split_starts(sbh_shard *sh, const uint64_t *starts, const uint64_t *ends
   if (rc) return rc;
   if (n_host) *n_host = 0;
   if (!n) return SBH_OK;
-  hipStream_t st = ctx->stream;
+  hipStream_t st = sh->st;
   const uint64_t end_res = sh->file_off + sh->n;
   // the eager bitmap from the stream start (reused when one is resident, e.g. sbh_run_shard's
   // over the owned range; a record start past its end takes the host path)
@@ -1575,7 +1621,7 @@ static int check_records_impl(sbh_shard *sh, const uint64_t *range_begin, const 
   if (rc) return rc;
   rc = set_device(ctx);
   if (rc) return rc;
-  hipStream_t st = ctx->stream;
+  hipStream_t st = sh->st;
   // the eager bitmap over the hull, aligned so its words line up with the truth words
   const uint64_t hb0 = begin & ~31ull;
   if (!(sh->bits_valid && sh->bits_rtc == rtc && sh->bits_begin <= hb0 && end <= sh->bits_end &&
@@ -1614,7 +1660,8 @@ static int check_records_impl(sbh_shard *sh, const uint64_t *range_begin, const 
   auto fetch = [&](uint64_t *dst, const uint64_t *src, uint64_t cap, uint64_t total) -> int {
     const uint64_t k = std::min(cap, total);
     if (!dst || !k) return SBH_OK;
-    HIPCHK(ctx, hipMemcpy(dst, src, 8 * k, hipMemcpyDeviceToHost));
+    HIPCHK(ctx, hipMemcpyAsync(dst, src, 8 * k, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
     std::sort(dst, dst + k);
     return SBH_OK;
   };
@@ -1661,7 +1708,7 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
   if (!sh->indexed) return fail(ctx, SBH_E_STATE, "inflate before index");
   if (sh->nctg < 0) return fail(ctx, SBH_E_STATE, "contig lengths not set");
   if (rtc < 0 || rtc > 1023) return fail(ctx, SBH_E_ARG, "readsToCheck must be in [0, 1023]");
-  hipStream_t sa = ctx->stream;
+  hipStream_t sa = sh->st;
   if (!sh->s_lz) HIPCHK(ctx, hipStreamCreateWithFlags(&sh->s_lz, hipStreamNonBlocking));
   if (!sh->s_eg) HIPCHK(ctx, hipStreamCreateWithFlags(&sh->s_eg, hipStreamNonBlocking));
   hipStream_t sl = sh->s_lz, se = sh->s_eg;
@@ -1837,8 +1884,10 @@ int sbh_run_shard(sbh_shard *sh, uint64_t index_start, uint64_t own_end_file, in
          !sh->pipe_fallback;
   uint64_t first = 0;
   int32_t delta = 0;
+  sh->run_first = ~0ull;
   if (tail && sh->h_ctr[8] != ~0ull) {
     first = sh->h_ctr[8];
+    sh->run_first = first;
     rc = SBH_OK;
     if (first < E0 && sh->h_ctr[16] == 0 && sh->h_ctr[19] != ~0ull) {  // count_records_impl's proof, done
       sh->cm_valid = false;
@@ -1862,6 +1911,7 @@ int sbh_run_shard(sbh_shard *sh, uint64_t index_start, uint64_t own_end_file, in
       res->count = 0;
       rc = SBH_OK;
     } else if (rc == SBH_OK) {
+      sh->run_first = first;
       rc = count_records_impl(sh, first, E, &res->count, &res->anomalies, &res->exit_flat);
       uint64_t bp = 0;
       uint32_t off = 0;
@@ -1927,7 +1977,7 @@ int sbh_run_stream(sbh_ctx *ctx, const void *host, uint64_t n, uint64_t file_off
 // CRC32 of the first nb blocks of the table (a window's owned blocks) against their footers.
 static int verify_crc_prefix(sbh_shard *sh, uint64_t nb, uint64_t *n_bad, uint64_t *first_bad, float *ms) {
   sbh_ctx *ctx = sh->ctx;
-  hipStream_t st = ctx->stream;
+  hipStream_t st = sh->st;
   unsigned long long *c = sh->ctr.p + 32;
   HIPCHK(ctx, hipMemsetAsync(c, 0, 8, st));
   HIPCHK(ctx, hipMemsetAsync(c + 1, 0xff, 8, st));
@@ -1977,24 +2027,43 @@ int sbh_run_stream2(sbh_ctx *ctx, const void *host, uint64_t n, uint64_t file_of
   hipPointerAttribute_t pa{};
   res->host_pinned = hipPointerGetAttributes(&pa, host) == hipSuccess && pa.type == hipMemoryTypeHost ? 1 : 0;
   (void)hipGetLastError();
-  // the window shard, the two window buffers and the copy stream persist in the context
-  // (grow-only), so repeated calls allocate nothing
-  if (!ctx->sc) {
-    ctx->sc = new StreamCache();
-    rc = sbh_shard_create(ctx, nullptr, 0, file_offset, file_size, 0, &ctx->sc->sh);
-    if (rc) {
-      delete ctx->sc;
-      ctx->sc = nullptr;
-      return res->status = rc;
-    }
-    ctx->sc->sh->comp.release();
-    HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->sc->cs, hipStreamNonBlocking));
-    for (int i = 0; i < 2; ++i) {
-      HIPCHK(ctx, hipEventCreate(&ctx->sc->done[i]));
-      HIPCHK(ctx, hipEventCreate(&ctx->sc->c0[i]));
+  // the window shard, the two window buffers and the copy stream persist in the context (grow-only),
+  // so repeated calls allocate nothing; concurrent callers each take their own cache from the pool
+  StreamCache *scp = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (!ctx->sc_free.empty()) {
+      scp = ctx->sc_free.back();
+      ctx->sc_free.pop_back();
     }
   }
-  StreamCache &R = *ctx->sc;
+  if (!scp) {
+    scp = new StreamCache();
+    rc = sbh_shard_create(ctx, nullptr, 0, file_offset, file_size, 0, &scp->sh);
+    if (rc) {
+      delete scp;
+      return res->status = rc;
+    }
+    scp->sh->comp.release();
+    hipError_t e = hipStreamCreateWithFlags(&scp->cs, hipStreamNonBlocking);
+    for (int i = 0; i < 2 && e == hipSuccess; ++i) {
+      e = hipEventCreate(&scp->done[i]);
+      if (e == hipSuccess) e = hipEventCreate(&scp->c0[i]);
+    }
+    if (e != hipSuccess) {
+      stream_cache_free(scp);
+      return res->status = fail(ctx, SBH_E_HIP, "run_stream2: %s", hipGetErrorString(e));
+    }
+  }
+  struct Return {  // the cache goes back to the pool on every return path
+    sbh_ctx *ctx;
+    StreamCache *sc;
+    ~Return() {
+      std::lock_guard<std::mutex> lk(ctx->mu);
+      ctx->sc_free.push_back(sc);
+    }
+  } give_back{ctx, scp};
+  StreamCache &R = *scp;
   struct Detach {  // the window buffers are never the shard's own: detach on every return path
     StreamCache &R;
     ~Detach() {
@@ -2040,7 +2109,7 @@ int sbh_run_stream2(sbh_ctx *ctx, const void *host, uint64_t n, uint64_t file_of
   };
   auto fit_buf = [&](int b, uint64_t need) -> hipError_t {  // grow buffer b (not in use) to `need` bytes
     hipError_t e = hipStreamSynchronize(R.cs);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(sh->st);
     if (e == hipSuccess) e = R.buf[b].ensure(need);
     return e;
   };
@@ -2077,7 +2146,7 @@ int sbh_run_stream2(sbh_ctx *ctx, const void *host, uint64_t n, uint64_t file_of
     const uint64_t lo2 = hi, hi2 = more ? win_end(lo2) : 0;
     if (prefetch && more) HIPCHK(ctx, enqueue(1 - cur, lo2, load_end(hi2)));
     const uint64_t ld = load_end(hi);
-    HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, R.done[cur], 0));
+    HIPCHK(ctx, hipStreamWaitEvent(sh->st, R.done[cur], 0));
     sh->comp.p = R.buf[cur].p;
     sh->comp.cap = R.buf[cur].cap;
     sh->file_off = lo;
@@ -2156,7 +2225,7 @@ int sbh_run_stream2(sbh_ctx *ctx, const void *host, uint64_t n, uint64_t file_of
     }
     if (rc == SBH_E_NEED_HALO && ld < data_end) {  // grow the halo and redo this window
       HIPCHK(ctx, hipStreamSynchronize(R.cs));
-      HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+      HIPCHK(ctx, hipStreamSynchronize(sh->st));
       account(0);
       account(1);
       halo *= 4;
@@ -2226,7 +2295,8 @@ int sbh_run_stream2(sbh_ctx *ctx, const void *host, uint64_t n, uint64_t file_of
       const uint64_t nb = (flat_base + r.flat_bytes + 7) / 8;
       if (nb > out_bits_cap) return res->status = fail(ctx, SBH_E_ARG, "out_bits_cap too small");
       wbits.assign((r.flat_bytes + 31) / 32 + 1, 0);
-      HIPCHK(ctx, hipMemcpy(wbits.data(), sh->bits.p, (r.flat_bytes + 7) / 8, hipMemcpyDeviceToHost));
+      HIPCHK(ctx, hipMemcpyAsync(wbits.data(), sh->bits.p, (r.flat_bytes + 7) / 8, hipMemcpyDeviceToHost, sh->st));
+      HIPCHK(ctx, hipStreamSynchronize(sh->st));
       for (uint64_t i = 0; i < r.flat_bytes; ++i)
         if ((wbits[i >> 5] >> (i & 31)) & 1u) out_bits[(flat_base + i) >> 3] |= (uint8_t)(1u << ((flat_base + i) & 7));
     }
@@ -2286,11 +2356,75 @@ int sbh_records_scan(sbh_shard *sh, uint64_t first, uint64_t end_flat, sbh_recor
   return records_finish(sh, n, total, out);
 }
 
+// One FileSplit of loadReadsAndPositions (load/.../CanLoadBam.scala:316-356) in one call:
+// FindBlockStart(start) (FindBlockStart.scala:8-36), then sbh_run_shard's step from that block --
+// MetadataStream + inflate + the eager check at every position of [Pos(blockStart, 0), Pos(end, 0))
+// + FindRecordStart from Pos(blockStart, 0) (FindRecordStart.scala:11-30) + the chain proof of the
+// records while pos < Pos(end, 0) (RecordStream.takeWhile, :338-355) -- then the record starts (and
+// with decode, BAMRecordCodec.decode's columns) for sbh_records_fetch.  The per-split facade
+// (jni/Native.scala GpuSplitPartition) made seven calls with a host round trip each.
+int sbh_split_records(sbh_shard *sh, uint64_t start, uint64_t end, int32_t k, int32_t rtc, int32_t mrs, int32_t decode,
+                      sbh_split_records_result *out) {
+  if (!sh || !out || end <= start) return SBH_E_ARG;
+  sbh_ctx *ctx = sh->ctx;
+  std::memset(out, 0, sizeof *out);
+  int rc = set_device(ctx);
+  if (rc) return rc;
+  auto &R = sh->rec;
+  R.valid = R.decoded = false;
+  uint64_t b = 0;
+  rc = sbh_find_block_start(sh, start, k, &b);
+  if (rc) return rc;
+  out->block_start = b;
+  sbh_shard_result r{};
+  rc = sbh_run_shard(sh, b, end, rtc, mrs, &r);
+  if (rc) return rc;
+  out->n_blocks = sh->nblocks;
+  out->flat_size = sh->utotal;
+  out->owned_flat = r.flat_bytes;
+  out->n_true = r.n_true;
+  uint64_t first = sh->run_first;
+  if (r.count == 0) {
+    // no record of the chain below Pos(end, 0): FindRecordStart's own answer decides between an
+    // empty split and NoReadFoundException(path, blockStart, maxReadSize)
+    int32_t delta = 0;
+    rc = sbh_find_record_start(sh, 0, rtc, mrs, &first, &delta);
+    if (rc == SBH_E_NO_READ_FOUND)
+      return fail_with(ctx, SBH_E_NO_READ_FOUND, {(int64_t)b, mrs},
+                       "Failed to find a valid read-start in %d attempts from %llu", mrs, (unsigned long long)b);
+    if (rc) return rc;
+    out->first_flat = first;
+    R.sz = sbh_records_sizes{0, 0, 0, 0, 0};
+    R.valid = true;
+    R.decoded = decode != 0;
+    return SBH_OK;
+  }
+  out->first_flat = first;
+  out->first_vpos = r.first_vpos;
+  const uint64_t total = seg_end_of(sh, first);
+  const uint64_t E = std::min(std::min(r.flat_bytes, sh->utotal), total);
+  HIPCHK(ctx, R.pos.ensure(r.count));
+  rc = records_positions(sh, first, E, total, r.count, r.anomalies, R.pos.p);
+  if (rc) return rc;
+  if (!decode) {
+    HIPCHK(ctx, hipStreamSynchronize(sh->st));
+    R.sz = sbh_records_sizes{r.count, 0, 0, 0, 0};
+    R.valid = true;
+    out->sizes = R.sz;
+    return SBH_OK;
+  }
+  rc = records_finish(sh, r.count, total, &out->sizes);
+  // the split's last record runs past the resident bytes: more halo, not a malformed record
+  if (rc == SBH_E_BAD_RECORD && !sh->at_eof)
+    return fail(ctx, SBH_E_NEED_HALO, "a record of the split runs past the shard");
+  return rc;
+}
+
 // Record starts of the chain from first while the start is < E, written at pos (cap n).
 static int records_positions(sbh_shard *sh, uint64_t first, uint64_t E, uint64_t total, uint64_t n, int32_t anomalies,
                              uint64_t *pos) {
   sbh_ctx *ctx = sh->ctx;
-  hipStream_t st = ctx->stream;
+  hipStream_t st = sh->st;
   auto &R = sh->rec;
   const bool covered = sh->bits_valid && sh->bits_begin <= first && E <= sh->bits_end && anomalies == 0;
   if (n && covered) {
@@ -2311,7 +2445,7 @@ static int records_positions(sbh_shard *sh, uint64_t first, uint64_t E, uint64_t
 // Sizes -> prefix offsets -> columns for the n record starts in R.pos.
 static int records_finish(sbh_shard *sh, uint64_t n, uint64_t total, sbh_records_sizes *out) {
   sbh_ctx *ctx = sh->ctx;
-  hipStream_t st = ctx->stream;
+  hipStream_t st = sh->st;
   auto &R = sh->rec;
   // per-record sizes (a trailing zero makes the exclusive scan's last entry the total)
   DBuf<uint64_t> *sz[4] = {&R.nm, &R.cg, &R.sq, &R.ax}, *of[4] = {&R.nmo, &R.cgo, &R.sqo, &R.axo};
@@ -2342,6 +2476,7 @@ static int records_finish(sbh_shard *sh, uint64_t n, uint64_t total, sbh_records
   HIPCHK(ctx, hipStreamSynchronize(st));
   R.sz = sbh_records_sizes{n, tot[0], tot[1], tot[2], tot[3]};
   R.valid = true;
+  R.decoded = true;
   *out = R.sz;
   return SBH_OK;
 }
@@ -2363,7 +2498,7 @@ int sbh_records_scan_regions(sbh_shard *sh, const uint64_t *chunk_begin, const u
   }
   int rc = set_device(ctx);
   if (rc) return rc;
-  hipStream_t st = ctx->stream;
+  hipStream_t st = sh->st;
   auto &R = sh->rec;
   R.valid = false;
   std::vector<uint64_t> cn(n_chunks, 0), cfirst(n_chunks, 0), cE(n_chunks, 0), ctot(n_chunks, 0);
@@ -2415,11 +2550,16 @@ int sbh_records_fetch(sbh_shard *sh, const sbh_records_out *o) {
   sbh_ctx *ctx = sh->ctx;
   auto &R = sh->rec;
   if (!R.valid) return fail(ctx, SBH_E_STATE, "records_fetch without a records_scan");
+  if (!R.decoded && (o->ref_id || o->pos || o->next_ref_id || o->next_pos || o->tlen || o->flag || o->bin || o->mapq ||
+                     o->name_off || o->cigar_off || o->seq_off || o->aux_off || o->names || o->cigar || o->seq ||
+                     o->qual || o->aux))
+    return fail(ctx, SBH_E_STATE, "records_fetch: only the starts were scanned (sbh_split_records, decode = 0)");
   int rc = set_device(ctx);
   if (rc) return rc;
   const uint64_t n = R.sz.n;
+  // (every column is copied on the shard's stream, then one wait)
   auto cp = [&](void *dst, const void *src, uint64_t bytes) -> hipError_t {
-    return dst && bytes ? hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) : hipSuccess;
+    return dst && bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, sh->st) : hipSuccess;
   };
   HIPCHK(ctx, cp(o->flat, R.pos.p, 8 * n));
   HIPCHK(ctx, cp(o->ref_id, R.ref_id.p, 4 * n));
@@ -2439,6 +2579,7 @@ int sbh_records_fetch(sbh_shard *sh, const sbh_records_out *o) {
   HIPCHK(ctx, cp(o->seq, R.seq.p, R.sz.bases));
   HIPCHK(ctx, cp(o->qual, R.qual.p, R.sz.bases));
   HIPCHK(ctx, cp(o->aux, R.aux.p, R.sz.aux_bytes));
+  HIPCHK(ctx, hipStreamSynchronize(sh->st));
   return SBH_OK;
 }
 
@@ -2461,20 +2602,26 @@ int sbh_bgzf_compress_level(sbh_ctx *ctx, const void *src, uint64_t n, int src_o
   if (out_cap < sbh_bgzf_compress_bound(n)) return fail(ctx, SBH_E_ARG, "bgzf_compress: out_cap < bound");
   int rc = set_device(ctx);
   if (rc) return rc;
-  hipStream_t st = ctx->stream;
-  struct Bufs {  // per-call scratch, freed on every return path
+  struct Bufs {  // per-call scratch (and stream), freed on every return path
     DBuf<uint8_t> in, slots, packed, recs;
     DBuf<uint16_t> prev;
     DBuf<uint32_t> toks, sizes;
     DBuf<uint64_t> offs, info;
     hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipStream_t own = nullptr;
     ~Bufs() {
+      if (own) (void)hipStreamSynchronize(own);
       in.release(), slots.release(), packed.release(), recs.release(), prev.release(), toks.release(), sizes.release(),
           offs.release(), info.release();
       if (e0) (void)hipEventDestroy(e0);
       if (e1) (void)hipEventDestroy(e1);
+      if (own) (void)hipStreamDestroy(own);
     }
   } B;
+  // a stream of the call's own unless the caller gave the context one: concurrent callers of one
+  // context (include/sparkbam.h, threading) neither wait for nor time each other's kernels
+  if (ctx->own_stream) HIPCHK(ctx, hipStreamCreateWithFlags(&B.own, hipStreamNonBlocking));
+  hipStream_t st = B.own ? B.own : ctx->stream;
   const uint8_t *d_src = static_cast<const uint8_t *>(src);
   if (!src_on_device && n) {
     HIPCHK(ctx, B.in.ensure(n));

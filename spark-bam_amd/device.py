@@ -7,7 +7,8 @@ import numpy as np
 from .records import record_columns
 
 from ._lib import (SBH_OK, SbhBlock, SbhCheckOpts, SbhCheckResult, SbhRecordsOut, SbhRecordsSizes,
-                   SbhShardResult, SbhStreamOpts, SbhStreamResult, SparkBamError, error_for, lib)
+                   SbhShardResult, SbhSplitRecordsResult, SbhStreamOpts, SbhStreamResult, SparkBamError, error_for,
+                   lib)
 
 
 def _check(ctx_handle, rc):
@@ -256,12 +257,18 @@ class Shard:
         except Exception:
             pass
 
-    def load(self, comp, file_offset):
-        """Replace the resident bytes with file bytes [file_offset, file_offset + comp.size)
-        of the same file, keeping the device buffers (sbh_shard_load)."""
-        arr = np.ascontiguousarray(comp, dtype=np.uint8)
-        self._c(lib().sbh_shard_load(self.h, _ptr(arr), int(arr.size), int(file_offset), 0))
-        self.n, self.file_offset = int(arr.size), int(file_offset)
+    def load(self, comp, file_offset, on_device=False, nbytes=None):
+        """Replace the resident bytes with file bytes [file_offset, file_offset + n) of the same
+        file, keeping the device buffers (sbh_shard_load): comp = host bytes (numpy uint8), or a
+        device pointer (int) with nbytes when on_device."""
+        if on_device:
+            n = int(nbytes)
+            self._c(lib().sbh_shard_load(self.h, C.c_void_p(int(comp)), n, int(file_offset), 1))
+        else:
+            arr = np.ascontiguousarray(comp, dtype=np.uint8)
+            n = int(arr.size)
+            self._c(lib().sbh_shard_load(self.h, _ptr(arr), n, int(file_offset), 0))
+        self.n, self.file_offset = n, int(file_offset)
         self.n_blocks = self.flat_size = 0
 
     # -- bgzf --------------------------------------------------------------
@@ -284,6 +291,27 @@ class Shard:
         return [(b.start, b.csize, b.usize, b.ustart, b.hsize, b.flags)
                 for b in arr[: self.n_blocks]]
 
+    def block_arrays(self):
+        """The block table as numpy arrays {start, ustart, usize} (sbh_get_blocks into one
+        structured array: no Python object per block)."""
+        dt = np.dtype([("start", "<u8"), ("ustart", "<u8"), ("csize", "<u4"), ("hsize", "<u4"), ("usize", "<u4"),
+                       ("flags", "<u4")])
+        a = np.zeros(max(self.n_blocks, 1), dtype=dt)
+        if self.n_blocks:
+            self._c(lib().sbh_get_blocks(self.h, 0, self.n_blocks, a.ctypes.data_as(C.c_void_p)))
+        a = a[:self.n_blocks]
+        return {"start": a["start"], "ustart": a["ustart"], "usize": a["usize"].astype(np.uint64)}
+
+    def vpos_of_flat(self, flat):
+        """Flat positions -> htsjdk virtual offsets over the block table (canonical: a position at
+        a block's end is Pos(next block, 0); empty blocks hold no positions)."""
+        b = self.block_arrays()
+        live = b["usize"] > 0
+        starts, ustarts = b["start"][live], b["ustart"][live]
+        flat = np.asarray(flat, dtype=np.uint64)
+        k = np.searchsorted(ustarts, flat, side="right") - 1
+        return (starts[k] << np.uint64(16)) | (flat - ustarts[k])
+
     def inflate(self):
         bad = C.c_uint64()
         self._c(lib().sbh_inflate(self.h, C.byref(bad)))
@@ -305,6 +333,13 @@ class Shard:
         if n:
             self._c(lib().sbh_read_flat(self.h, flat, n, _ptr(out)))
         return out
+
+    def read_flat_into(self, flat, n, out):
+        """Flat bytes [flat, flat + n) into the host array `out` (e.g. a PinnedBuffer's array)."""
+        if n:
+            if out.size < n:
+                raise ValueError("read_flat_into: buffer too small")
+            self._c(lib().sbh_read_flat(self.h, int(flat), int(n), _ptr(out)))
 
     def flat_of(self, block_pos, offset=0):
         out = C.c_uint64()
@@ -452,6 +487,26 @@ class Shard:
         self._c(lib().sbh_records_scan_regions(self.h, _ptr(cb), _ptr(ce), cb.size, _ptr(ir), _ptr(ib),
                                                _ptr(ie), ir.size, C.byref(sz)))
         return self._records_fetch(sz)
+
+    def split_records(self, start, end, bgzf_blocks_to_check=5, reads_to_check=10, max_read_size=100000000,
+                      decode=True):
+        """One FileSplit of loadReadsAndPositions in one call (sbh_split_records): FindBlockStart,
+        index + inflate, the eager check over [Pos(blockStart, 0), Pos(end, 0)), FindRecordStart
+        and the split's records.  Returns (info dict, columns): all columns when decode, else
+        only `flat` (the record starts)."""
+        r = SbhSplitRecordsResult()
+        self._c(lib().sbh_split_records(self.h, int(start), int(end), int(bgzf_blocks_to_check), int(reads_to_check),
+                                        int(max_read_size), 1 if decode else 0, C.byref(r)))
+        info = {f: getattr(r, f) for f, _ in SbhSplitRecordsResult._fields_ if f != "sizes"}
+        info["n"] = r.sizes.n
+        self.n_blocks, self.flat_size = r.n_blocks, r.flat_size  # (the index the call built: blocks())
+        if decode:
+            return info, self._records_fetch(r.sizes)
+        flat = np.empty(r.sizes.n, np.uint64)
+        if r.sizes.n:
+            out = SbhRecordsOut(flat=flat.ctypes.data)
+            self._c(lib().sbh_records_fetch(self.h, C.byref(out)))
+        return info, {"flat": flat}
 
     def _records_fetch(self, sz):
         cols = record_columns(sz.n, sz.name_bytes, sz.cigar_ops, sz.bases, sz.aux_bytes)

@@ -163,3 +163,31 @@ def test_second_member(ctx):
     assert got == (SBH_E_INFLATE_DATA, None) == zlib_outcome([raw1, raw2])
     got = inflate(ctx, good + good + EOF_MEMBER)
     assert got[0] is None and got[1] == zlib.decompress(raw1, -15) * 2
+
+
+@pytest.mark.parametrize("at,extra", [(3000, 0), (3000, 1), (3000, 20000), (10, 32768 - 10)])
+def test_long_far_match(ctx, at, extra):
+    # a 258-byte match (k_lz marks it with a start every 32 bytes) reaching exactly to the first
+    # byte, one byte past it, far past it, and distance 32768 at a small offset
+    lead = literals(at, 9)
+    toks = lead + [(258, len(lead) + extra)] + literals(6000, 10)
+    data, raw, u = member([toks], at + 6258)
+    got = inflate(ctx, data + EOF_MEMBER)
+    assert got == zlib_outcome([raw])
+    assert (got[0] is None) == (extra == 0)
+
+
+@pytest.mark.parametrize("extra", [0, 1, 5000])
+def test_far_match_after_carried_cut(ctx, extra):
+    # long matches fill k_lz's 6656-byte pointer pass before the chunk's 1536 tokens are used up,
+    # so the chunk is cut and carried; the (far) match comes after several such cuts
+    lead = literals(400, 11)
+    toks = list(lead)
+    for i in range(60):  # ~15 KB of 258-byte matches (several passes' worth), literals between
+        toks += [(258, 300 + i)] + literals(3, 100 + i)
+    n = len(expand(toks))
+    toks += [(100, n + extra)] + literals(4000, 12)
+    data, raw, u = member([toks], n + 4100)
+    got = inflate(ctx, data + EOF_MEMBER)
+    assert got == zlib_outcome([raw])
+    assert (got[0] is None) == (extra == 0)

@@ -6,6 +6,7 @@ OUT=${1:-gpurun_out/calib}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 cd - > /dev/null
+make -s -C tools calib  # (the calibration kernels: their own target, not part of `all`)
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 60 rocprofv3 --pmc $c -d "$OUT/$c" -o "$c" --output-format csv -- tools/calib_counters \
     > "$OUT/$c.out" 2> "$OUT/$c.log"

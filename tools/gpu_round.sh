@@ -10,6 +10,7 @@
 #   bash tools/gpu_round.sh fullab TAG RECORDS V...      full-checker A/B (tools/full_ab.py), same variants
 #   bash tools/gpu_round.sh pmc TAG ARGS...        counter passes (tools/pmc_collect.sh) over bench.py ARGS
 #   bash tools/gpu_round.sh trace TAG              kernel-trace timeline of 8 bench steps + idle gaps
+#   bash tools/gpu_round.sh ftrace TAG LASTMS ARGS...  kernel-trace of bench.py ARGS, idle gaps of its last LASTMS ms
 #   bash tools/gpu_round.sh allpos TAG GIB ARGS...  check-bam -s over configs[2]'s one GIB-GiB file
 #                                                  (tools/allpos_configC.py: a 2 GiB rehearsal first)
 set -o pipefail
@@ -65,6 +66,15 @@ trace)
     --no-cpu-baseline --no-full --no-e2e > gpurun_out/${T}_trbench.log 2>&1 || exit 9
   cp "$(find /tmp/${T}_tr -name '*.db' -print -quit)" gpurun_out/${T}_trace.db
   python3 tools/prof_gaps.py gpurun_out/${T}_trace.db --step-kernel k_lz --steps 6 --top 30 > gpurun_out/${T}_gaps.log 2>&1
+  ;;
+ftrace)
+  # kernel-trace timeline of bench.py ARGS and the busy / idle split of its last LASTMS ms
+  L=$1; shift
+  prof_env
+  timeout -k 10 400 rocprofv3 --kernel-trace -d /tmp/${T}_ft -o run -- python3 bench.py "$@" \
+    > gpurun_out/${T}_ftrace.json 2> gpurun_out/${T}_ftrace.err || exit 12
+  cp "$(find /tmp/${T}_ft -name '*.db' -print -quit)" gpurun_out/${T}_ftrace.db
+  python3 tools/prof_gaps.py gpurun_out/${T}_ftrace.db --last-ms $L --top 30 > gpurun_out/${T}_fgaps.log 2>&1
   ;;
 allpos)
   G=$1; shift
