@@ -36,7 +36,8 @@ import org.hammerlab.bam.index.Index.Chunk
 import org.hammerlab.bam.spark.{ BAMRecordRDD, NoReadFoundException, Split }
 import org.hammerlab.bam.spark.load.{ CanLoadBam, SplitRDD }
 import org.hammerlab.bgzf.{ EstimatedCompressionRatio, Pos }
-import org.hammerlab.bgzf.block.{ BGZFBlocksToCheck, Block, HeaderSearchFailedException, Metadata, StreamI }
+import org.hammerlab.bgzf.block.{ BGZFBlocksToCheck, Block, HeaderSearchFailedException, Metadata, SeekableStream,
+                                   SeekableUncompressedBytes, StreamI }
 import org.hammerlab.channel.{ ByteChannel, CachingChannel, SeekableByteChannel }
 import org.hammerlab.genomics.loci.set.LociSet
 import org.hammerlab.hadoop.splits.{ FileSplits, MaxSplitSize }
@@ -601,21 +602,133 @@ case class GpuStream(compressedBytes: ByteChannel with SeekableByteChannel, wind
   }
 }
 
+/** Drop-in for bgzf/.../block/Stream.scala's SeekableStream (:79-121): a SUBCLASS of the reference's
+  * own SeekableStream, so the reference's SeekableUncompressedBytes(blockStream) (UncompressedBytes
+  * .scala:65-87) and every caller of it take it unchanged -- only where the stream is built changes
+  * (GpuSeekableStream.uncompressedBytes, INTEGRATION.md).  Its blocks come from a WINDOW of the file
+  * (compressed bytes [p, p + window) plus a halo, in one reused shard) indexed and inflated on the
+  * device in one pass, the window's inflated bytes copied to the host once; the window replaces the
+  * reference's 100-block LRU: a seek back into it (CanLoadBam.scala:349 seeks to the split's first
+  * record right after FindRecordStart read past it) re-inflates nothing.  seek(newPos) is the
+  * reference's own (clear and reposition unless already there); _advance reads the block at the
+  * channel's position, and the empty block that ends the stream answers None (Stream.scala:56-58).
+  * Mirrored by spark_bam_amd.seekable.SeekableStream (tests/test_seekable_gpu.py). */
+class GpuSeekableStream(ch: SeekableByteChannel, window: Long = 16L << 20, halo: Long = 1L << 20)
+  extends SeekableStream(ch) {
+
+  private var buf: ByteBuffer = _
+  private var shard: GpuShard = _
+  private var contigs: Array[Int] = Array.empty
+  private var starts: Array[Long] = Array.empty  // the window's blocks (sorted starts) and their
+  private var table: Array[Long] = Array.empty   // (start, ustart, csize, hsize, usize, flags) rows
+  private var flat: Array[Byte] = Array.empty    // the window's inflated bytes, host copy
+  private var wHi = -1L
+  var windowsLoaded = 0
+
+  /** index + inflate the blocks from the block start p over [p, p + w + halo) */
+  private[gpu] def load(p: Long, w: Long = window): Unit = {
+    val size = ch.size
+    val m = math.min(size - p, w + halo)
+    if (buf == null || buf.capacity < m) {
+      if (buf != null) Native.hostFree(buf)
+      buf = Native.hostAlloc(math.max(m, 1L << 20))
+    }
+    buf.clear()
+    buf.limit(m.toInt)
+    val back = ch.position()
+    ch.seek(p)
+    ch.readFully(buf)
+    ch.seek(back)
+    buf.flip()
+    if (shard == null) shard = new GpuShard(buf, m, p, size, contigs)
+    else shard.reload(buf, m, p)
+    shard.load(p)
+    table = shard.blocks(0, shard.numBlocks)
+    starts = Array.tabulate(shard.numBlocks.toInt)(i ⇒ table(6 * i))
+    flat = if (shard.flatSize > 0) shard.flat(0, shard.flatSize.toInt) else Array.empty
+    wHi = p + m
+    windowsLoaded += 1
+  }
+
+  private def row(p: Long): Int = {
+    val i = java.util.Arrays.binarySearch(starts, p)
+    if (i < 0 || (table(6 * i + 5) & 2) != 0) -1 else i  // (2: a block cut off by the window's end)
+  }
+
+  override protected def _advance: Option[Block] = {
+    val start = compressedBytes.position()
+    if (start >= compressedBytes.size) return None  // (the reference's EOFException -> None)
+    var i = row(start)
+    if (i < 0) { load(start); i = row(start) }
+    val (ustart, csize, usize, flags) = (table(6 * i + 1), table(6 * i + 2), table(6 * i + 4), table(6 * i + 5))
+    compressedBytes.seek(start + csize)
+    if ((flags & 1) != 0) None  // dataLength == 2: the empty block ending the stream
+    else Some(Block(java.util.Arrays.copyOfRange(flat, ustart.toInt, (ustart + usize).toInt), start, csize.toInt))
+  }
+
+  /** FindRecordStart.withDelta from Pos(start, 0) on the window's shard (grown x4 while the search
+    * needs bytes past it): Some((pos, positions skipped)) or None. */
+  def findRecordStart(start: Long, contigLengths: Array[Int], readsToCheck: Int,
+                      maxReadSize: Int): Option[(Pos, Int)] = {
+    if (!java.util.Arrays.equals(contigs, contigLengths)) {
+      contigs = contigLengths
+      if (shard != null) Native.setContigs(Device.ctx, shard.sh, contigs)
+    }
+    var w = window
+    if (shard == null || row(start) < 0) load(start, w)
+    while (true) {
+      try {
+        return shard.findRecordStart(table(6 * row(start) + 1), readsToCheck, maxReadSize).map {
+          case (f, d) ⇒ (shard.posOf(f), d)
+        }
+      } catch {
+        case e: NeedHaloException if wHi < ch.size ⇒ w *= 4; load(start, w)
+      }
+    }
+    None
+  }
+
+  override def close(): Unit = {
+    if (shard != null) { shard.close(); shard = null }
+    if (buf != null) { Native.hostFree(buf); buf = null }
+    super.close()
+  }
+}
+
+object GpuSeekableStream {
+  /** the reference's SeekableUncompressedBytes over a GPU-inflated SeekableStream: what
+    * SeekableUncompressedBytes(ch) (UncompressedBytes.scala:79-86) builds, with the GPU stream */
+  def uncompressedBytes(ch: SeekableByteChannel, window: Long = 16L << 20): SeekableUncompressedBytes =
+    SeekableUncompressedBytes(new GpuSeekableStream(ch, window))
+}
+
 /** Drop-in for check/.../spark/FindRecordStart.scala:11-71 on the GPU: the first eager-true
-  * position at/after Pos(start, 0) within maxReadSize positions, searched on the device over a
-  * shard of the file from `start` (grown x4 while the search needs bytes past it).  Same
-  * signature; `uncompressedBytes` is not read (the device inflates the blocks itself). */
+  * position at/after Pos(start, 0) within maxReadSize positions.  Same signature.  When the
+  * caller's `uncompressedBytes` is GPU-backed (GpuSeekableStream) the search runs on that view's
+  * window shard -- the blocks its next reads will come from -- and the view is left at the found
+  * record, as the reference's withDelta leaves it (FindRecordStart.scala:30-63); otherwise a shard of
+  * the file from `start` (grown x4 while the search needs bytes past it). */
 object GpuFindRecordStart {
   def apply(path: Path,
             start: Long)(
       implicit
-      uncompressedBytes: org.hammerlab.bgzf.block.SeekableUncompressedBytes,
+      uncompressedBytes: SeekableUncompressedBytes,
       contigLengths: ContigLengths,
       readsToCheck: ReadsToCheck,
-      maxReadSize: MaxReadSize): Pos =
-    withDelta(path, Pos(start, 0))
-      .map(_._1)
-      .getOrElse(throw NoReadFoundException(path, start, maxReadSize))
+      maxReadSize: MaxReadSize): Pos = {
+    val found = uncompressedBytes.blockStream match {
+      case g: GpuSeekableStream ⇒
+        g.findRecordStart(start, GpuShard.contigArray(contigLengths), readsToCheck.n, maxReadSize.n).map(_._1)
+      case _ ⇒
+        withDelta(path, Pos(start, 0)).map(_._1)
+    }
+    found match {
+      case Some(pos) ⇒
+        uncompressedBytes.seek(pos)
+        pos
+      case None ⇒ throw NoReadFoundException(path, start, maxReadSize)
+    }
+  }
 
   /** FindRecordStart.withDelta: Some((pos, positions skipped)) or None */
   def withDelta(path: Path, start: Pos, halo0: Long = 1L << 20)(

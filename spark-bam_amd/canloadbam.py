@@ -53,6 +53,7 @@ class SplitWorker:
         self.contigs = np.ascontiguousarray(np.asarray(contigs, dtype=np.int32))
         self.sh = None
         self.pin = None
+        self.out_pin = None  # page-locked landing buffer of the record starts / bytes copied out
         # device_file: a device pointer to the whole file's bytes already in HBM (the facade bench's
         # resident mode: the split's bytes are copied device-to-device, no host read or H2D)
         self.device_file = device_file
@@ -92,7 +93,8 @@ class SplitWorker:
         while True:
             sh = self.load(read, start, min(self.size, end + halo))
             try:
-                info, cols = sh.split_records(start, end, bgzf_blocks_to_check, reads_to_check, max_read_size, decode)
+                info, cols = sh.split_records(start, end, bgzf_blocks_to_check, reads_to_check, max_read_size, decode,
+                                          flat_out=None if decode else self._flat_buf)
             except HeaderSearchFailedException as e:
                 raise e.with_path(path)
             except NoReadFoundException as e:
@@ -107,13 +109,39 @@ class SplitWorker:
             self.last = info
             return cols
 
+    def _flat_buf(self, n):
+        """n u64 slots of the worker's page-locked landing buffer (the record starts' copy-out
+        lands in page-locked memory: DMA, no runtime staging); returned as a fresh array."""
+        self._grow_out(8 * n)
+        return self.out_pin.array[:8 * n].view(np.uint64)
+
+    def _grow_out(self, nbytes):
+        if self.out_pin is None or self.out_pin.array.size < nbytes:
+            if self.out_pin is not None:
+                self.out_pin.close()
+            self.out_pin = PinnedBuffer(max(int(nbytes * 1.25), 1 << 20))
+
+    def fetch_record_bytes(self, flat):
+        """What jni/Native.scala's GpuRecordIterator copies out of HBM: the bytes from the first
+        record to the end of the last one (into the worker's page-locked buffer; a view of it).
+        `flat` = the split's record starts."""
+        sh = self.sh
+        last = int(flat[-1])
+        l4 = int(sh.read_flat(last, 4).view(np.uint32)[0])
+        lo, hi = int(flat[0]), last + 4 + l4
+        starts = np.array(flat, copy=True)  # (the starts live in the same landing buffer)
+        self._grow_out(hi - lo)
+        sh.read_flat_into(lo, hi - lo, self.out_pin.array)
+        return starts, self.out_pin.array[:hi - lo]
+
     def close(self):
         if self.sh is not None:
             self.sh.close()
             self.sh = None
-        if self.pin is not None:
-            self.pin.close()
-            self.pin = None
+        for b in (self.pin, self.out_pin):
+            if b is not None:
+                b.close()
+        self.pin = self.out_pin = None
 
 
 def split_partition(ctx, read, size, path, start, end, contigs, bgzf_blocks_to_check=DEFAULT_BGZF_BLOCKS_TO_CHECK,

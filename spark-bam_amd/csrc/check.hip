@@ -354,6 +354,7 @@ struct EagerOut {
   uint64_t xq_cap;                // 0: every exact check runs inline
   unsigned long long *true_spread;  // k_eager: per-wave true counts, folded into n_true by k_fold_true
   TileSum *tsum;                  // per tile: the chain proof's summary (nullptr: none)
+  const uint32_t *sieve = nullptr;  // k_lz's first-filter bitmap, bit p = flat position p (nullptr: sweep here)
 };
 
 // k_eager's true count goes to TRUE_SLOTS counters TRUE_STRIDE u64 apart (one atomic per
@@ -696,7 +697,31 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
   uint32_t msk[EMW];
 #pragma unroll
   for (uint32_t w = 0; w < EMW; ++w) msk[w] = 0;
-  {
+  if (o.sieve) {
+    // k_lz evaluated this filter (and the next refID / pos signs) on the bytes in its LDS ring:
+    // the thread's bits are the sieve's bits [s0 + 4 g0, + 4 EG), masked to the window, plus every
+    // position from fast_end on (near a segment end, decided below)
+    const uint64_t A = s0 + 4ull * g0;
+    const uint32_t *sw = o.sieve + (A >> 5);
+    const uint32_t sft = (uint32_t)(A & 31);
+    const int32_t ib = (int32_t)(4 * g0) - (int32_t)sa;  // window index of bit 0
+    const int32_t gl = 4 * ((int32_t)ngroups - (int32_t)g0);  // bits below this are groups < ngroups
+    uint32_t lo_w = sw[0];
+#pragma unroll
+    for (uint32_t w = 0; w < EMW; ++w) {
+      const uint32_t hi_w = sw[w + 1];
+      uint32_t m = sft ? (lo_w >> sft) | (hi_w << (32 - sft)) : lo_w;
+      lo_w = hi_w;
+      // bit b <-> window index ii = ib + 32 w + b: in the window [0, EW), its group < ngroups and
+      // < EG; from fast_end on every in-window position is kept
+      const int32_t i0 = ib + 32 * (int32_t)w;
+      auto upto = [](int32_t k) -> uint32_t { return k <= 0 ? 0u : k >= 32 ? ~0u : (1u << k) - 1u; };
+      const uint32_t in = ~upto(-i0) & upto((int32_t)EW - i0) & upto(gl - 32 * (int32_t)w) &
+                          upto(4 * (int32_t)EG - 32 * (int32_t)w);
+      m |= ~upto((int32_t)fast_end - i0);
+      msk[w] = m & in;
+    }
+  } else {
     uint32_t a = lds32[g0 + 1];
 #pragma unroll
     for (uint32_t gi = 0; gi < EG; ++gi) {
@@ -2132,12 +2157,13 @@ static inline uint32_t ngrid(uint64_t n, uint32_t t) { return (uint32_t)((n + t 
 hipError_t launch_eager(const uint8_t *U, uint64_t u_pad, uint64_t begin, uint64_t end, const uint64_t *seg_end,
                         uint32_t nseg, uint32_t open_last, const int32_t *ctg, int32_t nctg, int32_t rtc,
                         uint32_t *bits, unsigned long long *counters, hipStream_t st, uint64_t front,
-                        uint64_t *defer_pos, uint64_t defer_cap, uint64_t *xq_pos, uint64_t xq_cap, TileSum *tsum) {
+                        uint64_t *defer_pos, uint64_t defer_cap, uint64_t *xq_pos, uint64_t xq_cap, TileSum *tsum,
+                        const uint32_t *sieve) {
   if (end <= begin) return hipSuccess;
   Segs sg{seg_end, nseg, open_last};
   Ctg c{ctg, nctg};
   EagerOut o{bits,   counters,     counters + 1, counters + 2, front, defer_pos, counters + 3, defer_cap,
-             xq_pos, counters + 4, xq_cap,       counters + TRUE_SPREAD_OFF, tsum};
+             xq_pos, counters + 4, xq_cap,       counters + TRUE_SPREAD_OFF, tsum, sieve};
   hipLaunchKernelGGL(k_eager, dim3(ngrid(end - begin, ETILE)), dim3(T), 0, st, U, u_pad, begin, end, sg, c,
                      rtc, o);
   hipLaunchKernelGGL(k_fold_true, dim3(1), dim3(WAVE), 0, st, counters + TRUE_SPREAD_OFF, counters);

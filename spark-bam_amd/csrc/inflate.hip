@@ -2641,8 +2641,30 @@ __device__ __forceinline__ void chase8_asm(uint32_t (&c)[8], uint32_t pend, uint
 #ifndef SBH_LZ_WAVES_PER_EU
 #define SBH_LZ_WAVES_PER_EU (SBH_LZ_RING ? 6 : 4)  // (the register budget: 512 VGPRs / waves per SIMD)
 #endif
+#ifndef SBH_LZ_SIEVE
+#define SBH_LZ_SIEVE 1  // k_lz leaves k_eager's first filter as a bitmap (launch_lz's sieve)
+#endif
+// k_eager's first filter at the 16 positions of a granule: eager.Checker reads refID, pos, next
+// refID and next pos first (PosChecker.getRefPosError, check/.../PosChecker.scala:43-63; the
+// refID / next refID in [-1, n) and pos / next pos >= -1 parts need no contig length), so a
+// position failing one of them is false; d[] = the 48 bytes from the granule's first.
+__device__ __forceinline__ uint32_t sieve16(const uint32_t (&d)[12], uint32_t nref1) {
+  uint32_t m = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < 16; ++j) {
+    const uint32_t q = j >> 2, k = j & 3;
+    const uint32_t ref = __builtin_amdgcn_alignbyte(d[q + 2], d[q + 1], k);
+    const uint32_t pos = __builtin_amdgcn_alignbyte(d[q + 3], d[q + 2], k);
+    const uint32_t nrf = __builtin_amdgcn_alignbyte(d[q + 7], d[q + 6], k);
+    const uint32_t nps = __builtin_amdgcn_alignbyte(d[q + 8], d[q + 7], k);
+    m |= (ref + 1u < nref1 && nrf + 1u < nref1 && (int32_t)pos >= -1 && (int32_t)nps >= -1) ? 1u << j : 0u;
+  }
+  return m;
+}
+
 __global__ __launch_bounds__(LZ_THREADS, SBH_LZ_WAVES_PER_EU) void k_lz(const uint8_t *__restrict__ comp, DevBlocks bl, uint64_t nblocks,
-                                                    const uint32_t *__restrict__ tok, uint8_t *__restrict__ U) {
+                                                    const uint32_t *__restrict__ tok, uint8_t *__restrict__ U,
+                                                    uint32_t *__restrict__ sieve, uint32_t nref1) {
   __shared__ LzSmem sm;
   uint32_t *wsum = sm.pp.wsum;
   const uint64_t b = blockIdx.x;
@@ -2656,6 +2678,10 @@ __global__ __launch_bounds__(LZ_THREADS, SBH_LZ_WAVES_PER_EU) void k_lz(const ui
     const uint64_t src = bl.cstart[b] + bl.hsize[b] + 5;
     const uint32_t usize = bl.usize[b];
     const uint64_t g0 = G & ~15ull;
+    if (SBH_LZ_SIEVE && sieve) {  // (no ring here: the whole block is "undecided" for k_eager's filter)
+      uint16_t *sv = reinterpret_cast<uint16_t *>(sieve) + (g0 >> 4);
+      for (uint32_t q = t; q < (sh + usize + 15) / 16; q += LZ_THREADS) sv[q] = 0xffffu;
+    }
     for (uint32_t lo = 16 * t; lo < sh + usize; lo += 16 * LZ_THREADS) {
       if (lo >= sh && lo + 16 <= sh + usize) {
         const uint64_t a = src + (lo - sh);
@@ -2689,6 +2715,30 @@ __global__ __launch_bounds__(LZ_THREADS, SBH_LZ_WAVES_PER_EU) void k_lz(const ui
       }
     }
     from = to > from ? to : from;
+  };
+#endif
+#if SBH_LZ_RING && SBH_LZ_SIEVE
+  // k_eager's first filter on the bytes in the ring: granule G's 16 positions need image bytes
+  // [16 G, 16 G + 48), so its sieve word is written once granule G + 2 is final (flushed); a
+  // granule holding another block's positions (the first, when the block does not start on a
+  // granule) or positions whose 48 bytes run past the block is all ones -- k_eager decides those
+  // itself (both blocks write 0xffff to a shared granule)
+  uint16_t *const sv16 = sieve ? reinterpret_cast<uint16_t *>(sieve) + (g0u >> 4) : nullptr;
+  uint32_t svf = 0;  // first granule whose sieve word is not written yet (uniform)
+  auto lz_sieve = [&](uint32_t upto, uint32_t end_img) {
+    for (uint32_t q = svf + t; q < upto; q += LZ_THREADS) {
+      const uint32_t lo = q * 16;
+      uint32_t m = 0xffffu;
+      if (lo >= sh && lo + 48 <= end_img) {
+        const uint4 a = *reinterpret_cast<const uint4 *>(sm.img + lz_ri(lo));
+        const uint4 b2 = *reinterpret_cast<const uint4 *>(sm.img + lz_ri(lo + 16));
+        const uint4 c2 = *reinterpret_cast<const uint4 *>(sm.img + lz_ri(lo + 32));
+        const uint32_t d[12] = {a.x, a.y, a.z, a.w, b2.x, b2.y, b2.z, b2.w, c2.x, c2.y, c2.z, c2.w};
+        m = sieve16(d, nref1);
+      }
+      sv16[q] = (uint16_t)m;
+    }
+    svf = upto > svf ? upto : svf;
   };
 #endif
 
@@ -2774,6 +2824,9 @@ static_assert(!(SBH_LZ_CARRY && SBH_LZ_PREFETCH), "the token prefetch assumes ch
       // every byte before pb is final (the scan's or the last pass's barrier): its whole granules
       // leave the ring for U before the ring wraps onto them
       lz_flush(fl, (sh + pb) & ~15u);
+#if SBH_LZ_SIEVE
+      if (sv16 && fl >= 48) lz_sieve(fl / 16 - 2, ~0u);
+#endif
 #endif
       // slots start at the 16-byte LDS granule holding `pb`, so that each thread's 16
       // slots are one granule of the image
@@ -3160,6 +3213,9 @@ static_assert(!(SBH_LZ_CARRY && SBH_LZ_PREFETCH), "the token prefetch assumes ch
       }
     }
   }
+#if SBH_LZ_RING && SBH_LZ_SIEVE
+  if (sv16) lz_sieve(ngran, sh + usize);  // (the image is complete: the last barrier above)
+#endif
 }
 
 // The first block whose inflate status is not INF_OK (atomicMin; *first preset to ~0):
@@ -3202,13 +3258,16 @@ hipError_t launch_huff(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, 
 }
 
 hipError_t launch_lz(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, const uint32_t *tok_buf,
-                     uint64_t tok_base, uint8_t *U, hipStream_t stream) {
+                     uint64_t tok_base, uint8_t *U, hipStream_t stream, uint32_t *sieve, uint32_t nref1) {
   if (nblocks == 0) return hipSuccess;
   const uint32_t *tok = reinterpret_cast<const uint32_t *>(reinterpret_cast<uintptr_t>(tok_buf) - tok_base * 4);
+  if (!SBH_LZ_SIEVE || !SBH_LZ_RING) sieve = nullptr;
 #ifdef SBH_LZ_PAD  // occupancy probe: dynamic LDS that leaves one workgroup per CU
-  hipLaunchKernelGGL(k_lz, dim3((uint32_t)nblocks), dim3(LZ_THREADS), SBH_LZ_PAD, stream, comp, blocks, nblocks, tok, U);
+  hipLaunchKernelGGL(k_lz, dim3((uint32_t)nblocks), dim3(LZ_THREADS), SBH_LZ_PAD, stream, comp, blocks, nblocks, tok, U,
+                     sieve, nref1);
 #else
-  hipLaunchKernelGGL(k_lz, dim3((uint32_t)nblocks), dim3(LZ_THREADS), 0, stream, comp, blocks, nblocks, tok, U);
+  hipLaunchKernelGGL(k_lz, dim3((uint32_t)nblocks), dim3(LZ_THREADS), 0, stream, comp, blocks, nblocks, tok, U, sieve,
+                     nref1);
 #endif
   return hipGetLastError();
 }

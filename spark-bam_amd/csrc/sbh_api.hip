@@ -63,7 +63,8 @@ hipError_t build_chain(const uint8_t *comp, uint64_t n, const uint64_t *cand, ui
 hipError_t launch_eager(const uint8_t *U, uint64_t u_pad, uint64_t begin, uint64_t end, const uint64_t *seg_end,
                         uint32_t nseg, uint32_t open_last, const int32_t *ctg, int32_t nctg, int32_t rtc,
                         uint32_t *bits, unsigned long long *counters, hipStream_t st, uint64_t front,
-                        uint64_t *defer_pos, uint64_t defer_cap, uint64_t *xq_pos, uint64_t xq_cap, TileSum *tsum);
+                        uint64_t *defer_pos, uint64_t defer_cap, uint64_t *xq_pos, uint64_t xq_cap, TileSum *tsum,
+                        const uint32_t *sieve = nullptr);
 hipError_t launch_eager_xq(const uint8_t *U, uint64_t begin, const uint64_t *seg_end, uint32_t nseg,
                            uint32_t open_last, const int32_t *ctg, int32_t nctg, int32_t rtc, uint32_t *bits,
                            unsigned long long *counters, uint64_t *xq_pos, uint64_t cap, hipStream_t st);
@@ -181,6 +182,10 @@ struct sbh_shard {
   int32_t nctg = -1;
   DBuf<uint32_t> bits;
   DBuf<TileSum> tsum;
+  // k_lz's first-filter bitmap for k_eager (launch_lz's sieve), valid for the inflated bytes and
+  // the contig count it was computed with (sieve_nref1 = contigs + 1; 0: none)
+  DBuf<uint32_t> sieve;
+  uint32_t sieve_nref1 = 0;
   bool pipe_fallback = false;  // run_pipelined redid the eager pass (a deferral overflow)  // per quarter eager tile of bits (from bits_begin): the chain proof's summaries
   // chain marking (pointer doubling) over the set bits of [cm_first, cm_E) when the bitmap
   // is not the chain: node positions, per-word prefix counts, jumps, marks and their prefix
@@ -496,7 +501,7 @@ int sbh_shard_destroy(sbh_shard *sh) {
   sh->counts.release(); sh->cfirst.release(); sh->offs.release(); sh->cand.release(); sh->v.release(); sh->rank.release();
   sh->tmp.release(); sh->J0.release(); sh->J1.release(); sh->on.release(); sh->d_seg.release();
   sh->U.release(); sh->ctg.release(); sh->bits.release(); sh->words.release(); sh->close_pos.release();
-  sh->close_word.release(); sh->ctr.release(); sh->opix.release(); sh->tsum.release();
+  sh->close_word.release(); sh->ctr.release(); sh->opix.release(); sh->tsum.release(); sh->sieve.release();
   sh->comp2.release(); sh->aux2.release();
   for (hipStream_t st : sh->pf_stream) (void)hipStreamDestroy(st);
   for (uint8_t *p : sh->pf_pin) (void)hipHostFree(p);
@@ -539,6 +544,7 @@ int sbh_shard_load(sbh_shard *sh, const void *src, uint64_t n, uint64_t file_off
   sh->file_off = file_offset;
   sh->n = n;
   sh->at_eof = file_offset + n == sh->file_size;
+  sh->sieve_nref1 = 0;
   sh->indexed = sh->inflated = sh->bits_valid = sh->chain_ok = sh->cm_valid = false;
   sh->rec.valid = false;
   sh->ncand = 0;
@@ -676,6 +682,7 @@ int shard_prefetch_finish(sbh_shard *sh, bool use, double *copy_ms) {
   sh->file_off = sh->pf_off;
   sh->n = sh->pf_n;
   sh->at_eof = sh->file_off + sh->n == sh->file_size;
+  sh->sieve_nref1 = 0;
   sh->indexed = sh->inflated = sh->bits_valid = sh->chain_ok = sh->cm_valid = false;
   sh->rec.valid = false;
   sh->ncand = 0;
@@ -731,6 +738,7 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
   hipStream_t st = sh->st;
   int rc = set_device(ctx);
   if (rc) return rc;
+  sh->sieve_nref1 = 0;
   sh->indexed = sh->inflated = sh->bits_valid = sh->chain_ok = sh->cm_valid = false;
   sh->ncand = 0;
   const uint64_t rel = start - sh->file_off;
@@ -904,6 +912,20 @@ static int inflate_status(sbh_shard *sh, hipStream_t st, uint64_t *bad_block, co
                    (unsigned long long)b.start);
 }
 
+// SBH_SIEVE=0: k_eager sweeps refIDs itself (k_lz leaves no sieve), for A/B
+static bool sieve_on() {
+  const char *e = std::getenv("SBH_SIEVE");
+  return !(e && e[0] == '0');
+}
+// The sieve k_lz fills for k_eager (launch_lz): one bit per flat position of the shard, plus the
+// look-ahead an eager window past the last tile reads (masked there); nullptr when off or when the
+// contig count is not known yet.
+static uint32_t *sieve_for(sbh_shard *sh) {
+  if (!sieve_on() || sh->nctg < 0) return nullptr;
+  if (sh->sieve.ensure((sh->utotal + sh->pad + 65536) / 32 + 2) != hipSuccess) return nullptr;
+  return sh->sieve.p;
+}
+
 static DevBlocks blocks_from(DevBlocks d, uint64_t b) {
   return DevBlocks{d.cstart + b, d.csize + b, d.hsize + b, d.usize + b, d.ustart + b, d.flags + b, d.status + b, d.ntok + b};
 }
@@ -961,17 +983,20 @@ int sbh_inflate(sbh_shard *sh, uint64_t *bad_block) {
   const TokPlan P = tok_plan(sh, ~0ull);
   HIPCHK(ctx, sh->tok.ensure(P.tok_len));
   HIPCHK(ctx, hipMemsetAsync(sh->U.p + sh->utotal, 0, sh->pad, st));
+  uint32_t *sv = sieve_for(sh);
+  const uint32_t nref1 = (uint32_t)sh->nctg + 1;
   mark(sh, 2);
   for (const auto &bt : P.batches) {  // (one stream: a batch's k_lz finishes before the next k_huff)
     const DevBlocks d = blocks_from(sh->dev_blocks(), bt.first);
     const uint64_t base = P.reuse ? sh->hb[bt.first].ustart : 0;
     HIPCHK(ctx, launch_huff(sh->comp.p, d, bt.second - bt.first, sh->tok.p, base, st));
-    HIPCHK(ctx, launch_lz(sh->comp.p, d, bt.second - bt.first, sh->tok.p, base, sh->U.p, st));
+    HIPCHK(ctx, launch_lz(sh->comp.p, d, bt.second - bt.first, sh->tok.p, base, sh->U.p, st, sv, nref1));
   }
   mark(sh, 3);
   rc = inflate_status(sh, st, bad_block);
   if (rc) return rc;
   sh->inflated = true;
+  sh->sieve_nref1 = sv ? nref1 : 0;
   sh->bits_valid = sh->chain_ok = sh->cm_valid = false;
   return SBH_OK;
 }
@@ -1110,7 +1135,8 @@ static int eager_range(sbh_shard *sh, uint64_t begin, uint64_t end, int32_t rtc,
   mark(sh, 4);
   HIPCHK(ctx, launch_eager(sh->U.p, sh->utotal + sh->pad, begin, end, sh->d_seg.p, (uint32_t)sh->seg_end.size(),
                            sh->open_last ? 1 : 0, sh->ctg.p, sh->nctg, rtc, sh->bits.p, c, st, ~0ull, nullptr, 0,
-                           sh->xq.p, xq_cap(), tsum_on() ? sh->tsum.p : nullptr));
+                           sh->xq.p, xq_cap(), tsum_on() ? sh->tsum.p : nullptr,
+                           sh->sieve_nref1 && sh->sieve_nref1 == (uint32_t)sh->nctg + 1 ? sh->sieve.p : nullptr));
   HIPCHK(ctx, launch_eager_xq(sh->U.p, begin, sh->d_seg.p, (uint32_t)sh->seg_end.size(), sh->open_last ? 1 : 0,
                               sh->ctg.p, sh->nctg, rtc, sh->bits.p, c, sh->xq.p, xq_cap(), st));
   mark(sh, 5);
@@ -1726,6 +1752,9 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
   HIPCHK(ctx, hipMemsetAsync(c, 0, 48, sa));
   HIPCHK(ctx, hipMemsetAsync(c + 2, 0xff, 8, sa));
   sh->inflated = sh->bits_valid = sh->chain_ok = sh->cm_valid = false;
+  sh->sieve_nref1 = 0;
+  uint32_t *sv = sieve_for(sh);
+  const uint32_t nref1 = (uint32_t)sh->nctg + 1;
   sh->pipe_fallback = false;
   const uint64_t nbat = P.batches.size();
   // events: per batch [huff start, huff end, lz start, lz end, eager start, eager end]
@@ -1750,7 +1779,7 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
     HIPCHK(ctx, hipEventRecord(e[1], sa));
     HIPCHK(ctx, hipStreamWaitEvent(sl, e[1], 0));
     HIPCHK(ctx, hipEventRecord(e[2], sl));
-    HIPCHK(ctx, launch_lz(sh->comp.p, d, b1 - b0, sh->tok.p, base, sh->U.p, sl));
+    HIPCHK(ctx, launch_lz(sh->comp.p, d, b1 - b0, sh->tok.p, base, sh->U.p, sl, sv, nref1));
     HIPCHK(ctx, hipEventRecord(e[3], sl));
     // eager tiles whose staged windows lie below the inflated frontier
     const bool last = i + 1 == nbat;
@@ -1766,7 +1795,7 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
       HIPCHK(ctx, launch_eager(sh->U.p, sh->utotal + sh->pad, e_done, hi, sh->d_seg.p, (uint32_t)sh->seg_end.size(),
                                sh->open_last ? 1 : 0, sh->ctg.p, sh->nctg, rtc, sh->bits.p + e_done / 32, c, se,
                                front, sh->defer.p, DEFER_CAP, sh->xq.p, xq_cap(),
-                               tsum_on() ? sh->tsum.p + e_done / EAGER_SUB : nullptr));
+                               tsum_on() ? sh->tsum.p + e_done / EAGER_SUB : nullptr, sv));
       HIPCHK(ctx, hipEventRecord(e[5], se));
       eager_launched[i] = 1;
       e_done = hi;
@@ -1787,6 +1816,7 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
     if (rs) return rs;
   }
   sh->inflated = true;
+  sh->sieve_nref1 = sv ? nref1 : 0;
   if (sh->timing) {
     double hs = 0, ls = 0, es = 0;
     for (uint64_t i = 0; i < nbat; ++i) {

@@ -118,8 +118,13 @@ constexpr uint32_t WPRE_GROUP = 16;
 // in batches of blocks that reuse one bounded token buffer.
 hipError_t launch_huff(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, uint32_t *tok_buf, uint64_t tok_base,
                        hipStream_t stream);
+// sieve (optional): bit p of the flat bitmap = position p may pass eager.Checker's refID / next
+// refID range and pos / next pos sign tests (k_eager's first filter, evaluated by k_lz on the bytes
+// still in its LDS ring; 1 wherever the block's WG cannot decide: seams, stored blocks).  nref1 =
+// contigs + 1.
 hipError_t launch_lz(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, const uint32_t *tok_buf,
-                     uint64_t tok_base, uint8_t *U, hipStream_t stream);
+                     uint64_t tok_base, uint8_t *U, hipStream_t stream, uint32_t *sieve = nullptr,
+                     uint32_t nref1 = 0);
 // *first = the first block of [0, n) whose status is not INF_OK (~0 if none).
 hipError_t launch_first_bad(const uint32_t *status, uint64_t n, unsigned long long *first, hipStream_t stream);
 

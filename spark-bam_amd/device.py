@@ -300,7 +300,8 @@ class Shard:
         if self.n_blocks:
             self._c(lib().sbh_get_blocks(self.h, 0, self.n_blocks, a.ctypes.data_as(C.c_void_p)))
         a = a[:self.n_blocks]
-        return {"start": a["start"], "ustart": a["ustart"], "usize": a["usize"].astype(np.uint64)}
+        return {"start": a["start"], "ustart": a["ustart"], "usize": a["usize"].astype(np.uint64),
+                "csize": a["csize"].astype(np.uint64), "flags": a["flags"]}
 
     def vpos_of_flat(self, flat):
         """Flat positions -> htsjdk virtual offsets over the block table (canonical: a position at
@@ -489,7 +490,7 @@ class Shard:
         return self._records_fetch(sz)
 
     def split_records(self, start, end, bgzf_blocks_to_check=5, reads_to_check=10, max_read_size=100000000,
-                      decode=True):
+                      decode=True, flat_out=None):
         """One FileSplit of loadReadsAndPositions in one call (sbh_split_records): FindBlockStart,
         index + inflate, the eager check over [Pos(blockStart, 0), Pos(end, 0)), FindRecordStart
         and the split's records.  Returns (info dict, columns): all columns when decode, else
@@ -502,11 +503,12 @@ class Shard:
         self.n_blocks, self.flat_size = r.n_blocks, r.flat_size  # (the index the call built: blocks())
         if decode:
             return info, self._records_fetch(r.sizes)
-        flat = np.empty(r.sizes.n, np.uint64)
+        # flat_out(n) (optional): where the starts land (e.g. page-locked memory); copied to a fresh array
+        flat = np.empty(r.sizes.n, np.uint64) if flat_out is None else flat_out(r.sizes.n)
         if r.sizes.n:
             out = SbhRecordsOut(flat=flat.ctypes.data)
             self._c(lib().sbh_records_fetch(self.h, C.byref(out)))
-        return info, {"flat": flat}
+        return info, {"flat": flat if flat_out is None else flat.copy()}
 
     def _records_fetch(self, sz):
         cols = record_columns(sz.n, sz.name_bytes, sz.cigar_ops, sz.bases, sz.aux_bytes)

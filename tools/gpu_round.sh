@@ -11,6 +11,7 @@
 #   bash tools/gpu_round.sh pmc TAG ARGS...        counter passes (tools/pmc_collect.sh) over bench.py ARGS
 #   bash tools/gpu_round.sh trace TAG              kernel-trace timeline of 8 bench steps + idle gaps
 #   bash tools/gpu_round.sh ftrace TAG LASTMS ARGS...  kernel-trace of bench.py ARGS, idle gaps of its last LASTMS ms
+#   bash tools/gpu_round.sh abenv TAG "ENV_A" "ENV_B" ARGS...  bench.py ABAB of an environment toggle
 #   bash tools/gpu_round.sh allpos TAG GIB ARGS...  check-bam -s over configs[2]'s one GIB-GiB file
 #                                                  (tools/allpos_configC.py: a 2 GiB rehearsal first)
 set -o pipefail
@@ -75,6 +76,10 @@ ftrace)
     > gpurun_out/${T}_ftrace.json 2> gpurun_out/${T}_ftrace.err || exit 12
   cp "$(find /tmp/${T}_ft -name '*.db' -print -quit)" gpurun_out/${T}_ftrace.db
   python3 tools/prof_gaps.py gpurun_out/${T}_ftrace.db --last-ms $L --top 30 > gpurun_out/${T}_fgaps.log 2>&1
+  ;;
+abenv)
+  # bench.py A/B of an environment toggle: abenv TAG "ENV_A" "ENV_B" ARGS...
+  timeout -k 10 1500 bash tools/ab_env.sh "$T" "$@" || exit 13
   ;;
 allpos)
   G=$1; shift
