@@ -418,6 +418,9 @@ typedef struct {
   char *seq;                                               /* [bases] "=ACMGRSVTWYHKDBN" letters */
   uint8_t *qual;                                           /* [bases] phred (0xff: absent) */
   uint8_t *aux;                                            /* [aux_bytes] tags as stored */
+  uint64_t *vpos;                                          /* [n] record start as an htsjdk virtual
+                                                              position (canonical Pos, Pos.scala:12-43);
+                                                              available after sbh_split_records too */
 } sbh_records_out;
 int sbh_records_scan(sbh_shard *sh, uint64_t first_flat, uint64_t end_flat, sbh_records_sizes *out);
 int sbh_records_fetch(sbh_shard *sh, const sbh_records_out *out);

@@ -120,7 +120,7 @@ object Native {
                            maxReadSize: Int, decode: Boolean, out: Array[Long]): Unit
   /** out = {nRecords, nameBytes, cigarOps, bases, auxBytes} */
   @native def recordsScan(ctx: Long, sh: Long, first: Long, endFlat: Long, out: Array[Long]): Unit
-  /** 18 direct buffers in sbh_records_out order, sized from recordsScan's `sizes` */
+  /** 18 (or 19, + vpos) direct buffers in sbh_records_out order, sized from recordsScan's `sizes` */
   @native def recordsFetch(ctx: Long, sh: Long, sizes: Array[Long], columns: Array[ByteBuffer]): Unit
   /** htsjdk-rewrite's BGZF writer (sbh_bgzf_compress_level; level 5 = htsjdk's bytes):
     * returns the file length written into `out` (capacity >= bgzfBound(n)). */
@@ -768,24 +768,16 @@ object GpuFindRecordStart {
 class GpuRecordIterator(shard: GpuShard, sizes: Array[Long], header: SAMFileHeader)
   extends Iterator[(Pos, SAMRecord)] {
   private val n = sizes(0).toInt
-  private val flats: Array[Long] = {
+  // the starts (flat) and their canonical Pos as htsjdk virtual positions, both computed on the
+  // device (sbh_records_out fields 0 and 18: a start at a block's end is Pos(next, 0))
+  private val (flats, vposs): (Array[Long], Array[Long]) = {
     val b = ByteBuffer.allocateDirect(math.max(8, 8 * n)).order(ByteOrder.LITTLE_ENDIAN)
-    val cols = new Array[ByteBuffer](18)  // only the "flat" column (sbh_records_out field 0)
+    val v = ByteBuffer.allocateDirect(math.max(8, 8 * n)).order(ByteOrder.LITTLE_ENDIAN)
+    val cols = new Array[ByteBuffer](19)
     cols(0) = b
+    cols(18) = v
     Native.recordsFetch(Device.ctx, shard.sh, sizes, cols)
-    Array.tabulate(n)(i ⇒ b.getLong(8 * i))
-  }
-  // the block table, for Pos of each start (canonical: a start at a block's end is Pos(next, 0))
-  private val (bStart, bUstart) = {
-    val t = shard.blocks(0, shard.numBlocks)
-    val live = (0 until shard.numBlocks.toInt).filter(i ⇒ t(6 * i + 4) > 0)
-    (live.map(i ⇒ t(6 * i)).toArray, live.map(i ⇒ t(6 * i + 1)).toArray)
-  }
-  private def posOf(f: Long): Pos = {
-    var k = java.util.Arrays.binarySearch(bUstart, f)
-    if (k < 0) k = -k - 2
-    else while (k + 1 < bUstart.length && bUstart(k + 1) == f) k += 1
-    Pos(bStart(k), (f - bUstart(k)).toInt)
+    (Array.tabulate(n)(i ⇒ b.getLong(8 * i)), Array.tabulate(n)(i ⇒ v.getLong(8 * i)))
   }
   // the bytes of [first record, end of the last record), read once
   private val (lo, raw) =
@@ -828,7 +820,7 @@ class GpuRecordIterator(shard: GpuShard, sizes: Array[Long], header: SAMFileHead
       raw.getInt(o + 28) + 1,           // mateCoordinate
       raw.getInt(o + 32),               // insertSize
       rest)
-    posOf(f) → rec
+    Pos(vposs(i - 1)) → rec
   }
 }
 

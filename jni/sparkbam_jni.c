@@ -503,8 +503,9 @@ JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_splitRecords(JNIE
 JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_recordsFetch(JNIEnv *env, jobject self, jlong ctx,
                                                                             jlong sh, jlongArray sizes,
                                                                             jobjectArray cols) {
-  /* 18 direct buffers in sbh_records_out field order, each checked against the bytes of its
-   * column for the sizes recordsScan returned ({n, nameBytes, cigarOps, bases, auxBytes}) */
+  /* 18 (or 19: + vpos) direct buffers in sbh_records_out field order, each checked against the
+   * bytes of its column for the sizes recordsScan returned ({n, nameBytes, cigarOps, bases,
+   * auxBytes}) */
   jlong z[5];
   if ((*env)->GetArrayLength(env, sizes) < 5) {
     throw_arg(env, "recordsFetch: sizes must hold recordsScan's 5 values");
@@ -512,16 +513,18 @@ JNIEXPORT void JNICALL Java_org_hammerlab_bam_gpu_Native_00024_recordsFetch(JNIE
   }
   (*env)->GetLongArrayRegion(env, sizes, 0, 5, z);
   const uint64_t n = (uint64_t)z[0], nm = (uint64_t)z[1], cg = (uint64_t)z[2], bs = (uint64_t)z[3], ax = (uint64_t)z[4];
-  const uint64_t need[18] = {8 * n, 4 * n, 4 * n, 4 * n, 4 * n, 4 * n, 2 * n, 2 * n, n, 8 * (n + 1), 8 * (n + 1),
-                             8 * (n + 1), 8 * (n + 1), nm, 4 * cg, bs, bs, ax};
-  void *p[18];
+  const uint64_t need[19] = {8 * n, 4 * n, 4 * n, 4 * n, 4 * n, 4 * n, 2 * n, 2 * n, n, 8 * (n + 1), 8 * (n + 1),
+                             8 * (n + 1), 8 * (n + 1), nm, 4 * cg, bs, bs, ax, 8 * n};
+  void *p[19] = {NULL};
+  const jsize ncols = (*env)->GetArrayLength(env, cols) < 19 ? 18 : 19;
   int bad = 0;
-  for (jsize i = 0; i < 18 && !bad; ++i) p[i] = direct_n(env, (*env)->GetObjectArrayElement(env, cols, i), need[i], &bad);
+  for (jsize i = 0; i < ncols && !bad; ++i)
+    p[i] = direct_n(env, (*env)->GetObjectArrayElement(env, cols, i), need[i], &bad);
   if (bad) return;
   sbh_records_out o = {(uint64_t *)p[0], (int32_t *)p[1],  (int32_t *)p[2],  (int32_t *)p[3],  (int32_t *)p[4],
                        (int32_t *)p[5],  (uint16_t *)p[6], (uint16_t *)p[7], (uint8_t *)p[8],  (uint64_t *)p[9],
                        (uint64_t *)p[10], (uint64_t *)p[11], (uint64_t *)p[12], (char *)p[13], (uint32_t *)p[14],
-                       (char *)p[15], (uint8_t *)p[16], (uint8_t *)p[17]};
+                       (char *)p[15], (uint8_t *)p[16], (uint8_t *)p[17], (uint64_t *)p[18]};
   failed(env, ctx, sbh_records_fetch(SH(sh), &o));
 }
 

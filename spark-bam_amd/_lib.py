@@ -102,7 +102,7 @@ class SbhSplitRecordsResult(C.Structure):
 class SbhRecordsOut(C.Structure):  # host buffers (sbh_records_out); NULL = not copied
     _fields_ = [(f, C.c_void_p) for f in (
         "flat", "ref_id", "pos", "next_ref_id", "next_pos", "tlen", "flag", "bin", "mapq",
-        "name_off", "cigar_off", "seq_off", "aux_off", "names", "cigar", "seq", "qual", "aux")]
+        "name_off", "cigar_off", "seq_off", "aux_off", "names", "cigar", "seq", "qual", "aux", "vpos")]
 
 
 class SparkBamError(RuntimeError):

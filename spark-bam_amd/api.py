@@ -196,7 +196,6 @@ def load_reads(path_or_bytes, ctx=None, reads_to_check=DEFAULT_READS_TO_CHECK, w
                 break
         sh.check_eager(L.header_end, end, reads_to_check, want_bits=False)
         cols = sh.records(L.header_end, end)
-        cols["vpos"] = _vpos_of(cols["flat"], sh.blocks())
         return Reads(cols, L.names)
     finally:
         L.close()
@@ -260,7 +259,6 @@ def iter_reads(path_or_bytes, window=None, halo=4 << 20, ctx=None, reads_to_chec
                 finally:
                     sh.close()
             if cols is not None and cols["flat"].size:
-                cols["vpos"] = _vpos_of(cols["flat"], blocks)  # (flat: window-relative)
                 yield Reads(cols, names)
             if last:
                 return

@@ -22,7 +22,7 @@ from .api import (DEFAULT_BGZF_BLOCKS_TO_CHECK, DEFAULT_MAX_READ_SIZE, DEFAULT_R
                   file_splits)
 from .api import DEFAULT_SPLIT_SIZE as DEFAULT_MAX_SPLIT_SIZE
 from .device import Context, PinnedBuffer
-from .intervals import (DEFAULT_COMPRESSION_RATIO, _flat_of_pos, _vpos_of_flat, capped_cost_groups, chunk_size,
+from .intervals import (DEFAULT_COMPRESSION_RATIO, _flat_of_pos, capped_cost_groups, chunk_size,
                         get_interval_chunks, parse_loci, read_bai)
 from .intervals import DEFAULT_SPLIT_SIZE
 from .records import Reads, record_columns
@@ -105,8 +105,7 @@ class SplitWorker:
                     raise
                 halo *= 4
                 continue
-            cols["vpos"] = sh.vpos_of_flat(cols["flat"]) if cols["flat"].size else np.zeros(0, np.uint64)
-            self.last = info
+            self.last = info  # (cols["vpos"]: the starts' virtual positions, from the device)
             return cols
 
     def _flat_buf(self, n):
@@ -187,7 +186,6 @@ def split_partition_calls(ctx, read, size, path, start, end, contigs, bgzf_block
                 return _empty()
             sh.check_eager(0, owned, reads_to_check, want_bits=False)
             cols = sh.records(first, owned)
-            cols["vpos"] = _vpos_of_flat(sh.blocks(), cols["flat"]) if cols["flat"].size else np.zeros(0, np.uint64)
             return cols
         except SparkBamError as e:
             if e.code not in (SBH_E_NEED_HALO, SBH_E_NOT_FOUND, SBH_E_BAD_RECORD) or end + halo >= size:
@@ -313,8 +311,6 @@ def intervals_partition(ctx, read, size, chunks, intervals, contigs, reads_to_ch
                 if max(fe) > min(fb):
                     sh.check_eager(min(fb), max(fe), reads_to_check, want_bits=False)
                 cols = sh.records_regions(list(zip(fb, fe)), intervals)
-                cols["vpos"] = _vpos_of_flat(sh.blocks(), cols["flat"]) if cols["flat"].size \
-                    else np.zeros(0, np.uint64)
                 out.append(cols)
                 break
             except SparkBamError as e:

@@ -2642,7 +2642,10 @@ __device__ __forceinline__ void chase8_asm(uint32_t (&c)[8], uint32_t pend, uint
 #define SBH_LZ_WAVES_PER_EU (SBH_LZ_RING ? 6 : 4)  // (the register budget: 512 VGPRs / waves per SIMD)
 #endif
 #ifndef SBH_LZ_SIEVE
-#define SBH_LZ_SIEVE 1  // k_lz leaves k_eager's first filter as a bitmap (launch_lz's sieve)
+// 1: k_lz leaves k_eager's first filter as a bitmap (launch_lz's sieve; run with SBH_SIEVE=1).
+// Measured and not kept: k_eager -0.55 ms, k_lz +0.95 ms on config B -- the
+// filter's ~180 vector instructions per 16-byte granule are issue time k_lz does not have spare
+#define SBH_LZ_SIEVE 0
 #endif
 // k_eager's first filter at the 16 positions of a granule: eager.Checker reads refID, pos, next
 // refID and next pos first (PosChecker.getRefPosError, check/.../PosChecker.scala:43-63; the

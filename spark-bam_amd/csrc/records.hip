@@ -183,6 +183,25 @@ __global__ void k_compact_u64(const uint64_t *in, const uint64_t *keep, const ui
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n && keep[i]) out[kpre[i]] = in[i];
 }
+
+// Record start (flat) -> htsjdk virtual position, canonical as Pos is (bgzf/.../Pos.scala,
+// UncompressedBytes.curPos): the LAST block of the chain whose first flat byte is <= the start,
+// so a start at a block's end is Pos(next block, 0); empty blocks (usize 0) hold no position.
+__global__ void k_rec_vpos(const uint64_t *pos, uint64_t n, const uint64_t *ustart, const uint64_t *cstart,
+                           const uint32_t *usize, uint64_t nblocks, uint64_t file_off, uint64_t *vpos) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t f = pos[i];
+  uint64_t lo = 0, hi = nblocks;  // first block with ustart > f
+  while (lo < hi) {
+    const uint64_t m = (lo + hi) / 2;
+    if (ustart[m] <= f) lo = m + 1;
+    else hi = m;
+  }
+  uint64_t k = lo ? lo - 1 : 0;
+  while (k > 0 && usize[k] == 0) --k;
+  vpos[i] = (file_off + cstart[k]) << 16 | (f - ustart[k]);
+}
 }  // namespace
 
 namespace {
@@ -279,6 +298,14 @@ hipError_t launch_compact_u64(const uint64_t *in, const uint64_t *keep, const ui
                               uint64_t *out, hipStream_t st) {
   if (!n) return hipSuccess;
   hipLaunchKernelGGL(k_compact_u64, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, in, keep, kpre, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_rec_vpos(const uint64_t *pos, uint64_t n, DevBlocks bl, uint64_t nblocks, uint64_t file_off,
+                           uint64_t *vpos, hipStream_t st) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_rec_vpos, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, pos, n, bl.ustart, bl.cstart,
+                     bl.usize, nblocks, file_off, vpos);
   return hipGetLastError();
 }
 

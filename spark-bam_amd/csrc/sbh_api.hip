@@ -214,7 +214,7 @@ struct sbh_shard {
   DBuf<uint64_t> xq;  // long-record eager candidates for the wave-cooperative exact pass
   // record field extraction (sbh_records_scan / fetch): positions, sizes -> offsets, columns
   struct Recs {
-    DBuf<uint64_t> pos, wcnt, wpre, nm, cg, sq, ax, nmo, cgo, sqo, axo, keep, kpre, pos2;
+    DBuf<uint64_t> pos, wcnt, wpre, nm, cg, sq, ax, nmo, cgo, sqo, axo, keep, kpre, pos2, vpos;
     DBuf<int64_t> iv_b, iv_e;
     DBuf<int32_t> iv_ref;
     DBuf<int32_t> ref_id, p0, nref, npos, tlen;
@@ -226,7 +226,8 @@ struct sbh_shard {
     bool valid = false;
     bool decoded = false;  // the columns were decoded (else only the starts, sbh_split_records decode = 0)
     void release() {
-      for (auto *b : {&pos, &wcnt, &wpre, &nm, &cg, &sq, &ax, &nmo, &cgo, &sqo, &axo, &keep, &kpre, &pos2}) b->release();
+      for (auto *b : {&pos, &wcnt, &wpre, &nm, &cg, &sq, &ax, &nmo, &cgo, &sqo, &axo, &keep, &kpre, &pos2, &vpos})
+        b->release();
       iv_b.release(); iv_e.release(); iv_ref.release();
       for (auto *b : {&ref_id, &p0, &nref, &npos, &tlen}) b->release();
       flag.release(); bin.release(); mapq.release(); qual.release(); aux.release();
@@ -912,10 +913,11 @@ static int inflate_status(sbh_shard *sh, hipStream_t st, uint64_t *bad_block, co
                    (unsigned long long)b.start);
 }
 
-// SBH_SIEVE=0: k_eager sweeps refIDs itself (k_lz leaves no sieve), for A/B
+// SBH_SIEVE=1 (with k_lz built -DSBH_LZ_SIEVE=1): k_lz leaves k_eager's first filter as a bitmap
+// (measured slower, DESIGN.md §10: off by default; k_eager sweeps refIDs itself)
 static bool sieve_on() {
   const char *e = std::getenv("SBH_SIEVE");
-  return !(e && e[0] == '0');
+  return e && e[0] == '1';
 }
 // The sieve k_lz fills for k_eager (launch_lz): one bit per flat position of the shard, plus the
 // look-ahead an eager window past the last tile reads (masked there); nullptr when off or when the
@@ -2587,6 +2589,11 @@ int sbh_records_fetch(sbh_shard *sh, const sbh_records_out *o) {
   int rc = set_device(ctx);
   if (rc) return rc;
   const uint64_t n = R.sz.n;
+  if (o->vpos && n) {  // the starts' virtual positions, computed on the device from the block table
+    HIPCHK(ctx, R.vpos.ensure(n));
+    HIPCHK(ctx, launch_rec_vpos(R.pos.p, n, sh->dev_blocks(), sh->nblocks, sh->file_off, R.vpos.p, sh->st));
+    HIPCHK(ctx, hipMemcpyAsync(o->vpos, R.vpos.p, 8 * n, hipMemcpyDeviceToHost, sh->st));
+  }
   // (every column is copied on the shard's stream, then one wait)
   auto cp = [&](void *dst, const void *src, uint64_t bytes) -> hipError_t {
     return dst && bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, sh->st) : hipSuccess;

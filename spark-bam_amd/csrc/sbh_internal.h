@@ -153,6 +153,9 @@ hipError_t launch_region_keep(const uint8_t *U, const uint64_t *pos, uint64_t n,
                               hipStream_t st);
 hipError_t launch_compact_u64(const uint64_t *in, const uint64_t *keep, const uint64_t *kpre, uint64_t n,
                               uint64_t *out, hipStream_t st);
+// record starts (flat) -> htsjdk virtual positions over the device block table
+hipError_t launch_rec_vpos(const uint64_t *pos, uint64_t n, DevBlocks bl, uint64_t nblocks, uint64_t file_off,
+                           uint64_t *vpos, hipStream_t st);
 // BGZF footer CRC32 of every inflated, non-truncated block (crc.hip).
 hipError_t launch_block_crc(const uint8_t *comp, DevBlocks bl, uint64_t nblocks, const uint8_t *U,
                             unsigned long long *n_bad, unsigned long long *first_bad, hipStream_t st);

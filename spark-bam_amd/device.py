@@ -503,15 +503,20 @@ class Shard:
         self.n_blocks, self.flat_size = r.n_blocks, r.flat_size  # (the index the call built: blocks())
         if decode:
             return info, self._records_fetch(r.sizes)
-        # flat_out(n) (optional): where the starts land (e.g. page-locked memory); copied to a fresh array
-        flat = np.empty(r.sizes.n, np.uint64) if flat_out is None else flat_out(r.sizes.n)
-        if r.sizes.n:
-            out = SbhRecordsOut(flat=flat.ctypes.data)
+        # flat_out(n) (optional): where the starts and their virtual positions land (e.g. page-locked
+        # memory, 2 n u64); copied to fresh arrays
+        n = r.sizes.n
+        both = np.empty(2 * n, np.uint64) if flat_out is None else flat_out(2 * n)
+        if n:
+            out = SbhRecordsOut(flat=both.ctypes.data, vpos=both[n:].ctypes.data)
             self._c(lib().sbh_records_fetch(self.h, C.byref(out)))
-        return info, {"flat": flat if flat_out is None else flat.copy()}
+        if flat_out is None:
+            return info, {"flat": both[:n], "vpos": both[n:]}
+        return info, {"flat": both[:n].copy(), "vpos": both[n:].copy()}
 
     def _records_fetch(self, sz):
         cols = record_columns(sz.n, sz.name_bytes, sz.cigar_ops, sz.bases, sz.aux_bytes)
+        cols["vpos"] = np.empty(sz.n, np.uint64)  # (computed on the device from the block table)
         out = SbhRecordsOut(**{k: v.ctypes.data if v.size else None for k, v in cols.items()})
         self._c(lib().sbh_records_fetch(self.h, C.byref(out)))
         return cols

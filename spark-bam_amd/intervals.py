@@ -321,8 +321,6 @@ def load_bam_intervals(path, intervals, split_size=DEFAULT_SPLIT_SIZE,
                     if b > a:
                         sh.check_eager(a, b, reads_to_check, want_bits=False)
                     cols = sh.records_regions(fl, ivs)
-                    cols["vpos"] = _vpos_of_flat(sh.blocks(), cols["flat"]) if cols["flat"].size \
-                        else np.zeros(0, np.uint64)
                     batches.append(cols)
                     break
                 except SparkBamError as err:

@@ -121,3 +121,31 @@ def test_load_reads_windowed_header_only():
     for k in one.cols:
         assert win.cols[k].dtype == one.cols[k].dtype, k
         assert np.array_equal(win.cols[k], one.cols[k]), k
+
+
+@pytest.mark.parametrize("kind", ["short", "long", "adversarial"])
+def test_device_vpos_equals_host_mapping(kind):
+    """sbh_records_fetch's vpos column (k_rec_vpos: the last chain block whose first flat byte is
+    <= the start, empty blocks skipped) equals the host mapping over the block table (api._vpos_of)
+    and the oracle's canonical Pos -- records starting exactly at a block's end take Pos(next, 0)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tools"))
+    import synth
+    kw = {"short": dict(seed=0x5B4D0001, shape=0, level=6), "long": dict(seed=0x5B4D004C, shape=1, level=6),
+          "adversarial": dict(seed=0x5B4D00AD, shape=2, level=-1)}[kind]
+    data = synth.make_bam(synth.params(kw["seed"], shape=kw["shape"], level=kw["level"]),
+                          300 if kind == "long" else 20000)[0]
+    of = OracleFile(data)
+    with sb.Context(0) as ctx:
+        sh = ctx.shard(data)
+        sh.index(0)
+        sh.inflate()
+        sh.set_contigs(of.contig_len)
+        sh.check_eager(0, sh.flat_size, want_bits=False)
+        first, _ = sh.find_record_start(of.header_end)
+        cols = sh.records(first, sh.flat_size)
+        host = sb.api._vpos_of(cols["flat"], sh.blocks())
+        assert cols["vpos"].size > 0 and np.array_equal(cols["vpos"], host)
+        oracle = [(lambda b, o: b << 16 | o)(*of.pos_of(int(f))) for f in cols["flat"][:2000]]
+        assert cols["vpos"][:2000].tolist() == oracle
+        sh.close()
