@@ -92,7 +92,7 @@ def main():
     ap.add_argument("--no-pin", action="store_true", help="--file-gib: pageable host memory for the rank's bytes")
     ap.add_argument("--no-facade", action="store_true",
                     help="skip the load-API facade side measurement (loadReadsAndPositions per 32 MiB split)")
-    ap.add_argument("--facade-threads", type=int, default=4,
+    ap.add_argument("--facade-threads", type=int, default=8,
                     help="concurrent task threads of the facade measurement (a Spark executor's cores)")
     ap.add_argument("--facade-modes", default="hbm,pinned_host,hbm_records,calls_r05",
                     help="facade modes to run (comma list; see facade_bench)")
@@ -719,6 +719,15 @@ def facade_bench(sb, ctx, comp, file_size, contig_len, threads, torch, run, spli
     t0 = time.perf_counter()
     w.split(read, "bench.bam", a, e, decode=False)
     out["one_split_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
+    # the same split's host-side phases, one thread: shard refill (device-to-device), the one
+    # library call, the starts + vpos copy-out
+    t0 = time.perf_counter()
+    sh = w.load(read, a, min(file_size, e + (1 << 20)))
+    t1 = time.perf_counter()
+    info, cols = sh.split_records(a, e, decode=False, flat_out=w._flat_buf)
+    t2 = time.perf_counter()
+    out["one_split_phases_ms"] = {"shard_load": round((t1 - t0) * 1e3, 3),
+                                  "split_records+fetch": round((t2 - t1) * 1e3, 3)}
     out["one_split_stages_ms"] = dict(zip(["index", "inflate+eager", "k_eager", "split/count", "k_huff", "k_lz"],
                                           [round(x, 3) for x in w.sh.stage_times()]))
     for ws in pools.values():

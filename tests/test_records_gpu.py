@@ -18,6 +18,7 @@ FIXTURES = ["2.bam", "1.bam", "5k.bam", "1.2203053-2211029.bam", "2.100-1000.bam
 
 
 def assert_cols_equal(got, want):
+    got = {k: v for k, v in got.items() if k in want or k != "vpos"}  # (the oracle decode has no vpos)
     assert set(got) == set(want)
     for k in want:
         assert got[k].dtype == want[k].dtype, k

@@ -25,11 +25,11 @@ round)
   timeout -k 10 300 python -u bench.py > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err || exit 2
   prof_env
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/${T}_bprof -o run -- python3 bench.py --steps 5 --warmup 2 \
-    --no-cpu-baseline --no-full --no-e2e > gpurun_out/${T}_bprof.json 2> gpurun_out/${T}_bprof.log || exit 3
+    --no-cpu-baseline --no-full --no-e2e --no-facade > gpurun_out/${T}_bprof.json 2> gpurun_out/${T}_bprof.log || exit 3
   python3 tools/prof_stats.py "$(find /tmp/${T}_bprof -name '*.db' -print -quit)" > gpurun_out/${T}_kernel_stats.csv || exit 3
-  timeout -k 10 300 python -u bench.py --config D --no-cpu-baseline --no-full --no-e2e > gpurun_out/${T}_benchD.json \
+  timeout -k 10 300 python -u bench.py --config D --no-cpu-baseline --no-full --no-e2e --no-facade > gpurun_out/${T}_benchD.json \
     2> gpurun_out/${T}_benchD.err || exit 4
-  timeout -k 10 300 python -u bench.py --config E --no-cpu-baseline --no-full --no-e2e > gpurun_out/${T}_benchE.json \
+  timeout -k 10 300 python -u bench.py --config E --no-cpu-baseline --no-full --no-e2e --no-facade > gpurun_out/${T}_benchE.json \
     2> gpurun_out/${T}_benchE.err || exit 5
   ;;
 tests)

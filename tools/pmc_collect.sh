@@ -5,7 +5,7 @@
 #   bash tools/pmc_collect.sh gpurun_out/pmc "--no-cpu-baseline --no-e2e --steps 2 --warmup 1"
 set -euo pipefail
 OUT=${1:-gpurun_out/pmc}
-ARGS=${2:---no-cpu-baseline --no-e2e --steps 2 --warmup 1}
+ARGS=${2:---no-cpu-baseline --no-e2e --no-facade --steps 2 --warmup 1}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 cd - > /dev/null
