@@ -1694,7 +1694,11 @@ __global__ __launch_bounds__(256) void k_verify_chain_w(const uint8_t *U, const 
                                                          uint64_t bits_end, uint64_t from, uint64_t E, uint64_t total,
                                                          unsigned long long *n_anom, unsigned long long *first_anom,
                                                          unsigned long long *exit_pos, unsigned long long *n_set,
-                                                         const TileSum *tsum, const unsigned long long *from_dev) {
+                                                         const TileSum *tsum, const unsigned long long *from_dev,
+                                                         uint32_t *chunk_cnt) {
+  // chunk_cnt (optional): the set bits of [from, E) per wave chunk of VC_CHUNK words, chunk k =
+  // words [VC_CHUNK k, VC_CHUNK (k + 1)) from `begin` (the chunks are aligned to that grid): the
+  // split counts (sbh_split_starts) then read the bitmap only at their ends
   // from_dev: the chain's first record as another kernel left it on the device (k_first_set's
   // answer; ~0: none, nothing to prove)
   if (from_dev) {
@@ -1703,7 +1707,7 @@ __global__ __launch_bounds__(256) void k_verify_chain_w(const uint8_t *U, const 
   }
   const uint32_t lane = threadIdx.x & (WAVE - 1);
   constexpr uint32_t TWORDS = EAGER_SUB / 32;  // bitmap words per summarised quarter tile (from `begin`)
-  const uint64_t W0 = (from - begin) / 32 & ~3ull;
+  const uint64_t W0 = (from - begin) / 32 / VC_CHUNK * VC_CHUNK;  // (chunk-aligned; earlier words are masked)
   const uint64_t w_end = (E - begin + 31) / 32;
   const uint64_t w_lim = (bits_end - begin + 31) / 32;
   const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / WAVE);
@@ -1732,6 +1736,12 @@ __global__ __launch_bounds__(256) void k_verify_chain_w(const uint8_t *U, const 
     }
     const uint32_t cnt = __popc(v[0]) + __popc(v[1]) + __popc(v[2]) + __popc(v[3]);
     tot += cnt;
+    if (chunk_cnt) {  // (a wave chunk is VC_CHUNK words: its sum by one lane)
+      uint32_t cs = cnt;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) cs += __shfl_xor(cs, off, WAVE);
+      if (lane == 0) chunk_cnt[wave_w0 / VC_CHUNK] = cs;
+    }
     // a tile wholly inside [from, E) with a summary: its own pairs were checked by k_eager (their
     // anomalies added once, by the lane of its first word); only its last true position's step
     // is needed, from the summary, not from U
@@ -2242,12 +2252,12 @@ hipError_t launch_verify_chain_count(const uint8_t *U, const uint32_t *bits, uin
                                      uint64_t from, uint64_t E, uint64_t total, unsigned long long *n_anom,
                                      unsigned long long *first_anom, unsigned long long *exit_pos,
                                      unsigned long long *n_set, const TileSum *tsum, hipStream_t st,
-                                     const unsigned long long *from_dev) {
+                                     const unsigned long long *from_dev, uint32_t *chunk_cnt) {
   if (E <= from) return hipSuccess;  // (with from_dev: from is a lower bound of *from_dev)
-  const uint64_t nw = (E - begin + 31) / 32 - ((from - begin) / 32 & ~3ull);
+  const uint64_t nw = (E - begin + 31) / 32 - (from - begin) / 32 / VC_CHUNK * VC_CHUNK;
   const uint32_t grid = (uint32_t)std::min<uint64_t>(ngrid(nw, 1024), 2048);
   hipLaunchKernelGGL(k_verify_chain_w, dim3(grid), dim3(256), 0, st, U, bits, begin, bits_end, from, E, total,
-                     n_anom, first_anom, exit_pos, n_set, tsum, from_dev);
+                     n_anom, first_anom, exit_pos, n_set, tsum, from_dev, chunk_cnt);
   return hipGetLastError();
 }
 

@@ -82,7 +82,7 @@ hipError_t launch_verify_chain_count(const uint8_t *U, const uint32_t *bits, uin
                                      uint64_t from, uint64_t E, uint64_t total, unsigned long long *n_anom,
                                      unsigned long long *first_anom, unsigned long long *exit_pos,
                                      unsigned long long *n_set, const TileSum *tsum, hipStream_t st,
-                                     const unsigned long long *from_dev = nullptr);
+                                     const unsigned long long *from_dev = nullptr, uint32_t *chunk_cnt = nullptr);
 hipError_t launch_chain_walk(const uint8_t *U, uint64_t first, uint64_t E, uint64_t total,
                              unsigned long long *count, unsigned long long *last, hipStream_t st);
 }  // namespace sbh
@@ -196,6 +196,10 @@ struct sbh_shard {
   // the bitmap verified equal to the record chain over [chain_first, chain_E) (k_verify_chain)
   bool chain_ok = false;
   uint64_t chain_first = 0, chain_E = 0;
+  // that proof's set bits per VC_CHUNK bitmap words (chunk k = words [VC_CHUNK k, ...) from
+  // bits_begin), valid with chain_ok for the same range (cc_ok): the split counts' inner chunks
+  DBuf<uint32_t> cc;
+  bool cc_ok = false;
   bool bits_valid = false;
   uint64_t bits_begin = 0, bits_end = 0;
   uint64_t run_first = ~0ull;  // sbh_run_shard's first record (flat), ~0: none found
@@ -503,6 +507,7 @@ int sbh_shard_destroy(sbh_shard *sh) {
   sh->tmp.release(); sh->J0.release(); sh->J1.release(); sh->on.release(); sh->d_seg.release();
   sh->U.release(); sh->ctg.release(); sh->bits.release(); sh->words.release(); sh->close_pos.release();
   sh->close_word.release(); sh->ctr.release(); sh->opix.release(); sh->tsum.release(); sh->sieve.release();
+  sh->cc.release();
   sh->comp2.release(); sh->aux2.release();
   for (hipStream_t st : sh->pf_stream) (void)hipStreamDestroy(st);
   for (uint8_t *p : sh->pf_pin) (void)hipHostFree(p);
@@ -911,6 +916,12 @@ static int inflate_status(sbh_shard *sh, hipStream_t st, uint64_t *bad_block, co
   if (*hs == INF_BAD_ISIZE) return fail(ctx, SBH_E_BAD_ISIZE, "block %llu: ISIZE %u", (unsigned long long)b.start, b.usize);
   return fail_with(ctx, SBH_E_INFLATE_DATA, {(int64_t)b.start}, "block %llu: invalid deflate data",
                    (unsigned long long)b.start);
+}
+
+// SBH_SPLIT_CC=0: split counts by a popcount of each split's whole bitmap range (A/B)
+static bool split_cc_on() {
+  const char *e = std::getenv("SBH_SPLIT_CC");
+  return !(e && e[0] == '0');
 }
 
 // SBH_SIEVE=1 (with k_lz built -DSBH_LZ_SIEVE=1): k_lz leaves k_eager's first filter as a bitmap
@@ -1353,16 +1364,19 @@ static int count_records_impl(sbh_shard *sh, uint64_t first, uint64_t E, uint64_
     init[3] = ~0ull;
     if (!known) {
       HIPCHK(ctx, hipMemcpyAsync(c, init, 32, hipMemcpyHostToDevice, st));
+      HIPCHK(ctx, sh->cc.ensure((sh->bits_end - sh->bits_begin + 31) / 32 / VC_CHUNK + 2));
       // verify bitmap == chain and count the set bits in one pass (k_verify_chain_w: wave-
       // cooperative successors, so sparse bitmaps of long records cost no word-by-word scans)
       HIPCHK(ctx, launch_verify_chain_count(sh->U.p, sh->bits.p, sh->bits_begin, sh->bits_end, first, E, total, c,
-                                            c + 1, c + 3, c + 2, tsum_on() ? sh->tsum.p : nullptr, st));
+                                            c + 1, c + 3, c + 2, tsum_on() ? sh->tsum.p : nullptr, st, nullptr,
+                                            sh->cc.p));
       HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 16, c, 32, hipMemcpyDeviceToHost, st));
       HIPCHK(ctx, hipStreamSynchronize(st));
     }
     const uint64_t n = sh->h_ctr[18];
     if (sh->h_ctr[16] == 0 && sh->h_ctr[19] != ~0ull) {
       sh->chain_ok = true;
+      sh->cc_ok = true;  // (this proof's chunk counts, or the run's tail proof's over the same range)
       sh->chain_first = first;
       sh->chain_E = E;
       *count = n;
@@ -1558,8 +1572,12 @@ int sbh_split_starts(sbh_shard *sh, const uint64_t *starts, const uint64_t *ends
   HIPCHK(ctx, hipMemsetAsync(sh->sp_count.p, 0, 8 * n, st));
   if (dense) {
     HIPCHK(ctx, hipMemcpyAsync(sh->sp_code.p, code.data(), 4 * n, hipMemcpyHostToDevice, st));
-    HIPCHK(ctx, launch_split_popcount(sh->bits.p, sh->bits_begin, sh->sp_first.p, sh->sp_E.p, sh->sp_code.p, n, span,
-                                      sh->sp_count.p, st));
+    if (sh->cc_ok && split_cc_on())  // the proof's chunk counts: the bitmap read only at the ranges' ends
+      HIPCHK(ctx, launch_split_count_cc(sh->bits.p, sh->bits_begin, sh->cc.p, sh->sp_first.p, sh->sp_E.p,
+                                        sh->sp_code.p, n, sh->sp_count.p, st));
+    else
+      HIPCHK(ctx, launch_split_popcount(sh->bits.p, sh->bits_begin, sh->sp_first.p, sh->sp_E.p, sh->sp_code.p, n,
+                                        span, sh->sp_count.p, st));
   } else if (marked) {
     HIPCHK(ctx, hipMemcpyAsync(sh->sp_code.p, code.data(), 4 * n, hipMemcpyHostToDevice, st));
     HIPCHK(ctx, launch_split_cm_count(sh->cm_pos.p, sh->cm_mark.p, sh->cm_mpre.p, sh->cm_n, sh->sp_first.p,
@@ -1892,6 +1910,7 @@ int sbh_run_shard(sbh_shard *sh, uint64_t index_start, uint64_t own_end_file, in
   const uint64_t E0 = std::min(E, total0);
   unsigned long long *tbest = sh->ctr.p + 8, *tc = sh->ctr.p + 16;
   bool tail = rtc >= 0 && hi0 > 0;
+  if (tail && sh->cc.ensure((E + 31) / 32 / VC_CHUNK + 2) != hipSuccess) tail = false;
   auto tail_launch = [&](hipStream_t s) -> hipError_t {
     unsigned long long *init = sh->h_ctr + 600;  // pinned: anomalies, first anomaly, set bits, exit
     init[0] = 0;
@@ -1903,7 +1922,7 @@ int sbh_run_shard(sbh_shard *sh, uint64_t index_start, uint64_t own_end_file, in
     if (e == hipSuccess) e = hipMemcpyAsync(tc, init, 32, hipMemcpyHostToDevice, s);
     if (e == hipSuccess)
       e = launch_verify_chain_count(sh->U.p, sh->bits.p, 0, E, 0, E0, total0, tc, tc + 1, tc + 3, tc + 2, nullptr, s,
-                                    tbest);
+                                    tbest, sh->cc.p);
     if (e == hipSuccess) e = hipMemcpyAsync(sh->h_ctr + 8, tbest, 8, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipMemcpyAsync(sh->h_ctr + 16, tc, 32, hipMemcpyDeviceToHost, s);
     return e;
@@ -1924,6 +1943,7 @@ int sbh_run_shard(sbh_shard *sh, uint64_t index_start, uint64_t own_end_file, in
     if (first < E0 && sh->h_ctr[16] == 0 && sh->h_ctr[19] != ~0ull) {  // count_records_impl's proof, done
       sh->cm_valid = false;
       sh->chain_ok = true;
+      sh->cc_ok = true;
       sh->chain_first = first;
       sh->chain_E = E0;
       res->count = sh->h_ctr[18];

@@ -153,6 +153,13 @@ hipError_t launch_region_keep(const uint8_t *U, const uint64_t *pos, uint64_t n,
                               hipStream_t st);
 hipError_t launch_compact_u64(const uint64_t *in, const uint64_t *keep, const uint64_t *kpre, uint64_t n,
                               uint64_t *out, hipStream_t st);
+// the chain proof's chunk of bitmap words (k_verify_chain_w: one wave, 4 words per lane)
+constexpr uint64_t VC_CHUNK = 256;
+// split counts from the proof's per-chunk set-bit counts (splits.hip): counts[i] += set bits of
+// [first[i], E[i]) for the SPLIT_OK splits, the bitmap read only in each range's end chunks
+hipError_t launch_split_count_cc(const uint32_t *bits, uint64_t begin, const uint32_t *chunk_cnt, const uint64_t *first,
+                                 const uint64_t *E, const uint32_t *code, uint64_t nsplit, unsigned long long *counts,
+                                 hipStream_t st);
 // record starts (flat) -> htsjdk virtual positions over the device block table
 hipError_t launch_rec_vpos(const uint64_t *pos, uint64_t n, DevBlocks bl, uint64_t nblocks, uint64_t file_off,
                            uint64_t *vpos, hipStream_t st);

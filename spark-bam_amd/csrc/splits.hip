@@ -312,6 +312,43 @@ __global__ __launch_bounds__(TC_THREADS) void k_truth_compare(const uint32_t *eb
   }
 }
 
+
+// counts[i] += set bits of [first[i], E[i]) from the chain proof's per-chunk counts: the chunks
+// strictly inside the range (neither holds the range's first or last word) are summed, the
+// bitmap is popcounted only over the words before and after them.  One workgroup per split.
+__global__ __launch_bounds__(256) void k_split_count_cc(const uint32_t *bits, uint64_t begin, const uint32_t *cc,
+                                                        const uint64_t *first, const uint64_t *E, const uint32_t *code,
+                                                        uint64_t nsplit, unsigned long long *counts) {
+  const uint64_t i = blockIdx.x;
+  if (i >= nsplit || code[i] != SPLIT_OK) return;
+  const uint64_t from = first[i], to = E[i];
+  if (from >= to) return;
+  const uint64_t wa = (from - begin) / 32, wb = (to - begin + 31) / 32;  // words [wa, wb)
+  const uint64_t ca = wa / VC_CHUNK + 1, cb = (wb - 1) / VC_CHUNK;          // inner chunks [ca, cb)
+  uint32_t c = 0;
+  auto count = [&](uint64_t w) {
+    uint32_t v = bits[w];
+    const uint64_t p0 = begin + 32 * w;
+    if (p0 < from) v &= ~0u << (uint32_t)(from - p0);
+    if (p0 + 32 > to) v &= (to - p0) >= 32 ? ~0u : ((1u << (uint32_t)(to - p0)) - 1u);
+    c += __popc(v);
+  };
+  if (ca < cb) {
+    for (uint64_t k = ca + threadIdx.x; k < cb; k += 256) c += cc[k];
+    for (uint64_t w = wa + threadIdx.x; w < ca * VC_CHUNK; w += 256) count(w);
+    for (uint64_t w = cb * VC_CHUNK + threadIdx.x; w < wb; w += 256) count(w);
+  } else {
+    for (uint64_t w = wa + threadIdx.x; w < wb; w += 256) count(w);
+  }
+  __shared__ uint32_t part[256 / 64];
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x / 64] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long t = (unsigned long long)part[0] + part[1] + part[2] + part[3];
+    if (t) atomicAdd(&counts[i], t);
+  }
+}
 }  // namespace
 
 static inline uint32_t nblk(uint64_t n, uint32_t t) { return (uint32_t)((n + t - 1) / t); }
@@ -337,6 +374,17 @@ hipError_t launch_split_popcount(const uint32_t *bits, uint64_t begin, const uin
     hipLaunchKernelGGL(k_split_popcount, dim3((uint32_t)gx, (uint32_t)ns), dim3(256), 0, st, bits, begin, first + s0,
                        E + s0, code + s0, ns, counts + s0);
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_split_count_cc(const uint32_t *bits, uint64_t begin, const uint32_t *chunk_cnt, const uint64_t *first,
+                                 const uint64_t *E, const uint32_t *code, uint64_t nsplit, unsigned long long *counts,
+                                 hipStream_t st) {
+  if (!nsplit) return hipSuccess;
+  for (uint64_t s0 = 0; s0 < nsplit; s0 += 1u << 30)  // (grid.x holds 2^31 - 1 workgroups)
+    hipLaunchKernelGGL(k_split_count_cc, dim3((uint32_t)std::min<uint64_t>(nsplit - s0, 1u << 30)), dim3(256), 0, st,
+                       bits, begin, chunk_cnt, first + s0, E + s0, code + s0, std::min<uint64_t>(nsplit - s0, 1u << 30),
+                       counts + s0);
   return hipGetLastError();
 }
 
