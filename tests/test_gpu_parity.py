@@ -596,7 +596,9 @@ def test_shard_lifecycle_frees_hbm(ctx):
     memory where it was: every buffer a shard grows is released by sbh_shard_destroy (ADVICE r04:
     the eager tile-summary buffer was not)."""
     import ctypes as C
-    hip = C.CDLL("libamdhip64.so")
+    # the HIP runtime libsparkbam_hip.so itself links (torch, when imported earlier in the run,
+    # brings its own libamdhip64.so: a second runtime instance with no device state of ours)
+    hip = C.CDLL("libamdhip64.so.7")
     free, total = C.c_size_t(), C.c_size_t()
 
     def free_now():
