@@ -777,7 +777,7 @@ def latest_pmc(name):
 
 # The launches each timed stage's HIP events bracket: launch_huff is the k_hdr header pre-pass,
 # k_huff, the k_huff_tail finish of deferred final deflate blocks and the serial fallback.
-STAGE_KERNELS = {"k_huff": ("k_hdr", "k_huff", "k_huff_tail", "k_huff_serial")}
+STAGE_KERNELS = {"k_huff": ("k_hdr", "k_huff", "k_hdr_tail", "k_huff_tail", "k_huff_serial")}
 
 
 def stage_traffic(tj, dom):

@@ -2195,25 +2195,48 @@ __device__ __forceinline__ bool huff_serial_block(const DevBlocks &bl, uint64_t 
 #define SBH_HDR_WAVES 4
 #endif
 constexpr uint32_t HDR_WAVES = SBH_HDR_WAVES;  // blocks (one per wave) per k_hdr workgroup
+#ifndef SBH_TAIL_HDR
+#define SBH_TAIL_HDR 1  // the tails' headers decoded and tabled by k_hdr<true> between k_huff and k_huff_tail
+#endif
 
+// A tail's header record fits between its two leading words (tok[G + n1 ..]) and the end of the
+// block's token region; k_huff_tail reads it there, before any tail token is written over it.
+__device__ __forceinline__ bool tail_hdr_room(uint32_t n1, uint32_t usize) {
+  return SBH_TAIL_HDR && n1 <= usize && usize - n1 >= HDR_OUT_DW + 2;
+}
+
+// TAIL: the header of a tail k_huff left (INF_TAIL), at the bit its two leading words give --
+// the same record, in the same place, in the bit coordinates k_huff_tail decodes in (its stage
+// starts at the dword holding the tail's first bit).
+template <bool TAIL>
 __global__ __launch_bounds__(WAVE * HDR_WAVES) void k_hdr(const uint8_t *__restrict__ comp, DevBlocks bl,
                                                          uint64_t nblocks, uint32_t *__restrict__ tok) {
   __shared__ HdrSmem tw[HDR_WAVES];
   __shared__ uint32_t stagew[HDR_WAVES][HDR_STAGE_DW];
   const uint32_t lane = threadIdx.x & (WAVE - 1), wid = uni(threadIdx.x / WAVE);
   const uint64_t b = (uint64_t)blockIdx.x * HDR_WAVES + wid;  // waves work alone: no workgroup barriers
-  if (b >= nblocks || huff_serial_block(bl, b)) return;
+  if (b >= nblocks) return;
+  if (TAIL ? uni(bl.status[b]) != INF_TAIL : huff_serial_block(bl, b)) return;
   HdrSmem &t = tw[wid];
   uint32_t *stage = stagew[wid];
   const uint64_t cstart = bl.cstart[b];
   const uint32_t csize = bl.csize[b], hsize = bl.hsize[b], usize = bl.usize[b];
   const uint32_t data_len = csize - hsize - 8;
   const uint64_t dbyte = cstart + hsize;
-  const uint32_t skip = (uint32_t)(dbyte & 3) * 8;
-  const uint32_t limit = skip + data_len * 8;
-  const uint32_t ndw = min((limit + 31) / 32 + 2, HDR_STAGE_DW);
+  uint32_t skip = (uint32_t)(dbyte & 3) * 8;
+  uint32_t limit = skip + data_len * 8;
   // 64-bit byte address of the block's first deflate dword (no 32-bit dword index)
-  const uint32_t *g = reinterpret_cast<const uint32_t *>(comp + (dbyte & ~3ull));
+  const uint8_t *dbase = comp + (dbyte & ~3ull);
+  if (TAIL) {
+    const uint32_t n1 = uni(bl.ntok[b]);
+    if (!tail_hdr_room(n1, usize)) return;  // (k_huff_tail decodes this header itself)
+    const uint32_t p = uni(tok[bl.ustart[b] + n1]), pd = p >> 5;
+    dbase += 4ull * pd;
+    skip = p & 31;
+    limit -= 32 * pd;
+  }
+  const uint32_t ndw = min((limit + 31) / 32 + 2, HDR_STAGE_DW);
+  const uint32_t *g = reinterpret_cast<const uint32_t *>(dbase);
   for (uint32_t i = lane; i < ndw; i += WAVE) stage[i] = g[i];
   __builtin_amdgcn_wave_barrier();  // (a wave's LDS accesses complete in order)
   uint32_t *out = tok + bl.ustart[b] + usize - HDR_OUT_DW;
@@ -2423,16 +2446,31 @@ __global__ __launch_bounds__(TAIL_NT) void k_huff_tail(const uint8_t *__restrict
   const uint8_t *dbase = comp + (dbyte & ~3ull) + 4ull * pd;
   const uint32_t skip = p & 31, limit = limit0 - 32 * pd;
   const uint32_t ndw = (limit + 31) / 32 + 2;
+  // the tail's first header, from k_hdr<true> (same place and format as k_huff's first one)
+  const uint32_t *hd = tok + G + usize - HDR_OUT_DW;
+  const bool pre = tail_hdr_room(n1, usize) && uni(hd[HDR_STATUS]) == HDR_OK;
+  uint32_t pre_psym = 0, pre_last = 0;
+  if (pre) {
+    for (uint32_t i = tid; i < HDR_SENT; i += TAIL_NT) sm.t.tab[i] = hd[i];
+    for (uint32_t i = tid; i < 352; i += TAIL_NT) {  // sent[320] then pk[2][16]
+      const uint32_t v = hd[HDR_SENT + i];
+      if (i < 320) sm.t.sent[i] = v;
+      else sm.t.pk[(i - 320) >> 4][(i - 320) & 15] = v;
+    }
+    pre_psym = uni(hd[HDR_PSYM]);
+    pre_last = uni(hd[HDR_LAST]);
+  }
   uint32_t n2 = 0, rc;
   if (ndw <= TAIL_DW) {
     const uint32_t *g = reinterpret_cast<const uint32_t *>(dbase);
     for (uint32_t i = tid; i < ndw; i += TAIL_NT) sm.stage[i] = g[i];
     __syncthreads();
-    rc = inflate_par<true>(sm, dbase, skip, limit, usize - out1, tk, tid, lane, wid, n2, false, 0, 0, out1, false,
-                           nullptr, nullptr);
+    rc = inflate_par<true>(sm, dbase, skip, limit, usize - out1, tk, tid, lane, wid, n2, pre, pre_psym, pre_last, out1,
+                           false, nullptr, nullptr);
   } else {
-    rc = inflate_par<false>(sm, dbase, skip, limit, usize - out1, tk, tid, lane, wid, n2, false, 0, 0, out1, false,
-                            nullptr, nullptr);
+    __syncthreads();
+    rc = inflate_par<false>(sm, dbase, skip, limit, usize - out1, tk, tid, lane, wid, n2, pre, pre_psym, pre_last,
+                            out1, false, nullptr, nullptr);
   }
   if (tid == 0) {
     bl.status[b] = uni(rc) == PAR_OK ? INF_OK : INF_SERIAL;
@@ -3247,10 +3285,13 @@ hipError_t launch_huff(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, 
   hipLaunchKernelGGL(k_huff_serial<false>, dim3((uint32_t)grid), dim3(WAVES * WAVE), 0, stream, comp, blocks, nblocks,
                      tok);
 #else
-  hipLaunchKernelGGL(k_hdr, dim3((uint32_t)((nblocks + HDR_WAVES - 1) / HDR_WAVES)), dim3(WAVE * HDR_WAVES), 0, stream,
-                     comp, blocks, nblocks, tok);
+  const dim3 hdr_grid((uint32_t)((nblocks + HDR_WAVES - 1) / HDR_WAVES)), hdr_wg(WAVE * HDR_WAVES);
+  hipLaunchKernelGGL(k_hdr<false>, hdr_grid, hdr_wg, 0, stream, comp, blocks, nblocks, tok);
   hipLaunchKernelGGL(k_huff, dim3((uint32_t)nblocks), dim3(HT), 0, stream, comp, blocks, nblocks, tok);
 #if SBH_TAIL
+#if SBH_TAIL_HDR
+  hipLaunchKernelGGL(k_hdr<true>, hdr_grid, hdr_wg, 0, stream, comp, blocks, nblocks, tok);
+#endif
   hipLaunchKernelGGL(k_huff_tail, dim3((uint32_t)nblocks), dim3(TAIL_NT), 0, stream, comp, blocks, nblocks, tok);
 #endif
   const uint64_t grid = (nblocks + WAVES - 1) / WAVES;

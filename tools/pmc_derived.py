@@ -15,7 +15,7 @@ import sys
 def load(path):
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in csv.DictReader(open(path)):
-        m = re.search(r"(k_\w+)", r["Kernel_Name"])
+        m = re.search(r"(k_\w+)", r["Kernel_Name"].replace("k_hdr<true>", "k_hdr_tail"))
         if m:
             agg[m.group(1)][r["Counter_Name"]] += float(r["Counter_Value"])
     return agg

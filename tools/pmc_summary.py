@@ -13,7 +13,7 @@ def main(path):
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     ndisp = collections.defaultdict(set)
     for r in csv.DictReader(open(path)):
-        m = re.search(r"(k_\w+)", r["Kernel_Name"])
+        m = re.search(r"(k_\w+)", r["Kernel_Name"].replace("k_hdr<true>", "k_hdr_tail"))
         k = m.group(1) if m else r["Kernel_Name"][:40]
         agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
         ndisp[k].add(r["Dispatch_Id"])

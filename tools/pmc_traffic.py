@@ -26,7 +26,7 @@ def src_hash(d):
 def per_kernel(path):
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
-        m = re.search(r"(k_\w+)", r["Kernel_Name"])
+        m = re.search(r"(k_\w+)", r["Kernel_Name"].replace("k_hdr<true>", "k_hdr_tail"))
         if m:
             agg[m.group(1)].append(float(r["Counter_Value"]))
     return {k: sorted(v)[len(v) // 2] for k, v in agg.items()}
