@@ -396,6 +396,9 @@ constexpr uint32_t ESTAGE = EW + 512;     // staged bytes (records near the end 
 #define SBH_EQ_CHUNK 4096
 #endif
 constexpr uint32_t EQ_CHUNK = SBH_EQ_CHUNK;  // survivor-queue capacity
+#ifndef SBH_EAGER_SHIFT_SWEEP
+#define SBH_EAGER_SHIFT_SWEEP 1  // k_eager's refID sweep: tests shifted into each word (see k_eager)
+#endif
 static_assert(EAGER_REACH >= ESTAGE + 32 + 16, "EAGER_REACH covers the staged window");
 
 // PosChecker.getRefPosError with the contig length already loaded (len_idx: len[idx]
@@ -697,6 +700,17 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
   uint32_t msk[EMW];
 #pragma unroll
   for (uint32_t w = 0; w < EMW; ++w) msk[w] = 0;
+  // bit b of msk[w] <-> window index ib + 32 w + b; the bits a word keeps: in the window [0, EW),
+  // group < ngroups and < EG; from fast_end on every in-window position is kept (decided below)
+  const int32_t ib = (int32_t)(4 * g0) - (int32_t)sa;
+  const int32_t gl = 4 * ((int32_t)ngroups - (int32_t)g0);
+  auto upto = [](int32_t k) -> uint32_t { return k <= 0 ? 0u : k >= 32 ? ~0u : (1u << k) - 1u; };
+  auto word_keep = [&](uint32_t w, uint32_t m) -> uint32_t {
+    const int32_t i0 = ib + 32 * (int32_t)w;
+    const uint32_t in = ~upto(-i0) & upto((int32_t)EW - i0) & upto(gl - 32 * (int32_t)w) &
+                        upto(4 * (int32_t)EG - 32 * (int32_t)w);
+    return (m | ~upto((int32_t)fast_end - i0)) & in;
+  };
   if (o.sieve) {
     // k_lz evaluated this filter (and the next refID / pos signs) on the bytes in its LDS ring:
     // the thread's bits are the sieve's bits [s0 + 4 g0, + 4 EG), masked to the window, plus every
@@ -704,22 +718,35 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
     const uint64_t A = s0 + 4ull * g0;
     const uint32_t *sw = o.sieve + (A >> 5);
     const uint32_t sft = (uint32_t)(A & 31);
-    const int32_t ib = (int32_t)(4 * g0) - (int32_t)sa;  // window index of bit 0
-    const int32_t gl = 4 * ((int32_t)ngroups - (int32_t)g0);  // bits below this are groups < ngroups
     uint32_t lo_w = sw[0];
 #pragma unroll
     for (uint32_t w = 0; w < EMW; ++w) {
       const uint32_t hi_w = sw[w + 1];
-      uint32_t m = sft ? (lo_w >> sft) | (hi_w << (32 - sft)) : lo_w;
+      const uint32_t m = sft ? (lo_w >> sft) | (hi_w << (32 - sft)) : lo_w;
       lo_w = hi_w;
-      // bit b <-> window index ii = ib + 32 w + b: in the window [0, EW), its group < ngroups and
-      // < EG; from fast_end on every in-window position is kept
-      const int32_t i0 = ib + 32 * (int32_t)w;
-      auto upto = [](int32_t k) -> uint32_t { return k <= 0 ? 0u : k >= 32 ? ~0u : (1u << k) - 1u; };
-      const uint32_t in = ~upto(-i0) & upto((int32_t)EW - i0) & upto(gl - 32 * (int32_t)w) &
-                          upto(4 * (int32_t)EG - 32 * (int32_t)w);
-      m |= ~upto((int32_t)fast_end - i0);
-      msk[w] = m & in;
+      msk[w] = word_keep(w, m);
+    }
+  } else if (SBH_EAGER_SHIFT_SWEEP) {
+    // each word's 32 refID tests shifted into it last position first (m = 2 m + test: one
+    // add-with-carry per position, no per-position range logic); the word's range after
+    static_assert(EMW * 8 >= EG, "the words cover the thread's groups");
+#pragma unroll
+    for (uint32_t w = 0; w < EMW; ++w) {
+      constexpr uint32_t GW = 8;  // groups (of 4 positions) per word
+      uint32_t d[GW + 1];         // staged dwords g0 + 8 w + 1 .. + 9: bytes 4..7 of every position's record
+#pragma unroll
+      for (uint32_t j = 0; j <= GW; ++j) d[j] = 8 * w + j <= EG ? lds32[g0 + 8 * w + j + 1] : 0u;
+      uint32_t m = 0;
+#pragma unroll
+      for (int32_t j = GW - 1; j >= 0; --j) {
+        if (8 * w + (uint32_t)j >= EG) continue;
+#pragma unroll
+        for (int32_t k = 3; k >= 0; --k) {
+          const uint32_t ref = __builtin_amdgcn_alignbyte(d[j + 1], d[j], (uint32_t)k);
+          m = m + m + (ref + 1u < nref1 ? 1u : 0u);
+        }
+      }
+      msk[w] = word_keep(w, m);
     }
   } else {
     uint32_t a = lds32[g0 + 1];
