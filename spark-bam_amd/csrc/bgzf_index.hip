@@ -118,59 +118,76 @@ __device__ __forceinline__ bool cand_at(const uint8_t *comp, uint64_t n, uint64_
   return p >= from && p + 18 <= n && header_at(comp, p);
 }
 
+#ifndef SBH_CAND_CPW
+#define SBH_CAND_CPW 1  // chunks per k_cand_count workgroup (A/B r06o: 4 chunks, all loads in flight, index +0.045 ms on config B)
+#endif
+constexpr uint32_t CAND_CPW = SBH_CAND_CPW;
+
 __global__ __launch_bounds__(256) void k_cand_count(const uint8_t *comp, uint64_t n, uint64_t from,
-                                                     uint64_t *counts, uint32_t *first) {
-  __shared__ uint32_t c, f;
-  if (threadIdx.x == 0) { c = 0; f = ~0u; }
-  __syncthreads();
-  const uint64_t cbase = (uint64_t)blockIdx.x * CHUNK;
-  uint32_t mine = 0, myfirst = ~0u;
-  constexpr uint32_t NV = CHUNK / 4096;
-  // all of the thread's 16-byte loads in flight at once (whole chunks: no per-load test)
-  uint4 vv[NV];
-  if (cbase + CHUNK <= n) {
-#pragma unroll
-    for (uint32_t i = 0; i < NV; ++i)
-      vv[i] = *reinterpret_cast<const uint4 *>(comp + cbase + i * 4096 + threadIdx.x * 16);
-  } else {  // ragged end of the shard
-#pragma unroll
-    for (uint32_t i = 0; i < NV; ++i) {
-      const uint64_t p0 = cbase + i * 4096 + threadIdx.x * 16;
-      uint32_t w[4] = {0, 0, 0, 0};
-      for (uint32_t k = 0; k < 16 && p0 + k < n; ++k) w[k >> 2] |= (uint32_t)comp[p0 + k] << (8 * (k & 3));
-      vv[i] = make_uint4(w[0], w[1], w[2], w[3]);
-    }
+                                                     uint64_t *counts, uint32_t *first, uint64_t nchunks) {
+  __shared__ uint32_t c[CAND_CPW], f[CAND_CPW];
+  if (threadIdx.x < CAND_CPW) {
+    c[threadIdx.x] = 0;
+    f[threadIdx.x] = ~0u;
   }
+  __syncthreads();
+  constexpr uint32_t NV = CHUNK / 4096;
+  const uint64_t chunk0 = (uint64_t)blockIdx.x * CAND_CPW;
+  // all of the thread's 16-byte loads of every chunk in flight at once (whole chunks: no
+  // per-load test)
+  uint4 vv[CAND_CPW][NV];
 #pragma unroll
-  for (uint32_t i = 0; i < NV; ++i) {
-    const uint32_t o0 = i * 4096 + threadIdx.x * 16;
-    const uint64_t p0 = cbase + o0;
-    const uint4 v = vv[i];
-    // the whole 4-byte magic (31 139 8 4) is tested in registers where the vector holds it,
-    // so the header check's dependent loads run only for near-certain headers (and for a
-    // 31 in the vector's last 3 bytes), not for every 31 byte (1 in 256 of deflate data)
-    const uint32_t m31 = eq16(v, 0x1f1f1f1fu);
-    if (m31) {
-      const uint32_t mh = m31 & (eq16(v, 0x8b8b8b8bu) >> 1) & (eq16(v, 0x08080808u) >> 2) & (eq16(v, 0x04040404u) >> 3);
-      uint32_t mq = (mh & 0x1fffu) | (m31 & 0xe000u);
-      while (mq) {
-        const uint32_t k = __builtin_ctz(mq);
-        mq &= mq - 1;
-        if (cand_at(comp, n, from, p0 + k)) {
-          ++mine;
-          myfirst = min(myfirst, o0 + k);
-        }
+  for (uint32_t ci = 0; ci < CAND_CPW; ++ci) {
+    const uint64_t cbase = (chunk0 + ci) * CHUNK;
+    if (cbase + CHUNK <= n) {
+#pragma unroll
+      for (uint32_t i = 0; i < NV; ++i)
+        vv[ci][i] = *reinterpret_cast<const uint4 *>(comp + cbase + i * 4096 + threadIdx.x * 16);
+    } else {  // ragged end of the shard (or a chunk past it)
+#pragma unroll
+      for (uint32_t i = 0; i < NV; ++i) {
+        const uint64_t p0 = cbase + i * 4096 + threadIdx.x * 16;
+        uint32_t w[4] = {0, 0, 0, 0};
+        for (uint32_t k = 0; k < 16 && p0 + k < n; ++k) w[k >> 2] |= (uint32_t)comp[p0 + k] << (8 * (k & 3));
+        vv[ci][i] = make_uint4(w[0], w[1], w[2], w[3]);
       }
     }
   }
-  if (mine) {
-    atomicAdd(&c, mine);
-    atomicMin(&f, myfirst);
+#pragma unroll
+  for (uint32_t ci = 0; ci < CAND_CPW; ++ci) {
+    const uint64_t cbase = (chunk0 + ci) * CHUNK;
+    uint32_t mine = 0, myfirst = ~0u;
+#pragma unroll
+    for (uint32_t i = 0; i < NV; ++i) {
+      const uint32_t o0 = i * 4096 + threadIdx.x * 16;
+      const uint64_t p0 = cbase + o0;
+      const uint4 v = vv[ci][i];
+      // the whole 4-byte magic (31 139 8 4) is tested in registers where the vector holds it,
+      // so the header check's dependent loads run only for near-certain headers (and for a
+      // 31 in the vector's last 3 bytes), not for every 31 byte (1 in 256 of deflate data)
+      const uint32_t m31 = eq16(v, 0x1f1f1f1fu);
+      if (m31) {
+        const uint32_t mh = m31 & (eq16(v, 0x8b8b8b8bu) >> 1) & (eq16(v, 0x08080808u) >> 2) & (eq16(v, 0x04040404u) >> 3);
+        uint32_t mq = (mh & 0x1fffu) | (m31 & 0xe000u);
+        while (mq) {
+          const uint32_t k = __builtin_ctz(mq);
+          mq &= mq - 1;
+          if (cand_at(comp, n, from, p0 + k)) {
+            ++mine;
+            myfirst = min(myfirst, o0 + k);
+          }
+        }
+      }
+    }
+    if (mine) {
+      atomicAdd(&c[ci], mine);
+      atomicMin(&f[ci], myfirst);
+    }
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    counts[blockIdx.x] = c;
-    first[blockIdx.x] = f;
+  if (threadIdx.x < CAND_CPW && chunk0 + threadIdx.x < nchunks) {
+    counts[chunk0 + threadIdx.x] = c[threadIdx.x];
+    first[chunk0 + threadIdx.x] = f[threadIdx.x];
   }
 }
 
@@ -409,7 +426,8 @@ uint64_t cand_chunks(uint64_t n) { return (n + CHUNK - 1) / CHUNK; }
 
 hipError_t launch_cand_count(const uint8_t *comp, uint64_t n, uint64_t from, uint64_t *counts, uint32_t *first,
                              uint64_t nchunks, hipStream_t st) {
-  hipLaunchKernelGGL(k_cand_count, dim3((uint32_t)nchunks), dim3(256), 0, st, comp, n, from, counts, first);
+  const uint64_t grid = (nchunks + CAND_CPW - 1) / CAND_CPW;
+  if (grid) hipLaunchKernelGGL(k_cand_count, dim3((uint32_t)grid), dim3(256), 0, st, comp, n, from, counts, first, nchunks);
   return hipGetLastError();
 }
 hipError_t launch_cand_write(const uint8_t *comp, uint64_t n, uint64_t from, const uint64_t *counts,

@@ -3268,8 +3268,9 @@ __global__ void k_first_bad(const uint32_t *status, uint64_t n, unsigned long lo
 
 }  // namespace
 
-hipError_t launch_first_bad(const uint32_t *status, uint64_t n, unsigned long long *first, hipStream_t stream) {
-  hipError_t e = hipMemsetAsync(first, 0xff, sizeof(unsigned long long), stream);
+hipError_t launch_first_bad(const uint32_t *status, uint64_t n, unsigned long long *first, hipStream_t stream,
+                            bool init) {
+  hipError_t e = init ? hipMemsetAsync(first, 0xff, sizeof(unsigned long long), stream) : hipSuccess;
   if (e != hipSuccess || n == 0) return e;
   hipLaunchKernelGGL(k_first_bad, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, status, n, first);
   return hipGetLastError();

@@ -243,6 +243,11 @@ struct sbh_shard {
   DBuf<uint64_t> sp_start, sp_end, sp_first, sp_E, sp_vpos;
   DBuf<uint32_t> sp_code;
   DBuf<unsigned long long> sp_count;
+  // sbh_split_starts' fast path: [start, end, first, E, count] x n + code x n in one device
+  // buffer and its page-locked mirror (one copy each way)
+  DBuf<uint64_t> sp_pack;
+  uint64_t *sp_pin = nullptr;
+  uint64_t sp_pin_cap = 0;
   DBuf<uint32_t> tbits;
   DBuf<uint64_t> t_rb, t_re, t_fp, t_fn;
   // the next window prefetched by a host thread (shard_prefetch): spare compressed bytes and
@@ -526,6 +531,8 @@ int sbh_shard_destroy(sbh_shard *sh) {
     b->release();
   sh->sp_code.release();
   sh->sp_count.release();
+  sh->sp_pack.release();
+  if (sh->sp_pin) (void)hipHostFree(sh->sp_pin);
   sh->tbits.release();
   sh->cm_pos.release(); sh->cm_wcnt.release(); sh->cm_wpre.release(); sh->cm_mark.release(); sh->cm_mpre.release();
   sh->cm_j.release(); sh->cm_j2.release(); sh->cm_j0.release();
@@ -895,13 +902,20 @@ int sbh_get_blocks(sbh_shard *sh, uint64_t first, uint64_t count, sbh_block *out
 // After the inflate kernels on `st`: the first block whose status is not INF_OK decides the
 // error (the reference's exception for that block); 8 bytes come back, not every status.
 // `extra`/`extra_dst`/`extra_n` ride along in the same round trip.
+// whole_ctr: the caller set ctr[0, CTR_RUN_WORDS) from ctr_run_template (fb = ~0 included), and
+// those words all come back to h_ctr in one copy (the eager counters, the step tail's answers)
+constexpr uint32_t CTR_RUN_WORDS = 101;
 static int inflate_status(sbh_shard *sh, hipStream_t st, uint64_t *bad_block, const void *extra = nullptr,
-                          void *extra_dst = nullptr, size_t extra_n = 0) {
+                          void *extra_dst = nullptr, size_t extra_n = 0, bool whole_ctr = false) {
   sbh_ctx *ctx = sh->ctx;
   unsigned long long *fb = sh->ctr.p + 100;
-  HIPCHK(ctx, launch_first_bad(sh->b_status.p, sh->nblocks, fb, st));
-  HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 100, fb, 8, hipMemcpyDeviceToHost, st));
-  if (extra_n) HIPCHK(ctx, hipMemcpyAsync(extra_dst, extra, extra_n, hipMemcpyDeviceToHost, st));
+  HIPCHK(ctx, launch_first_bad(sh->b_status.p, sh->nblocks, fb, st, !whole_ctr));
+  if (whole_ctr) {
+    HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr, sh->ctr.p, CTR_RUN_WORDS * 8, hipMemcpyDeviceToHost, st));
+  } else {
+    HIPCHK(ctx, hipMemcpyAsync(sh->h_ctr + 100, fb, 8, hipMemcpyDeviceToHost, st));
+    if (extra_n) HIPCHK(ctx, hipMemcpyAsync(extra_dst, extra, extra_n, hipMemcpyDeviceToHost, st));
+  }
   HIPCHK(ctx, hipStreamSynchronize(st));
   const uint64_t i = sh->h_ctr[100];
   if (i == ~0ull) return SBH_OK;
@@ -1521,11 +1535,79 @@ int sbh_split_starts(sbh_shard *sh, const uint64_t *starts, const uint64_t *ends
     sh->bits_rtc = rtc;
     if (rc == SBH_E_NEED_HALO) sh->bits_end = std::min<uint64_t>(sh->utotal, sh->h_ctr[2]);
   }
+  auto rel_start = [&](uint64_t i) -> uint64_t {  // (a start off the shard: host path, flagged below)
+    return starts[i] < sh->file_off || starts[i] >= end_res ? 0 : starts[i] - sh->file_off;
+  };
+  auto rel_end = [&](uint64_t i) -> uint64_t { return ends[i] >= sh->file_off ? ends[i] - sh->file_off : 0; };
+  const SplitArgs a{sh->comp.p, sh->n, sh->at_eof ? 1 : 0, sh->cand.p, sh->ncand, sh->cand_from, k,
+                    sh->b_cstart.p, sh->b_ustart.p, sh->b_flags.p, sh->nblocks, sh->utotal,
+                    sh->hb.empty() ? 0 : sh->hb.back().start - sh->file_off, sh->d_seg.p,
+                    (uint32_t)sh->seg_end.size(), sh->bits.p, sh->bits_begin, sh->bits_end,
+                    (int64_t)std::max(mrs, 0)};
+  // Fast path (the step's case): the chain proof covers the splits and left its chunk counts.
+  // The ranges go over in one copy, the prologue and the counts run back to back, and
+  // [first, E, count, code] come back in one copy: one round trip.  A split whose range leaves
+  // the proven chain (SPLIT_NOCOUNT) sends the call down the general path below.
+  if (sh->chain_ok && sh->cc_ok && sh->chain_E > 0 && split_cc_on()) {
+    const uint64_t words = 5 * n + (n + 1) / 2;
+    if (sh->sp_pin_cap < words) {
+      if (sh->sp_pin) (void)hipHostFree(sh->sp_pin);
+      sh->sp_pin = nullptr;
+      sh->sp_pin_cap = 0;
+      HIPCHK(ctx, hipHostMalloc(reinterpret_cast<void **>(&sh->sp_pin), words * 8));
+      sh->sp_pin_cap = words;
+    }
+    HIPCHK(ctx, sh->sp_pack.ensure(words));
+    uint64_t *hp = sh->sp_pin, *dp = sh->sp_pack.p;
+    for (uint64_t i = 0; i < n; ++i) {
+      hp[i] = rel_start(i);
+      hp[n + i] = rel_end(i);
+    }
+    uint32_t *dcode = reinterpret_cast<uint32_t *>(dp + 5 * n);
+    HIPCHK(ctx, hipMemcpyAsync(dp, hp, 16 * n, hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, launch_split_prologue(a, dp, dp + n, n, dp + 2 * n, dp + 3 * n, dcode, st));
+    HIPCHK(ctx, launch_split_count_cc(sh->bits.p, sh->bits_begin, sh->cc.p, dp + 2 * n, dp + 3 * n, dcode, n,
+                                      reinterpret_cast<unsigned long long *>(dp + 4 * n), st, sh->chain_first,
+                                      sh->chain_E));
+    // (the same page-locked words: the stream runs the copy in after the copy out has read them)
+    HIPCHK(ctx, hipMemcpyAsync(hp + 2 * n, dp + 2 * n, (words - 2 * n) * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    const uint64_t *first = hp + 2 * n, *E = hp + 3 * n, *cnt = hp + 4 * n;
+    const uint32_t *code = reinterpret_cast<const uint32_t *>(hp + 5 * n);
+    bool all = true;
+    for (uint64_t i = 0; i < n && all; ++i)
+      all = !(code[i] == SPLIT_OK && starts[i] >= sh->file_off && starts[i] < end_res && first[i] < E[i] &&
+              cnt[i] == SPLIT_NOCOUNT);
+    if (all) {
+      uint64_t nh = 0;
+      for (uint64_t i = 0; i < n; ++i) {
+        const uint32_t ci = starts[i] < sh->file_off || starts[i] >= end_res ? SPLIT_HOST : code[i];
+        if (ci == SPLIT_OK) {
+          uint64_t bp = 0;
+          uint32_t off = 0;
+          rc = sbh_pos_of(sh, first[i], &bp, &off);
+          if (rc) return rc;
+          first_vpos[i] = (bp << 16) | off;
+          counts[i] = first[i] < E[i] ? cnt[i] : 0;
+          status[i] = SBH_OK;
+        } else if (ci == SPLIT_NOREAD) {
+          first_vpos[i] = counts[i] = 0;
+          status[i] = SBH_E_NO_READ_FOUND;
+        } else {
+          ++nh;
+          first_vpos[i] = counts[i] = 0;
+          // (sbh_split leaves sp_pin alone: first / E / cnt stay valid)
+          status[i] = sbh_split(sh, starts[i], ends[i], k, rtc, mrs, &first_vpos[i], &counts[i]);
+        }
+      }
+      if (n_host) *n_host = nh;
+      return SBH_OK;
+    }
+  }
   std::vector<uint64_t> rs(n), re(n);
   for (uint64_t i = 0; i < n; ++i) {
-    rs[i] = starts[i] >= sh->file_off ? starts[i] - sh->file_off : ~0ull;
-    re[i] = ends[i] >= sh->file_off ? ends[i] - sh->file_off : 0;
-    if (starts[i] < sh->file_off || starts[i] >= end_res) rs[i] = 0;  // host path (flagged below)
+    rs[i] = rel_start(i);
+    re[i] = rel_end(i);
   }
   HIPCHK(ctx, sh->sp_start.ensure(n));
   HIPCHK(ctx, sh->sp_end.ensure(n));
@@ -1535,11 +1617,6 @@ int sbh_split_starts(sbh_shard *sh, const uint64_t *starts, const uint64_t *ends
   HIPCHK(ctx, sh->sp_count.ensure(n));
   HIPCHK(ctx, hipMemcpyAsync(sh->sp_start.p, rs.data(), 8 * n, hipMemcpyHostToDevice, st));
   HIPCHK(ctx, hipMemcpyAsync(sh->sp_end.p, re.data(), 8 * n, hipMemcpyHostToDevice, st));
-  const SplitArgs a{sh->comp.p, sh->n, sh->at_eof ? 1 : 0, sh->cand.p, sh->ncand, sh->cand_from, k,
-                    sh->b_cstart.p, sh->b_ustart.p, sh->b_flags.p, sh->nblocks, sh->utotal,
-                    sh->hb.empty() ? 0 : sh->hb.back().start - sh->file_off, sh->d_seg.p,
-                    (uint32_t)sh->seg_end.size(), sh->bits.p, sh->bits_begin, sh->bits_end,
-                    (int64_t)std::max(mrs, 0)};
   HIPCHK(ctx, launch_split_prologue(a, sh->sp_start.p, sh->sp_end.p, n, sh->sp_first.p, sh->sp_E.p, sh->sp_code.p, st));
   std::vector<uint64_t> first(n), E(n);
   std::vector<uint32_t> code(n);
@@ -1755,13 +1832,21 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
   if (sh->nctg < 0) return fail(ctx, SBH_E_STATE, "contig lengths not set");
   if (rtc < 0 || rtc > 1023) return fail(ctx, SBH_E_ARG, "readsToCheck must be in [0, 1023]");
   hipStream_t sa = sh->st;
-  if (!sh->s_lz) HIPCHK(ctx, hipStreamCreateWithFlags(&sh->s_lz, hipStreamNonBlocking));
-  if (!sh->s_eg) HIPCHK(ctx, hipStreamCreateWithFlags(&sh->s_eg, hipStreamNonBlocking));
-  hipStream_t sl = sh->s_lz, se = sh->s_eg;
   HIPCHK(ctx, sh->U.ensure(sh->utotal + sh->pad));
   const uint64_t nb = sh->nblocks;
   const uint64_t npipe = std::max<uint64_t>(1, std::min<uint64_t>(PIPE_MAX_BATCHES, nb / pipe_min_blocks()));
   const TokPlan P = tok_plan(sh, (nb + npipe - 1) / std::max<uint64_t>(npipe, 1));
+  // one batch (the default): every launch on the shard's stream, no cross-stream event waits
+  // (each cost the step ~15 us of idle device between the stages)
+  hipStream_t sl = sa, se = sa;
+  if (P.batches.size() > 1) {
+    if (!sh->s_lz) HIPCHK(ctx, hipStreamCreateWithFlags(&sh->s_lz, hipStreamNonBlocking));
+    if (!sh->s_eg) HIPCHK(ctx, hipStreamCreateWithFlags(&sh->s_eg, hipStreamNonBlocking));
+    sl = sh->s_lz;
+    se = sh->s_eg;
+  }
+  // s waits for e, recorded on `on` (nothing to wait for on the same stream)
+  auto wait = [](hipStream_t s, hipEvent_t e, hipStream_t on) { return s == on ? hipSuccess : hipStreamWaitEvent(s, e, 0); };
   HIPCHK(ctx, sh->tok.ensure(P.tok_len));
   HIPCHK(ctx, sh->bits.ensure((E + 31) / 32 + 1));
   if (tsum_on()) HIPCHK(ctx, sh->tsum.ensure((E + EAGER_TILE - 1) / EAGER_TILE * 4 + 4));
@@ -1769,8 +1854,15 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
   HIPCHK(ctx, sh->xq.ensure(2 * XQ_CAP_MAX));
   HIPCHK(ctx, hipMemsetAsync(sh->U.p + sh->utotal, 0, sh->pad, sa));
   unsigned long long *c = sh->ctr.p;
-  HIPCHK(ctx, hipMemsetAsync(c, 0, 48, sa));
-  HIPCHK(ctx, hipMemsetAsync(c + 2, 0xff, 8, sa));
+  {
+    // ctr[0, CTR_RUN_WORDS) in one copy: k_eager's counters [0, 6) (first-unknown [2] = ~0), the
+    // step tail's FindRecordStart best [8] = ~0 and chain-proof counters [16, 20) = {0, ~0, 0, ~0},
+    // k_first_bad's [100] = ~0; the rest (per-call regions) zero
+    unsigned long long *tpl = sh->h_ctr + 1024;  // pinned
+    std::memset(tpl, 0, CTR_RUN_WORDS * 8);
+    tpl[2] = tpl[8] = tpl[17] = tpl[19] = tpl[100] = ~0ull;
+    HIPCHK(ctx, hipMemcpyAsync(c, tpl, CTR_RUN_WORDS * 8, hipMemcpyHostToDevice, sa));
+  }
   sh->inflated = sh->bits_valid = sh->chain_ok = sh->cm_valid = false;
   sh->sieve_nref1 = 0;
   uint32_t *sv = sieve_for(sh);
@@ -1782,8 +1874,8 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
     if (!pev(sh, i)) return fail(ctx, SBH_E_HIP, "hipEventCreate failed");
   hipEvent_t *ev = sh->pev.data();
   HIPCHK(ctx, hipEventRecord(ev[6 * nbat], sa));  // setup done: the other streams start after it
-  HIPCHK(ctx, hipStreamWaitEvent(sl, ev[6 * nbat], 0));
-  HIPCHK(ctx, hipStreamWaitEvent(se, ev[6 * nbat], 0));
+  HIPCHK(ctx, wait(sl, ev[6 * nbat], sa));
+  HIPCHK(ctx, wait(se, ev[6 * nbat], sa));
   const DevBlocks all = sh->dev_blocks();
   uint64_t e_done = 0;
   std::vector<int> eager_launched(nbat, 0);
@@ -1793,11 +1885,11 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
     const DevBlocks d = blocks_from(all, b0);
     const uint64_t base = P.reuse ? sh->hb[b0].ustart : 0;
     // a reused token buffer: this batch's k_huff overwrites what the previous k_lz reads
-    if (P.reuse && i) HIPCHK(ctx, hipStreamWaitEvent(sa, ev[6 * (i - 1) + 3], 0));
+    if (P.reuse && i) HIPCHK(ctx, wait(sa, ev[6 * (i - 1) + 3], sl));
     HIPCHK(ctx, hipEventRecord(e[0], sa));
     HIPCHK(ctx, launch_huff(sh->comp.p, d, b1 - b0, sh->tok.p, base, sa));
     HIPCHK(ctx, hipEventRecord(e[1], sa));
-    HIPCHK(ctx, hipStreamWaitEvent(sl, e[1], 0));
+    HIPCHK(ctx, wait(sl, e[1], sa));
     HIPCHK(ctx, hipEventRecord(e[2], sl));
     HIPCHK(ctx, launch_lz(sh->comp.p, d, b1 - b0, sh->tok.p, base, sh->U.p, sl, sv, nref1));
     HIPCHK(ctx, hipEventRecord(e[3], sl));
@@ -1810,7 +1902,7 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
       hi = std::min(hi, E);
     }
     if (hi > e_done) {
-      HIPCHK(ctx, hipStreamWaitEvent(se, e[3], 0));
+      HIPCHK(ctx, wait(se, e[3], sl));
       HIPCHK(ctx, hipEventRecord(e[4], se));
       HIPCHK(ctx, launch_eager(sh->U.p, sh->utotal + sh->pad, e_done, hi, sh->d_seg.p, (uint32_t)sh->seg_end.size(),
                                sh->open_last ? 1 : 0, sh->ctg.p, sh->nctg, rtc, sh->bits.p + e_done / 32, c, se,
@@ -1821,7 +1913,7 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
       e_done = hi;
     }
   }
-  HIPCHK(ctx, hipStreamWaitEvent(se, ev[6 * (nbat - 1) + 3], 0));
+  HIPCHK(ctx, wait(se, ev[6 * (nbat - 1) + 3], sl));
   HIPCHK(ctx, launch_eager_defer(sh->U.p, 0, sh->d_seg.p, (uint32_t)sh->seg_end.size(), sh->open_last ? 1 : 0,
                                  sh->ctg.p, sh->nctg, rtc, sh->bits.p, c, sh->defer.p, DEFER_CAP, se));
   HIPCHK(ctx, hipEventRecord(ev[6 * nbat + 2], se));
@@ -1829,10 +1921,10 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
                               sh->ctg.p, sh->nctg, rtc, sh->bits.p, c, sh->xq.p, xq_cap(), se));
   HIPCHK(ctx, hipEventRecord(ev[6 * nbat + 3], se));
   HIPCHK(ctx, hipEventRecord(ev[6 * nbat + 1], se));
-  HIPCHK(ctx, hipStreamWaitEvent(sa, ev[6 * nbat + 1], 0));
+  HIPCHK(ctx, wait(sa, ev[6 * nbat + 1], se));
   if (pre_sync) HIPCHK(ctx, pre_sync(sa));
   {
-    const int rs = inflate_status(sh, sa, nullptr, c, sh->h_ctr, 48);
+    const int rs = inflate_status(sh, sa, nullptr, nullptr, nullptr, 0, true);
     if (rs) return rs;
   }
   sh->inflated = true;
@@ -1911,20 +2003,13 @@ int sbh_run_shard(sbh_shard *sh, uint64_t index_start, uint64_t own_end_file, in
   unsigned long long *tbest = sh->ctr.p + 8, *tc = sh->ctr.p + 16;
   bool tail = rtc >= 0 && hi0 > 0;
   if (tail && sh->cc.ensure((E + 31) / 32 / VC_CHUNK + 2) != hipSuccess) tail = false;
+  // (tbest and tc start as run_pipelined's counter template sets them, and come back to h_ctr[8]
+  // and h_ctr[16, 20) with its one status copy)
   auto tail_launch = [&](hipStream_t s) -> hipError_t {
-    unsigned long long *init = sh->h_ctr + 600;  // pinned: anomalies, first anomaly, set bits, exit
-    init[0] = 0;
-    init[1] = ~0ull;
-    init[2] = 0;
-    init[3] = ~0ull;
-    hipError_t e = hipMemsetAsync(tbest, 0xff, 8, s);
-    if (e == hipSuccess) e = launch_first_set(sh->bits.p, 0, 0, hi0, tbest, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(tc, init, 32, hipMemcpyHostToDevice, s);
+    hipError_t e = launch_first_set(sh->bits.p, 0, 0, hi0, tbest, s);
     if (e == hipSuccess)
       e = launch_verify_chain_count(sh->U.p, sh->bits.p, 0, E, 0, E0, total0, tc, tc + 1, tc + 3, tc + 2, nullptr, s,
                                     tbest, sh->cc.p);
-    if (e == hipSuccess) e = hipMemcpyAsync(sh->h_ctr + 8, tbest, 8, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(sh->h_ctr + 16, tc, 32, hipMemcpyDeviceToHost, s);
     return e;
   };
   rc = tail ? run_pipelined(sh, E, rtc, &res->n_true, tail_launch) : run_pipelined(sh, E, rtc, &res->n_true);

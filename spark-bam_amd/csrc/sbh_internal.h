@@ -126,7 +126,9 @@ hipError_t launch_lz(const uint8_t *comp, DevBlocks blocks, uint64_t nblocks, co
                      uint64_t tok_base, uint8_t *U, hipStream_t stream, uint32_t *sieve = nullptr,
                      uint32_t nref1 = 0);
 // *first = the first block of [0, n) whose status is not INF_OK (~0 if none).
-hipError_t launch_first_bad(const uint32_t *status, uint64_t n, unsigned long long *first, hipStream_t stream);
+// (init: set *first to ~0 first; false when the caller already did)
+hipError_t launch_first_bad(const uint32_t *status, uint64_t n, unsigned long long *first, hipStream_t stream,
+                            bool init = true);
 
 // Record field extraction (records.hip): device columns of a decoded batch (the host
 // view is sbh_records_out in sparkbam.h).
@@ -157,9 +159,11 @@ hipError_t launch_compact_u64(const uint64_t *in, const uint64_t *keep, const ui
 constexpr uint64_t VC_CHUNK = 256;
 // split counts from the proof's per-chunk set-bit counts (splits.hip): counts[i] += set bits of
 // [first[i], E[i]) for the SPLIT_OK splits, the bitmap read only in each range's end chunks
+// (chain_E != 0: counts are written, not added, and a range outside [chain_first, chain_E) gets
+// SPLIT_NOCOUNT)
 hipError_t launch_split_count_cc(const uint32_t *bits, uint64_t begin, const uint32_t *chunk_cnt, const uint64_t *first,
                                  const uint64_t *E, const uint32_t *code, uint64_t nsplit, unsigned long long *counts,
-                                 hipStream_t st);
+                                 hipStream_t st, uint64_t chain_first = 0, uint64_t chain_E = 0);
 // record starts (flat) -> htsjdk virtual positions over the device block table
 hipError_t launch_rec_vpos(const uint64_t *pos, uint64_t n, DevBlocks bl, uint64_t nblocks, uint64_t file_off,
                            uint64_t *vpos, hipStream_t st);
@@ -226,6 +230,7 @@ static_assert(CTR_CALL_END <= CTR_TRUE_SPREAD && CTR_NEXT18 + 4 <= CTR_WORDS, "c
 constexpr uint32_t SPLIT_OK = 0;    // first record and flat end decided on the device
 constexpr uint32_t SPLIT_HOST = 1;  // off the common path: the exact per-split host path decides
 constexpr uint32_t SPLIT_NOREAD = 2;  // FindBlockStart lands on an empty block: NoReadFoundException (no records)
+constexpr unsigned long long SPLIT_NOCOUNT = ~0ull;  // (sbh_split_starts fast path) the count is the host's to decide
 struct SplitArgs {
   const uint8_t *comp;
   uint64_t n;

@@ -316,13 +316,24 @@ __global__ __launch_bounds__(TC_THREADS) void k_truth_compare(const uint32_t *eb
 // counts[i] += set bits of [first[i], E[i]) from the chain proof's per-chunk counts: the chunks
 // strictly inside the range (neither holds the range's first or last word) are summed, the
 // bitmap is popcounted only over the words before and after them.  One workgroup per split.
+// (chain_E != 0: every split's count is written, not added -- 0 when it has no range, and
+// SPLIT_NOCOUNT when its range leaves the proven [chain_first, chain_E): the host then decides)
 __global__ __launch_bounds__(256) void k_split_count_cc(const uint32_t *bits, uint64_t begin, const uint32_t *cc,
                                                         const uint64_t *first, const uint64_t *E, const uint32_t *code,
-                                                        uint64_t nsplit, unsigned long long *counts) {
+                                                        uint64_t nsplit, unsigned long long *counts,
+                                                        uint64_t chain_first, uint64_t chain_E) {
   const uint64_t i = blockIdx.x;
-  if (i >= nsplit || code[i] != SPLIT_OK) return;
+  if (i >= nsplit) return;
+  const bool direct = chain_E != 0;
   const uint64_t from = first[i], to = E[i];
-  if (from >= to) return;
+  if (code[i] != SPLIT_OK || from >= to) {
+    if (direct && threadIdx.x == 0) counts[i] = 0;
+    return;
+  }
+  if (direct && (from < chain_first || to > chain_E)) {
+    if (threadIdx.x == 0) counts[i] = SPLIT_NOCOUNT;
+    return;
+  }
   const uint64_t wa = (from - begin) / 32, wb = (to - begin + 31) / 32;  // words [wa, wb)
   const uint64_t ca = wa / VC_CHUNK + 1, cb = (wb - 1) / VC_CHUNK;          // inner chunks [ca, cb)
   uint32_t c = 0;
@@ -346,7 +357,10 @@ __global__ __launch_bounds__(256) void k_split_count_cc(const uint32_t *bits, ui
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned long long t = (unsigned long long)part[0] + part[1] + part[2] + part[3];
-    if (t) atomicAdd(&counts[i], t);
+    if (direct)
+      counts[i] = t;
+    else if (t)
+      atomicAdd(&counts[i], t);
   }
 }
 }  // namespace
@@ -379,12 +393,12 @@ hipError_t launch_split_popcount(const uint32_t *bits, uint64_t begin, const uin
 
 hipError_t launch_split_count_cc(const uint32_t *bits, uint64_t begin, const uint32_t *chunk_cnt, const uint64_t *first,
                                  const uint64_t *E, const uint32_t *code, uint64_t nsplit, unsigned long long *counts,
-                                 hipStream_t st) {
+                                 hipStream_t st, uint64_t chain_first, uint64_t chain_E) {
   if (!nsplit) return hipSuccess;
   for (uint64_t s0 = 0; s0 < nsplit; s0 += 1u << 30)  // (grid.x holds 2^31 - 1 workgroups)
     hipLaunchKernelGGL(k_split_count_cc, dim3((uint32_t)std::min<uint64_t>(nsplit - s0, 1u << 30)), dim3(256), 0, st,
                        bits, begin, chunk_cnt, first + s0, E + s0, code + s0, std::min<uint64_t>(nsplit - s0, 1u << 30),
-                       counts + s0);
+                       counts + s0, chain_first, chain_E);
   return hipGetLastError();
 }
 
