@@ -163,6 +163,8 @@ int sbh_inflate(sbh_shard *sh, uint64_t *bad_block);
 int sbh_verify_crc(sbh_shard *sh, uint64_t *n_bad, uint64_t *first_bad);
 /* Copy flat bytes [flat, flat + n) to host memory. */
 int sbh_read_flat(sbh_shard *sh, uint64_t flat, uint64_t n, uint8_t *out);
+/* Device pointer of the flat bytes (read-only: the library keeps the zero pad past the flat
+ * end between calls and does not re-zero it when the size is unchanged). */
 const void *sbh_flat_device_ptr(sbh_shard *sh);
 
 /* Pos <-> flat (canonical positions, Pos.scala; curPos rolls to the next block). */

@@ -130,6 +130,7 @@ __global__ __launch_bounds__(256) void k_cand_count(const uint8_t *comp, uint64_
     c[threadIdx.x] = 0;
     f[threadIdx.x] = ~0u;
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0) counts[nchunks] = 0;  // (the scan's n + 1st entry: offs[nchunks] = total)
   __syncthreads();
   constexpr uint32_t NV = CHUNK / 4096;
   const uint64_t chunk0 = (uint64_t)blockIdx.x * CAND_CPW;
@@ -369,8 +370,15 @@ __global__ void k_chain_emit(const uint8_t *comp, uint64_t n, const uint64_t *ca
 
 // The block table as the host's sbh_block records (start = file offset, ustart, csize | hsize
 // << 32, usize | flags << 32): one device-to-host copy lands it in place.
-__global__ void k_pack_blocks(DevBlocks bl, uint64_t n, uint64_t file_off, uint64_t *out) {
+// (trailer, optional: out[4 n] = the chain length rank[n - 1] + v[n - 1], out[4 n + 1, + 4) = the
+// next18 words k_chain_emit left -- so the table, its length and the next header come back in one copy)
+__global__ void k_pack_blocks(DevBlocks bl, uint64_t n, uint64_t file_off, uint64_t *out, const uint64_t *rank,
+                              const uint64_t *v, const uint64_t *next18) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0 && rank) {
+    out[4 * n] = rank[n - 1] + v[n - 1];
+    for (int k = 0; k < 3; ++k) out[4 * n + 1 + k] = next18[k];
+  }
   if (i >= n) return;
   uint64_t *r = out + 4 * i;
   r[0] = bl.cstart[i] + file_off;
@@ -442,8 +450,9 @@ hipError_t launch_cand_write(const uint8_t *comp, uint64_t n, uint64_t from, con
 // nc), on (u8 x nc), v/rank (u64 x nc each), tmp (scan).  Writes the block table and usz (u64
 // per block, zero past the chain); the block count is rank[nc - 1] + v[nc - 1] (no host round
 // trip here: the caller copies those two words back with the block table).
-hipError_t launch_pack_blocks(DevBlocks bl, uint64_t n, uint64_t file_off, uint64_t *out, hipStream_t st) {
-  if (n) hipLaunchKernelGGL(k_pack_blocks, dim3(nblk(n, 256)), dim3(256), 0, st, bl, n, file_off, out);
+hipError_t launch_pack_blocks(DevBlocks bl, uint64_t n, uint64_t file_off, uint64_t *out, hipStream_t st,
+                              const uint64_t *rank, const uint64_t *v, const uint64_t *next18) {
+  if (n) hipLaunchKernelGGL(k_pack_blocks, dim3(nblk(n, 256)), dim3(256), 0, st, bl, n, file_off, out, rank, v, next18);
   return hipGetLastError();
 }
 

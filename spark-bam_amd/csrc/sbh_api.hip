@@ -56,7 +56,9 @@ hipError_t launch_cand_count(const uint8_t *comp, uint64_t n, uint64_t from, uin
 hipError_t launch_cand_write(const uint8_t *comp, uint64_t n, uint64_t from, const uint64_t *counts,
                              const uint32_t *first, const uint64_t *offs, uint64_t *cand, uint64_t nchunks,
                              hipStream_t st);
-hipError_t launch_pack_blocks(DevBlocks bl, uint64_t n, uint64_t file_off, uint64_t *out, hipStream_t st);
+hipError_t launch_pack_blocks(DevBlocks bl, uint64_t n, uint64_t file_off, uint64_t *out, hipStream_t st,
+                              const uint64_t *rank = nullptr, const uint64_t *v = nullptr,
+                              const uint64_t *next18 = nullptr);
 hipError_t build_chain(const uint8_t *comp, uint64_t n, const uint64_t *cand, uint64_t nc, uint64_t start_rel,
                        int64_t *J0, int64_t *J1, uint8_t *on, uint64_t *v, uint64_t *rank, uint64_t *tmp,
                        DevBlocks bl, uint64_t *usz, uint8_t *next18, uint64_t *sidx, bool linear, hipStream_t st);
@@ -176,6 +178,9 @@ struct sbh_shard {
   // inflate
   bool inflated = false;
   DBuf<uint8_t> U;
+  // U's pad [utotal, + pad) is zero for this utotal and allocation (only k_lz writes U, and only
+  // below utotal): a step over the same shard skips the memset (an unaligned one is 3 fills)
+  uint64_t u_pad_clean = ~0ull, u_pad_cap = 0;
   DBuf<uint32_t> tok;  // LZ77 tokens between k_huff and k_lz (4 B per flat byte)
   // checker
   DBuf<int32_t> ctg;
@@ -510,7 +515,7 @@ int sbh_shard_destroy(sbh_shard *sh) {
   sh->tok.release();
   sh->counts.release(); sh->cfirst.release(); sh->offs.release(); sh->cand.release(); sh->v.release(); sh->rank.release();
   sh->tmp.release(); sh->J0.release(); sh->J1.release(); sh->on.release(); sh->d_seg.release();
-  sh->U.release(); sh->ctg.release(); sh->bits.release(); sh->words.release(); sh->close_pos.release();
+  sh->U.release(); sh->u_pad_clean = ~0ull; sh->ctg.release(); sh->bits.release(); sh->words.release(); sh->close_pos.release();
   sh->close_word.release(); sh->ctr.release(); sh->opix.release(); sh->tsum.release(); sh->sieve.release();
   sh->cc.release();
   sh->comp2.release(); sh->aux2.release();
@@ -780,17 +785,18 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
     if ((rc = start_is_header()) != SBH_OK) return rc;
   }
   if (nchunks && rel + 18 <= n) {
-    HIPCHK(ctx, sh->counts.ensure(nchunks));
+    // (counts[nchunks] = 0, written by k_cand_count: the scan over nchunks + 1 entries leaves the
+    // candidate total in offs[nchunks], one word back)
+    HIPCHK(ctx, sh->counts.ensure(nchunks + 1));
     HIPCHK(ctx, sh->cfirst.ensure(nchunks));
-    HIPCHK(ctx, sh->offs.ensure(nchunks));
-    HIPCHK(ctx, sh->tmp.ensure(scan_tmp_words(nchunks) + scan_tmp_words(1 << 24)));
+    HIPCHK(ctx, sh->offs.ensure(nchunks + 1));
+    HIPCHK(ctx, sh->tmp.ensure(scan_tmp_words(nchunks + 1) + scan_tmp_words(1 << 24)));
     HIPCHK(ctx, launch_cand_count(sh->comp.p, n, srel, sh->counts.p, sh->cfirst.p, nchunks, st));
-    HIPCHK(ctx, scan_exclusive_u64(sh->counts.p, sh->offs.p, nchunks, sh->tmp.p, st));
-    HIPCHK(ctx, hipMemcpyAsync(&sh->h_ctr[0], sh->offs.p + nchunks - 1, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipMemcpyAsync(&sh->h_ctr[1], sh->counts.p + nchunks - 1, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, scan_exclusive_u64(sh->counts.p, sh->offs.p, nchunks + 1, sh->tmp.p, st));
+    HIPCHK(ctx, hipMemcpyAsync(&sh->h_ctr[0], sh->offs.p + nchunks, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipStreamSynchronize(st));
     if ((rc = start_is_header()) != SBH_OK) return rc;
-    nc = sh->h_ctr[0] + sh->h_ctr[1];
+    nc = sh->h_ctr[0];
   }
   uint64_t nchain = 0;
   // the 18 bytes after the last chain block (the next header, checked below), written by
@@ -804,7 +810,7 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
     HIPCHK(ctx, sh->on.ensure(nc));
     HIPCHK(ctx, sh->v.ensure(nc));
     HIPCHK(ctx, sh->rank.ensure(nc));
-    HIPCHK(ctx, sh->tmp.ensure(scan_tmp_words(nc) + scan_tmp_words(nchunks)));
+    HIPCHK(ctx, sh->tmp.ensure(scan_tmp_words(nc) + scan_tmp_words(nchunks + 1)));
     HIPCHK(ctx, launch_cand_write(sh->comp.p, n, srel, sh->counts.p, sh->cfirst.p, sh->offs.p, sh->cand.p, nchunks, st));
     HIPCHK(ctx, sh->b_cstart.ensure(nc));
     HIPCHK(ctx, sh->b_ustart.ensure(nc));
@@ -820,10 +826,9 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
   sh->cand_from = srel;
   // host copy of the block table (Pos mapping, segments)
   static_assert(sizeof(sbh_block) == 32, "k_pack_blocks writes 32-byte sbh_block records");
-  sh->hb.resize(nc);
+  sh->hb.resize(nc + 1);  // (+ the trailer k_pack_blocks leaves after the table)
   if (nc) {
-    unsigned long long *lastw = sh->h_ctr + 540;  // pinned: rank[nc - 1], v[nc - 1]
-    HIPCHK(ctx, sh->blkpack.ensure(4 * nc));
+    HIPCHK(ctx, sh->blkpack.ensure(4 * nc + 4));
     // the linear chain first (every candidate from the start on is chained: no pointer jumping);
     // its flag comes back with the table, and a chain that is not linear is rebuilt by jumping
     for (int pass = chain_jump_only() ? 1 : 0; pass < 2; ++pass) {
@@ -835,16 +840,16 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
       // back with the block table, so the table is packed and copied for all nc candidates and
       // cut after
       HIPCHK(ctx, scan_exclusive_u64(sh->usz.p, sh->b_ustart.p, nc, sh->tmp.p, st));
-      HIPCHK(ctx, launch_pack_blocks(sh->dev_blocks(), nc, sh->file_off, sh->blkpack.p, st));
-      HIPCHK(ctx, hipMemcpyAsync(sh->hb.data(), sh->blkpack.p, nc * 32, hipMemcpyDeviceToHost, st));
-      HIPCHK(ctx, hipMemcpyAsync(lastw, sh->rank.p + nc - 1, 8, hipMemcpyDeviceToHost, st));
-      HIPCHK(ctx, hipMemcpyAsync(lastw + 1, sh->v.p + nc - 1, 8, hipMemcpyDeviceToHost, st));
-      // (+ the not-linear flag and the empty-block count)
-      HIPCHK(ctx, hipMemcpyAsync(nx, next18_dev, 24, hipMemcpyDeviceToHost, st));
+      // the table with a 32-byte trailer (hb[nc]): the chain length, then the next18 words (+ the
+      // not-linear flag and the empty-block count) -- one copy into hb's page-locked storage
+      HIPCHK(ctx, launch_pack_blocks(sh->dev_blocks(), nc, sh->file_off, sh->blkpack.p, st, sh->rank.p, sh->v.p,
+                                     reinterpret_cast<const uint64_t *>(next18_dev)));
+      HIPCHK(ctx, hipMemcpyAsync(sh->hb.data(), sh->blkpack.p, (nc + 1) * 32, hipMemcpyDeviceToHost, st));
       HIPCHK(ctx, hipStreamSynchronize(st));
+      std::memcpy(nx, reinterpret_cast<const uint64_t *>(sh->hb.data() + nc) + 1, 24);
       if (pass == 1 || !nx[NEXT18_NONLIN]) break;
     }
-    nchain = lastw[0] + lastw[1];
+    nchain = *reinterpret_cast<const uint64_t *>(sh->hb.data() + nc);
   }
   sh->hb.resize(nchain);
   // stream end: a truncated last block is not part of the resident stream
@@ -953,6 +958,16 @@ static uint32_t *sieve_for(sbh_shard *sh) {
   return sh->sieve.p;
 }
 
+static hipError_t zero_u_pad(sbh_shard *sh, hipStream_t st) {
+  if (sh->u_pad_clean == sh->utotal && sh->u_pad_cap == sh->U.cap) return hipSuccess;
+  const hipError_t e = hipMemsetAsync(sh->U.p + sh->utotal, 0, sh->pad, st);
+  if (e == hipSuccess) {
+    sh->u_pad_clean = sh->utotal;
+    sh->u_pad_cap = sh->U.cap;
+  }
+  return e;
+}
+
 static DevBlocks blocks_from(DevBlocks d, uint64_t b) {
   return DevBlocks{d.cstart + b, d.csize + b, d.hsize + b, d.usize + b, d.ustart + b, d.flags + b, d.status + b, d.ntok + b};
 }
@@ -1009,7 +1024,7 @@ int sbh_inflate(sbh_shard *sh, uint64_t *bad_block) {
   HIPCHK(ctx, sh->U.ensure(sh->utotal + sh->pad));
   const TokPlan P = tok_plan(sh, ~0ull);
   HIPCHK(ctx, sh->tok.ensure(P.tok_len));
-  HIPCHK(ctx, hipMemsetAsync(sh->U.p + sh->utotal, 0, sh->pad, st));
+  HIPCHK(ctx, zero_u_pad(sh, st));
   uint32_t *sv = sieve_for(sh);
   const uint32_t nref1 = (uint32_t)sh->nctg + 1;
   mark(sh, 2);
@@ -1852,7 +1867,7 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
   if (tsum_on()) HIPCHK(ctx, sh->tsum.ensure((E + EAGER_TILE - 1) / EAGER_TILE * 4 + 4));
   HIPCHK(ctx, sh->defer.ensure(DEFER_CAP));
   HIPCHK(ctx, sh->xq.ensure(2 * XQ_CAP_MAX));
-  HIPCHK(ctx, hipMemsetAsync(sh->U.p + sh->utotal, 0, sh->pad, sa));
+  HIPCHK(ctx, zero_u_pad(sh, sa));
   unsigned long long *c = sh->ctr.p;
   {
     // ctr[0, CTR_RUN_WORDS) in one copy: k_eager's counters [0, 6) (first-unknown [2] = ~0), the
