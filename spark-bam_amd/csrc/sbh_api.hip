@@ -218,6 +218,10 @@ struct sbh_shard {
   uint64_t pad = 4096;
   // pipelined run (run_pipelined): extra streams, per-batch events, deferred positions
   hipStream_t s_lz = nullptr, s_eg = nullptr;
+  // sbh_run_stream2's window shard: its pipeline keeps three streams even for one batch (the
+  // next window's copy in flight on the copy stream serialized a one-stream pipeline behind it:
+  // e2e 130 -> 84 GB/s, profiles/r06_ab/r06u_*)
+  bool window_shard = false;
   std::vector<hipEvent_t> pev;
   DBuf<uint64_t> defer;
   DBuf<uint64_t> xq;  // long-record eager candidates for the wave-cooperative exact pass
@@ -886,7 +890,7 @@ int sbh_index(sbh_shard *sh, uint64_t start, uint64_t *n_blocks, uint64_t *flat_
   }
   sh->seg_end.push_back(total);
   HIPCHK(ctx, sh->d_seg.ensure(sh->seg_end.size()));
-  HIPCHK(ctx, hipMemcpyAsync(sh->d_seg.p, sh->seg_end.data(), sh->seg_end.size() * 8, hipMemcpyHostToDevice, st));
+  HIPCHK(ctx, set_words(sh->d_seg.p, sh->seg_end.data(), sh->seg_end.size(), st));
   sh->nblocks = nchain;
   sh->utotal = total;
   sh->index_start = start;
@@ -1579,7 +1583,7 @@ int sbh_split_starts(sbh_shard *sh, const uint64_t *starts, const uint64_t *ends
       hp[n + i] = rel_end(i);
     }
     uint32_t *dcode = reinterpret_cast<uint32_t *>(dp + 5 * n);
-    HIPCHK(ctx, hipMemcpyAsync(dp, hp, 16 * n, hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, set_words(dp, hp, 2 * n, st));
     HIPCHK(ctx, launch_split_prologue(a, dp, dp + n, n, dp + 2 * n, dp + 3 * n, dcode, st));
     HIPCHK(ctx, launch_split_count_cc(sh->bits.p, sh->bits_begin, sh->cc.p, dp + 2 * n, dp + 3 * n, dcode, n,
                                       reinterpret_cast<unsigned long long *>(dp + 4 * n), st, sh->chain_first,
@@ -1851,10 +1855,12 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
   const uint64_t nb = sh->nblocks;
   const uint64_t npipe = std::max<uint64_t>(1, std::min<uint64_t>(PIPE_MAX_BATCHES, nb / pipe_min_blocks()));
   const TokPlan P = tok_plan(sh, (nb + npipe - 1) / std::max<uint64_t>(npipe, 1));
-  // one batch (the default): every launch on the shard's stream, no cross-stream event waits
-  // (each cost the step ~15 us of idle device between the stages)
+  // one batch (the default) of a resident shard: every launch on the shard's stream, no
+  // cross-stream event waits (each cost the step ~15 us of idle device between the stages)
   hipStream_t sl = sa, se = sa;
-  if (P.batches.size() > 1) {
+  static const char *ps = std::getenv("SBH_PIPE_STREAMS");  // (A/B: 3 = three streams for every shard)
+  static const bool three = ps && std::atoi(ps) == 3;
+  if (P.batches.size() > 1 || sh->window_shard || three) {
     if (!sh->s_lz) HIPCHK(ctx, hipStreamCreateWithFlags(&sh->s_lz, hipStreamNonBlocking));
     if (!sh->s_eg) HIPCHK(ctx, hipStreamCreateWithFlags(&sh->s_eg, hipStreamNonBlocking));
     sl = sh->s_lz;
@@ -1876,7 +1882,7 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
     unsigned long long *tpl = sh->h_ctr + 1024;  // pinned
     std::memset(tpl, 0, CTR_RUN_WORDS * 8);
     tpl[2] = tpl[8] = tpl[17] = tpl[19] = tpl[100] = ~0ull;
-    HIPCHK(ctx, hipMemcpyAsync(c, tpl, CTR_RUN_WORDS * 8, hipMemcpyHostToDevice, sa));
+    HIPCHK(ctx, set_words(reinterpret_cast<uint64_t *>(c), reinterpret_cast<const uint64_t *>(tpl), CTR_RUN_WORDS, sa));
   }
   sh->inflated = sh->bits_valid = sh->chain_ok = sh->cm_valid = false;
   sh->sieve_nref1 = 0;
@@ -2197,6 +2203,7 @@ int sbh_run_stream2(sbh_ctx *ctx, const void *host, uint64_t n, uint64_t file_of
       return res->status = rc;
     }
     scp->sh->comp.release();
+    scp->sh->window_shard = true;
     hipError_t e = hipStreamCreateWithFlags(&scp->cs, hipStreamNonBlocking);
     for (int i = 0; i < 2 && e == hipSuccess; ++i) {
       e = hipEventCreate(&scp->done[i]);

@@ -247,6 +247,8 @@ struct SplitArgs {
   uint64_t bits_begin, bits_end;
   int64_t mrs;
 };
+// n host words to dst on st: up to 128 as a kernel's arguments (no DMA), more by a copy
+hipError_t set_words(uint64_t *dst, const uint64_t *src, uint64_t n, hipStream_t st);
 hipError_t launch_split_prologue(const SplitArgs &a, const uint64_t *starts, const uint64_t *ends, uint64_t nsplit,
                                  uint64_t *first, uint64_t *E, uint32_t *code, hipStream_t st);
 hipError_t launch_split_popcount(const uint32_t *bits, uint64_t begin, const uint64_t *first, const uint64_t *E,

@@ -432,4 +432,26 @@ hipError_t launch_truth_compare(const uint32_t *ebits, uint64_t ebegin, const ui
   return hipGetLastError();
 }
 
+// A few words from the host into device memory through the kernel's arguments instead of a
+// host-to-device copy: a copy on a kernel stream queues behind any large copy in flight on the
+// same DMA engine (sbh_run_stream2 prefetches the next window while this one's kernels run).
+namespace {
+constexpr uint32_t SET_WORDS_MAX = 128;
+struct Words {
+  uint64_t w[SET_WORDS_MAX];
+};
+__global__ __launch_bounds__(SET_WORDS_MAX) void k_set_words(uint64_t *dst, Words v, uint32_t n) {
+  if (threadIdx.x < n) dst[threadIdx.x] = v.w[threadIdx.x];
+}
+}  // namespace
+
+hipError_t set_words(uint64_t *dst, const uint64_t *src, uint64_t n, hipStream_t st) {
+  if (!n) return hipSuccess;
+  if (n > SET_WORDS_MAX) return hipMemcpyAsync(dst, src, n * 8, hipMemcpyHostToDevice, st);
+  Words v;
+  for (uint64_t i = 0; i < n; ++i) v.w[i] = src[i];
+  hipLaunchKernelGGL(k_set_words, dim3(1), dim3(SET_WORDS_MAX), 0, st, dst, v, (uint32_t)n);
+  return hipGetLastError();
+}
+
 }  // namespace sbh

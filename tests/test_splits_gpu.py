@@ -102,6 +102,37 @@ def test_split_starts_after_run_shard_owned_range(ctx, files):
         sh.close()
 
 
+@pytest.mark.parametrize("name", ["2.bam", "short_l6", "long", "adversarial", "adversarial_empty"])
+def test_split_starts_fast_path_after_run(ctx, files, name):
+    """After sbh_run_shard (chain proof + chunk counts resident) sbh_split_starts takes its one-
+    round-trip path: counts written by the count kernel, a range leaving the proven chain (the
+    empty blocks' later segments, bait) sent down the general path.  Twice in a row, against
+    sbh_split per split and the oracle."""
+    data = files[name]
+    of, sh = loaded(ctx, data)
+    try:
+        try:
+            sh.run(0, data.size)
+        except sb.SparkBamError:
+            pass  # (a corpus whose owned range has no record: the splits still decide alone)
+        splits = file_splits(data.size, max(data.size // 13, 20000))
+        for _ in range(2):
+            status, v, n, n_host = sh.split_starts(splits)
+            for i, (s, e) in enumerate(splits):
+                rc, vr, nr = of.split(s, e)
+                if rc == OR_OK:
+                    assert int(status[i]) == 0 and int(n[i]) == nr and (nr == 0 or int(v[i]) == vr), (i, s, e)
+                else:  # as the per-split path decides it
+                    try:
+                        v1, n1 = sh.split(s, e)
+                        st1 = 0
+                    except sb.SparkBamError as err:
+                        st1, v1, n1 = err.code, 0, 0
+                    assert (int(status[i]), int(n[i])) == (st1, n1), (i, s, e)
+    finally:
+        sh.close()
+
+
 def test_chain_from(ctx, files):
     data = files["2.bam"]
     of, sh = loaded(ctx, data)
