@@ -218,10 +218,7 @@ struct sbh_shard {
   uint64_t pad = 4096;
   // pipelined run (run_pipelined): extra streams, per-batch events, deferred positions
   hipStream_t s_lz = nullptr, s_eg = nullptr;
-  // sbh_run_stream2's window shard: its pipeline keeps three streams even for one batch (the
-  // next window's copy in flight on the copy stream serialized a one-stream pipeline behind it:
-  // e2e 130 -> 84 GB/s, profiles/r06_ab/r06u_*)
-  bool window_shard = false;
+  hipStream_t cs = nullptr;  // sbh_shard_load's copy stream (created on first use)
   std::vector<hipEvent_t> pev;
   DBuf<uint64_t> defer;
   DBuf<uint64_t> xq;  // long-record eager candidates for the wave-cooperative exact pass
@@ -532,6 +529,7 @@ int sbh_shard_destroy(sbh_shard *sh) {
     if (e) (void)hipEventDestroy(e);
   if (sh->s_lz) (void)hipStreamDestroy(sh->s_lz);
   if (sh->s_eg) (void)hipStreamDestroy(sh->s_eg);
+  if (sh->cs) (void)hipStreamDestroy(sh->cs);
   sh->defer.release();
   sh->xq.release();
   sh->rec.release();
@@ -558,9 +556,21 @@ int sbh_shard_load(sbh_shard *sh, const void *src, uint64_t n, uint64_t file_off
   if (rc) return rc;
   HIPCHK(ctx, hipStreamSynchronize(sh->st));  // (no kernel may still read the old bytes)
   HIPCHK(ctx, sh->comp.ensure(n + sh->pad));
+  // the copy on the shard's copy stream, at another priority than every compute stream: its
+  // hardware queue is then never one another task's kernels wait behind (see sbh_run_stream2)
+  hipStream_t cs = sh->st;
+  if (!std::getenv("SBH_LOAD_ON_SHARD_STREAM")) {
+    if (!sh->cs) {
+      int least = 0, greatest = 0;
+      if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess && greatest != least)
+        HIPCHK(ctx, hipStreamCreateWithPriority(&sh->cs, hipStreamNonBlocking, greatest));
+    }
+    if (sh->cs) cs = sh->cs;
+  }
   if (n)
     HIPCHK(ctx, hipMemcpyAsync(sh->comp.p, src, n, comp_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
-                               sh->st));
+                               cs));
+  if (cs != sh->st) HIPCHK(ctx, hipStreamSynchronize(cs));
   HIPCHK(ctx, hipMemsetAsync(sh->comp.p + n, 0, sh->pad, sh->st));
   HIPCHK(ctx, hipStreamSynchronize(sh->st));
   sh->file_off = file_offset;
@@ -1860,7 +1870,7 @@ static int run_pipelined(sbh_shard *sh, uint64_t E, int32_t rtc, uint64_t *n_tru
   hipStream_t sl = sa, se = sa;
   static const char *ps = std::getenv("SBH_PIPE_STREAMS");  // (A/B: 3 = three streams for every shard)
   static const bool three = ps && std::atoi(ps) == 3;
-  if (P.batches.size() > 1 || sh->window_shard || three) {
+  if (P.batches.size() > 1 || three) {
     if (!sh->s_lz) HIPCHK(ctx, hipStreamCreateWithFlags(&sh->s_lz, hipStreamNonBlocking));
     if (!sh->s_eg) HIPCHK(ctx, hipStreamCreateWithFlags(&sh->s_eg, hipStreamNonBlocking));
     sl = sh->s_lz;
@@ -2203,8 +2213,15 @@ int sbh_run_stream2(sbh_ctx *ctx, const void *host, uint64_t n, uint64_t file_of
       return res->status = rc;
     }
     scp->sh->comp.release();
-    scp->sh->window_shard = true;
-    hipError_t e = hipStreamCreateWithFlags(&scp->cs, hipStreamNonBlocking);
+    // the copy stream at another priority than the compute streams: its hardware queue then comes
+    // from another pool, so no compute stream shares it (a copy in flight on a shared queue held
+    // the next window's kernels behind it: e2e 130 -> 84 GB/s depending on stream creation order)
+    int least = 0, greatest = 0;
+    hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+    if (e == hipSuccess)
+      e = greatest != least && !std::getenv("SBH_CS_SAME_PRIORITY")
+              ? hipStreamCreateWithPriority(&scp->cs, hipStreamNonBlocking, greatest)
+              : hipStreamCreateWithFlags(&scp->cs, hipStreamNonBlocking);
     for (int i = 0; i < 2 && e == hipSuccess; ++i) {
       e = hipEventCreate(&scp->done[i]);
       if (e == hipSuccess) e = hipEventCreate(&scp->c0[i]);
@@ -2280,16 +2297,21 @@ int sbh_run_stream2(sbh_ctx *ctx, const void *host, uint64_t n, uint64_t file_of
     if (hipEventElapsedTime(&ms, R.c0[b], R.done[b]) == hipSuccess) h2d_ms += ms;
     timed[b] = false;
   };
+  uint64_t win_len[2] = {0, 0};  // bytes copied into each window buffer
   auto enqueue = [&](int b, uint64_t lo, uint64_t ld) -> hipError_t {
     hipError_t e = hipSuccess;
     if (R.buf[b].cap < ld - lo + pad) {  // an oversized (split-aligned) window
       e = fit_buf(b, ld - lo + pad);
       if (e != hipSuccess) return e;
     }
+    // (the copy stream carries the copy alone: the window's zero pad is set on the shard's stream
+    // after it waits for the copy -- a fill queued behind the copy on the copy stream would be a
+    // kernel waiting on the DMA, and a hardware queue the copy stream shares with a compute
+    // stream would hold that stream's kernels behind it)
     e = hipEventRecord(R.c0[b], R.cs);
     if (e == hipSuccess) e = hipMemcpyAsync(R.buf[b].p, src + (lo - file_offset), ld - lo, hipMemcpyHostToDevice, R.cs);
-    if (e == hipSuccess) e = hipMemsetAsync(R.buf[b].p + (ld - lo), 0, pad, R.cs);
     if (e == hipSuccess) e = hipEventRecord(R.done[b], R.cs);
+    win_len[b] = ld - lo;
     timed[b] = e == hipSuccess;
     return e;
   };
@@ -2306,6 +2328,7 @@ int sbh_run_stream2(sbh_ctx *ctx, const void *host, uint64_t n, uint64_t file_of
     if (prefetch && more) HIPCHK(ctx, enqueue(1 - cur, lo2, load_end(hi2)));
     const uint64_t ld = load_end(hi);
     HIPCHK(ctx, hipStreamWaitEvent(sh->st, R.done[cur], 0));
+    HIPCHK(ctx, hipMemsetAsync(R.buf[cur].p + win_len[cur], 0, pad, sh->st));
     sh->comp.p = R.buf[cur].p;
     sh->comp.cap = R.buf[cur].cap;
     sh->file_off = lo;
