@@ -311,19 +311,35 @@ template <uint32_t NV>
 __device__ __forceinline__ void stage_vec(uint4 *lds, const uint8_t *U, uint64_t s0, uint64_t u_pad) {
   constexpr uint32_t R = (NV + T - 1) / T;
   const uint4 *g = reinterpret_cast<const uint4 *>(U + s0);
+  // every lane loads in every round (a vector out of range reads U's first one instead, and is
+  // zeroed after): a load under a branch made the compiler wait for each one before the next
   uint4 v[R];
+  bool in[R];
 #pragma unroll
   for (uint32_t r = 0; r < R; ++r) {
     const uint32_t i = threadIdx.x + r * T;
-    v[r] = make_uint4(0, 0, 0, 0);
-    if (i < NV && s0 + 16ull * i + 16 <= u_pad) v[r] = g[i];
+    in[r] = i < NV && s0 + 16ull * i + 16 <= u_pad;
+    v[r] = *(in[r] ? g + i : reinterpret_cast<const uint4 *>(U));
   }
 #pragma unroll
   for (uint32_t r = 0; r < R; ++r) {
     const uint32_t i = threadIdx.x + r * T;
-    if (i < NV) lds[i] = v[r];
+    if (i < NV) lds[i] = in[r] ? v[r] : make_uint4(0, 0, 0, 0);
   }
 }
+
+// One dword of every 128-byte line of [p, p + n) (a lane per line) loaded into a register that
+// nothing waits for: the lines come into L2 / MALL for the workgroup that stages them later.
+// The caller keeps the result live (l2_keep) past a wait the compiler places for its own later
+// loads -- vector loads return in order, so that wait covers this one too and the register is
+// never reused while the load is in flight.
+__device__ __forceinline__ uint32_t l2_touch(const uint8_t *p, uint64_t n) {
+  uint32_t v = 0;
+  const uint64_t off = (uint64_t)threadIdx.x * 128;
+  if (off < n) asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p + off) : "memory");
+  return v;
+}
+__device__ __forceinline__ void l2_keep(uint32_t v) { asm volatile("" ::"v"(v)); }
 
 __device__ __forceinline__ uint32_t seg_index(const Segs &sg, uint64_t p, uint32_t from) {
   uint32_t k = from;
@@ -396,6 +412,9 @@ constexpr uint32_t ESTAGE = EW + 512;     // staged bytes (records near the end 
 #define SBH_EQ_CHUNK 4096
 #endif
 constexpr uint32_t EQ_CHUNK = SBH_EQ_CHUNK;  // survivor-queue capacity
+#ifndef SBH_EAGER_PF
+#define SBH_EAGER_PF 0  // k_eager: the tile this many workgroups ahead is touched into L2 (A/B r06zb: 1024 slower, k_eager 2.42 -> 2.50 ms)
+#endif
 #ifndef SBH_EAGER_SHIFT_SWEEP
 #define SBH_EAGER_SHIFT_SWEEP 1  // k_eager's refID sweep: tests shifted into each word (see k_eager)
 #endif
@@ -524,6 +543,14 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
   const uint64_t c0 = __builtin_readcyclecounter();
   uint32_t nsurv = 0, ncand = 0, nexact = 0;
 #endif
+  // the window of the tile SBH_EAGER_PF workgroups on (the one that starts about when this one
+  // ends, on the same XCD) into L2 / MALL while this one stages its own
+  uint32_t pfv = 0;
+  if (SBH_EAGER_PF) {
+    const uint64_t tn = begin + ((uint64_t)blockIdx.x + SBH_EAGER_PF) * ETILE;
+    const uint64_t sn = tn & ~15ull;
+    if (tn < end && sn < u_pad) pfv = l2_touch(U + sn, std::min<uint64_t>(ESTAGE + 32, u_pad - sn));
+  }
   stage_vec<NV>(ldsv, U, s0, u_pad);
   for (uint32_t i = threadIdx.x; i < EW / 32; i += T) { ok[i] = 0; nrm[i] = 0; und[i] = 0; }
   for (uint32_t i = threadIdx.x; i < ETILE / 32; i += T) res[i] = 0;
@@ -536,6 +563,7 @@ __global__ __launch_bounds__(T) void k_eager(const uint8_t *__restrict__ U, uint
     ts_dirty = 0;
   }
   __syncthreads();
+  l2_keep(pfv);
   Src s{U, lds32, s0, ESTAGE};  // >= EW + 15 + 44: every phase-A read is staged
   const uint32_t k0 = seg0;
   const uint64_t e0 = seg_end0;  // positions below e0 are in segment k0 (nearly all)

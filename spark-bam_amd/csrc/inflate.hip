@@ -2237,7 +2237,16 @@ __global__ __launch_bounds__(WAVE * HDR_WAVES) void k_hdr(const uint8_t *__restr
   }
   const uint32_t ndw = min((limit + 31) / 32 + 2, HDR_STAGE_DW);
   const uint32_t *g = reinterpret_cast<const uint32_t *>(dbase);
-  for (uint32_t i = lane; i < ndw; i += WAVE) stage[i] = g[i];
+  {
+    // every load before any store (index clamped: a load in the loop was waited for before the next)
+    constexpr uint32_t R = (HDR_STAGE_DW + WAVE - 1) / WAVE;
+    uint32_t v[R];
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) v[r] = g[min(lane + r * WAVE, ndw - 1)];
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r)
+      if (lane + r * WAVE < ndw) stage[lane + r * WAVE] = v[r];
+  }
   __builtin_amdgcn_wave_barrier();  // (a wave's LDS accesses complete in order)
   uint32_t *out = tok + bl.ustart[b] + usize - HDR_OUT_DW;
   const HdrSrc src{stage, ndw};
@@ -2342,20 +2351,23 @@ __global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__rest
     // the first deflate block's header, decoded and tabled by k_hdr at the end of this
     // block's token region (read here before any token is written over it)
     const uint32_t *hd = tok + G + usize - HDR_OUT_DW;
-    const bool pre = uni(hd[HDR_STATUS]) == HDR_OK;
-    uint32_t pre_psym = 0, pre_last = 0;
-    // the record's dwords go to registers first, so their loads are in flight together
-    // with the stage's and only the LDS stores wait
+    // the record's dwords go to registers first, loaded before its status is known (its place is
+    // inside the token region whatever the status: PAR_MIN_USIZE > HDR_OUT_DW), so the record,
+    // its status and the stage are one round trip and only the LDS stores wait
     constexpr uint32_t NTV = HDR_SENT / HT, NSV = (320 + 32 + HT - 1) / HT;
     uint32_t tv[NTV], sv[NSV];
-    if (pre) {
 #pragma unroll
-      for (uint32_t k = 0; k < NTV; ++k) tv[k] = hd[tid + k * HT];
+    for (uint32_t k = 0; k < NTV; ++k) tv[k] = hd[tid + k * HT];
 #pragma unroll
-      for (uint32_t k = 0; k < NSV; ++k) sv[k] = tid + k * HT < 352 ? hd[HDR_SENT + tid + k * HT] : 0u;
-      pre_psym = uni(hd[HDR_PSYM]);
-      pre_last = uni(hd[HDR_LAST]);
-    }
+    for (uint32_t k = 0; k < NSV; ++k) sv[k] = hd[HDR_SENT + min(tid + k * HT, 351u)];
+    const uint32_t h_st = hd[HDR_STATUS], h_psym = hd[HDR_PSYM], h_last = hd[HDR_LAST];
+    bool pre = false;
+    uint32_t pre_psym = 0, pre_last = 0;
+    auto take_record = [&]() {  // (after the stage's loads are issued: its wait covers the record's)
+      pre = uni(h_st) == HDR_OK;
+      pre_psym = pre ? uni(h_psym) : 0u;
+      pre_last = pre ? uni(h_last) : 0u;
+    };
     auto put_tables = [&]() {
 #pragma unroll
       for (uint32_t k = 0; k < NTV; ++k) sm.t.tab[tid + k * HT] = tv[k];
@@ -2368,7 +2380,16 @@ __global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__rest
     };
     if (ndw <= STAGE_DW) {
       const uint32_t *g = reinterpret_cast<const uint32_t *>(dbase);
-      for (uint32_t i = tid; i < ndw; i += HT) sm.stage[i] = g[i];
+      // every stage load before any store (the index clamped): a loop of loads and stores left a
+      // remainder whose loads were each waited for before the next
+      constexpr uint32_t RS = (STAGE_DW + HT - 1) / HT;
+      uint32_t sg[RS];
+#pragma unroll
+      for (uint32_t r = 0; r < RS; ++r) sg[r] = g[min(tid + r * HT, ndw - 1)];
+#pragma unroll
+      for (uint32_t r = 0; r < RS; ++r)
+        if (tid + r * HT < ndw) sm.stage[tid + r * HT] = sg[r];
+      take_record();
       if (pre) put_tables();
       __syncthreads();
 #ifdef SBH_HUFF_PROBE
@@ -2377,6 +2398,7 @@ __global__ __launch_bounds__(HT, SBH_HUFF_OCC) void k_huff(const uint8_t *__rest
       rc = inflate_par<true>(sm, dbase, skip, limit, usize, tok + G, tid, lane, wid, ntok, pre, pre_psym, pre_last, 0,
                              SBH_TAIL != 0, &tail_p, &tail_out);
     } else {
+      take_record();
       if (pre) {
         put_tables();
         __syncthreads();
@@ -2447,27 +2469,48 @@ __global__ __launch_bounds__(TAIL_NT) void k_huff_tail(const uint8_t *__restrict
   const uint32_t skip = p & 31, limit = limit0 - 32 * pd;
   const uint32_t ndw = (limit + 31) / 32 + 2;
   // the tail's first header, from k_hdr<true> (same place and format as k_huff's first one)
+  // (the record is read whatever its status -- its place is inside the token region, usize >=
+  // PAR_MIN_USIZE -- so the record, its status and the stage are loaded in one round trip)
   const uint32_t *hd = tok + G + usize - HDR_OUT_DW;
-  const bool pre = tail_hdr_room(n1, usize) && uni(hd[HDR_STATUS]) == HDR_OK;
+  constexpr uint32_t NTV = HDR_SENT / TAIL_NT, NSV = (352 + TAIL_NT - 1) / TAIL_NT;
+  uint32_t tv[NTV], sv[NSV];
+#pragma unroll
+  for (uint32_t k = 0; k < NTV; ++k) tv[k] = hd[tid + k * TAIL_NT];
+#pragma unroll
+  for (uint32_t k = 0; k < NSV; ++k) sv[k] = hd[HDR_SENT + min(tid + k * TAIL_NT, 351u)];
+  const uint32_t h_st = hd[HDR_STATUS], h_psym = hd[HDR_PSYM], h_last = hd[HDR_LAST];
+  bool pre = false;
   uint32_t pre_psym = 0, pre_last = 0;
-  if (pre) {
-    for (uint32_t i = tid; i < HDR_SENT; i += TAIL_NT) sm.t.tab[i] = hd[i];
-    for (uint32_t i = tid; i < 352; i += TAIL_NT) {  // sent[320] then pk[2][16]
-      const uint32_t v = hd[HDR_SENT + i];
-      if (i < 320) sm.t.sent[i] = v;
-      else sm.t.pk[(i - 320) >> 4][(i - 320) & 15] = v;
+  auto take_record = [&]() {
+    pre = tail_hdr_room(n1, usize) && uni(h_st) == HDR_OK;
+    if (!pre) return;
+    pre_psym = uni(h_psym);
+    pre_last = uni(h_last);
+#pragma unroll
+    for (uint32_t k = 0; k < NTV; ++k) sm.t.tab[tid + k * TAIL_NT] = tv[k];
+#pragma unroll
+    for (uint32_t k = 0; k < NSV; ++k) {  // sent[320] then pk[2][16]
+      const uint32_t i = tid + k * TAIL_NT;
+      if (i < 320) sm.t.sent[i] = sv[k];
+      else if (i < 352) sm.t.pk[(i - 320) >> 4][(i - 320) & 15] = sv[k];
     }
-    pre_psym = uni(hd[HDR_PSYM]);
-    pre_last = uni(hd[HDR_LAST]);
-  }
+  };
   uint32_t n2 = 0, rc;
   if (ndw <= TAIL_DW) {
     const uint32_t *g = reinterpret_cast<const uint32_t *>(dbase);
-    for (uint32_t i = tid; i < ndw; i += TAIL_NT) sm.stage[i] = g[i];
+    constexpr uint32_t R = (TAIL_DW + TAIL_NT - 1) / TAIL_NT;
+    uint32_t v[R];  // (every load before any store, the index clamped)
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) v[r] = g[min(tid + r * TAIL_NT, ndw - 1)];
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r)
+      if (tid + r * TAIL_NT < ndw) sm.stage[tid + r * TAIL_NT] = v[r];
+    take_record();
     __syncthreads();
     rc = inflate_par<true>(sm, dbase, skip, limit, usize - out1, tk, tid, lane, wid, n2, pre, pre_psym, pre_last, out1,
                            false, nullptr, nullptr);
   } else {
+    take_record();
     __syncthreads();
     rc = inflate_par<false>(sm, dbase, skip, limit, usize - out1, tk, tid, lane, wid, n2, pre, pre_psym, pre_last,
                             out1, false, nullptr, nullptr);
@@ -2813,13 +2856,18 @@ static_assert(!(SBH_LZ_CARRY && SBH_LZ_PREFETCH), "the token prefetch assumes ch
     uint32_t x[LZ_TPT], len[LZ_TPT], dist[LZ_TPT], off[LZ_TPT];
     bool match[LZ_TPT];
     uint32_t mysum = 0;
+#if !SBH_LZ_PREFETCH
+    // all of the thread's token loads first, every lane loading (the index clamped): a load under
+    // a branch, or one after the previous token's decoding, was waited for before the next one
+    // was issued -- LZ_TPT HBM round trips per chunk instead of one
+#pragma unroll
+    for (uint32_t k = 0; k < LZ_TPT; ++k) x[k] = tk[min(i0 + k, n - 1)];
+#endif
 #pragma unroll
     for (uint32_t k = 0; k < LZ_TPT; ++k) {
 #if SBH_LZ_PREFETCH
       x[k] = xn[k];
       xn[k] = i0 + LZ_CHUNK + k < n ? tk[i0 + LZ_CHUNK + k] : 0;
-#else
-      x[k] = i0 + k < n ? tk[i0 + k] : 0;
 #endif
       match[k] = i0 + k < n && (x[k] & TOK_MATCH) != 0;
       len[k] = i0 + k >= n ? 0 : match[k] ? (x[k] >> 16) & 0x1ff : 1 + ((x[k] >> 24) & 1u);  // (TOK_PAIR: 2)
