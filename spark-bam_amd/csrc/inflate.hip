@@ -2766,15 +2766,29 @@ __global__ __launch_bounds__(LZ_THREADS, SBH_LZ_WAVES_PER_EU) void k_lz(const ui
       uint16_t *sv = reinterpret_cast<uint16_t *>(sieve) + (g0 >> 4);
       for (uint32_t q = t; q < (sh + usize + 15) / 16; q += LZ_THREADS) sv[q] = 0xffffu;
     }
-    for (uint32_t lo = 16 * t; lo < sh + usize; lo += 16 * LZ_THREADS) {
+    // the thread's whole granules: every load first (a granule past the payload reads the
+    // first one again and is not stored), then the stores -- one round trip, not one per granule
+    constexpr uint32_t NG = (65536u + 16u + 16u * LZ_THREADS - 1u) / (16u * LZ_THREADS);
+    uint32_t d[NG][5];
+#pragma unroll
+    for (uint32_t r = 0; r < NG; ++r) {
+      const uint32_t lo = 16 * t + 16 * LZ_THREADS * r;
+      const bool whole = lo >= sh && lo + 16 <= sh + usize;
+      const uint64_t a = src + (whole ? lo - sh : 0u);
+      const uint32_t *w = reinterpret_cast<const uint32_t *>(comp + (a & ~3ull));
+#pragma unroll
+      for (uint32_t j = 0; j < 5; ++j) d[r][j] = w[j];
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < NG; ++r) {
+      const uint32_t lo = 16 * t + 16 * LZ_THREADS * r;
+      if (lo >= sh + usize) break;
       if (lo >= sh && lo + 16 <= sh + usize) {
-        const uint64_t a = src + (lo - sh);
-        const uint32_t *w = reinterpret_cast<const uint32_t *>(comp + (a & ~3ull));
-        const uint32_t k = (uint32_t)a & 3u, d0 = w[0], d1 = w[1], d2 = w[2], d3 = w[3], d4 = w[4];
+        const uint32_t k = (uint32_t)(src + (lo - sh)) & 3u;
         *reinterpret_cast<uint4 *>(U + g0 + lo) =
-            make_uint4(__builtin_amdgcn_alignbyte(d1, d0, k), __builtin_amdgcn_alignbyte(d2, d1, k),
-                       __builtin_amdgcn_alignbyte(d3, d2, k), __builtin_amdgcn_alignbyte(d4, d3, k));
-      } else {
+            make_uint4(__builtin_amdgcn_alignbyte(d[r][1], d[r][0], k), __builtin_amdgcn_alignbyte(d[r][2], d[r][1], k),
+                       __builtin_amdgcn_alignbyte(d[r][3], d[r][2], k), __builtin_amdgcn_alignbyte(d[r][4], d[r][3], k));
+      } else {  // the block's partial first / last granule
         for (uint32_t j = 0; j < 16; ++j) {
           const uint32_t x = lo + j;
           if (x >= sh && x < sh + usize) U[g0 + x] = comp[src + (x - sh)];
