@@ -2845,6 +2845,9 @@ __global__ __launch_bounds__(LZ_THREADS, SBH_LZ_WAVES_PER_EU) void k_lz(const ui
   uint64_t tp0 = __builtin_readcyclecounter(), t_pre = 0, t_rounds = 0, t_init = 0, t_w = 0, t_ch = 0, t_mk = 0, t_b1 = 0;
   uint32_t nrounds = 0, njumps = 0, nlong = 0;
 #endif
+#ifndef SBH_LZ_TOUCH
+#define SBH_LZ_TOUCH 1  // k_lz: the next chunk's tokens touched into L2 while this chunk's load
+#endif
 #ifndef SBH_LZ_PREFETCH
 // the next chunk's tokens loaded one chunk ahead (0: at the chunk's top).  At the ring's 80 VGPRs
 // the prefetched tokens were spilled to scratch right after their load (which then waited for
@@ -2876,6 +2879,17 @@ static_assert(!(SBH_LZ_CARRY && SBH_LZ_PREFETCH), "the token prefetch assumes ch
     // was issued -- LZ_TPT HBM round trips per chunk instead of one
 #pragma unroll
     for (uint32_t k = 0; k < LZ_TPT; ++k) x[k] = tk[min(i0 + k, n - 1)];
+#if SBH_LZ_TOUCH
+    // the next chunk's tokens (as if this chunk is not cut) touched into L2, a dword per 128-byte
+    // line, behind this chunk's own loads: their wait covers the touch, and the next chunk's
+    // loads then come from L2 instead of HBM
+    uint32_t tch = 0;
+    {
+      const uint32_t nx0 = c0 + LZ_CHUNK + 32 * t;
+      if (t < LZ_CHUNK / 32 && nx0 < n)
+        asm volatile("global_load_dword %0, %1, off" : "=v"(tch) : "v"(tk + nx0) : "memory");
+    }
+#endif
 #endif
 #pragma unroll
     for (uint32_t k = 0; k < LZ_TPT; ++k) {
@@ -2888,6 +2902,9 @@ static_assert(!(SBH_LZ_CARRY && SBH_LZ_PREFETCH), "the token prefetch assumes ch
       dist[k] = x[k] & 0xffff;
       mysum += len[k];
     }
+#if !SBH_LZ_PREFETCH && SBH_LZ_TOUCH
+    asm volatile("" ::"v"(tch));  // (live until the tokens' wait above has covered it)
+#endif
     for (uint32_t w = t; w < SB_WORDS; w += LZ_THREADS) sm.pp.sbits[w] = 0;  // ordered by the scan's barrier
     uint32_t chunk_len;
     off[0] = base + block_scan<LZ_THREADS>(mysum, wsum, &chunk_len);
